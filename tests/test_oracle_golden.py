@@ -1,0 +1,99 @@
+"""Pin the CPU oracle (oracle/ref_net.py) against goldens produced by the
+reference itself (tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_state, load_golden
+from oracle.boards import encode_batch, synth_positions, synth_targets, encode, valid_mask
+from oracle.ref_net import RefModel, RefNet, load_numpy_state, param_count
+
+CFGS = [("3x64", 3, 64), ("6x128", 6, 128)]
+
+
+@pytest.mark.parametrize("tag,blocks,ch", CFGS)
+def test_oracle_init_rng_order_matches_reference(tag, blocks, ch):
+    g = load_golden(tag)
+    torch.manual_seed(0)
+    net = RefNet(blocks, ch)
+    for k, v in net.state_dict().items():
+        if v.dtype.is_floating_point:
+            assert np.isclose(v.double().sum().item(), g[f"init_sum/{k}"], rtol=0, atol=1e-9), k
+            assert np.isclose(v.double().abs().sum().item(), g[f"init_abs/{k}"], rtol=1e-12), k
+
+
+@pytest.mark.parametrize("tag,blocks,ch", CFGS)
+def test_oracle_forward_matches_reference(tag, blocks, ch):
+    torch.set_num_threads(4)
+    g = load_golden(tag)
+    m = RefModel(blocks, ch)
+    load_numpy_state(m.net, golden_state(g))
+    x = encode_batch(g["fwd/boards"], g["fwd/players"])
+    probs, values, logits = m.predict(x, with_logits=True)
+    np.testing.assert_allclose(probs, g["fwd/probs"], atol=1e-6, rtol=0)
+    np.testing.assert_allclose(values, g["fwd/values"], atol=1e-6, rtol=0)
+    np.testing.assert_allclose(logits, g["fwd/logits"], atol=1e-5, rtol=1e-6)
+    # fp32 reference vs its own fp64 run: the tolerance floor is well under 1e-5
+    assert np.abs(g["fwd/probs"] - g["fwd/probs64"]).max() < 1e-5
+    assert np.abs(g["fwd/values"] - g["fwd/values64"]).max() < 1e-5
+
+
+@pytest.mark.parametrize("tag,blocks,ch", CFGS)
+def test_oracle_train_step_matches_reference(tag, blocks, ch):
+    torch.set_num_threads(4)
+    g = load_golden(tag)
+    m = RefModel(blocks, ch)
+    load_numpy_state(m.net, golden_state(g))
+    losses = []
+    for s in range(2):
+        x = encode_batch(g[f"train/boards{s}"], g[f"train/players{s}"])
+        li = m.train_batch(x, g[f"train/pi{s}"], g[f"train/z{s}"])
+        losses.append([li["policy_loss"], li["value_loss"], li["total_loss"]])
+    np.testing.assert_allclose(np.array(losses), g["train/losses"], rtol=1e-5, atol=1e-6)
+    check_train_state(m, g)
+    sd = m.net.state_dict()
+    for k in sd:
+        if "running" in k or "num_batches" in k:
+            np.testing.assert_allclose(sd[k].numpy(), g[f"train/buf/{k}"], atol=1e-4, rtol=1e-3, err_msg=k)
+
+
+def check_train_state(m, g, lr=1e-3, steps=2):
+    """Adam makes the sign of near-zero gradients decide a +-lr update, so the
+    reference is not reproducible across thread counts: oracle(1 or 4 threads)
+    vs reference(8 threads) differs by up to 7e-4 on 0.02-0.4 % of elements
+    (measured).  Gate: moments tight, >= 99 % of params within 2e-5, and every
+    param within the largest change two disagreeing Adam steps can make."""
+    bad = tot = 0
+    for n, p in m.net.named_parameters():
+        idx = g[f"train/idx/{n}"]
+        got = p.detach().reshape(-1).cpu().numpy()[idx]
+        d = np.abs(got - g[f"train/param/{n}"])
+        assert d.max() <= 2 * steps * lr * 1.01, (n, d.max())
+        bad += int((d > 2e-5).sum())
+        tot += d.size
+        st = m.optimizer.state[p]
+        ea = st["exp_avg"].reshape(-1).cpu().numpy()[idx]
+        np.testing.assert_allclose(ea, g[f"train/exp_avg/{n}"], atol=2e-5, rtol=1e-3, err_msg=n)
+        es = st["exp_avg_sq"].reshape(-1).cpu().numpy()[idx]
+        np.testing.assert_allclose(es, g[f"train/exp_avg_sq/{n}"], atol=1e-8, rtol=1e-3, err_msg=n)
+    assert bad <= 0.01 * tot, (bad, tot)
+
+
+def test_param_counts():
+    # SURVEY §8(a) a2 [measured]
+    assert param_count(3, 64) == 340_010
+    assert param_count(6, 128) == 1_892_650
+    assert param_count(10, 256) == 11_930_922
+    net = RefNet(3, 64)
+    assert sum(p.numel() for p in net.parameters()) == 340_010
+
+
+def test_encoding_contract():
+    b, p = synth_positions(8, seed=5)
+    for bi, pi in zip(b, p):
+        e = encode(bi, int(pi))
+        assert e.shape == (3, 15, 15) and e.dtype == np.float32
+        assert np.all(e[2] == 1.0)                         # constant plane, gomoku.py:148
+        assert np.array_equal(e[0], (bi == pi).astype(np.float32))
+        assert np.array_equal(e[1], (bi == 3 - pi).astype(np.float32))
+        assert np.array_equal(valid_mask(bi), (bi.reshape(-1) == 0).astype(np.float32))
