@@ -1,0 +1,342 @@
+// C-ABI of the policy/value engine (include/azg_pv.h): handle lifecycle,
+// flat-buffer layout, workspace management and the forward orchestration.
+// Compiled by hipcc for gfx950 together with the kernel translation units.
+#include "../../include/azg_pv.h"
+#include "pv_internal.h"
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+using namespace azg;
+
+static thread_local std::string g_err;
+
+static int32_t fail(const char* what, hipError_t e = hipSuccess)
+{
+    g_err = what;
+    if (e != hipSuccess) {
+        g_err += ": ";
+        g_err += hipGetErrorString(e);
+    }
+    return 1;
+}
+
+#define AZG_TRY(expr, what)                      \
+    do {                                         \
+        hipError_t _e = (expr);                  \
+        if (_e != hipSuccess) return fail(what, _e); \
+    } while (0)
+
+extern "C" {
+
+int32_t azg_pv_abi_version(void) { return 1; }
+
+const char* azg_pv_last_error(void) { return g_err.c_str(); }
+
+int32_t azg_pv_create(const azg_pv_config* cfg, azg_pv** out)
+{
+    if (!cfg || !out) return fail("azg_pv_create: null argument");
+    *out = nullptr;
+    if (cfg->board != BOARD) return fail("azg_pv_create: only board=15 is built");
+    if (cfg->in_ch != 3) return fail("azg_pv_create: in_ch must be 3 (games/gomoku.py:146-150)");
+    if (cfg->channels != 64 && cfg->channels != 128 && cfg->channels != 256)
+        return fail("azg_pv_create: channels must be 64, 128 or 256");
+    if (cfg->blocks < 0 || cfg->blocks > 64) return fail("azg_pv_create: blocks out of range");
+    azg_pv* h = new (std::nothrow) azg_pv();
+    if (!h) return fail("azg_pv_create: out of host memory");
+    h->cfg = *cfg;
+    h->C = cfg->channels;
+    h->NB = cfg->blocks;
+    build_layout(h);
+    *out = h;
+    return 0;
+}
+
+int32_t azg_pv_destroy(azg_pv* h)
+{
+    if (!h) return 0;
+    if (h->wbase) (void)hipDeviceSynchronize();
+    free_workspace(h);
+    if (h->wbase) (void)hipFree(h->wbase);
+    if (h->bn_desc_dev) (void)hipFree(h->bn_desc_dev);
+    for (auto& e : h->prof_ev) (void)hipEventDestroy(e);
+    delete h;
+    return 0;
+}
+
+int64_t azg_pv_param_count(const azg_pv* h) { return h ? h->nparams : -1; }
+int64_t azg_pv_bn_count(const azg_pv* h) { return h ? h->nbn : -1; }
+int32_t azg_pv_num_param_tensors(const azg_pv* h) { return h ? (int32_t)h->poff.size() : -1; }
+
+int32_t azg_pv_param_layout(const azg_pv* h, int64_t* offsets, int64_t* numels)
+{
+    if (!h || !offsets || !numels) return fail("azg_pv_param_layout: null argument");
+    for (size_t i = 0; i < h->poff.size(); ++i) {
+        offsets[i] = h->poff[i];
+        numels[i] = h->pnum[i];
+    }
+    return 0;
+}
+
+int32_t azg_pv_bind(azg_pv* h, float* params, float* grads, float* bn_stats)
+{
+    if (!h || !params || !bn_stats) return fail("azg_pv_bind: null handle/params/bn_stats");
+    if (!h->wbase) {   // device workspace is allocated at first bind (create is host-only)
+        const int C = h->C;
+        size_t floats = 0;
+        floats += (size_t)2 * h->NB * 9 * C * C;   // wpack
+        floats += (size_t)27 * C;                  // wstem
+        floats += (size_t)h->nfold * 2;            // scale, shift
+        floats += (size_t)2 * PIX * ACTIONS;       // wpfT
+        floats += (size_t)PIX * VHID;              // wv1T
+        float* base = nullptr;
+        hipError_t e = hipMalloc(&base, floats * sizeof(float));
+        if (e != hipSuccess) return fail("azg_pv_bind: hipMalloc(packed weights)", e);
+        h->wbase = base;
+        h->wpack = base; base += (size_t)2 * h->NB * 9 * C * C;
+        h->wstem = base; base += (size_t)27 * C;
+        h->scale = base; base += h->nfold;
+        h->shift = base; base += h->nfold;
+        h->wpfT = base; base += (size_t)2 * PIX * ACTIONS;
+        h->wv1T = base; base += (size_t)PIX * VHID;
+        e = hipMalloc(&h->bn_desc_dev, sizeof(BnDesc) * h->bn_desc.size());
+        if (e == hipSuccess)
+            e = hipMemcpy(h->bn_desc_dev, h->bn_desc.data(), sizeof(BnDesc) * h->bn_desc.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) return fail("azg_pv_bind: bn descriptor upload", e);
+    }
+    h->params = params;
+    h->grads = grads;
+    h->bn = bn_stats;
+    h->dirty = true;
+    return 0;
+}
+
+int32_t azg_pv_mark_dirty(azg_pv* h)
+{
+    if (!h) return fail("azg_pv_mark_dirty: null handle");
+    h->dirty = true;
+    return 0;
+}
+
+int32_t azg_pv_forward(azg_pv* h, const float* x, int32_t batch, float* probs, float* values,
+                       float* logits, void* stream)
+{
+    if (!h || !h->params) return fail("azg_pv_forward: handle not bound (azg_pv_bind)");
+    if (!x || !probs || !values) return fail("azg_pv_forward: null x/probs/values");
+    if (batch <= 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (int32_t r = ensure_eval_workspace(h, batch, st)) return r;
+    if (h->dirty) {
+        if (int32_t r = repack(h, st)) return r;
+        h->dirty = false;
+    }
+    return forward_eval(h, x, batch, probs, values, logits, st);
+}
+
+int32_t azg_pv_profile_enable(azg_pv* h, int32_t enable)
+{
+    if (!h) return fail("azg_pv_profile_enable: null handle");
+    if (enable && h->prof_ev.empty()) {
+        h->prof_ev.resize(2 * 8192);
+        for (auto& e : h->prof_ev) AZG_TRY(hipEventCreate(&e), "azg_pv_profile_enable: hipEventCreate");
+        h->prof_cls.assign(8192, 0);
+    }
+    if (enable) AZG_TRY(hipDeviceSynchronize(), "azg_pv_profile_enable: sync");
+    h->prof_on = enable != 0;
+    h->prof_used = 0;
+    for (int i = 0; i < AZG_PROF_NCLASS; ++i) { h->prof_ms[i] = 0.0; h->prof_n[i] = 0; }
+    return 0;
+}
+
+int32_t azg_pv_profile_read(azg_pv* h, double* ms, int64_t* launches)
+{
+    if (!h || !ms || !launches) return fail("azg_pv_profile_read: null argument");
+    for (int i = 0; i < h->prof_used; ++i) {
+        AZG_TRY(hipEventSynchronize(h->prof_ev[2 * i + 1]), "azg_pv_profile_read: sync");
+        float t = 0.f;
+        AZG_TRY(hipEventElapsedTime(&t, h->prof_ev[2 * i], h->prof_ev[2 * i + 1]), "azg_pv_profile_read: elapsed");
+        h->prof_ms[h->prof_cls[i]] += t;
+        h->prof_n[h->prof_cls[i]] += 1;
+    }
+    h->prof_used = 0;
+    for (int i = 0; i < AZG_PROF_NCLASS; ++i) { ms[i] = h->prof_ms[i]; launches[i] = h->prof_n[i]; }
+    return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+
+namespace azg {
+
+int32_t set_error(const char* what, hipError_t e) { return fail(what, e); }
+
+int prof_begin(azg_pv* h, int cls, hipStream_t st)
+{
+    if (!h->prof_on || h->prof_used >= (int)h->prof_cls.size()) return -1;
+    const int i = h->prof_used++;
+    h->prof_cls[i] = cls;
+    (void)hipEventRecord(h->prof_ev[2 * i], st);
+    return i;
+}
+
+void prof_end(azg_pv* h, int pair, hipStream_t st)
+{
+    if (pair >= 0) (void)hipEventRecord(h->prof_ev[2 * pair + 1], st);
+}
+
+void build_layout(azg_pv* h)
+{
+    const int C = h->C, NB = h->NB;
+    h->poff.clear();
+    h->pnum.clear();
+    int64_t off = 0;
+    auto add = [&](int64_t n) { h->poff.push_back(off); h->pnum.push_back(n); off += n; return (int)h->poff.size() - 1; };
+    // nn.Module.parameters() order of network.py:41-73
+    h->t_stem_w = add((int64_t)C * 27);
+    h->t_stem_g = add(C);
+    h->t_stem_b = add(C);
+    h->t_blk.assign(NB, {});
+    for (int i = 0; i < NB; ++i) {
+        h->t_blk[i].w1 = add((int64_t)C * C * 9);
+        h->t_blk[i].g1 = add(C);
+        h->t_blk[i].b1 = add(C);
+        h->t_blk[i].w2 = add((int64_t)C * C * 9);
+        h->t_blk[i].g2 = add(C);
+        h->t_blk[i].b2 = add(C);
+    }
+    h->t_pc_w = add(2 * C);
+    h->t_pbn_g = add(2);
+    h->t_pbn_b = add(2);
+    h->t_pfc_w = add((int64_t)ACTIONS * 2 * PIX);
+    h->t_pfc_b = add(ACTIONS);
+    h->t_vc_w = add(C);
+    h->t_vbn_g = add(1);
+    h->t_vbn_b = add(1);
+    h->t_vfc1_w = add((int64_t)VHID * PIX);
+    h->t_vfc1_b = add(VHID);
+    h->t_vfc2_w = add(VHID);
+    h->t_vfc2_b = add(1);
+    h->nparams = off;
+
+    // BN layers: stem, (bn1, bn2) per block, policy_bn, value_bn
+    h->bn_desc.clear();
+    int stat = 0, fold = 0;
+    auto addbn = [&](int g, int b, int c) {
+        BnDesc d{};
+        d.gamma_off = (int)h->poff[g];
+        d.beta_off = (int)h->poff[b];
+        d.stat_off = stat;
+        d.c = c;
+        d.out_off = fold;
+        h->bn_desc.push_back(d);
+        stat += 2 * c;
+        fold += c;
+        return (int)h->bn_desc.size() - 1;
+    };
+    h->bn_stem = addbn(h->t_stem_g, h->t_stem_b, C);
+    h->bn_blk.assign(NB, {});
+    for (int i = 0; i < NB; ++i) {
+        h->bn_blk[i].first = addbn(h->t_blk[i].g1, h->t_blk[i].b1, C);
+        h->bn_blk[i].second = addbn(h->t_blk[i].g2, h->t_blk[i].b2, C);
+    }
+    h->bn_pol = addbn(h->t_pbn_g, h->t_pbn_b, 2);
+    h->bn_val = addbn(h->t_vbn_g, h->t_vbn_b, 1);
+    h->nbn = stat;
+    h->nfold = fold;
+}
+
+void free_workspace(azg_pv* h)
+{
+    for (int i = 0; i < 3; ++i) {
+        if (h->act[i]) (void)hipFree(h->act[i]);
+        h->act[i] = nullptr;
+    }
+    h->act_cap = 0;
+    free_train_workspace(h);
+}
+
+int32_t ensure_eval_workspace(azg_pv* h, int batch, hipStream_t st)
+{
+    if (batch <= h->act_cap) return 0;
+    int cap = h->act_cap ? h->act_cap : 64;
+    while (cap < batch) cap *= 2;
+    for (int i = 0; i < 3; ++i) {
+        if (h->act[i]) (void)hipFree(h->act[i]);
+        h->act[i] = nullptr;
+    }
+    h->act_cap = 0;
+    const size_t bytes = (size_t)cap * PADPIX * h->C * sizeof(float);
+    for (int i = 0; i < 3; ++i) {
+        hipError_t e = hipMalloc(&h->act[i], bytes);
+        if (e != hipSuccess) return fail("ensure_eval_workspace: hipMalloc(activations)", e);
+        // zero halo: written once, never touched by the kernels
+        e = hipMemsetAsync(h->act[i], 0, bytes, st);
+        if (e != hipSuccess) return fail("ensure_eval_workspace: hipMemsetAsync", e);
+    }
+    h->act_cap = cap;
+    return 0;
+}
+
+int32_t repack(azg_pv* h, hipStream_t st)
+{
+    const int C = h->C;
+    const float* P = h->params;
+    AZG_TRY(launch_pack_stem(P + h->poff[h->t_stem_w], h->wstem, C, st), "repack: stem");
+    for (int i = 0; i < h->NB; ++i) {
+        AZG_TRY(launch_pack_conv3x3(P + h->poff[h->t_blk[i].w1], h->wpack + (size_t)(2 * i) * 9 * C * C, C, st),
+                "repack: conv1");
+        AZG_TRY(launch_pack_conv3x3(P + h->poff[h->t_blk[i].w2], h->wpack + (size_t)(2 * i + 1) * 9 * C * C, C, st),
+                "repack: conv2");
+    }
+    AZG_TRY(launch_transpose(P + h->poff[h->t_pfc_w], h->wpfT, ACTIONS, 2 * PIX, st), "repack: policy_fc^T");
+    AZG_TRY(launch_transpose(P + h->poff[h->t_vfc1_w], h->wv1T, VHID, PIX, st), "repack: value_fc1^T");
+    AZG_TRY(launch_fold_bn(P, h->bn, h->bn_desc_dev, (int)h->bn_desc.size(), h->scale, h->shift, st),
+            "repack: fold_bn");
+    return 0;
+}
+
+int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* values, float* logits,
+                     hipStream_t st)
+{
+    const int C = h->C;
+    const int M = batch * PIX;
+    const float* P = h->params;
+    const BnDesc* bd = h->bn_desc.data();
+    int pr = prof_begin(h, AZG_PROF_STEM, st);
+    AZG_TRY(launch_stem(C, EPI_BN_RELU, x, h->wstem, h->scale + bd[h->bn_stem].out_off,
+                        h->shift + bd[h->bn_stem].out_off, h->act[0], batch, st),
+            "forward: stem");
+    prof_end(h, pr, st);
+    float* X = h->act[0];
+    float* H = h->act[1];
+    float* Y = h->act[2];
+    for (int i = 0; i < h->NB; ++i) {
+        const BnDesc& b1 = bd[h->bn_blk[i].first];
+        const BnDesc& b2 = bd[h->bn_blk[i].second];
+        pr = prof_begin(h, AZG_PROF_CONV3X3, st);
+        AZG_TRY(launch_conv3x3(C, EPI_BN_RELU, X, h->wpack + (size_t)(2 * i) * 9 * C * C, h->scale + b1.out_off,
+                               h->shift + b1.out_off, nullptr, H, M, st),
+                "forward: conv1");
+        prof_end(h, pr, st);
+        pr = prof_begin(h, AZG_PROF_CONV3X3, st);
+        AZG_TRY(launch_conv3x3(C, EPI_BN_RES_RELU, H, h->wpack + (size_t)(2 * i + 1) * 9 * C * C,
+                               h->scale + b2.out_off, h->shift + b2.out_off, X, Y, M, st),
+                "forward: conv2");
+        prof_end(h, pr, st);
+        float* t = X; X = Y; Y = t;
+    }
+    const int ho = bd[h->bn_pol].out_off;   // policy (2) then value (1): contiguous
+    pr = prof_begin(h, AZG_PROF_HEADS, st);
+    AZG_TRY(launch_heads_fwd(C, X, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], h->scale + ho, h->shift + ho,
+                             h->wpfT, P + h->poff[h->t_pfc_b], h->wv1T, P + h->poff[h->t_vfc1_b],
+                             P + h->poff[h->t_vfc2_w], P + h->poff[h->t_vfc2_b], probs, values, logits, batch, st),
+            "forward: heads");
+    prof_end(h, pr, st);
+    return 0;
+}
+
+}  // namespace azg

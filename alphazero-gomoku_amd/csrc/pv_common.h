@@ -1,0 +1,52 @@
+// Shared definitions for the gfx950 policy/value kernels.
+//
+// Activation layout in HBM ("padded NHWC"): act[b][17][17][C] fp32, the 1-pixel
+// zero halo is written once at allocation and never touched again, so every
+// 3x3 tap of an interior pixel is an unconditional load.  Pixel m of the batch
+// (m = b*225 + y*15 + x) lives at element ((b*289 + (y+1)*17 + (x+1)) * C).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace azg {
+
+constexpr int BOARD = 15;
+constexpr int PIX = BOARD * BOARD;        // 225
+constexpr int PADW = BOARD + 2;           // 17
+constexpr int PADPIX = PADW * PADW;       // 289
+constexpr int ACTIONS = PIX;              // 225
+constexpr int VHID = 64;                  // value_fc1 width (network.py:70)
+constexpr float BN_EPS = 1e-5f;           // nn.BatchNorm2d default
+constexpr float BN_MOMENTUM = 0.1f;       // nn.BatchNorm2d default
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// element offset of interior pixel m in a padded NHWC tensor with C channels
+__device__ __forceinline__ int pad_off(int m, int C) {
+    int b = m / PIX;
+    int p = m - b * PIX;
+    int y = p / BOARD;
+    int x = p - y * BOARD;
+    return (b * PADPIX + (y + 1) * PADW + (x + 1)) * C;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+enum Epi : int {
+    EPI_BN_RELU = 0,      // relu(acc*scale + shift)
+    EPI_BN_RES_RELU = 1,  // relu(acc*scale + shift + resid)
+    EPI_RAW = 2,          // acc (train-mode conv output, dgrad)
+};
+
+}  // namespace azg

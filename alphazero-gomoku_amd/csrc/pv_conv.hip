@@ -1,0 +1,269 @@
+// 3x3 convolution (pad 1, no bias) as an fp32-MFMA implicit GEMM for gfx950,
+// with the BatchNorm / residual / ReLU epilogue fused.
+//
+// Replaces the ATen conv2d + batch_norm + relu (+ in-place residual add) chain of
+// the reference ResidualBlock (network.py:9-26) and stem (network.py:94-96).
+//
+// GEMM view: rows m = pixel of the batch (B*225), cols n = output channel,
+// K = 9 taps x C input channels.  A[m][k] is read straight from the padded NHWC
+// activation (the halo makes every tap an unconditional 16-byte load), B is the
+// weight re-packed to [kchunk][n][32] so a K-chunk of 32 is one contiguous block.
+//
+// Tile: 128 pixels x min(C,128) channels per 256-thread workgroup, K-chunk 32.
+// 4 waves in 2x2, each owning 64 x (BN/2) outputs as 32x32 accumulators of
+// v_mfma_f32_32x32x2_f32 (exact f32 FMA chain: the parity budget is 1e-5 fp32,
+// so no bf16/xf32).  LDS holds two chunks (double buffer) with rows padded to
+// 36 floats: every ds_read_b128 fragment load is bank-conflict free
+// (row*36 mod 64 = 4*(9*row mod 16)).  Global->LDS staging is register staged
+// and issued before the MFMAs of the current chunk (async-STAGE split), one
+// barrier per chunk.
+//
+// Lane l of an MFMA step s uses K index h*16+s (h = l>>5) for both A and B, so
+// each lane's 16 A values and 16 B values of a chunk are contiguous in LDS.
+#include "pv_common.h"
+
+namespace azg {
+
+template <int C>
+struct ConvTile {
+    static constexpr int BM = 128;
+    static constexpr int BN = C < 128 ? C : 128;
+    static constexpr int BK = 32;
+    static constexpr int LDK = BK + 4;
+    static constexpr int CG = C / BK;
+    static constexpr int NCH = 9 * CG;
+    static constexpr int WN = BN / 2;
+    static constexpr int TM = 2;
+    static constexpr int TN = WN / 32;
+    static constexpr int A_LD = BM * BK / 4 / 256;
+    static constexpr int B_LD = BN * BK / 4 / 256;
+    static constexpr int LDS_BYTES = 2 * (BM + BN) * LDK * 4;
+};
+
+template <int C, int EPI>
+__global__ __launch_bounds__(256, 2) void conv3x3_mfma(
+    const float* __restrict__ in, const float* __restrict__ wp,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ resid, float* __restrict__ out, int M)
+{
+    using T = ConvTile<C>;
+    constexpr int BM = T::BM, BN = T::BN, BK = T::BK, LDK = T::LDK;
+    constexpr int CG = T::CG, NCH = T::NCH, WN = T::WN, TM = T::TM, TN = T::TN;
+    constexpr int A_LD = T::A_LD, B_LD = T::B_LD;
+
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* As = smem;                    // [2][BM][LDK]
+    float* Bs = smem + 2 * BM * LDK;     // [2][BN][LDK]
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int m0 = blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+
+    // staging: thread -> (row sr + 32 i, floats sc..sc+3)
+    const int sr = tid >> 3, sc = (tid & 7) * 4;
+    int abase[A_LD];
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+        int m = m0 + sr + 32 * i;
+        m = m < M ? m : M - 1;           // tail rows: clamp to a valid pixel, never stored
+        abase[i] = pad_off(m, C) + sc;
+    }
+    const float* wsrc = wp + (size_t)(n0 + sr) * BK + sc;
+
+    f32x4 ra[A_LD], rb[B_LD];
+    auto gload = [&](int kc) {
+        const int tap = kc / CG, cg = kc - tap * CG;
+        const int ky = tap / 3, kx = tap - ky * 3;
+        const int toff = ((ky - 1) * PADW + (kx - 1)) * C + cg * BK;
+#pragma unroll
+        for (int i = 0; i < A_LD; ++i) ra[i] = *(const f32x4*)(in + abase[i] + toff);
+        const float* wk = wsrc + (size_t)kc * C * BK;
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) rb[i] = *(const f32x4*)(wk + 32 * i * BK);
+    };
+    auto lstore = [&](int buf) {
+        float* a = As + buf * BM * LDK;
+        float* b = Bs + buf * BN * LDK;
+#pragma unroll
+        for (int i = 0; i < A_LD; ++i) *(f32x4*)(a + (sr + 32 * i) * LDK + sc) = ra[i];
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) *(f32x4*)(b + (sr + 32 * i) * LDK + sc) = rb[i];
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int r32 = lane & 31, h = lane >> 5;
+    const int arow = (wm * 64 + r32) * LDK + h * 16;
+    const int brow = (wn * WN + r32) * LDK + h * 16;
+
+    gload(0);
+    lstore(0);
+    __syncthreads();
+
+    for (int kc = 0; kc < NCH; ++kc) {
+        const int cur = kc & 1;
+        if (kc + 1 < NCH) gload(kc + 1);
+        const float* Ab = As + cur * BM * LDK;
+        const float* Bb = Bs + cur * BN * LDK;
+        f32x4 a[TM][4], b[TN][4];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a[i][q] = *(const f32x4*)(Ab + arow + i * 32 * LDK + q * 4);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b[j][q] = *(const f32x4*)(Bb + brow + j * 32 * LDK + q * 4);
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s >> 2][s & 3], b[j][s >> 2][s & 3],
+                                                                    acc[i][j], 0, 0, 0);
+        if (kc + 1 < NCH) lstore(cur ^ 1);
+        __syncthreads();
+    }
+
+    // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * WN + j * 32 + r32;
+        float s_ = 1.f, t_ = 0.f;
+        if (EPI != EPI_RAW) { s_ = scale[col]; t_ = shift[col]; }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m < M) {
+                    const int o = pad_off(m, C) + col;
+                    float v = acc[i][j][r];
+                    if (EPI == EPI_BN_RELU) {
+                        v = fmaxf(v * s_ + t_, 0.f);
+                    } else if (EPI == EPI_BN_RES_RELU) {
+                        v = fmaxf(v * s_ + t_ + resid[o], 0.f);
+                    }
+                    out[o] = v;
+                }
+            }
+        }
+    }
+}
+
+// Stem conv 3->C (K = 27) on the VALU: 0.2 % of the forward FLOPs.  One
+// workgroup per board; the board's 3 input planes are staged into LDS with a
+// zero halo; each thread owns one output channel (27 weights in registers) and a
+// strided set of pixels.  Weight layout ws[k][c], k = ci*9 + ky*3 + kx.
+template <int C, int EPI>
+__global__ __launch_bounds__(256) void stem_conv(
+    const float* __restrict__ x, const float* __restrict__ ws,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    float* __restrict__ out)
+{
+    __shared__ float xs[3 * PADPIX];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const float* xb = x + (size_t)b * 3 * PIX;
+    for (int i = tid; i < 3 * PADPIX; i += 256) {
+        const int ci = i / PADPIX, rem = i - ci * PADPIX;
+        const int yy = rem / PADW, xx = rem - yy * PADW;
+        float v = 0.f;
+        if (yy >= 1 && yy <= BOARD && xx >= 1 && xx <= BOARD) v = xb[ci * PIX + (yy - 1) * BOARD + (xx - 1)];
+        xs[i] = v;
+    }
+    __syncthreads();
+    constexpr int CPT = C < 256 ? 1 : C / 256;      // channels per thread
+    constexpr int TPP = C < 256 ? C : 256;          // threads per pixel
+    constexpr int PPI = 256 / TPP;                  // pixels per iteration
+    const int c0 = tid % TPP;
+    const int pp = tid / TPP;
+#pragma unroll
+    for (int cc = 0; cc < CPT; ++cc) {
+        const int c = c0 + cc * TPP;
+        float w[27];
+#pragma unroll
+        for (int k = 0; k < 27; ++k) w[k] = ws[k * C + c];
+        float s_ = 1.f, t_ = 0.f;
+        if (EPI != EPI_RAW) { s_ = scale[c]; t_ = shift[c]; }
+        for (int p = pp; p < PIX; p += PPI) {
+            const int y = p / BOARD, xq = p - y * BOARD;
+            float acc = 0.f;
+#pragma unroll
+            for (int ci = 0; ci < 3; ++ci)
+#pragma unroll
+                for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                    for (int kx = 0; kx < 3; ++kx)
+                        acc = fmaf(xs[ci * PADPIX + (y + ky) * PADW + (xq + kx)], w[ci * 9 + ky * 3 + kx], acc);
+            float v = acc;
+            if (EPI == EPI_BN_RELU) v = fmaxf(v * s_ + t_, 0.f);
+            out[(size_t)(b * PADPIX + (y + 1) * PADW + (xq + 1)) * C + c] = v;
+        }
+    }
+}
+
+// ---- host launchers ------------------------------------------------------
+
+template <int C, int EPI>
+static hipError_t launch_conv_t(const float* in, const float* wp, const float* scale, const float* shift,
+                                const float* resid, float* out, int M, hipStream_t st)
+{
+    using T = ConvTile<C>;
+    static bool attr_done = false;
+    if (!attr_done) {
+        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_mfma<C, EPI>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS_BYTES);
+        if (e != hipSuccess) return e;
+        attr_done = true;
+    }
+    dim3 grid((M + T::BM - 1) / T::BM, C / T::BN);
+    hipLaunchKernelGGL((conv3x3_mfma<C, EPI>), grid, dim3(256), T::LDS_BYTES, st,
+                       in, wp, scale, shift, resid, out, M);
+    return hipGetLastError();
+}
+
+hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, const float* scale,
+                          const float* shift, const float* resid, float* out, int M, hipStream_t st)
+{
+#define AZG_CONV_CASE(CC)                                                                            \
+    case CC:                                                                                         \
+        if (epi == EPI_BN_RELU) return launch_conv_t<CC, EPI_BN_RELU>(in, wp, scale, shift, resid, out, M, st); \
+        if (epi == EPI_BN_RES_RELU) return launch_conv_t<CC, EPI_BN_RES_RELU>(in, wp, scale, shift, resid, out, M, st); \
+        return launch_conv_t<CC, EPI_RAW>(in, wp, scale, shift, resid, out, M, st);
+    switch (C) {
+        AZG_CONV_CASE(64)
+        AZG_CONV_CASE(128)
+        AZG_CONV_CASE(256)
+        default: return hipErrorInvalidValue;
+    }
+#undef AZG_CONV_CASE
+}
+
+hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const float* scale,
+                       const float* shift, float* out, int B, hipStream_t st)
+{
+#define AZG_STEM_CASE(CC)                                                                              \
+    case CC:                                                                                           \
+        if (epi == EPI_RAW) hipLaunchKernelGGL((stem_conv<CC, EPI_RAW>), dim3(B), dim3(256), 0, st, x, ws, scale, shift, out); \
+        else hipLaunchKernelGGL((stem_conv<CC, EPI_BN_RELU>), dim3(B), dim3(256), 0, st, x, ws, scale, shift, out); \
+        return hipGetLastError();
+    switch (C) {
+        AZG_STEM_CASE(64)
+        AZG_STEM_CASE(128)
+        AZG_STEM_CASE(256)
+        default: return hipErrorInvalidValue;
+    }
+#undef AZG_STEM_CASE
+}
+
+}  // namespace azg

@@ -1,0 +1,100 @@
+// Internal (non-ABI) declarations shared by the C-ABI and the kernel launchers.
+#pragma once
+#include "pv_common.h"
+#include "../../include/azg_pv.h"
+
+#include <vector>
+
+namespace azg {
+
+struct BnDesc {
+    int gamma_off;
+    int beta_off;
+    int stat_off;
+    int c;
+    int out_off;
+    int pad[3];
+};
+
+struct BlockTensors { int w1, g1, b1, w2, g2, b2; };
+struct BlockBn { int first, second; };
+
+// kernel launchers (pv_conv.hip, pv_heads.hip, pv_pack.hip, pv_train.hip)
+hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, const float* scale,
+                          const float* shift, const float* resid, float* out, int M, hipStream_t st);
+hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const float* scale,
+                       const float* shift, float* out, int B, hipStream_t st);
+hipError_t launch_heads_fwd(int C, const float* act, const float* wpc, const float* wvc,
+                            const float* hscale, const float* hshift, const float* wpfT,
+                            const float* bpf, const float* wv1T, const float* bv1,
+                            const float* wv2, const float* bv2, float* probs, float* values,
+                            float* logits, int B, hipStream_t st);
+hipError_t launch_pack_conv3x3(const float* w, float* wp, int C, hipStream_t st);
+hipError_t launch_pack_dgrad(const float* w, float* wd, int C, hipStream_t st);
+hipError_t launch_pack_stem(const float* w, float* ws, int C, hipStream_t st);
+hipError_t launch_transpose(const float* src, float* dst, int R, int Cc, hipStream_t st);
+hipError_t launch_fold_bn(const float* params, const float* stats, const void* desc, int nlayers,
+                          float* scale, float* shift, hipStream_t st);
+
+}  // namespace azg
+
+struct azg_pv {
+    azg_pv_config cfg{};
+    int C = 0, NB = 0;
+
+    // flat layout (nn.Module.parameters() order)
+    std::vector<int64_t> poff, pnum;
+    int64_t nparams = 0, nbn = 0;
+    int nfold = 0;
+    int t_stem_w = 0, t_stem_g = 0, t_stem_b = 0;
+    std::vector<azg::BlockTensors> t_blk;
+    int t_pc_w = 0, t_pbn_g = 0, t_pbn_b = 0, t_pfc_w = 0, t_pfc_b = 0;
+    int t_vc_w = 0, t_vbn_g = 0, t_vbn_b = 0, t_vfc1_w = 0, t_vfc1_b = 0, t_vfc2_w = 0, t_vfc2_b = 0;
+    std::vector<azg::BnDesc> bn_desc;
+    int bn_stem = 0, bn_pol = 0, bn_val = 0;
+    std::vector<azg::BlockBn> bn_blk;
+    void* bn_desc_dev = nullptr;
+
+    // bound torch-owned buffers
+    float* params = nullptr;
+    float* grads = nullptr;
+    float* bn = nullptr;
+    bool dirty = true;
+
+    // packed / derived weights (one allocation)
+    float* wbase = nullptr;
+    float* wpack = nullptr;   // 2*NB x [9*C/32][C][32]
+    float* wstem = nullptr;   // [27][C]
+    float* scale = nullptr;   // folded BN (eval)
+    float* shift = nullptr;
+    float* wpfT = nullptr;    // [450][225]
+    float* wv1T = nullptr;    // [225][64]
+
+    // eval activations: 3 padded NHWC buffers
+    float* act[3] = {nullptr, nullptr, nullptr};
+    int act_cap = 0;
+
+    // train workspace (pv_train.hip)
+    void* train = nullptr;
+
+    // kernel-class event timing (azg_pv_profile_*)
+    bool prof_on = false;
+    std::vector<hipEvent_t> prof_ev;     // pairs
+    std::vector<int> prof_cls;           // class per used pair
+    int prof_used = 0;
+    double prof_ms[AZG_PROF_NCLASS] = {};
+    int64_t prof_n[AZG_PROF_NCLASS] = {};
+};
+
+namespace azg {
+int32_t set_error(const char* what, hipError_t e);
+void build_layout(azg_pv* h);
+void free_workspace(azg_pv* h);
+void free_train_workspace(azg_pv* h);
+int32_t ensure_eval_workspace(azg_pv* h, int batch, hipStream_t st);
+int32_t repack(azg_pv* h, hipStream_t st);
+int prof_begin(azg_pv* h, int cls, hipStream_t st);   // returns pair index or -1
+void prof_end(azg_pv* h, int pair, hipStream_t st);
+int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* values, float* logits,
+                     hipStream_t st);
+}  // namespace azg

@@ -1,0 +1,113 @@
+// Weight re-packing and BatchNorm folding (run when parameters change).
+//
+// Torch layouts in (network.py:41-73): conv [Cout][Cin][3][3], linear [out][in].
+// Packed layouts out:
+//   res conv  -> wp[kc][n][32], kc = tap*(C/32) + cin/32, tap = ky*3 + kx
+//   dgrad     -> wd[kc][n=cin][32 of cout] for the flipped tap (transpose conv)
+//   stem      -> ws[k][c], k = cin*9 + ky*3 + kx
+//   FC        -> W^T [in][out]
+// Eval-mode BN fold, as ATen's CPU inference path (alpha = invstd*gamma,
+// beta = bias - mean*alpha, y = x*alpha + beta):
+//   invstd = 1/sqrt(running_var + eps)
+#include "pv_internal.h"
+
+namespace azg {
+
+
+__global__ void pack_conv3x3_kernel(const float* __restrict__ w, float* __restrict__ wp, int C)
+{
+    const int total = 9 * C * C;
+    const int cg_n = C / 32;
+    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+        const int k = idx & 31;
+        const int n = (idx >> 5) % C;
+        const int kc = idx / (32 * C);
+        const int tap = kc / cg_n, cg = kc - tap * cg_n;
+        const int ci = cg * 32 + k;
+        wp[idx] = w[(n * C + ci) * 9 + tap];
+    }
+}
+
+// transpose-conv packing for dgrad: dX[ci] at pixel q = sum over taps t' and
+// cout of dY[co] at q + off(t') * W[co][ci][2-ky'][2-kx'] where t' = (ky',kx').
+__global__ void pack_dgrad_kernel(const float* __restrict__ w, float* __restrict__ wd, int C)
+{
+    const int total = 9 * C * C;
+    const int cg_n = C / 32;
+    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+        const int k = idx & 31;              // cout within chunk
+        const int n = (idx >> 5) % C;        // cin (output of dgrad)
+        const int kc = idx / (32 * C);
+        const int tap = kc / cg_n, cg = kc - tap * cg_n;
+        const int co = cg * 32 + k;
+        const int ftap = 8 - tap;            // (2-ky)*3 + (2-kx)
+        wd[idx] = w[(co * C + n) * 9 + ftap];
+    }
+}
+
+__global__ void pack_stem_kernel(const float* __restrict__ w, float* __restrict__ ws, int C)
+{
+    const int total = 27 * C;
+    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+        const int c = idx % C, k = idx / C;
+        ws[idx] = w[c * 27 + k];
+    }
+}
+
+__global__ void transpose_kernel(const float* __restrict__ src, float* __restrict__ dst, int R, int Cc)
+{
+    const int total = R * Cc;
+    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+        const int r = idx / Cc, c = idx - r * Cc;
+        dst[c * R + r] = src[idx];
+    }
+}
+
+__global__ void fold_bn_kernel(const float* __restrict__ params, const float* __restrict__ stats,
+                               const BnDesc* __restrict__ desc, float* __restrict__ scale,
+                               float* __restrict__ shift)
+{
+    const BnDesc d = desc[blockIdx.x];
+    for (int c = threadIdx.x; c < d.c; c += blockDim.x) {
+        const float invstd = 1.0f / sqrtf(stats[d.stat_off + d.c + c] + BN_EPS);
+        const float alpha = invstd * params[d.gamma_off + c];
+        scale[d.out_off + c] = alpha;
+        shift[d.out_off + c] = params[d.beta_off + c] - stats[d.stat_off + c] * alpha;
+    }
+}
+
+static inline int nblk(int total) { int b = (total + 255) / 256; return b > 4096 ? 4096 : b; }
+
+hipError_t launch_pack_conv3x3(const float* w, float* wp, int C, hipStream_t st)
+{
+    hipLaunchKernelGGL(pack_conv3x3_kernel, dim3(nblk(9 * C * C)), dim3(256), 0, st, w, wp, C);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_dgrad(const float* w, float* wd, int C, hipStream_t st)
+{
+    hipLaunchKernelGGL(pack_dgrad_kernel, dim3(nblk(9 * C * C)), dim3(256), 0, st, w, wd, C);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_stem(const float* w, float* ws, int C, hipStream_t st)
+{
+    hipLaunchKernelGGL(pack_stem_kernel, dim3(nblk(27 * C)), dim3(256), 0, st, w, ws, C);
+    return hipGetLastError();
+}
+
+hipError_t launch_transpose(const float* src, float* dst, int R, int Cc, hipStream_t st)
+{
+    hipLaunchKernelGGL(transpose_kernel, dim3(nblk(R * Cc)), dim3(256), 0, st, src, dst, R, Cc);
+    return hipGetLastError();
+}
+
+hipError_t launch_fold_bn(const float* params, const float* stats, const void* desc, int nlayers,
+                          float* scale, float* shift, hipStream_t st)
+{
+    hipLaunchKernelGGL(fold_bn_kernel, dim3(nlayers), dim3(256), 0, st, params, stats,
+                       (const BnDesc*)desc, scale, shift);
+    return hipGetLastError();
+}
+
+}  // namespace azg

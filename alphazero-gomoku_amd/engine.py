@@ -1,0 +1,153 @@
+"""PolicyValueEngine: owns one libazg_pv handle and the torch-owned flat buffers
+it computes on (parameters, gradients, Adam moments, BN running stats).
+
+Layout contract (include/azg_pv.h): parameters / gradients / moments are flat
+fp32 buffers in nn.Module.parameters() order with torch's per-tensor layout;
+BN running stats are [mean(c) | var(c)] per BatchNorm layer in module order.
+Each nn.Parameter / BN buffer of the module becomes a view into these buffers,
+so state_dict(), load_state_dict() and torch.save() keep working unchanged.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.nn as nn
+
+from _native import AzgConfig, check, load_library, ptr
+
+
+def _stream(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class PolicyValueEngine:
+    def __init__(self, net: nn.Module, blocks: int, channels: int, board: int, device):
+        if board != 15:
+            raise ValueError("the gfx950 kernels are built for 15x15 boards only")
+        self.lib = load_library()
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("PolicyValueEngine needs a HIP (MI355X) device; there is no CPU path")
+        cfg = AzgConfig(blocks, channels, board, 3)
+        h = ctypes.c_void_p()
+        check(self.lib.azg_pv_create(ctypes.byref(cfg), ctypes.byref(h)), self.lib)
+        self.h = h
+        self.net = net
+        self.blocks, self.channels = blocks, channels
+        n = self.lib.azg_pv_num_param_tensors(h)
+        offs = (ctypes.c_int64 * n)()
+        nums = (ctypes.c_int64 * n)()
+        check(self.lib.azg_pv_param_layout(h, offs, nums), self.lib)
+        params = list(net.parameters())
+        if len(params) != n or any(p.numel() != nums[i] for i, p in enumerate(params)):
+            raise RuntimeError("module parameters do not match the engine layout")
+        self.nparam = int(self.lib.azg_pv_param_count(h))
+        dev = self.device
+        with torch.no_grad():
+            self.flat_params = torch.empty(self.nparam, dtype=torch.float32, device=dev)
+            self.flat_grads = torch.zeros(self.nparam, dtype=torch.float32, device=dev)
+            self.param_views = []
+            self.grad_views = []
+            for i, p in enumerate(params):
+                o, k = int(offs[i]), int(nums[i])
+                v = self.flat_params[o:o + k].view_as(p)
+                v.copy_(p.data.to(dev, torch.float32))
+                p.data = v
+                gv = self.flat_grads[o:o + k].view_as(p)
+                p.grad = gv
+                self.param_views.append(v)
+                self.grad_views.append(gv)
+            bns = [m for m in net.modules() if isinstance(m, nn.BatchNorm2d)]
+            self.nbn = int(self.lib.azg_pv_bn_count(h))
+            if sum(2 * b.num_features for b in bns) != self.nbn:
+                raise RuntimeError("BatchNorm layers do not match the engine layout")
+            self.flat_bn = torch.empty(self.nbn, dtype=torch.float32, device=dev)
+            self.flat_nbt = torch.zeros(len(bns), dtype=torch.int64, device=dev)
+            o = 0
+            for i, b in enumerate(bns):
+                c = b.num_features
+                self.flat_bn[o:o + c].copy_(b.running_mean)
+                self.flat_bn[o + c:o + 2 * c].copy_(b.running_var)
+                self.flat_nbt[i].copy_(b.num_batches_tracked)
+                b.running_mean = self.flat_bn[o:o + c]
+                b.running_var = self.flat_bn[o + c:o + 2 * c]
+                b.num_batches_tracked = self.flat_nbt[i]
+                o += 2 * c
+        self.params = params
+        check(self.lib.azg_pv_bind(h, ptr(self.flat_params), ptr(self.flat_grads), ptr(self.flat_bn)), self.lib)
+        self._seen = self._versions()
+        self._out_cache = {}
+
+    # -- housekeeping -------------------------------------------------------
+    def _versions(self):
+        # nn.Parameter keeps its own version counter after `p.data = view`, so sum them;
+        # BN buffers ARE views of flat_bn and share its counter.
+        return (self.flat_params._version, self.flat_bn._version, sum(p._version for p in self.params))
+
+    def sync_dirty(self):
+        """Parameters or BN stats were modified in place through torch (load_state_dict,
+        copy_, optimizer from outside): re-derive packed weights before the next call."""
+        v = self._versions()
+        if v != self._seen:
+            check(self.lib.azg_pv_mark_dirty(self.h), self.lib)
+            self._seen = v
+
+    def mark_dirty(self):
+        check(self.lib.azg_pv_mark_dirty(self.h), self.lib)
+
+    def reattach_grads(self):
+        for p, g in zip(self.params, self.grad_views):
+            if p.grad is None or p.grad.data_ptr() != g.data_ptr():
+                p.grad = g
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.lib.azg_pv_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- compute ------------------------------------------------------------
+    def forward(self, x: torch.Tensor, want_logits: bool = False):
+        """Eval-mode forward on device.  x: [B,3,15,15] fp32 (any device/dtype)."""
+        x = x.to(self.device, torch.float32).contiguous()
+        B = int(x.shape[0])
+        probs = torch.empty((B, 225), dtype=torch.float32, device=self.device)
+        values = torch.empty((B, 1), dtype=torch.float32, device=self.device)
+        logits = torch.empty((B, 225), dtype=torch.float32, device=self.device) if want_logits else None
+        self.forward_into(x, probs, values, logits)
+        return probs, values, logits
+
+    def forward_into(self, x, probs, values, logits=None):
+        self.sync_dirty()
+        check(self.lib.azg_pv_forward(self.h, ptr(x), int(x.shape[0]), ptr(probs), ptr(values), ptr(logits),
+                                      _stream(self.device)), self.lib)
+
+    def train_backward(self, x, pis, zs, losses):
+        self.sync_dirty()
+        check(self.lib.azg_pv_train_backward(self.h, ptr(x), ptr(pis), ptr(zs), int(x.shape[0]), ptr(losses),
+                                             _stream(self.device)), self.lib)
+        self._seen = self._versions()
+        self.reattach_grads()
+
+    def train_apply(self, exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps, wd, max_norm, total_norm=None):
+        check(self.lib.azg_pv_train_apply(self.h, ptr(exp_avg), ptr(exp_avg_sq), int(step), float(lr),
+                                          float(beta1), float(beta2), float(eps), float(wd), float(max_norm),
+                                          ptr(total_norm), _stream(self.device)), self.lib)
+
+    # -- instrumentation ----------------------------------------------------
+    def profile_enable(self, on: bool = True):
+        check(self.lib.azg_pv_profile_enable(self.h, 1 if on else 0), self.lib)
+
+    def profile_read(self) -> dict:
+        """{class: (ms_total, launches)} since the last profile_enable (synchronises)."""
+        from _native import PROF_CLASSES
+        ms = (ctypes.c_double * 8)()
+        n = (ctypes.c_int64 * 8)()
+        check(self.lib.azg_pv_profile_read(self.h, ms, n), self.lib)
+        return {PROF_CLASSES[i]: (ms[i], int(n[i])) for i in range(8) if n[i]}

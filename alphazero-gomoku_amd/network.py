@@ -1,0 +1,286 @@
+"""Drop-in replacement for the reference ``network.py`` whose compute runs on
+hand-written gfx950 HIP kernels (libazg_pv.so, include/azg_pv.h).
+
+Same public surface as the reference (network.py:9-265):
+  * ``ResidualBlock``, ``AlphaZeroNet`` -- same sub-module names, parameter order,
+    state_dict keys and initialisation (so ``torch.manual_seed(s)`` + ctor gives the
+    reference's weights bit for bit); ``forward`` runs the HIP eval path.
+  * ``PyTorchModel(board_size, action_size, device, n_res_blocks=3, channels=64, lr,
+    weight_decay)`` with ``predict``, ``predict_batch``, ``train_batch``, ``save``,
+    ``load``, ``make_batch_from_states`` and the attributes ``.net``, ``.optimizer``,
+    ``.board_size``, ``.action_size``, ``.device``; plus ``policy_value`` /
+    ``train_step`` aliases named by the north star, and device-resident variants
+    (``predict_device``) for the batched self-play driver.
+
+Differences, by design: the device must be a HIP GPU (there is no CPU path: the
+reference's CPU fallback, network.py:152, raises here) and the board must be 15x15.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from engine import PolicyValueEngine
+
+
+class ResidualBlock(nn.Module):
+    """Parameter container of reference network.py:9-26 (compute: pv_conv.hip)."""
+
+    def __init__(self, channels: int):
+        super().__init__()
+        self.conv1 = nn.Conv2d(channels, channels, kernel_size=3, padding=1, bias=False)
+        self.bn1 = nn.BatchNorm2d(channels)
+        self.conv2 = nn.Conv2d(channels, channels, kernel_size=3, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(channels)
+
+
+class AlphaZeroNet(nn.Module):
+    """Reference network.py:29-117.  Parameters live in the engine's flat buffers
+    once attached to a device (``attach``); forward() is the HIP eval path."""
+
+    def __init__(self, in_channels: int = 3, board_size: int = 15, action_size: int = 15 * 15,
+                 n_res_blocks: int = 6, channels: int = 128):
+        super().__init__()
+        self.board_size = board_size
+        self.action_size = action_size
+        self.channels = channels
+        self.n_res_blocks = n_res_blocks
+        self.conv = nn.Conv2d(in_channels, channels, kernel_size=3, padding=1, bias=False)
+        self.bn = nn.BatchNorm2d(channels)
+        self.res_blocks = nn.ModuleList([ResidualBlock(channels) for _ in range(n_res_blocks)])
+        self.policy_conv = nn.Conv2d(channels, 2, kernel_size=1, bias=False)
+        self.policy_bn = nn.BatchNorm2d(2)
+        self.policy_fc = nn.Linear(2 * board_size * board_size, action_size)
+        self.value_conv = nn.Conv2d(channels, 1, kernel_size=1, bias=False)
+        self.value_bn = nn.BatchNorm2d(1)
+        self.value_fc1 = nn.Linear(board_size * board_size, 64)
+        self.value_fc2 = nn.Linear(64, 1)
+        self._init_weights()
+        self.engine: Optional[PolicyValueEngine] = None
+
+    def _init_weights(self):
+        # network.py:75-83 (same RNG consumption order)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, nonlinearity="relu")
+            elif isinstance(m, nn.Linear):
+                nn.init.kaiming_uniform_(m.weight, nonlinearity="relu")
+                if m.bias is not None:
+                    nn.init.constant_(m.bias, 0)
+
+    def attach(self, device) -> "AlphaZeroNet":
+        """Move parameters into the engine's device buffers (once)."""
+        if self.engine is None:
+            self.engine = PolicyValueEngine(self, self.n_res_blocks, self.channels, self.board_size, device)
+        return self
+
+    def to(self, *args, **kwargs):  # keep `.to("cuda")` working like the reference
+        dev = None
+        if args and isinstance(args[0], (str, torch.device)):
+            dev = torch.device(args[0])
+        elif "device" in kwargs:
+            dev = torch.device(kwargs["device"])
+        if dev is not None and dev.type == "cuda":
+            return self.attach(dev)
+        if self.engine is not None:
+            raise RuntimeError("AlphaZeroNet is bound to a HIP device; moving it is not supported")
+        return super().to(*args, **kwargs)
+
+    def mark_dirty(self):
+        """Call after mutating parameters through ``.data`` (not tracked by autograd versions)."""
+        if self.engine is not None:
+            self.engine.mark_dirty()
+
+    def forward(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(logits [B,225], value [B,1]) with BN running statistics (eval semantics).
+        Train-mode BN runs only inside PyTorchModel.train_batch (fused with backward)."""
+        if self.engine is None:
+            raise RuntimeError("AlphaZeroNet.forward needs a HIP device: call .to('cuda') first")
+        if self.training:
+            raise RuntimeError("train-mode forward is fused into PyTorchModel.train_batch; "
+                               "call .eval() for inference")
+        _, value, logits = self.engine.forward(x, want_logits=True)
+        return logits, value
+
+    def predict(self, state):
+        """network.py:119-129: single unbatched state -> (logits, value)."""
+        st = torch.as_tensor(np.asarray(state), dtype=torch.float32).unsqueeze(0)
+        return self(st)
+
+
+class HipAdam(torch.optim.Adam):
+    """torch.optim.Adam bookkeeping (param_groups, state_dict format: step /
+    exp_avg / exp_avg_sq per parameter) whose moments live in flat device buffers
+    updated by the fused clip+Adam kernel (azg_pv_train_apply)."""
+
+    def __init__(self, net: AlphaZeroNet, lr: float = 1e-3, weight_decay: float = 1e-4):
+        super().__init__(net.parameters(), lr=lr, weight_decay=weight_decay)
+        self._net = net
+        eng = net.engine
+        self.flat_exp_avg = torch.zeros_like(eng.flat_params)
+        self.flat_exp_avg_sq = torch.zeros_like(eng.flat_params)
+
+    def _views(self, p, i):
+        eng = self._net.engine
+        o = int(eng.param_views[i].storage_offset())
+        return (self.flat_exp_avg[o:o + p.numel()].view_as(p), self.flat_exp_avg_sq[o:o + p.numel()].view_as(p))
+
+    def _ensure_state(self):
+        """Lazily create torch-format state (as torch does on the first step)."""
+        for i, p in enumerate(self._net.engine.params):
+            st = self.state[p]
+            if "exp_avg" not in st:
+                ea, es = self._views(p, i)
+                ea.zero_()
+                es.zero_()
+                st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                st["exp_avg"] = ea
+                st["exp_avg_sq"] = es
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        with torch.no_grad():
+            for i, p in enumerate(self._net.engine.params):
+                st = self.state.get(p)
+                if not st or "exp_avg" not in st:
+                    continue
+                ea, es = self._views(p, i)
+                ea.copy_(st["exp_avg"])
+                es.copy_(st["exp_avg_sq"])
+                st["exp_avg"], st["exp_avg_sq"] = ea, es
+                if not torch.is_tensor(st["step"]):
+                    st["step"] = torch.tensor(float(st["step"]), dtype=torch.float32)
+                else:
+                    st["step"] = st["step"].detach().to("cpu", torch.float32)
+
+    def hip_step(self, max_norm: float = float("inf"), total_norm: Optional[torch.Tensor] = None):
+        """One optimiser step on the bound flat grads: clip to max_norm, then Adam."""
+        self._ensure_state()
+        g = self.param_groups[0]
+        if g.get("amsgrad") or g.get("maximize"):
+            raise NotImplementedError("amsgrad/maximize are not used by the reference")
+        first = self.state[self._net.engine.params[0]]
+        step = int(first["step"].item()) + 1
+        b1, b2 = g["betas"]
+        self._net.engine.train_apply(self.flat_exp_avg, self.flat_exp_avg_sq, step, g["lr"], b1, b2,
+                                     g["eps"], g["weight_decay"], max_norm, total_norm)
+        for p in self._net.engine.params:
+            self.state[p]["step"].fill_(float(step))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        self.hip_step()
+        return loss
+
+
+class PyTorchModel:
+    """Reference network.py:132-265 surface over the HIP engine."""
+
+    def __init__(self,
+                 board_size: int = 15,
+                 action_size: Optional[int] = None,
+                 device: Optional[str] = None,
+                 n_res_blocks: int = 3,
+                 channels: int = 64,
+                 lr: float = 1e-3,
+                 weight_decay: float = 1e-4):
+        self.board_size = board_size
+        self.action_size = action_size if action_size is not None else board_size * board_size
+        self.device = device or ("cuda" if torch.cuda.is_available() else "cpu")
+        if not str(self.device).startswith("cuda"):
+            raise RuntimeError(
+                f"PyTorchModel(device={self.device!r}): this build computes only on HIP devices "
+                "(MI355X, gfx950); there is no CPU fallback")
+        self.net = AlphaZeroNet(in_channels=3, board_size=board_size, action_size=self.action_size,
+                                n_res_blocks=n_res_blocks, channels=channels).attach(self.device)
+        self.optimizer = HipAdam(self.net, lr=lr, weight_decay=weight_decay)
+        self.value_loss_fn = nn.MSELoss()
+        self.policy_loss_fn = nn.KLDivLoss(reduction="batchmean")
+        self.max_grad_norm = 3.0                        # network.py:223
+        self.grad_hook = None                           # DP: all-reduce of the flat grads
+        self._losses = None
+
+    @property
+    def engine(self) -> PolicyValueEngine:
+        return self.net.engine
+
+    # ---------------- inference ----------------
+    def predict(self, encoded_states: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """network.py:168-183: (probs [B,225] float32, values [B,1] float32) with BN
+        running stats; the module's train/eval flag is left as it was."""
+        x = torch.from_numpy(np.ascontiguousarray(encoded_states, dtype=np.float32))
+        probs, values = self.predict_device(x)
+        return probs.cpu().numpy(), values.cpu().numpy()
+
+    def predict_device(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Device-resident predict: x [B,3,15,15] -> (probs, values) on the GPU."""
+        probs, values, _ = self.engine.forward(x)
+        return probs, values
+
+    policy_value = predict
+
+    def predict_batch(self, states_list: list) -> Tuple[np.ndarray, np.ndarray]:
+        return self.predict(self.make_batch_from_states(states_list))
+
+    # ---------------- training ----------------
+    def train_batch(self, states: np.ndarray, target_pis: np.ndarray, target_vs: np.ndarray,
+                    epochs: int = 1) -> dict:
+        """network.py:199-235: per epoch zero_grad, train-mode forward, KLDiv(batchmean)
+        + MSE, backward, clip_grad_norm_(3.0), Adam step.  Leaves the net in train mode."""
+        self.net.train()
+        dev = self.engine.device
+        s = torch.from_numpy(np.ascontiguousarray(states, dtype=np.float32)).to(dev)
+        t = torch.from_numpy(np.ascontiguousarray(target_pis, dtype=np.float32)).to(dev)
+        z = torch.from_numpy(np.ascontiguousarray(target_vs, dtype=np.float32).reshape(-1, 1)).to(dev)
+        return self.train_batch_device(s, t, z, epochs)
+
+    def train_batch_device(self, s: torch.Tensor, t: torch.Tensor, z: torch.Tensor, epochs: int = 1) -> dict:
+        self.net.train()
+        eng = self.engine
+        acc = torch.zeros(3, dtype=torch.float64, device=eng.device)
+        losses = torch.empty(3, dtype=torch.float32, device=eng.device)
+        for _ in range(epochs):
+            eng.train_backward(s, t, z, losses)
+            if self.grad_hook is not None:
+                self.grad_hook(eng.flat_grads)
+            self.optimizer.hip_step(self.max_grad_norm)
+            eng.flat_nbt.add_(1)
+            acc += losses
+        vals = (acc / float(epochs)).tolist()
+        return {"policy_loss": vals[0], "value_loss": vals[1], "total_loss": vals[2]}
+
+    train_step = train_batch
+
+    # ---------------- checkpoints ----------------
+    def save(self, path: str) -> None:
+        """network.py:240-248 format: {"net", "opt", "board_size", "action_size"}."""
+        d = os.path.dirname(path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        net_sd = {k: v.detach().clone() for k, v in self.net.state_dict().items()}
+        opt_sd = self.optimizer.state_dict()
+        opt_sd = {"state": {i: {k: (v.detach().clone() if torch.is_tensor(v) else v) for k, v in st.items()}
+                            for i, st in opt_sd["state"].items()},
+                  "param_groups": opt_sd["param_groups"]}
+        torch.save({"net": net_sd, "opt": opt_sd, "board_size": self.board_size,
+                    "action_size": self.action_size}, path)
+
+    def load(self, path: str, map_location: Optional[str] = None) -> None:
+        """network.py:250-258; optimizer-state errors are ignored as in the reference."""
+        map_location = map_location or self.device
+        state = torch.load(path, map_location=map_location, weights_only=True)
+        self.net.load_state_dict(state["net"])
+        if "opt" in state and state["opt"] is not None:
+            try:
+                self.optimizer.load_state_dict(state["opt"])
+            except Exception:
+                pass
+
+    @staticmethod
+    def make_batch_from_states(list_of_encoded_states: list) -> np.ndarray:
+        return np.stack(list_of_encoded_states, axis=0).astype(np.float32)

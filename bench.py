@@ -1,0 +1,183 @@
+"""Benchmark: BASELINE.json configs[1] -- batch-512 policy/value forward of the
+6-block/128-filter ResNet on synthetic legal 15x15 positions, one MI355X per rank.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+N>1 is launched by the driver as torchrun (one process per GPU, RCCL).  Self-play
+leaf evaluation shards by game, so every rank runs its own independent batches
+(weak scaling, no collective in the timed region).  A step = one forward of 512
+boards already resident in HBM.  Prints ONE JSON line on rank 0 with a live
+`roofline` for the dominant kernel (the fused 3x3 conv, timed by hipEvents on its
+own stream over the timed region) and a bounded `cpu_baseline` (the CPU oracle,
+i.e. the reference's PyTorch-CPU algorithm, timed on this host).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "alphazero-gomoku_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np
+import torch
+
+METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
+BLOCKS, CHANNELS, BATCH = 6, 128, 512
+FLOP_CONV = 2 * 225 * CHANNELS * 9 * CHANNELS            # per board per 3x3 res conv = 66,355,200
+FLOP_BOARD = 798_221_828                                 # whole forward, SURVEY §8(d)
+PEAK_F32_MFMA = 157.3e12                                 # MI355X_MICROARCH.md: FP32 matrix peak
+
+
+def dist_setup(n_gpus: int):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return rank, world, local, dist
+    return 0, 1, 0, None
+
+
+def barrier_sync(dist, local):
+    if dist is not None:
+        dist.barrier(device_ids=[local])
+    torch.cuda.synchronize()
+
+
+def cpu_baseline(seconds: float = 12.0) -> dict:
+    """Oracle (PyTorch-CPU restatement of reference network.py) timed on this host:
+    batches of 64 boards until ~`seconds` elapse."""
+    from oracle.boards import encode_batch, synth_positions
+    from oracle.ref_net import RefModel
+    threads = max(1, min(16, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    ref = RefModel(BLOCKS, CHANNELS)
+    b, p = synth_positions(64, seed=99)
+    x = encode_batch(b, p)
+    ref.predict(x)                       # warm-up
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        ref.predict(x)
+        n += 64
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 2), "unit": "boards/s", "cores": threads, "kind": "port",
+            "sample": f"{n} boards as {n // 64} predict() batches of 64, 6x128, torch-CPU oracle "
+                      f"(oracle/ref_net.py = reference network.py:168-183 restated), {dt:.1f}s, "
+                      f"{threads} threads"}
+
+
+def load_traffic():
+    path = os.path.join(REPO, "profiles", "conv_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        if d.get("config") == f"{BLOCKS}x{CHANNELS}_B{BATCH}":
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=BATCH)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    rank, world, local, dist = dist_setup(args.gpus)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from network import PyTorchModel
+    from synth import synth_encoded
+
+    torch.manual_seed(0)
+    model = PyTorchModel(board_size=15, device=str(dev), n_res_blocks=BLOCKS, channels=CHANNELS)
+    eng = model.engine
+    B = args.batch
+    x = torch.from_numpy(synth_encoded(B, seed=1234 + rank)).to(dev)
+    probs = torch.empty((B, 225), device=dev)
+    values = torch.empty((B, 1), device=dev)
+
+    for _ in range(args.warmup):
+        eng.forward_into(x, probs, values)
+    barrier_sync(dist, local)
+
+    eng.profile_enable(True)
+    barrier_sync(dist, local)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.forward_into(x, probs, values)
+    barrier_sync(dist, local)
+    elapsed = time.perf_counter() - t0
+    prof = eng.profile_read()
+    eng.profile_enable(False)
+
+    assert torch.isfinite(probs).all() and torch.isfinite(values).all()
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    boards = B * args.steps * world
+    value = boards / elapsed
+    conv_ms, conv_n = prof.get("conv3x3", (0.0, 0))
+    conv_avg_s = conv_ms / 1e3 / max(conv_n, 1)
+    achieved = FLOP_CONV * B / conv_avg_s
+    roof = {"bound": "mfma", "achieved": round(achieved / 1e12, 3), "peak": PEAK_F32_MFMA / 1e12,
+            "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA, 4), "traffic": load_traffic(),
+            "kernel": "azg::conv3x3_mfma<128,*> (fused 3x3 conv + BN + residual + ReLU)",
+            "avg_launch_us": round(conv_avg_s * 1e6, 2), "launches": conv_n,
+            "flop_per_launch": FLOP_CONV * B}
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "boards/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded legal 15x15 positions; seeded Kaiming init weights, no checkpoint)",
+        "config": {"workload": "configs[1]: batch-512 policy/value forward (eval BN, softmax + tanh), "
+                               "6-block/128-filter ResNet, inputs resident in HBM",
+                   "global_batch": B * world, "per_gpu_batch": B, "net": f"{BLOCKS}x{CHANNELS}",
+                   "parallelism": f"replicas{world} (games shard by GPU; no collective in timed region)"},
+        "roofline": roof,
+        "whole_forward_mfma_frac": round(value / world * FLOP_BOARD / PEAK_F32_MFMA, 4),
+        "kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in prof.items()},
+    }
+    if not args.no_cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    else:
+        out["cpu_baseline"] = None
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,119 @@
+/*
+ * azg_pv.h -- C-ABI of the MI355X (gfx950) policy/value engine.
+ *
+ * The reference has no FFI layer: its boundary is Python duck typing at
+ * network.PyTorchModel (reference network.py:132-265).  This library sits BELOW
+ * a Python class that reproduces that surface (alphazero-gomoku_amd/network.py);
+ * each entry point below replaces the ATen work behind one reference call:
+ *
+ *   azg_pv_forward        <- PyTorchModel.predict            (network.py:168-183)
+ *                            = AlphaZeroNet.forward in eval mode (network.py:85-117)
+ *                              + F.softmax(dim=1) (network.py:180)
+ *   azg_pv_train_backward <- train_batch: zero_grad, train-mode forward, log_softmax,
+ *                            KLDiv(batchmean) + MSE, loss.backward()  (network.py:213-222)
+ *   azg_pv_train_apply    <- clip_grad_norm_(params, 3.0) + Adam.step()
+ *                                                            (network.py:223-224, 161)
+ *   azg_pv_create/destroy <- AlphaZeroNet.__init__ shape config (network.py:41-73)
+ *
+ * Conventions
+ *  - All pointers are DEVICE pointers (HIP, gfx950) unless stated; fp32 everywhere.
+ *  - Python/torch owns every tensor: parameters, gradients and Adam moments are
+ *    flat buffers in nn.Module.parameters() order with torch's own per-tensor
+ *    layout (see azg_pv_param_layout); BN running stats are a flat buffer of
+ *    [mean(c) | var(c)] per BatchNorm layer in module order.  The handle owns only
+ *    its workspace (packed weights, activations, partial sums).
+ *  - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream); every
+ *    entry point is asynchronous on it, does no host sync and no allocation
+ *    unless the batch exceeds the workspace high-water mark.
+ *  - Return value: 0 = ok, nonzero = error; azg_pv_last_error() gives the text
+ *    (thread-local).  No C++ exception crosses the ABI.
+ *  - One handle per process/GPU; not re-entrant (the reference host is
+ *    single-threaded too).
+ */
+#ifndef AZG_PV_H
+#define AZG_PV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct azg_pv azg_pv;
+
+typedef struct {
+    int32_t blocks;    /* residual blocks (reference default 3; BASELINE 6; Pente 10) */
+    int32_t channels;  /* 64, 128 or 256 */
+    int32_t board;     /* 15 (only 15x15 is built) */
+    int32_t in_ch;     /* 3 input planes */
+} azg_pv_config;
+
+/* Version of this ABI (bumped on incompatible change). */
+int32_t azg_pv_abi_version(void);
+
+const char* azg_pv_last_error(void);
+
+int32_t azg_pv_create(const azg_pv_config* cfg, azg_pv** out);
+int32_t azg_pv_destroy(azg_pv* h);
+
+/* Number of trainable parameters (flat length) and of BN running-stat floats. */
+int64_t azg_pv_param_count(const azg_pv* h);
+int64_t azg_pv_bn_count(const azg_pv* h);
+int32_t azg_pv_num_param_tensors(const azg_pv* h);
+/* HOST arrays of length azg_pv_num_param_tensors: element offset and numel of each
+ * parameter tensor inside the flat buffer, in nn.Module.parameters() order. */
+int32_t azg_pv_param_layout(const azg_pv* h, int64_t* offsets, int64_t* numels);
+
+/* Bind torch-owned flat buffers.  params/grads: azg_pv_param_count floats each;
+ * bn_stats: azg_pv_bn_count floats.  grads may be NULL for inference-only use. */
+int32_t azg_pv_bind(azg_pv* h, float* params, float* grads, float* bn_stats);
+
+/* Parameters or BN stats changed outside the library (load_state_dict, copy_):
+ * re-derive packed weights / folded BN before the next forward. */
+int32_t azg_pv_mark_dirty(azg_pv* h);
+
+/* Eval-mode forward (BN running stats).  x: [batch,3,15,15] NCHW fp32.
+ * probs: [batch,225] softmax(logits); values: [batch,1] tanh; logits: optional
+ * [batch,225] (NULL to skip). */
+int32_t azg_pv_forward(azg_pv* h, const float* x, int32_t batch,
+                       float* probs, float* values, float* logits, void* stream);
+
+/* Train-mode forward + loss + backward on the local batch (reference
+ * network.py:213-222).  Writes d(loss)/d(param) into the bound grad buffer
+ * (overwrites: zero_grad semantics), updates BN running stats (momentum 0.1,
+ * unbiased var), and writes {policy_loss, value_loss, total_loss} as 3 floats
+ * to losses (device).  pis: [batch,225]; zs: [batch,1]. */
+int32_t azg_pv_train_backward(azg_pv* h, const float* x, const float* pis,
+                              const float* zs, int32_t batch, float* losses,
+                              void* stream);
+
+/* clip_grad_norm_(max_norm) over the bound grads (call after any DP all-reduce
+ * of the grad buffer), then one Adam step (torch semantics: L2-coupled weight
+ * decay, bias correction for `step`, which is the post-increment step count).
+ * exp_avg / exp_avg_sq: flat buffers like params.  total_norm (device, 1 float,
+ * may be NULL) receives the pre-clip global L2 norm. */
+int32_t azg_pv_train_apply(azg_pv* h, float* exp_avg, float* exp_avg_sq,
+                           int64_t step, float lr, float beta1, float beta2,
+                           float eps, float weight_decay, float max_norm,
+                           float* total_norm, void* stream);
+
+/* Kernel-class event timing (bench / roofline instrumentation).  When enabled,
+ * every launch of a profiled class is bracketed by hipEvents on the stream it is
+ * launched on; azg_pv_profile_read synchronises those events and returns the
+ * summed device time (ms) and launch count per class since the last enable. */
+enum {
+    AZG_PROF_CONV3X3 = 0,   /* residual 3x3 conv, eval epilogue        */
+    AZG_PROF_STEM = 1,
+    AZG_PROF_HEADS = 2,
+    AZG_PROF_TRAIN_CONV = 3, /* train-mode 3x3 conv fwd + dgrad        */
+    AZG_PROF_TRAIN_WGRAD = 4,
+    AZG_PROF_TRAIN_OTHER = 5,
+    AZG_PROF_NCLASS = 8
+};
+int32_t azg_pv_profile_enable(azg_pv* h, int32_t enable);
+int32_t azg_pv_profile_read(azg_pv* h, double* ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AZG_PV_H */

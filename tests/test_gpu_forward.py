@@ -1,0 +1,133 @@
+"""GPU parity of the eval forward (azg_pv_forward via PyTorchModel.predict)
+against the reference goldens and the CPU oracle.  Tolerance: 1e-5 absolute on
+probs and values (BASELINE north_star), bit-exact legal-move mask, masked policy
+argmax exact except on rows whose top-2 gap is below 2x tolerance."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_state, has_gpu, load_golden
+from oracle.boards import encode_batch, synth_positions, valid_mask
+from oracle.ref_net import RefModel, load_numpy_state, state_to_numpy
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")]
+
+TOL = 1e-5
+
+
+def make_model(blocks, ch, state=None, seed=0):
+    from network import PyTorchModel
+    torch.manual_seed(seed)
+    m = PyTorchModel(board_size=15, device="cuda", n_res_blocks=blocks, channels=ch)
+    if state is not None:
+        m.net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in state.items()})
+    return m
+
+
+def argmax_check(probs, ref_probs, boards):
+    masks = np.stack([valid_mask(b) for b in boards])
+    a = np.argmax(probs * masks, axis=1)
+    rm = ref_probs * masks
+    r = np.argmax(rm, axis=1)
+    srt = np.sort(rm, axis=1)
+    gap = srt[:, -1] - srt[:, -2]
+    bad = (a != r) & (gap >= 2 * TOL)
+    assert not bad.any(), np.nonzero(bad)
+
+
+@pytest.mark.parametrize("tag,blocks,ch", [("3x64", 3, 64), ("6x128", 6, 128)])
+def test_forward_matches_reference_goldens(tag, blocks, ch):
+    g = load_golden(tag)
+    m = make_model(blocks, ch, golden_state(g))
+    x = encode_batch(g["fwd/boards"], g["fwd/players"])
+    probs, values = m.predict(x)
+    assert probs.dtype == np.float32 and probs.shape == (64, 225)
+    assert values.dtype == np.float32 and values.shape == (64, 1)
+    np.testing.assert_allclose(probs, g["fwd/probs"], atol=TOL, rtol=0)
+    np.testing.assert_allclose(values, g["fwd/values"], atol=TOL, rtol=0)
+    # against fp64: no worse than the reference's own fp32 spread + tolerance
+    assert np.abs(probs - g["fwd/probs64"]).max() <= np.abs(g["fwd/probs"] - g["fwd/probs64"]).max() + TOL
+    _, _, logits = m.engine.forward(torch.from_numpy(x), want_logits=True)
+    np.testing.assert_allclose(logits.cpu().numpy(), g["fwd/logits"], atol=1e-4, rtol=1e-5)
+    argmax_check(probs, g["fwd/probs"], g["fwd/boards"])
+
+
+@pytest.mark.parametrize("blocks,ch,B", [(6, 128, 512), (10, 256, 96), (3, 64, 300), (1, 64, 1)])
+def test_forward_matches_oracle(blocks, ch, B):
+    """Seeded init for every config (10x256 weights regenerated here from the seed;
+    its init RNG order is pinned by test_oracle_init_rng_order_matches_reference).
+    BN running stats are set to a calibrated state so activations stay O(1)."""
+    torch.set_num_threads(8)
+    ref = RefModel(blocks, ch)
+    torch.manual_seed(1)
+    calib_bn(ref, seed=blocks * 1000 + ch)
+    m = make_model(blocks, ch, state_to_numpy(ref.net))
+    b, p = synth_positions(B, seed=B + ch)
+    x = encode_batch(b, p)
+    probs, values = m.predict(x)
+    rp, rv = ref.predict(x)
+    # fp64 re-run of the oracle: untrained (seeded-init) weights are ill-conditioned
+    # enough that the oracle's own fp32 error reaches ~1e-5 (10x256: 1.2e-5 measured),
+    # so the 1e-5 gate is widened per element by the oracle's fp32-vs-fp64 spread.
+    r64 = RefModel(blocks, ch, dtype=torch.float64)
+    r64.net.load_state_dict({k: (v.double() if v.dtype.is_floating_point else v)
+                             for k, v in ref.net.state_dict().items()})
+    p64, v64 = r64.predict(x)
+    for got, r32, r_64 in ((probs, rp, p64), (values, rv, v64)):
+        floor = np.abs(r32 - r_64)
+        assert np.all(np.abs(got - r32) <= TOL + floor), np.abs(got - r32).max()
+        assert np.all(np.abs(got - r_64) <= TOL + floor), np.abs(got - r_64).max()
+    argmax_check(probs, rp, b)
+
+
+def calib_bn(ref, seed):
+    """Give BN running stats the statistics of real activations (train-mode passes
+    without optimizer steps), as a trained net has."""
+    b, p = synth_positions(64, seed=seed)
+    x = torch.from_numpy(encode_batch(b, p))
+    ref.net.train()
+    for mod in ref.net.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.momentum = None   # cumulative average
+    with torch.no_grad():
+        for _ in range(3):
+            ref.net(x)
+    for mod in ref.net.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.momentum = 0.1
+    ref.net.eval()
+
+
+def test_forward_is_batch_independent():
+    """Each board's outputs are bit-identical whatever batch or position it is in."""
+    m = make_model(3, 64)
+    b, p = synth_positions(130, seed=3)
+    x = encode_batch(b, p)
+    probs, values = m.predict(x)
+    for i in (0, 63, 64, 129):
+        pi, vi = m.predict(x[i:i + 1])
+        assert np.array_equal(pi[0], probs[i]) and np.array_equal(vi[0], values[i])
+    perm = np.random.default_rng(0).permutation(130)
+    pp, vp = m.predict(x[perm])
+    assert np.array_equal(pp, probs[perm]) and np.array_equal(vp, values[perm])
+
+
+def test_empty_and_full_boards():
+    m = make_model(3, 64)
+    empty = np.zeros((15, 15), np.int8)
+    full = np.indices((15, 15)).sum(0) % 2 + 1
+    x = encode_batch(np.stack([empty, full.astype(np.int8)]), np.array([1, 2]))
+    probs, values = m.predict(x)
+    assert np.allclose(probs.sum(1), 1.0, atol=1e-5) and np.all(np.abs(values) <= 1)
+
+
+def test_load_state_dict_invalidates_packed_weights():
+    m = make_model(3, 64, seed=0)
+    x = encode_batch(*synth_positions(8, seed=9))
+    p0, _ = m.predict(x)
+    other = make_model(3, 64, seed=1)
+    m.net.load_state_dict(other.net.state_dict())
+    p1, _ = m.predict(x)
+    q1, _ = other.predict(x)
+    assert not np.array_equal(p0, p1)
+    assert np.array_equal(p1, q1)
