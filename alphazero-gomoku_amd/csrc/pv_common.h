@@ -47,6 +47,7 @@ enum Epi : int {
     EPI_BN_RELU = 0,      // relu(acc*scale + shift)
     EPI_BN_RES_RELU = 1,  // relu(acc*scale + shift + resid)
     EPI_RAW = 2,          // acc (train-mode conv output, dgrad)
+    EPI_ADD = 3,          // acc + resid (dgrad into an existing residual gradient)
 };
 
 }  // namespace azg

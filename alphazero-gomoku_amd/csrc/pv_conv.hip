@@ -9,14 +9,14 @@
 // activation (the halo makes every tap an unconditional 16-byte load), B is the
 // weight re-packed to [kchunk][n][32] so a K-chunk of 32 is one contiguous block.
 //
-// Tile: 128 pixels x min(C,128) channels per 256-thread workgroup, K-chunk 32.
-// 4 waves in 2x2, each owning 64 x (BN/2) outputs as 32x32 accumulators of
-// v_mfma_f32_32x32x2_f32 (exact f32 FMA chain: the parity budget is 1e-5 fp32,
-// so no bf16/xf32).  LDS holds two chunks (double buffer) with rows padded to
-// 36 floats: every ds_read_b128 fragment load is bank-conflict free
-// (row*36 mod 64 = 4*(9*row mod 16)).  Global->LDS staging is register staged
-// and issued before the MFMAs of the current chunk (async-STAGE split), one
-// barrier per chunk.
+// Tile: BM pixels x BN channels per 256-thread workgroup (shape picked per
+// launch, see pick_conv_tile), K-chunk 32.  4 waves, each owning TM x TN 32x32
+// accumulators of v_mfma_f32_32x32x2_f32 (exact f32 FMA chain: the parity budget
+// is 1e-5 fp32, so no bf16/xf32).  LDS holds two chunks (double buffer) of
+// unpadded 128-B rows whose 16-B chunks are XOR-swizzled by row, so every
+// ds_read_b128 fragment load is bank-conflict free.  Global->LDS staging is
+// register staged and issued before the MFMAs of the current chunk
+// (async-STAGE split), one barrier per chunk.
 //
 // Lane l of an MFMA step s uses K index h*16+s (h = l>>5) for both A and B, so
 // each lane's 16 A values and 16 B values of a chunk are contiguous in LDS.
@@ -24,29 +24,34 @@
 
 namespace azg {
 
-template <int C>
+// Tile shape: BM = WM*TM*32 pixels x BN channels; 4 waves as WM x WN (WN = 4/WM),
+// each wave TM x TN accumulators of 32x32.  Several shapes are compiled; the host
+// picks the one that balances the tile count over the 256 CUs best (pick_tile).
+template <int C, int BN_, int WM_, int TM_>
 struct ConvTile {
-    static constexpr int BM = 128;
-    static constexpr int BN = C < 128 ? C : 128;
+    static constexpr int BN = BN_;
+    static constexpr int WM = WM_;
+    static constexpr int WN = 4 / WM_;
+    static constexpr int TM = TM_;
+    static constexpr int TN = BN_ / (WN * 32);
+    static constexpr int BM = WM * TM * 32;
     static constexpr int BK = 32;
-    static constexpr int LDK = BK + 4;
+    static constexpr int LDK = BK;          // unpadded rows; XOR-swizzled 16-B chunks
     static constexpr int CG = C / BK;
     static constexpr int NCH = 9 * CG;
-    static constexpr int WN = BN / 2;
-    static constexpr int TM = 2;
-    static constexpr int TN = WN / 32;
     static constexpr int A_LD = BM * BK / 4 / 256;
     static constexpr int B_LD = BN * BK / 4 / 256;
     static constexpr int LDS_BYTES = 2 * (BM + BN) * LDK * 4;
+    static_assert(TN >= 1 && WN * TN * 32 == BN, "bad tile");
 };
 
-template <int C, int EPI>
+template <int C, int BN_, int WM_, int TM_, int EPI>
 __global__ __launch_bounds__(256, 2) void conv3x3_mfma(
     const float* __restrict__ in, const float* __restrict__ wp,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ resid, float* __restrict__ out, int M)
 {
-    using T = ConvTile<C>;
+    using T = ConvTile<C, BN_, WM_, TM_>;
     constexpr int BM = T::BM, BN = T::BN, BK = T::BK, LDK = T::LDK;
     constexpr int CG = T::CG, NCH = T::NCH, WN = T::WN, TM = T::TM, TN = T::TN;
     constexpr int A_LD = T::A_LD, B_LD = T::B_LD;
@@ -57,7 +62,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
-    const int wm = wid >> 1, wn = wid & 1;
+    const int wm = wid / WN, wn = wid % WN;
     const int m0 = blockIdx.x * BM;
     const int n0 = blockIdx.y * BN;
 
@@ -83,13 +88,16 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(
 #pragma unroll
         for (int i = 0; i < B_LD; ++i) rb[i] = *(const f32x4*)(wk + 32 * i * BK);
     };
+    // 16-B chunk c of LDS row r is stored at chunk c ^ ((r >> 1) & 7): the 16 rows a
+    // ds_read_b128 lane group touches land on 16 distinct 4-bank slots.
+    const int wchunk = ((tid & 7) ^ ((sr >> 1) & 7)) * 4;
     auto lstore = [&](int buf) {
         float* a = As + buf * BM * LDK;
         float* b = Bs + buf * BN * LDK;
 #pragma unroll
-        for (int i = 0; i < A_LD; ++i) *(f32x4*)(a + (sr + 32 * i) * LDK + sc) = ra[i];
+        for (int i = 0; i < A_LD; ++i) *(f32x4*)(a + (sr + 32 * i) * LDK + wchunk) = ra[i];
 #pragma unroll
-        for (int i = 0; i < B_LD; ++i) *(f32x4*)(b + (sr + 32 * i) * LDK + sc) = rb[i];
+        for (int i = 0; i < B_LD; ++i) *(f32x4*)(b + (sr + 32 * i) * LDK + wchunk) = rb[i];
     };
 
     f32x16 acc[TM][TN];
@@ -101,50 +109,71 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     const int r32 = lane & 31, h = lane >> 5;
-    const int arow = (wm * 64 + r32) * LDK + h * 16;
-    const int brow = (wn * WN + r32) * LDK + h * 16;
+    const int swz = (r32 >> 1) & 7;
+    const int arow = (wm * TM * 32 + r32) * LDK;
+    const int brow = (wn * TN * 32 + r32) * LDK;
 
     gload(0);
     lstore(0);
     __syncthreads();
 
-    for (int kc = 0; kc < NCH; ++kc) {
-        const int cur = kc & 1;
-        if (kc + 1 < NCH) gload(kc + 1);
-        const float* Ab = As + cur * BM * LDK;
-        const float* Bb = Bs + cur * BN * LDK;
-        f32x4 a[TM][4], b[TN][4];
+    // Two-level K sum for accuracy: each tap's C-long chain accumulates into `at`
+    // (one MFMA chain of C/2 steps), which is then added into `acc`: the rounding
+    // error grows like chain(C) + 9 instead of chain(9*C) (fp32 parity budget).
+    for (int tap = 0; tap < 9; ++tap) {
+        f32x16 at[TM][TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) a[i][q] = *(const f32x4*)(Ab + arow + i * 32 * LDK + q * 4);
+            for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+                for (int r = 0; r < 16; ++r) at[i][j][r] = 0.f;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) b[j][q] = *(const f32x4*)(Bb + brow + j * 32 * LDK + q * 4);
+        for (int cg = 0; cg < CG; ++cg) {
+            const int kc = tap * CG + cg;
+            const int cur = kc & 1;
+            if (kc + 1 < NCH) gload(kc + 1);
+            // keep the next chunk's global loads at the top of the chunk: without this
+            // fence hipcc sinks them to just before their vmcnt wait (latency exposed)
+            __builtin_amdgcn_sched_barrier(0);
+            const float* Ab = As + cur * BM * LDK;
+            const float* Bb = Bs + cur * BN * LDK;
 #pragma unroll
-        for (int s = 0; s < 16; ++s)
+            for (int q = 0; q < 4; ++q) {
+                f32x4 a[TM], b[TN];
+                const int rc = ((h * 4 + q) ^ swz) * 4;
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
+                for (int i = 0; i < TM; ++i) a[i] = *(const f32x4*)(Ab + arow + i * 32 * LDK + rc);
 #pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s >> 2][s & 3], b[j][s >> 2][s & 3],
-                                                                    acc[i][j], 0, 0, 0);
-        if (kc + 1 < NCH) lstore(cur ^ 1);
-        __syncthreads();
+                for (int j = 0; j < TN; ++j) b[j] = *(const f32x4*)(Bb + brow + j * 32 * LDK + rc);
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            at[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], at[i][j], 0, 0, 0);
+            }
+            if (kc + 1 < NCH) lstore(cur ^ 1);
+            __syncthreads();
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] += at[i][j];
     }
 
     // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-        const int col = n0 + wn * WN + j * 32 + r32;
+        const int col = n0 + wn * TN * 32 + j * 32 + r32;
         float s_ = 1.f, t_ = 0.f;
-        if (EPI != EPI_RAW) { s_ = scale[col]; t_ = shift[col]; }
+        if (EPI == EPI_BN_RELU || EPI == EPI_BN_RES_RELU) { s_ = scale[col]; t_ = shift[col]; }
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (m < M) {
                     const int o = pad_off(m, C) + col;
                     float v = acc[i][j][r];
@@ -152,6 +181,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(
                         v = fmaxf(v * s_ + t_, 0.f);
                     } else if (EPI == EPI_BN_RES_RELU) {
                         v = fmaxf(v * s_ + t_ + resid[o], 0.f);
+                    } else if (EPI == EPI_ADD) {
+                        v = v + resid[o];
                     }
                     out[o] = v;
                 }
@@ -214,39 +245,96 @@ __global__ __launch_bounds__(256) void stem_conv(
 
 // ---- host launchers ------------------------------------------------------
 
-template <int C, int EPI>
+template <int C, int BN, int WM, int TM, int EPI>
 static hipError_t launch_conv_t(const float* in, const float* wp, const float* scale, const float* shift,
                                 const float* resid, float* out, int M, hipStream_t st)
 {
-    using T = ConvTile<C>;
+    using T = ConvTile<C, BN, WM, TM>;
     static bool attr_done = false;
     if (!attr_done) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_mfma<C, EPI>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_mfma<C, BN, WM, TM, EPI>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS_BYTES);
         if (e != hipSuccess) return e;
         attr_done = true;
     }
     dim3 grid((M + T::BM - 1) / T::BM, C / T::BN);
-    hipLaunchKernelGGL((conv3x3_mfma<C, EPI>), grid, dim3(256), T::LDS_BYTES, st,
+    hipLaunchKernelGGL((conv3x3_mfma<C, BN, WM, TM, EPI>), grid, dim3(256), T::LDS_BYTES, st,
                        in, wp, scale, shift, resid, out, M);
     return hipGetLastError();
+}
+
+template <int C, int BN, int WM, int TM>
+static hipError_t launch_conv_epi(int epi, const float* in, const float* wp, const float* scale, const float* shift,
+                                  const float* resid, float* out, int M, hipStream_t st)
+{
+    switch (epi) {
+        case EPI_BN_RELU: return launch_conv_t<C, BN, WM, TM, EPI_BN_RELU>(in, wp, scale, shift, resid, out, M, st);
+        case EPI_BN_RES_RELU: return launch_conv_t<C, BN, WM, TM, EPI_BN_RES_RELU>(in, wp, scale, shift, resid, out, M, st);
+        case EPI_ADD: return launch_conv_t<C, BN, WM, TM, EPI_ADD>(in, wp, scale, shift, resid, out, M, st);
+        default: return launch_conv_t<C, BN, WM, TM, EPI_RAW>(in, wp, scale, shift, resid, out, M, st);
+    }
+}
+
+// Tile shapes {BM, BN}: index into the switch below.
+struct TileShape { int bm, bn; };
+static const TileShape kShapes[] = {{128, 128}, {96, 128}, {160, 128}, {64, 128}, {128, 64}, {64, 64}};
+constexpr int kNumCUs = 256;
+
+// Pick the shape that wastes the fewest workgroup slots: 2 workgroups fit per CU
+// (LDS <= 80 KB, <= 128 VGPRs), tiles run in rounds of 512 slots, so the cost is
+// rounds * slot work.  Ties go to the larger tile (more operand reuse).
+int pick_conv_tile(int C, int M)
+{
+    int best = -1;
+    double best_eff = -1.0;
+    for (int i = 0; i < (int)(sizeof(kShapes) / sizeof(kShapes[0])); ++i) {
+        const int bm = kShapes[i].bm, bn = kShapes[i].bn;
+        if (bn > C) continue;
+        if (C == 64 && !(bm == 128 || bm == 64)) continue;
+        const long slots = 2L * kNumCUs;
+        const long tiles = (long)((M + bm - 1) / bm) * (C / bn);
+        const long rounds = (tiles + slots - 1) / slots;
+        double eff = (double)M * C / ((double)rounds * slots * bm * bn);
+        eff *= 1.0 - 0.03 * (bm * bn < 128 * 128) - 0.03 * (bm * bn < 64 * 128);
+        if (eff > best_eff + 1e-9) { best_eff = eff; best = i; }
+    }
+    return best;
+}
+
+hipError_t launch_conv3x3_shape(int shape, int C, int epi, const float* in, const float* wp, const float* scale,
+                                const float* shift, const float* resid, float* out, int M, hipStream_t st)
+{
+#define AZG_SHAPES(CC)                                                                                          \
+    switch (shape) {                                                                                            \
+        case 0: return launch_conv_epi<CC, (CC < 128 ? CC : 128), 2, 2>(epi, in, wp, scale, shift, resid, out, M, st); \
+        case 1: return launch_conv_epi<CC, 128, 1, 3>(epi, in, wp, scale, shift, resid, out, M, st);            \
+        case 2: return launch_conv_epi<CC, 128, 1, 5>(epi, in, wp, scale, shift, resid, out, M, st);            \
+        case 3: return launch_conv_epi<CC, 128, 2, 1>(epi, in, wp, scale, shift, resid, out, M, st);            \
+        case 4: return launch_conv_epi<CC, 64, 2, 2>(epi, in, wp, scale, shift, resid, out, M, st);             \
+        case 5: return launch_conv_epi<CC, 64, 2, 1>(epi, in, wp, scale, shift, resid, out, M, st);             \
+        default: return hipErrorInvalidValue;                                                                   \
+    }
+    switch (C) {
+        case 64:
+            switch (shape) {
+                case 0: return launch_conv_epi<64, 64, 2, 2>(epi, in, wp, scale, shift, resid, out, M, st);
+                case 5: return launch_conv_epi<64, 64, 2, 1>(epi, in, wp, scale, shift, resid, out, M, st);
+                case 4: return launch_conv_epi<64, 64, 2, 2>(epi, in, wp, scale, shift, resid, out, M, st);
+                default: return hipErrorInvalidValue;
+            }
+        case 128: AZG_SHAPES(128)
+        case 256: AZG_SHAPES(256)
+        default: return hipErrorInvalidValue;
+    }
+#undef AZG_SHAPES
 }
 
 hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, const float* scale,
                           const float* shift, const float* resid, float* out, int M, hipStream_t st)
 {
-#define AZG_CONV_CASE(CC)                                                                            \
-    case CC:                                                                                         \
-        if (epi == EPI_BN_RELU) return launch_conv_t<CC, EPI_BN_RELU>(in, wp, scale, shift, resid, out, M, st); \
-        if (epi == EPI_BN_RES_RELU) return launch_conv_t<CC, EPI_BN_RES_RELU>(in, wp, scale, shift, resid, out, M, st); \
-        return launch_conv_t<CC, EPI_RAW>(in, wp, scale, shift, resid, out, M, st);
-    switch (C) {
-        AZG_CONV_CASE(64)
-        AZG_CONV_CASE(128)
-        AZG_CONV_CASE(256)
-        default: return hipErrorInvalidValue;
-    }
-#undef AZG_CONV_CASE
+    int shape = pick_conv_tile(C, M);
+    if (C == 64 && shape == 3) shape = 5;
+    return launch_conv3x3_shape(shape, C, epi, in, wp, scale, shift, resid, out, M, st);
 }
 
 hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const float* scale,

@@ -1,22 +1,1121 @@
-// Train step (placeholder until the training kernels land).
+// Train step of the policy/value net (reference network.py:199-235):
+//   train-mode forward (BN batch statistics, running-stat update), log_softmax,
+//   KLDivLoss(batchmean) + MSELoss, backward, clip_grad_norm_(3.0), Adam.
+//
+// Numerics follow ATen's CPU kernels the reference runs on:
+//  * BN train stats: two-pass mean / biased var accumulated in double, invstd =
+//    1/sqrt(var+eps) in double then stored fp32; y = x*alpha + beta with
+//    alpha = invstd*gamma, beta = bias - mean*alpha; running stats updated in
+//    double with the unbiased var (momentum 0.1).  Here: per-128-row tile (mean,
+//    M2) in fp32, combined across tiles exactly in fp64.
+//  * BN backward: sum = S dy, dotp = S (x-mean) dy, k = dotp*invstd^2/N,
+//    dx = (dy - sum/N - (x-mean)*k) * invstd * gamma; dgamma = dotp*invstd.
+//  * Adam (torch single-tensor path): g += wd*p; m.lerp_(g, 1-b1);
+//    v = v*b2 + (1-b2)*g*g; denom = sqrt(v)/sqrt(bc2) + eps; p -= lr/bc1 * m/denom.
+//  * clip_grad_norm_: total = ||grads||_2, coef = min(max_norm/(total+1e-6), 1),
+//    grads *= coef (always).
 #include "pv_internal.h"
 
+#include <cmath>
+#include <cstdlib>
+#include <vector>
+
 namespace azg {
-void free_train_workspace(azg_pv* h) { (void)h; }
+
+hipError_t launch_wgrad(int C, const float* dz, const float* x, float* slab, float* dw, int M, int S, int rps,
+                        hipStream_t st);
+
+constexpr int TROWS = 128;   // rows per statistics tile
+
+struct TrainWS {
+    int cap = 0;
+    std::vector<float*> allocs;
+    float* z0 = nullptr;
+    float* a0 = nullptr;
+    std::vector<float*> z1, hh, z2, xo;
+    float *gX = nullptr, *DZ = nullptr, *DH = nullptr, *GR = nullptr;
+    float* wdpack = nullptr;     // dgrad-packed conv weights, 2*NB x 9*C*C
+    // per BN layer, at BnDesc::out_off (nfold floats each)
+    float *bmean = nullptr, *binv = nullptr, *bscale = nullptr, *bshift = nullptr;
+    float *bgm = nullptr, *bk = nullptr, *biw = nullptr;
+    // partials
+    float *part_a = nullptr, *part_b = nullptr;   // [ntile][C]
+    float* hpart = nullptr;                        // [ntile][3][C]
+    float* spart = nullptr;                        // [B][27][C]
+    float* slab = nullptr;                         // wgrad split-K slabs
+    int S = 0, rps = 0;
+    // heads
+    float *zh = nullptr, *fp = nullptr, *fv = nullptr, *hv = nullptr, *dpre = nullptr;
+    float *dlogits = nullptr, *dfp = nullptr, *dfv = nullptr, *dhv = nullptr, *dzh = nullptr, *lossb = nullptr;
+    // optimizer
+    double* npart = nullptr;     // grad sq-sum partials
+    float* scal = nullptr;       // [0] total norm, [1] clip coef
+    // debug snapshots of gX (AZG_DEBUG_SNAP=1): after heads, after each block
+    std::vector<float*> snap;
+};
+
+static TrainWS* ws_of(azg_pv* h) { return (TrainWS*)h->train; }
+
+void free_train_workspace(azg_pv* h)
+{
+    TrainWS* w = ws_of(h);
+    if (!w) return;
+    for (float* p : w->allocs) (void)hipFree(p);
+    delete w;
+    h->train = nullptr;
+}
+
+// ---------------------------------------------------------------------------
+// kernels
+
+__device__ __forceinline__ double block_sum_d(double v, double* red)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    double s = 0.0;
+    const int nw = blockDim.x >> 6;
+    for (int i = 0; i < nw; ++i) s += red[i];
+    __syncthreads();
+    return s;
+}
+
+// per-tile column (mean, M2) of a padded NHWC tensor (two passes over the tile)
+template <int C>
+__global__ __launch_bounds__(256) void col_stats_kernel(const float* __restrict__ z, float* __restrict__ pmean,
+                                                        float* __restrict__ pm2, int M)
+{
+    constexpr int TPC = 256 / C;
+    __shared__ float red[256];
+    const int c = threadIdx.x % C, rg = threadIdx.x / C;
+    const int m0 = blockIdx.x * TROWS;
+    const int rows = min(TROWS, M - m0);
+    float s = 0.f;
+    for (int r = rg; r < rows; r += TPC) s += z[pad_off(m0 + r, C) + c];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    float tot = 0.f;
+    for (int g = 0; g < TPC; ++g) tot += red[g * C + c];
+    const float mean = tot / (float)rows;
+    __syncthreads();
+    float q = 0.f;
+    for (int r = rg; r < rows; r += TPC) {
+        const float d = z[pad_off(m0 + r, C) + c] - mean;
+        q = fmaf(d, d, q);
+    }
+    red[threadIdx.x] = q;
+    __syncthreads();
+    if (rg == 0) {
+        float m2 = 0.f;
+        for (int g = 0; g < TPC; ++g) m2 += red[g * C + c];
+        pmean[blockIdx.x * C + c] = mean;
+        pm2[blockIdx.x * C + c] = m2;
+    }
+}
+
+// combine tile partials -> batch stats, apply coefficients, running-stat update.
+// One workgroup per channel of BN layer `d`.
+__global__ __launch_bounds__(256) void bn_finalize_kernel(
+    const float* __restrict__ pmean, const float* __restrict__ pm2, int ntile, int M, int C, const BnDesc* desc,
+    int layer, const float* __restrict__ params, float* __restrict__ stats, float* __restrict__ bmean,
+    float* __restrict__ binv, float* __restrict__ bscale, float* __restrict__ bshift)
+{
+    __shared__ double red[8];
+    const BnDesc d = desc[layer];
+    const int c = blockIdx.x;
+    double s = 0.0;
+    for (int t = threadIdx.x; t < ntile; t += blockDim.x) {
+        const int cnt = min(TROWS, M - t * TROWS);
+        s += (double)cnt * (double)pmean[t * C + c];
+    }
+    s = block_sum_d(s, red);
+    const double mean = s / (double)M;
+    double q = 0.0;
+    for (int t = threadIdx.x; t < ntile; t += blockDim.x) {
+        const int cnt = min(TROWS, M - t * TROWS);
+        const double dm = (double)pmean[t * C + c] - mean;
+        q += (double)pm2[t * C + c] + (double)cnt * dm * dm;
+    }
+    q = block_sum_d(q, red);
+    if (threadIdx.x == 0) {
+        const double var = q / (double)M;
+        const float mean_f = (float)mean;
+        const float inv_f = (float)(1.0 / sqrt(var + (double)BN_EPS));
+        const float alpha = inv_f * params[d.gamma_off + c];
+        bmean[d.out_off + c] = mean_f;
+        binv[d.out_off + c] = inv_f;
+        bscale[d.out_off + c] = alpha;
+        bshift[d.out_off + c] = params[d.beta_off + c] - mean_f * alpha;
+        const double unb = M > 1 ? q / (double)(M - 1) : var;
+        float* rm = stats + d.stat_off;
+        float* rv = stats + d.stat_off + d.c;
+        rm[c] = (float)((double)BN_MOMENTUM * mean + (1.0 - (double)BN_MOMENTUM) * (double)rm[c]);
+        rv[c] = (float)((double)BN_MOMENTUM * unb + (1.0 - (double)BN_MOMENTUM) * (double)rv[c]);
+    }
+}
+
+// a = relu(z*scale + shift [+ res]) over the interior of padded NHWC tensors
+template <int C, bool RES>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ z, const float* __restrict__ res,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, float* __restrict__ out,
+                                                       int M)
+{
+    constexpr int F4 = C / 4;
+    const int total = M * F4;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const int m = i / F4, c = (i - m * F4) * 4;
+        const int o = pad_off(m, C) + c;
+        f32x4 v = *(const f32x4*)(z + o);
+        const f32x4 s = *(const f32x4*)(scale + c);
+        const f32x4 t = *(const f32x4*)(shift + c);
+        f32x4 r;
+        if (RES) r = *(const f32x4*)(res + o);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float y = v[k] * s[k] + t[k];
+            if (RES) y += r[k];
+            v[k] = fmaxf(y, 0.f);
+        }
+        *(f32x4*)(out + o) = v;
+    }
+}
+
+// BN backward partial sums per tile: dy = g * (act > 0); S dy, S (z-mean) dy
+template <int C>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ g,
+                                                            const float* __restrict__ act,
+                                                            const float* __restrict__ z,
+                                                            const float* __restrict__ mean, float* __restrict__ pa,
+                                                            float* __restrict__ pb, int M)
+{
+    constexpr int TPC = 256 / C;
+    __shared__ float red[2][256];
+    const int c = threadIdx.x % C, rg = threadIdx.x / C;
+    const int m0 = blockIdx.x * TROWS;
+    const int rows = min(TROWS, M - m0);
+    const float mu = mean[c];
+    float s = 0.f, q = 0.f;
+    for (int r = rg; r < rows; r += TPC) {
+        const int o = pad_off(m0 + r, C) + c;
+        const float dy = act[o] > 0.f ? g[o] : 0.f;
+        s += dy;
+        q = fmaf(z[o] - mu, dy, q);
+    }
+    red[0][threadIdx.x] = s;
+    red[1][threadIdx.x] = q;
+    __syncthreads();
+    if (rg == 0) {
+        float a = 0.f, b = 0.f;
+        for (int k = 0; k < TPC; ++k) {
+            a += red[0][k * C + c];
+            b += red[1][k * C + c];
+        }
+        pa[blockIdx.x * C + c] = a;
+        pb[blockIdx.x * C + c] = b;
+    }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
+    const float* __restrict__ pa, const float* __restrict__ pb, int ntile, int M, int C, const BnDesc* desc,
+    int layer, const float* __restrict__ params, float* __restrict__ grads, const float* __restrict__ binv,
+    float* __restrict__ bgm, float* __restrict__ bk, float* __restrict__ biw)
+{
+    __shared__ double red[8];
+    const BnDesc d = desc[layer];
+    const int c = blockIdx.x;
+    double s = 0.0, q = 0.0;
+    for (int t = threadIdx.x; t < ntile; t += blockDim.x) {
+        s += (double)pa[t * C + c];
+        q += (double)pb[t * C + c];
+    }
+    s = block_sum_d(s, red);
+    q = block_sum_d(q, red);
+    if (threadIdx.x == 0) {
+        const double inv = (double)binv[d.out_off + c];
+        grads[d.gamma_off + c] = (float)(q * inv);
+        grads[d.beta_off + c] = (float)s;
+        bgm[d.out_off + c] = (float)(s / (double)M);
+        bk[d.out_off + c] = (float)(q * inv * inv / (double)M);
+        biw[d.out_off + c] = (float)inv * params[d.gamma_off + c];
+    }
+}
+
+// dz = ((dy - gm) - (z - mean)*k) * invstd*gamma ; optional gres = dy
+template <int C, bool GRES>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const float* __restrict__ g, const float* __restrict__ act, const float* __restrict__ z,
+    const float* __restrict__ mean, const float* __restrict__ gm, const float* __restrict__ kk,
+    const float* __restrict__ iw, float* __restrict__ dz, float* __restrict__ gres, int M)
+{
+    constexpr int F4 = C / 4;
+    const int total = M * F4;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const int m = i / F4, c = (i - m * F4) * 4;
+        const int o = pad_off(m, C) + c;
+        const f32x4 gv = *(const f32x4*)(g + o);
+        const f32x4 av = *(const f32x4*)(act + o);
+        const f32x4 zv = *(const f32x4*)(z + o);
+        const f32x4 mu = *(const f32x4*)(mean + c);
+        const f32x4 g_ = *(const f32x4*)(gm + c);
+        const f32x4 k_ = *(const f32x4*)(kk + c);
+        const f32x4 w_ = *(const f32x4*)(iw + c);
+        f32x4 out, dyv;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float dy = av[q] > 0.f ? gv[q] : 0.f;
+            dyv[q] = dy;
+            out[q] = ((dy - g_[q]) - (zv[q] - mu[q]) * k_[q]) * w_[q];
+        }
+        *(f32x4*)(dz + o) = out;
+        if (GRES) *(f32x4*)(gres + o) = dyv;
+    }
+}
+
+// heads: raw 1x1 projections zh[b][ch][p], ch 0,1 = policy_conv, 2 = value_conv
+template <int C>
+__global__ __launch_bounds__(256) void heads_proj_kernel(const float* __restrict__ act,
+                                                         const float* __restrict__ wpc,
+                                                         const float* __restrict__ wvc, float* __restrict__ zh,
+                                                         int M)
+{
+    constexpr int CPL = C / 64;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    float w0[CPL], w1[CPL], w2[CPL];
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+        w0[q] = wpc[lane * CPL + q];
+        w1[q] = wpc[C + lane * CPL + q];
+        w2[q] = wvc[lane * CPL + q];
+    }
+    for (int m = blockIdx.x * 4 + wid; m < M; m += gridDim.x * 4) {
+        const float* row = act + pad_off(m, C) + lane * CPL;
+        float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) {
+            const float a = row[q];
+            d0 = fmaf(a, w0[q], d0);
+            d1 = fmaf(a, w1[q], d1);
+            d2 = fmaf(a, w2[q], d2);
+        }
+        d0 = wave_sum(d0);
+        d1 = wave_sum(d1);
+        d2 = wave_sum(d2);
+        if (lane == 0) {
+            const int b = m / PIX, p = m - b * PIX;
+            zh[(b * 3 + 0) * PIX + p] = d0;
+            zh[(b * 3 + 1) * PIX + p] = d1;
+            zh[(b * 3 + 2) * PIX + p] = d2;
+        }
+    }
+}
+
+// head BN stats (3 channels over B*225), two-pass in double; one block per channel
+__global__ __launch_bounds__(256) void head_stats_kernel(const float* __restrict__ zh, int B, const BnDesc* desc,
+                                                         int pol_layer, int val_layer,
+                                                         const float* __restrict__ params,
+                                                         float* __restrict__ stats, float* __restrict__ bmean,
+                                                         float* __restrict__ binv, float* __restrict__ bscale,
+                                                         float* __restrict__ bshift)
+{
+    __shared__ double red[8];
+    const int ch = blockIdx.x;
+    const BnDesc d = desc[ch < 2 ? pol_layer : val_layer];
+    const int c = ch < 2 ? ch : 0;
+    const int N = B * PIX;
+    double s = 0.0;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        const int b = i / PIX, p = i - b * PIX;
+        s += (double)zh[(b * 3 + ch) * PIX + p];
+    }
+    s = block_sum_d(s, red);
+    const double mean = s / (double)N;
+    double q = 0.0;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        const int b = i / PIX, p = i - b * PIX;
+        const double dd = (double)zh[(b * 3 + ch) * PIX + p] - mean;
+        q += dd * dd;
+    }
+    q = block_sum_d(q, red);
+    if (threadIdx.x == 0) {
+        const double var = q / (double)N;
+        const float mean_f = (float)mean;
+        const float inv_f = (float)(1.0 / sqrt(var + (double)BN_EPS));
+        const float alpha = inv_f * params[d.gamma_off + c];
+        bmean[d.out_off + c] = mean_f;
+        binv[d.out_off + c] = inv_f;
+        bscale[d.out_off + c] = alpha;
+        bshift[d.out_off + c] = params[d.beta_off + c] - mean_f * alpha;
+        const double unb = N > 1 ? q / (double)(N - 1) : var;
+        float* rm = stats + d.stat_off;
+        float* rv = stats + d.stat_off + d.c;
+        rm[c] = (float)((double)BN_MOMENTUM * mean + (1.0 - (double)BN_MOMENTUM) * (double)rm[c]);
+        rv[c] = (float)((double)BN_MOMENTUM * unb + (1.0 - (double)BN_MOMENTUM) * (double)rv[c]);
+    }
+}
+
+struct HeadsArgs {
+    const float* zh;
+    const float* hscale;   // [3]: policy ch0, ch1, value (folded train BN)
+    const float* hshift;
+    const float* wpf;      // policy_fc.weight [225][450]
+    const float* wpfT;     // [450][225]
+    const float* bpf;
+    const float* wv1;      // value_fc1.weight [64][225]
+    const float* wv1T;     // [225][64]
+    const float* bv1;
+    const float* wv2;      // [64]
+    const float* bv2;
+    const float* pis;      // [B][225]
+    const float* zs;       // [B]
+    float* fp;
+    float* fv;
+    float* hv;
+    float* dpre;
+    float* dlogits;
+    float* dfp;
+    float* dfv;
+    float* dhv;
+    float* lossb;          // [B][2]
+    int B;
+};
+
+// per board: head forward (train BN), loss terms, and the backward down to the
+// (masked) post-BN head features.  One 256-thread workgroup per board.
+__global__ __launch_bounds__(256) void heads_train_kernel(HeadsArgs a)
+{
+    __shared__ float sfp[2 * PIX];
+    __shared__ float sfv[PIX];
+    __shared__ float slog[ACTIONS];
+    __shared__ float sdl[ACTIONS];
+    __shared__ float shv[VHID];
+    __shared__ float sdhv[VHID];
+    __shared__ float red[8];
+    __shared__ float sv;
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const float* zb = a.zh + (size_t)b * 3 * PIX;
+    for (int k = tid; k < 3 * PIX; k += 256) {
+        const int ch = k / PIX;
+        const float y = fmaxf(zb[k] * a.hscale[ch] + a.hshift[ch], 0.f);
+        if (ch < 2) {
+            sfp[k] = y;
+            a.fp[(size_t)b * 2 * PIX + k] = y;
+        } else {
+            sfv[k - 2 * PIX] = y;
+            a.fv[(size_t)b * PIX + k - 2 * PIX] = y;
+        }
+    }
+    __syncthreads();
+    // logits (threads < 225) and value hidden layer (threads < 64)
+    if (tid < ACTIONS) {
+        float acc = 0.f;
+        for (int k = 0; k < 2 * PIX; ++k) acc = fmaf(a.wpfT[k * ACTIONS + tid], sfp[k], acc);
+        slog[tid] = acc + a.bpf[tid];
+    }
+    if (tid < VHID) {
+        float acc = 0.f;
+        for (int k = 0; k < PIX; ++k) acc = fmaf(a.wv1T[k * VHID + tid], sfv[k], acc);
+        shv[tid] = fmaxf(acc + a.bv1[tid], 0.f);
+    }
+    __syncthreads();
+    if (wid == 0) {
+        // log_softmax, KL term, dlogits
+        float mx = -INFINITY;
+        for (int j = lane; j < ACTIONS; j += 64) mx = fmaxf(mx, slog[j]);
+        mx = wave_max(mx);
+        float se = 0.f;
+        for (int j = lane; j < ACTIONS; j += 64) se += expf(slog[j] - mx);
+        se = wave_sum(se);
+        const float lse = logf(se);
+        const float* t = a.pis + (size_t)b * ACTIONS;
+        float kl = 0.f, st = 0.f;
+        for (int j = lane; j < ACTIONS; j += 64) {
+            const float tj = t[j];
+            const float lp = (slog[j] - mx) - lse;
+            if (tj > 0.f) kl += tj * (logf(tj) - lp);
+            st += tj;
+        }
+        kl = wave_sum(kl);
+        st = wave_sum(st);
+        const float invB = 1.f / (float)a.B;
+        for (int j = lane; j < ACTIONS; j += 64) {
+            const float lp = (slog[j] - mx) - lse;
+            const float d = (expf(lp) * st - t[j]) * invB;
+            sdl[j] = d;
+            a.dlogits[(size_t)b * ACTIONS + j] = d;
+        }
+        if (lane == 0) a.lossb[b * 2 + 0] = kl;
+    } else if (wid == 1) {
+        // value: v = tanh(w2.hv + b2); (v-z)^2; dpre = 2(v-z)/B (1-v^2)
+        float pre = wave_sum(a.wv2[lane] * shv[lane]) + a.bv2[0];
+        const float v = tanhf(pre);
+        const float z = a.zs[b];
+        const float dv = 2.f * (v - z) / (float)a.B;
+        const float dp = dv * (1.f - v * v);
+        const float dh = shv[lane] > 0.f ? dp * a.wv2[lane] : 0.f;
+        sdhv[lane] = dh;
+        a.dhv[(size_t)b * VHID + lane] = dh;
+        a.hv[(size_t)b * VHID + lane] = shv[lane];
+        if (lane == 0) {
+            a.lossb[b * 2 + 1] = (v - z) * (v - z);
+            a.dpre[b] = dp;
+            sv = v;
+        }
+    }
+    __syncthreads();
+    // dfp[k] = (S_j Wpf[j][k] dl_j) * (fp>0);  dfv[k] = (S_i Wv1[i][k] dhv_i) * (fv>0)
+    for (int k = tid; k < 2 * PIX; k += 256) {
+        float acc = 0.f;
+        for (int j = 0; j < ACTIONS; ++j) acc = fmaf(a.wpf[j * 2 * PIX + k], sdl[j], acc);
+        a.dfp[(size_t)b * 2 * PIX + k] = sfp[k] > 0.f ? acc : 0.f;
+    }
+    for (int k = tid; k < PIX; k += 256) {
+        float acc = 0.f;
+        for (int i = 0; i < VHID; ++i) acc = fmaf(a.wv1[i * PIX + k], sdhv[i], acc);
+        a.dfv[(size_t)b * PIX + k] = sfv[k] > 0.f ? acc : 0.f;
+    }
+    (void)red;
+    (void)sv;
+}
+
+// FC weight/bias grads of the heads + the loss means.
+__global__ __launch_bounds__(256) void heads_wgrad_kernel(const float* __restrict__ dlogits,
+                                                          const float* __restrict__ fp,
+                                                          const float* __restrict__ dhv,
+                                                          const float* __restrict__ fv,
+                                                          const float* __restrict__ dpre,
+                                                          const float* __restrict__ hv,
+                                                          const float* __restrict__ lossb, int B,
+                                                          float* __restrict__ g_pfw, float* __restrict__ g_pfb,
+                                                          float* __restrict__ g_v1w, float* __restrict__ g_v1b,
+                                                          float* __restrict__ g_v2w, float* __restrict__ g_v2b,
+                                                          float* __restrict__ losses)
+{
+    const int n_pfw = ACTIONS * 2 * PIX, n_v1w = VHID * PIX;
+    const int total = n_pfw + ACTIONS + n_v1w + VHID + VHID + 1;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        float s = 0.f;
+        if (i < n_pfw) {
+            const int j = i / (2 * PIX), k = i - j * 2 * PIX;
+            for (int b = 0; b < B; ++b) s = fmaf(dlogits[b * ACTIONS + j], fp[b * 2 * PIX + k], s);
+            g_pfw[i] = s;
+        } else if (i < n_pfw + ACTIONS) {
+            const int j = i - n_pfw;
+            for (int b = 0; b < B; ++b) s += dlogits[b * ACTIONS + j];
+            g_pfb[j] = s;
+        } else if (i < n_pfw + ACTIONS + n_v1w) {
+            const int r = i - n_pfw - ACTIONS;
+            const int u = r / PIX, k = r - u * PIX;
+            for (int b = 0; b < B; ++b) s = fmaf(dhv[b * VHID + u], fv[b * PIX + k], s);
+            g_v1w[r] = s;
+        } else if (i < n_pfw + ACTIONS + n_v1w + VHID) {
+            const int u = i - n_pfw - ACTIONS - n_v1w;
+            for (int b = 0; b < B; ++b) s += dhv[b * VHID + u];
+            g_v1b[u] = s;
+        } else if (i < n_pfw + ACTIONS + n_v1w + 2 * VHID) {
+            const int u = i - n_pfw - ACTIONS - n_v1w - VHID;
+            for (int b = 0; b < B; ++b) s = fmaf(dpre[b], hv[b * VHID + u], s);
+            g_v2w[u] = s;
+        } else {
+            for (int b = 0; b < B; ++b) s += dpre[b];
+            g_v2b[0] = s;
+            double pl = 0.0, vl = 0.0;
+            for (int b = 0; b < B; ++b) {
+                pl += (double)lossb[2 * b];
+                vl += (double)lossb[2 * b + 1];
+            }
+            const float plf = (float)(pl / (double)B), vlf = (float)(vl / (double)B);
+            losses[0] = plf;
+            losses[1] = vlf;
+            losses[2] = plf + vlf;
+        }
+    }
+}
+
+// head BN backward (3 channels): grads of gamma/beta and dzh.  One block per channel.
+__global__ __launch_bounds__(256) void head_bn_bwd_kernel(const float* __restrict__ zh,
+                                                          const float* __restrict__ dfp,
+                                                          const float* __restrict__ dfv, int B,
+                                                          const BnDesc* desc, int pol_layer, int val_layer,
+                                                          const float* __restrict__ params,
+                                                          float* __restrict__ grads, const float* __restrict__ bmean,
+                                                          const float* __restrict__ binv, float* __restrict__ dzh)
+{
+    __shared__ double red[8];
+    const int ch = blockIdx.x;
+    const BnDesc d = desc[ch < 2 ? pol_layer : val_layer];
+    const int c = ch < 2 ? ch : 0;
+    const int N = B * PIX;
+    const float mu = bmean[d.out_off + c], inv = binv[d.out_off + c];
+    auto dy_at = [&](int b, int p) {
+        return ch < 2 ? dfp[(size_t)b * 2 * PIX + ch * PIX + p] : dfv[(size_t)b * PIX + p];
+    };
+    double s = 0.0, q = 0.0;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        const int b = i / PIX, p = i - b * PIX;
+        const double dy = (double)dy_at(b, p);
+        s += dy;
+        q += ((double)zh[(b * 3 + ch) * PIX + p] - (double)mu) * dy;
+    }
+    s = block_sum_d(s, red);
+    q = block_sum_d(q, red);
+    const double invd = (double)inv;
+    if (threadIdx.x == 0) {
+        grads[d.gamma_off + c] = (float)(q * invd);
+        grads[d.beta_off + c] = (float)s;
+    }
+    const float gm = (float)(s / (double)N);
+    const float kk = (float)(q * invd * invd / (double)N);
+    const float iw = inv * params[d.gamma_off + c];
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        const int b = i / PIX, p = i - b * PIX;
+        const float dy = dy_at(b, p);
+        const float zz = zh[(b * 3 + ch) * PIX + p];
+        dzh[(b * 3 + ch) * PIX + p] = ((dy - gm) - (zz - mu) * kk) * iw;
+    }
+}
+
+// gX[m][c] = S_ch dzh[m][ch] * Wh[ch][c]; partial S_m dzh[m][ch] X[m][c] per tile
+template <int C>
+__global__ __launch_bounds__(256) void heads_bwd_proj_kernel(const float* __restrict__ act,
+                                                             const float* __restrict__ dzh,
+                                                             const float* __restrict__ wpc,
+                                                             const float* __restrict__ wvc,
+                                                             float* __restrict__ gx, float* __restrict__ hpart,
+                                                             int M)
+{
+    constexpr int TPC = 256 / C;
+    __shared__ float red[3][256];
+    const int c = threadIdx.x % C, rg = threadIdx.x / C;
+    const int m0 = blockIdx.x * TROWS;
+    const int rows = min(TROWS, M - m0);
+    const float w0 = wpc[c], w1 = wpc[C + c], w2 = wvc[c];
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    for (int r = rg; r < rows; r += TPC) {
+        const int m = m0 + r;
+        const int b = m / PIX, p = m - b * PIX;
+        const float d0 = dzh[(b * 3 + 0) * PIX + p];
+        const float d1 = dzh[(b * 3 + 1) * PIX + p];
+        const float d2 = dzh[(b * 3 + 2) * PIX + p];
+        const int o = pad_off(m, C) + c;
+        const float xv = act[o];
+        s0 = fmaf(d0, xv, s0);
+        s1 = fmaf(d1, xv, s1);
+        s2 = fmaf(d2, xv, s2);
+        gx[o] = d0 * w0 + d1 * w1 + d2 * w2;
+    }
+    red[0][threadIdx.x] = s0;
+    red[1][threadIdx.x] = s1;
+    red[2][threadIdx.x] = s2;
+    __syncthreads();
+    if (rg == 0) {
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+        for (int k = 0; k < TPC; ++k) {
+            a0 += red[0][k * C + c];
+            a1 += red[1][k * C + c];
+            a2 += red[2][k * C + c];
+        }
+        hpart[(blockIdx.x * 3 + 0) * C + c] = a0;
+        hpart[(blockIdx.x * 3 + 1) * C + c] = a1;
+        hpart[(blockIdx.x * 3 + 2) * C + c] = a2;
+    }
+}
+
+// out[j] = S_t part[t][j] for j < n (fixed order)
+__global__ void sum_partials_kernel(const float* __restrict__ part, int ntile, int n, float* __restrict__ out0,
+                                    float* __restrict__ out1, int split)
+{
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        float s = 0.f;
+        for (int t = 0; t < ntile; ++t) s += part[(size_t)t * n + j];
+        if (j < split) out0[j] = s;
+        else out1[j - split] = s;
+    }
+}
+
+// stem weight gradient partials per board: part[b][k][c] = S_p dz[p][c] * xpatch[p][k]
+template <int C>
+__global__ __launch_bounds__(256) void stem_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dz,
+                                                         float* __restrict__ spart)
+{
+    __shared__ float xs[3 * PADPIX];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const float* xb = x + (size_t)b * 3 * PIX;
+    for (int i = tid; i < 3 * PADPIX; i += 256) {
+        const int ci = i / PADPIX, rem = i - ci * PADPIX;
+        const int yy = rem / PADW, xx = rem - yy * PADW;
+        float v = 0.f;
+        if (yy >= 1 && yy <= BOARD && xx >= 1 && xx <= BOARD) v = xb[ci * PIX + (yy - 1) * BOARD + (xx - 1)];
+        xs[i] = v;
+    }
+    __syncthreads();
+    constexpr int TPC = C < 256 ? 256 / C : 1;
+    __shared__ float red[27][256];
+    const int c = tid % C, rg = tid / C;
+    if (C <= 256) {
+        float acc[27];
+#pragma unroll
+        for (int k = 0; k < 27; ++k) acc[k] = 0.f;
+        for (int p = rg; p < PIX; p += TPC) {
+            const int y = p / BOARD, xq = p - y * BOARD;
+            const float d = dz[(size_t)(b * PADPIX + (y + 1) * PADW + (xq + 1)) * C + c];
+#pragma unroll
+            for (int ci = 0; ci < 3; ++ci)
+#pragma unroll
+                for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                    for (int kx = 0; kx < 3; ++kx)
+                        acc[ci * 9 + ky * 3 + kx] =
+                            fmaf(d, xs[ci * PADPIX + (y + ky) * PADW + (xq + kx)], acc[ci * 9 + ky * 3 + kx]);
+        }
+#pragma unroll
+        for (int k = 0; k < 27; ++k) red[k][tid] = acc[k];
+        __syncthreads();
+        if (rg == 0) {
+            for (int k = 0; k < 27; ++k) {
+                float s = 0.f;
+                for (int g = 0; g < TPC; ++g) s += red[k][g * C + c];
+                spart[((size_t)b * 27 + k) * C + c] = s;
+            }
+        }
+    }
+}
+
+// sum stem partials over boards -> grads[c*27 + k]
+__global__ void stem_wgrad_reduce_kernel(const float* __restrict__ spart, int B, int C, float* __restrict__ g)
+{
+    const int total = 27 * C;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const int k = i / C, c = i - k * C;
+        float s = 0.f;
+        for (int b = 0; b < B; ++b) s += spart[((size_t)b * 27 + k) * C + c];
+        g[c * 27 + k] = s;
+    }
+}
+
+// ---- optimizer --------------------------------------------------------------
+
+__global__ __launch_bounds__(256) void grad_sqsum_kernel(const float* __restrict__ g, int64_t n,
+                                                         double* __restrict__ part)
+{
+    __shared__ double red[8];
+    double s = 0.0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double v = (double)g[i];
+        s += v * v;
+    }
+    s = block_sum_d(s, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void grad_norm_finalize_kernel(const double* __restrict__ part, int nb,
+                                                                 float max_norm, float* __restrict__ scal,
+                                                                 float* __restrict__ total_norm)
+{
+    __shared__ double red[8];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) s += part[i];
+    s = block_sum_d(s, red);
+    if (threadIdx.x == 0) {
+        const float tn = (float)sqrt(s);
+        float coef = max_norm / (tn + 1e-6f);
+        coef = coef < 1.f ? coef : 1.f;
+        scal[0] = tn;
+        scal[1] = coef;
+        if (total_norm) total_norm[0] = tn;
+    }
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                   const float* __restrict__ scal, float lr_bc1, float b1w,
+                                                   float b2, float one_m_b2, float bc2_sqrt, float eps, float wd)
+{
+    const float coef = scal[1];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        float gi = g[i] * coef;
+        g[i] = gi;
+        const float pi = p[i];
+        if (wd != 0.f) gi = gi + wd * pi;
+        float mi = m[i];
+        mi = mi + b1w * (gi - mi);                 // lerp, weight < 0.5 branch
+        float vi = v[i] * b2;
+        vi = vi + one_m_b2 * gi * gi;              // addcmul
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        p[i] = pi + (-lr_bc1) * (mi / denom);      // addcdiv
+        m[i] = mi;
+        v[i] = vi;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// orchestration
+
+static int32_t alloc_into(TrainWS* w, float** p, size_t floats, hipStream_t st, bool zero)
+{
+    hipError_t e = hipMalloc(p, floats * sizeof(float));
+    if (e != hipSuccess) return set_error("train workspace: hipMalloc", e);
+    w->allocs.push_back(*p);
+    if (zero) {
+        e = hipMemsetAsync(*p, 0, floats * sizeof(float), st);
+        if (e != hipSuccess) return set_error("train workspace: hipMemsetAsync", e);
+    }
+    return 0;
+}
+
+static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
+{
+    TrainWS* w = ws_of(h);
+    if (w && w->cap >= B) return 0;
+    int cap = w ? w->cap : 0;
+    if (w) free_train_workspace(h);
+    cap = cap ? cap : 128;
+    while (cap < B) cap *= 2;
+    w = new TrainWS();
+    h->train = w;
+    w->cap = cap;
+    const int C = h->C, NB = h->NB;
+    const size_t act = (size_t)cap * PADPIX * C;
+    const int M = cap * PIX;
+    const int ntile = (M + TROWS - 1) / TROWS;
+    int32_t r = 0;
+#define A(ptr, n, z) if ((r = alloc_into(w, &(ptr), (n), st, (z)))) return r
+    A(w->z0, act, true);
+    A(w->a0, act, true);
+    w->z1.assign(NB, nullptr); w->hh.assign(NB, nullptr); w->z2.assign(NB, nullptr); w->xo.assign(NB, nullptr);
+    for (int i = 0; i < NB; ++i) {
+        A(w->z1[i], act, true);
+        A(w->hh[i], act, true);
+        A(w->z2[i], act, true);
+        A(w->xo[i], act, true);
+    }
+    A(w->gX, act, true);
+    A(w->DZ, act, true);
+    A(w->DH, act, true);
+    A(w->GR, act, true);
+    A(w->wdpack, (size_t)(2 * NB > 0 ? 2 * NB : 1) * 9 * C * C, false);
+    const size_t nf = h->nfold;
+    A(w->bmean, nf, true); A(w->binv, nf, true); A(w->bscale, nf, true); A(w->bshift, nf, true);
+    A(w->bgm, nf, true); A(w->bk, nf, true); A(w->biw, nf, true);
+    A(w->part_a, (size_t)ntile * C, false);
+    A(w->part_b, (size_t)ntile * C, false);
+    A(w->hpart, (size_t)ntile * 3 * C, false);
+    A(w->spart, (size_t)cap * 27 * C, false);
+    // split-K for wgrad: ~512 rows per split
+    w->rps = 512;
+    w->S = (M + w->rps - 1) / w->rps;
+    A(w->slab, (size_t)w->S * 9 * C * C, false);
+    A(w->zh, (size_t)cap * 3 * PIX, false);
+    A(w->fp, (size_t)cap * 2 * PIX, false);
+    A(w->fv, (size_t)cap * PIX, false);
+    A(w->hv, (size_t)cap * VHID, false);
+    A(w->dpre, (size_t)cap, false);
+    A(w->dlogits, (size_t)cap * ACTIONS, false);
+    A(w->dfp, (size_t)cap * 2 * PIX, false);
+    A(w->dfv, (size_t)cap * PIX, false);
+    A(w->dhv, (size_t)cap * VHID, false);
+    A(w->dzh, (size_t)cap * 3 * PIX, false);
+    A(w->lossb, (size_t)cap * 2, false);
+    float* np = nullptr;
+    A(np, 2 * 1024, false);
+    w->npart = (double*)np;
+    A(w->scal, 4, true);
+    if (getenv("AZG_DEBUG_SNAP")) {
+        w->snap.assign(NB + 1, nullptr);
+        for (int i = 0; i <= NB; ++i) A(w->snap[i], act, true);
+    }
+#undef A
+    return 0;
+}
+
+static inline int grid_for(int64_t total) { int64_t b = (total + 255) / 256; return (int)(b > 8192 ? 8192 : b); }
+
+#define AZG_CK(expr, what)                               \
+    do {                                                 \
+        hipError_t _e = (expr);                          \
+        if (_e == hipSuccess) _e = hipGetLastError();    \
+        if (_e != hipSuccess) return set_error(what, _e); \
+    } while (0)
+
+template <int C>
+static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, const float* zs, int B,
+                                float* losses, hipStream_t st)
+{
+    TrainWS* w = ws_of(h);
+    const int NB = h->NB;
+    const int M = B * PIX;
+    const int ntile = (M + TROWS - 1) / TROWS;
+    const float* P = h->params;
+    float* G = h->grads;
+    const BnDesc* bd = h->bn_desc.data();
+    const BnDesc* bdd = (const BnDesc*)h->bn_desc_dev;
+    const int gM = grid_for((int64_t)M * C / 4);
+
+    auto stats = [&](const float* z, int layer) -> int32_t {
+        int pr = prof_begin(h, AZG_PROF_TRAIN_OTHER, st);
+        hipLaunchKernelGGL((col_stats_kernel<C>), dim3(ntile), dim3(256), 0, st, z, w->part_a, w->part_b, M);
+        AZG_CK(hipGetLastError(), "train: col_stats");
+        hipLaunchKernelGGL(bn_finalize_kernel, dim3(bd[layer].c), dim3(256), 0, st, w->part_a, w->part_b, ntile, M,
+                           C, bdd, layer, P, h->bn, w->bmean, w->binv, w->bscale, w->bshift);
+        AZG_CK(hipGetLastError(), "train: bn_finalize");
+        prof_end(h, pr, st);
+        return 0;
+    };
+    auto apply = [&](const float* z, const float* res, int layer, float* out) -> int32_t {
+        const int o = bd[layer].out_off;
+        if (res)
+            hipLaunchKernelGGL((bn_apply_kernel<C, true>), dim3(gM), dim3(256), 0, st, z, res, w->bscale + o,
+                               w->bshift + o, out, M);
+        else
+            hipLaunchKernelGGL((bn_apply_kernel<C, false>), dim3(gM), dim3(256), 0, st, z, res, w->bscale + o,
+                               w->bshift + o, out, M);
+        AZG_CK(hipGetLastError(), "train: bn_apply");
+        return 0;
+    };
+    auto conv = [&](int epi, const float* in, const float* wp, const float* res, float* out) -> int32_t {
+        int pr = prof_begin(h, AZG_PROF_TRAIN_CONV, st);
+        AZG_CK(launch_conv3x3(C, epi, in, wp, nullptr, nullptr, res, out, M, st), "train: conv3x3");
+        prof_end(h, pr, st);
+        return 0;
+    };
+    auto bwd_bn = [&](const float* g, const float* act, const float* z, int layer, float* dz, float* gres) -> int32_t {
+        const int o = bd[layer].out_off;
+        hipLaunchKernelGGL((bn_bwd_reduce_kernel<C>), dim3(ntile), dim3(256), 0, st, g, act, z, w->bmean + o,
+                           w->part_a, w->part_b, M);
+        AZG_CK(hipGetLastError(), "train: bn_bwd_reduce");
+        hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bd[layer].c), dim3(256), 0, st, w->part_a, w->part_b, ntile,
+                           M, C, bdd, layer, P, G, w->binv, w->bgm, w->bk, w->biw);
+        AZG_CK(hipGetLastError(), "train: bn_bwd_finalize");
+        if (gres)
+            hipLaunchKernelGGL((bn_bwd_apply_kernel<C, true>), dim3(gM), dim3(256), 0, st, g, act, z, w->bmean + o,
+                               w->bgm + o, w->bk + o, w->biw + o, dz, gres, M);
+        else
+            hipLaunchKernelGGL((bn_bwd_apply_kernel<C, false>), dim3(gM), dim3(256), 0, st, g, act, z, w->bmean + o,
+                               w->bgm + o, w->bk + o, w->biw + o, dz, gres, M);
+        AZG_CK(hipGetLastError(), "train: bn_bwd_apply");
+        return 0;
+    };
+    auto wgrad = [&](const float* dz, const float* xin, int tensor) -> int32_t {
+        int pr = prof_begin(h, AZG_PROF_TRAIN_WGRAD, st);
+        AZG_CK(launch_wgrad(C, dz, xin, w->slab, G + h->poff[tensor], M, (M + w->rps - 1) / w->rps, w->rps, st),
+               "train: wgrad");
+        prof_end(h, pr, st);
+        return 0;
+    };
+    int32_t r;
+#define R(x) if ((r = (x))) return r
+
+    // ---- forward (train-mode BN) ----
+    AZG_CK(launch_stem(C, EPI_RAW, x, h->wstem, nullptr, nullptr, w->z0, B, st), "train: stem");
+    R(stats(w->z0, h->bn_stem));
+    R(apply(w->z0, nullptr, h->bn_stem, w->a0));
+    const float* X = w->a0;
+    for (int i = 0; i < NB; ++i) {
+        R(conv(EPI_RAW, X, h->wpack + (size_t)(2 * i) * 9 * C * C, nullptr, w->z1[i]));
+        R(stats(w->z1[i], h->bn_blk[i].first));
+        R(apply(w->z1[i], nullptr, h->bn_blk[i].first, w->hh[i]));
+        R(conv(EPI_RAW, w->hh[i], h->wpack + (size_t)(2 * i + 1) * 9 * C * C, nullptr, w->z2[i]));
+        R(stats(w->z2[i], h->bn_blk[i].second));
+        R(apply(w->z2[i], X, h->bn_blk[i].second, w->xo[i]));
+        X = w->xo[i];
+    }
+    // ---- heads forward + loss + backward to the tower output ----
+    {
+        int pr = prof_begin(h, AZG_PROF_TRAIN_OTHER, st);
+        hipLaunchKernelGGL((heads_proj_kernel<C>), dim3((M + 15) / 16), dim3(256), 0, st, X,
+                           P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], w->zh, M);
+        AZG_CK(hipGetLastError(), "train: heads_proj");
+        hipLaunchKernelGGL(head_stats_kernel, dim3(3), dim3(256), 0, st, w->zh, B, bdd, h->bn_pol, h->bn_val, P,
+                           h->bn, w->bmean, w->binv, w->bscale, w->bshift);
+        AZG_CK(hipGetLastError(), "train: head_stats");
+        const int ho = bd[h->bn_pol].out_off;
+        HeadsArgs ha;
+        ha.zh = w->zh;
+        ha.hscale = w->bscale + ho;
+        ha.hshift = w->bshift + ho;
+        ha.wpf = P + h->poff[h->t_pfc_w];
+        ha.wpfT = h->wpfT;
+        ha.bpf = P + h->poff[h->t_pfc_b];
+        ha.wv1 = P + h->poff[h->t_vfc1_w];
+        ha.wv1T = h->wv1T;
+        ha.bv1 = P + h->poff[h->t_vfc1_b];
+        ha.wv2 = P + h->poff[h->t_vfc2_w];
+        ha.bv2 = P + h->poff[h->t_vfc2_b];
+        ha.pis = pis;
+        ha.zs = zs;
+        ha.fp = w->fp; ha.fv = w->fv; ha.hv = w->hv; ha.dpre = w->dpre; ha.dlogits = w->dlogits;
+        ha.dfp = w->dfp; ha.dfv = w->dfv; ha.dhv = w->dhv; ha.lossb = w->lossb;
+        ha.B = B;
+        hipLaunchKernelGGL(heads_train_kernel, dim3(B), dim3(256), 0, st, ha);
+        AZG_CK(hipGetLastError(), "train: heads_train");
+        const int64_t nw = (int64_t)ACTIONS * 2 * PIX + ACTIONS + VHID * PIX + 2 * VHID + 1;
+        hipLaunchKernelGGL(heads_wgrad_kernel, dim3(grid_for(nw)), dim3(256), 0, st, w->dlogits, w->fp, w->dhv,
+                           w->fv, w->dpre, w->hv, w->lossb, B, G + h->poff[h->t_pfc_w], G + h->poff[h->t_pfc_b],
+                           G + h->poff[h->t_vfc1_w], G + h->poff[h->t_vfc1_b], G + h->poff[h->t_vfc2_w],
+                           G + h->poff[h->t_vfc2_b], losses);
+        AZG_CK(hipGetLastError(), "train: heads_wgrad");
+        hipLaunchKernelGGL(head_bn_bwd_kernel, dim3(3), dim3(256), 0, st, w->zh, w->dfp, w->dfv, B, bdd, h->bn_pol,
+                           h->bn_val, P, G, w->bmean, w->binv, w->dzh);
+        AZG_CK(hipGetLastError(), "train: head_bn_bwd");
+        hipLaunchKernelGGL((heads_bwd_proj_kernel<C>), dim3(ntile), dim3(256), 0, st, X, w->dzh,
+                           P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], w->gX, w->hpart, M);
+        AZG_CK(hipGetLastError(), "train: heads_bwd_proj");
+        // policy_conv.weight [2][C] then value_conv.weight [C]: partial layout [t][3][C]
+        hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(3 * C)), dim3(256), 0, st, w->hpart, ntile, 3 * C,
+                           G + h->poff[h->t_pc_w], G + h->poff[h->t_vc_w], 2 * C);
+        AZG_CK(hipGetLastError(), "train: heads proj wgrad");
+        prof_end(h, pr, st);
+    }
+    auto snap = [&](int k) -> int32_t {
+        if (!w->snap.empty())
+            AZG_CK(hipMemcpyAsync(w->snap[k], w->gX, (size_t)B * PADPIX * C * sizeof(float), hipMemcpyDeviceToDevice, st),
+                   "train: snapshot");
+        return 0;
+    };
+    R(snap(0));
+    // ---- tower backward ----
+    for (int i = NB - 1; i >= 0; --i) {
+        const float* Xin = i == 0 ? w->a0 : w->xo[i - 1];
+        R(bwd_bn(w->gX, w->xo[i], w->z2[i], h->bn_blk[i].second, w->DZ, w->GR));
+        R(wgrad(w->DZ, w->hh[i], h->t_blk[i].w2));
+        R(conv(EPI_RAW, w->DZ, w->wdpack + (size_t)(2 * i + 1) * 9 * C * C, nullptr, w->DH));
+        R(bwd_bn(w->DH, w->hh[i], w->z1[i], h->bn_blk[i].first, w->DZ, nullptr));
+        R(wgrad(w->DZ, Xin, h->t_blk[i].w1));
+        R(conv(EPI_ADD, w->DZ, w->wdpack + (size_t)(2 * i) * 9 * C * C, w->GR, w->gX));
+        R(snap(NB - i));
+    }
+    // ---- stem backward ----
+    R(bwd_bn(w->gX, w->a0, w->z0, h->bn_stem, w->DZ, nullptr));
+    hipLaunchKernelGGL((stem_wgrad_kernel<C>), dim3(B), dim3(256), 0, st, x, w->DZ, w->spart);
+    AZG_CK(hipGetLastError(), "train: stem_wgrad");
+    hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(grid_for(27 * C)), dim3(256), 0, st, w->spart, B, C,
+                       G + h->poff[h->t_stem_w]);
+    AZG_CK(hipGetLastError(), "train: stem_wgrad_reduce");
+#undef R
+    return 0;
+}
+
+int32_t train_backward(azg_pv* h, const float* x, const float* pis, const float* zs, int B, float* losses,
+                       hipStream_t st)
+{
+    if (int32_t r = ensure_train_ws(h, B, st)) return r;
+    if (int32_t r = repack(h, st)) return r;
+    TrainWS* w = ws_of(h);
+    const int C = h->C;
+    for (int i = 0; i < 2 * h->NB; ++i) {
+        const int blk = i / 2;
+        const int t = (i & 1) ? h->t_blk[blk].w2 : h->t_blk[blk].w1;
+        hipError_t e = launch_pack_dgrad(h->params + h->poff[t], w->wdpack + (size_t)i * 9 * C * C, C, st);
+        if (e != hipSuccess) return set_error("train: pack_dgrad", e);
+    }
+    int32_t r;
+    switch (C) {
+        case 64: r = train_backward_t<64>(h, x, pis, zs, B, losses, st); break;
+        case 128: r = train_backward_t<128>(h, x, pis, zs, B, losses, st); break;
+        case 256: r = train_backward_t<256>(h, x, pis, zs, B, losses, st); break;
+        default: return set_error("train: bad channels", hipErrorInvalidValue);
+    }
+    h->dirty = true;   // running stats changed -> eval fold must be redone
+    return r;
+}
+
+int32_t train_apply(azg_pv* h, float* exp_avg, float* exp_avg_sq, int64_t step, float lr, float beta1, float beta2,
+                    float eps, float wd, float max_norm, float* total_norm, hipStream_t st)
+{
+    if (int32_t r = ensure_train_ws(h, 1, st)) return r;
+    TrainWS* w = ws_of(h);
+    const int64_t n = h->nparams;
+    const int nb = 1024;
+    int pr = prof_begin(h, AZG_PROF_TRAIN_OTHER, st);
+    hipLaunchKernelGGL(grad_sqsum_kernel, dim3(nb), dim3(256), 0, st, h->grads, n, w->npart);
+    AZG_CK(hipGetLastError(), "apply: grad_sqsum");
+    hipLaunchKernelGGL(grad_norm_finalize_kernel, dim3(1), dim3(256), 0, st, w->npart, nb, max_norm, w->scal,
+                       total_norm);
+    AZG_CK(hipGetLastError(), "apply: grad_norm_finalize");
+    const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+    const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+    const float lr_bc1 = (float)((double)lr / bc1);
+    const float bc2_sqrt = (float)std::sqrt(bc2);
+    hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, st, h->params, h->grads, exp_avg, exp_avg_sq,
+                       n, w->scal, lr_bc1, (float)(1.0 - (double)beta1), beta2, (float)(1.0 - (double)beta2),
+                       bc2_sqrt, eps, wd);
+    AZG_CK(hipGetLastError(), "apply: adam");
+    prof_end(h, pr, st);
+    h->dirty = true;
+    return 0;
+}
+
 }  // namespace azg
+
+namespace azg {
+__global__ void unpad_kernel(const float* __restrict__ src, float* __restrict__ dst, int M, int C)
+{
+    const int total = M * C;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const int m = i / C, c = i - m * C;
+        dst[i] = src[pad_off(m, C) + c];
+    }
+}
+}  // namespace azg
+
+extern "C" int32_t azg_pv_debug_copy(azg_pv* h, int32_t which, int32_t index, float* dst, int32_t batch,
+                                     void* stream)
+{
+    using namespace azg;
+    TrainWS* w = ws_of(h);
+    if (!w || batch > w->cap || !dst) return set_error("azg_pv_debug_copy: no train workspace / bad batch", hipSuccess);
+    const float* src = nullptr;
+    const bool blk = which >= 2 && which <= 5;
+    if (blk && (index < 0 || index >= h->NB)) return set_error("azg_pv_debug_copy: bad block index", hipSuccess);
+    switch (which) {
+        case 0: src = w->z0; break;
+        case 1: src = w->a0; break;
+        case 2: src = w->z1[index]; break;
+        case 3: src = w->hh[index]; break;
+        case 4: src = w->z2[index]; break;
+        case 5: src = w->xo[index]; break;
+        case 6: src = w->gX; break;
+        case 7: src = w->DZ; break;
+        case 8: src = w->DH; break;
+        case 9: src = w->GR; break;
+        case 10:
+            if (index < 0 || index >= (int)w->snap.size()) return set_error("azg_pv_debug_copy: no snapshot (AZG_DEBUG_SNAP)", hipSuccess);
+            src = w->snap[index];
+            break;
+        case 11: case 12: case 13: {   // head features, raw: fp [B][450], fv [B][225], hv [B][64]
+            const float* hs = which == 11 ? w->fp : which == 12 ? w->fv : w->hv;
+            const size_t n = (size_t)batch * (which == 11 ? 2 * PIX : which == 12 ? PIX : VHID);
+            hipError_t e = hipMemcpyAsync(dst, hs, n * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream);
+            return e == hipSuccess ? 0 : set_error("azg_pv_debug_copy", e);
+        }
+        default: return set_error("azg_pv_debug_copy: bad buffer id", hipSuccess);
+    }
+    const int M = batch * PIX;
+    hipLaunchKernelGGL(unpad_kernel, dim3(grid_for((int64_t)M * h->C)), dim3(256), 0, (hipStream_t)stream, src, dst,
+                       M, h->C);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : set_error("azg_pv_debug_copy", e);
+}
 
 extern "C" int32_t azg_pv_train_backward(azg_pv* h, const float* x, const float* pis, const float* zs,
                                          int32_t batch, float* losses, void* stream)
 {
-    (void)h; (void)x; (void)pis; (void)zs; (void)batch; (void)losses; (void)stream;
-    return azg::set_error("azg_pv_train_backward: not built yet", hipSuccess);
+    if (!h || !h->params || !h->grads) return azg::set_error("azg_pv_train_backward: handle not bound with grads", hipSuccess);
+    if (!x || !pis || !zs || !losses) return azg::set_error("azg_pv_train_backward: null argument", hipSuccess);
+    if (batch < 2) return azg::set_error("azg_pv_train_backward: batch must be >= 2 (train-mode BatchNorm)", hipSuccess);
+    return azg::train_backward(h, x, pis, zs, batch, losses, (hipStream_t)stream);
 }
 
 extern "C" int32_t azg_pv_train_apply(azg_pv* h, float* exp_avg, float* exp_avg_sq, int64_t step, float lr,
                                       float beta1, float beta2, float eps, float weight_decay, float max_norm,
                                       float* total_norm, void* stream)
 {
-    (void)h; (void)exp_avg; (void)exp_avg_sq; (void)step; (void)lr; (void)beta1; (void)beta2; (void)eps;
-    (void)weight_decay; (void)max_norm; (void)total_norm; (void)stream;
-    return azg::set_error("azg_pv_train_apply: not built yet", hipSuccess);
+    if (!h || !h->params || !h->grads) return azg::set_error("azg_pv_train_apply: handle not bound with grads", hipSuccess);
+    if (!exp_avg || !exp_avg_sq) return azg::set_error("azg_pv_train_apply: null moments", hipSuccess);
+    if (step < 1) return azg::set_error("azg_pv_train_apply: step must be >= 1", hipSuccess);
+    return azg::train_apply(h, exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps, weight_decay, max_norm, total_norm,
+                            (hipStream_t)stream);
 }

@@ -141,6 +141,23 @@ class PolicyValueEngine:
                                           ptr(total_norm), _stream(self.device)), self.lib)
 
     # -- instrumentation ----------------------------------------------------
+    DEBUG_BUFFERS = {"z0": 0, "a0": 1, "z1": 2, "h": 3, "z2": 4, "xo": 5, "gX": 6, "DZ": 7, "DH": 8, "GR": 9, "snap": 10}
+
+    HEAD_BUFFERS = {"fp": (11, 450), "fv": (12, 225), "hv": (13, 64)}
+
+    def debug_tensor(self, name: str, batch: int, index: int = 0) -> torch.Tensor:
+        """Interior [batch,15,15,C] of a train-workspace buffer from the last train step
+        (head features fp/fv/hv: [batch, n])."""
+        if name in self.HEAD_BUFFERS:
+            which, n = self.HEAD_BUFFERS[name]
+            out = torch.empty((batch, n), dtype=torch.float32, device=self.device)
+            check(self.lib.azg_pv_debug_copy(self.h, which, 0, ptr(out), batch, _stream(self.device)), self.lib)
+            return out
+        out = torch.empty((batch, 15, 15, self.channels), dtype=torch.float32, device=self.device)
+        check(self.lib.azg_pv_debug_copy(self.h, self.DEBUG_BUFFERS[name], index, ptr(out), batch,
+                                         _stream(self.device)), self.lib)
+        return out
+
     def profile_enable(self, on: bool = True):
         check(self.lib.azg_pv_profile_enable(self.h, 1 if on else 0), self.lib)
 

@@ -113,6 +113,16 @@ enum {
 int32_t azg_pv_profile_enable(azg_pv* h, int32_t enable);
 int32_t azg_pv_profile_read(azg_pv* h, double* ms, int64_t* launches);
 
+/* Debug/test access to train-workspace activations of the last train step:
+ * copies the interior [batch][15][15][C] (NHWC) of buffer `which` (block `index`
+ * where relevant) into dst (device, batch*225*C floats), stream-ordered.
+ * which: 0 z0 (stem conv out), 1 a0 (stem act), 2 z1[i], 3 h[i], 4 z2[i],
+ * 5 xo[i] (block out), 6 gX, 7 DZ, 8 DH, 9 GR, 10 gX snapshot i (env
+ * AZG_DEBUG_SNAP), and raw head features (no unpadding): 11 policy features
+ * [batch][450], 12 value features [batch][225], 13 value hidden [batch][64]. */
+int32_t azg_pv_debug_copy(azg_pv* h, int32_t which, int32_t index, float* dst,
+                          int32_t batch, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,159 @@
+"""GPU parity of the train step (azg_pv_train_backward + azg_pv_train_apply via
+PyTorchModel.train_batch) against the CPU oracle (autograd) and the reference
+goldens.
+
+Tolerances (fp32; stated per check):
+  * gradients: |g_gpu - g_ref| <= 1e-4 * max|g_ref| (per tensor) + 1e-7 -- fp32
+    backward through 7-13 BN layers with different summation orders;
+  * losses: 1e-5 relative;
+  * params after Adam: the reference itself is not reproducible across thread
+    counts here (sign of near-zero gradients decides +-lr): same gate as
+    tests/test_oracle_golden.py::check_train_state.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import golden_state, has_gpu, load_golden
+from oracle.boards import encode_batch, synth_positions, synth_targets
+from oracle.ref_net import RefModel, load_numpy_state, state_to_numpy
+from test_oracle_golden import check_train_state
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")]
+
+
+def make_model(blocks, ch, state=None, seed=0):
+    from network import PyTorchModel
+    torch.manual_seed(seed)
+    m = PyTorchModel(board_size=15, device="cuda", n_res_blocks=blocks, channels=ch)
+    if state is not None:
+        m.net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in state.items()})
+    return m
+
+
+def oracle_grads(ref, x, pi, z):
+    """network.py:213-222 up to loss.backward() (no clip, no step)."""
+    ref.net.train()
+    ref.optimizer.zero_grad()
+    logits, values = ref.net(torch.from_numpy(x))
+    pl = ref.policy_loss_fn(F.log_softmax(logits, dim=1), torch.from_numpy(pi))
+    vl = ref.value_loss_fn(values, torch.from_numpy(z))
+    (pl + vl).backward()
+    return ({n: p.grad.detach().numpy().copy() for n, p in ref.net.named_parameters()},
+            (float(pl), float(vl), float(pl + vl)))
+
+
+def gpu_masks(eng, blocks, B):
+    """0/1 ReLU masks of the GPU's own train-mode forward (NCHW / [B, n])."""
+    nchw = lambda t: (t > 0).double().permute(0, 3, 1, 2).cpu().numpy()
+    mk = {"a0": nchw(eng.debug_tensor("a0", B))}
+    for i in range(blocks):
+        mk[f"h{i}"] = nchw(eng.debug_tensor("h", B, i))
+        mk[f"xo{i}"] = nchw(eng.debug_tensor("xo", B, i))
+    for n in ("fp", "fv", "hv"):
+        mk[n] = (eng.debug_tensor(n, B) > 0).double().cpu().numpy()
+    return mk
+
+
+@pytest.mark.parametrize("tag,blocks,ch,B", [("3x64", 3, 64, 128), ("6x128", 6, 128, 128), ("3x64", 3, 64, 37)])
+def test_gradients_match_oracle(tag, blocks, ch, B):
+    """Gradients vs fp64 autograd with the GPU's ReLU masks (oracle.masked_grads_fp64):
+    |g_gpu - g_64| <= 2e-5 * max|g_64| + 1e-8 per tensor.  The fp32 CPU oracle (own
+    masks) is reported beside it: mask flips at near-zero pre-activations make two
+    correct fp32 implementations differ by up to ~1e-2 relative there."""
+    from oracle.ref_net import masked_grads_fp64
+    torch.set_num_threads(8)
+    g = load_golden(tag)
+    st = golden_state(g)
+    m = make_model(blocks, ch, st)
+    b, p = synth_positions(B, seed=77 + B)
+    x = encode_batch(b, p)
+    pi, z = synth_targets(B, seed=78 + B)
+    eng = m.engine
+    dev = eng.device
+    losses = torch.empty(3, device=dev)
+    eng.train_backward(torch.from_numpy(x).to(dev), torch.from_numpy(pi).to(dev), torch.from_numpy(z).to(dev),
+                       losses)
+    want, (pl, vl) = masked_grads_fp64(st, blocks, ch, x, pi, z, gpu_masks(eng, blocks, B))
+    np.testing.assert_allclose(losses.cpu().numpy(), [pl, vl, pl + vl], rtol=1e-5, atol=1e-7)
+    ref = RefModel(blocks, ch)
+    load_numpy_state(ref.net, st)
+    want32, _ = oracle_grads(ref, x, pi, z)
+    bad = []
+    for n, prm in m.net.named_parameters():
+        gg = prm.grad.detach().cpu().numpy().astype(np.float64)
+        w = want[n]
+        err, scale = np.abs(gg - w).max(), np.abs(w).max()
+        e32 = np.abs(want32[n] - w).max()
+        print(f"{tag} B={B} {n:28s} |gpu-64|={err:.2e} |cpu32-64|={e32:.2e} max|g|={scale:.2e} "
+              f"rel={err / (scale + 1e-30):.1e}")
+        if err > 2e-5 * scale + 1e-8:
+            bad.append(n)
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("tag,blocks,ch", [("3x64", 3, 64), ("6x128", 6, 128)])
+def test_train_batch_matches_reference_goldens(tag, blocks, ch):
+    g = load_golden(tag)
+    m = make_model(blocks, ch, golden_state(g))
+    losses = []
+    for s in range(2):
+        x = encode_batch(g[f"train/boards{s}"], g[f"train/players{s}"])
+        li = m.train_batch(x, g[f"train/pi{s}"], g[f"train/z{s}"])
+        losses.append([li["policy_loss"], li["value_loss"], li["total_loss"]])
+    np.testing.assert_allclose(np.array(losses), g["train/losses"], rtol=1e-5, atol=1e-6)
+    check_train_state(m, g)
+    sd = m.net.state_dict()
+    for k in sd:
+        if "running" in k or "num_batches" in k:
+            np.testing.assert_allclose(sd[k].cpu().numpy(), g[f"train/buf/{k}"], atol=1e-4, rtol=1e-3, err_msg=k)
+    assert int(sd["bn.num_batches_tracked"]) == int(g["train/buf/bn.num_batches_tracked"])
+    # optimizer state in torch format
+    osd = m.optimizer.state_dict()
+    assert len(osd["state"]) == len(list(m.net.parameters()))
+    assert float(osd["state"][0]["step"]) == 2.0
+
+
+def test_clip_and_adam_match_torch():
+    """azg_pv_train_apply == clip_grad_norm_(3.0) + torch Adam on identical grads,
+    including a clipping case (grads scaled up) and weight decay."""
+    m = make_model(1, 64)
+    eng = m.engine
+    torch.manual_seed(3)
+    params0 = eng.flat_params.detach().cpu().clone()
+    for scale in (1e-3, 10.0):
+        grads = torch.randn(eng.nparam) * scale
+        eng.flat_grads.copy_(grads.to(eng.device))
+        m.optimizer.hip_step(3.0)
+        torch.cuda.synchronize()
+    # torch reference on CPU
+    p = torch.nn.Parameter(params0.clone())
+    opt = torch.optim.Adam([p], lr=1e-3, weight_decay=1e-4)
+    torch.manual_seed(3)
+    for scale in (1e-3, 10.0):
+        p.grad = torch.randn(eng.nparam) * scale
+        torch.nn.utils.clip_grad_norm_([p], 3.0)
+        opt.step()
+    got = eng.flat_params.detach().cpu()
+    np.testing.assert_allclose(got.numpy(), p.detach().numpy(), atol=2e-6, rtol=0)
+    st = opt.state[p]
+    np.testing.assert_allclose(m.optimizer.flat_exp_avg.cpu().numpy(), st["exp_avg"].numpy(), rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(m.optimizer.flat_exp_avg_sq.cpu().numpy(), st["exp_avg_sq"].numpy(), rtol=1e-5,
+                               atol=1e-12)
+
+
+def test_train_then_predict_uses_new_weights():
+    m = make_model(2, 64)
+    b, p = synth_positions(64, seed=5)
+    x = encode_batch(b, p)
+    pi, z = synth_targets(64, seed=6)
+    p0, _ = m.predict(x)
+    m.train_batch(x, pi, z, epochs=3)
+    p1, v1 = m.predict(x)
+    ref = RefModel(2, 64)
+    load_numpy_state(ref.net, state_to_numpy(m.net))
+    rp, rv = ref.predict(x)
+    assert not np.allclose(p0, p1)
+    np.testing.assert_allclose(p1, rp, atol=1e-5)
+    np.testing.assert_allclose(v1, rv, atol=1e-5)

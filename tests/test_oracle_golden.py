@@ -61,8 +61,11 @@ def check_train_state(m, g, lr=1e-3, steps=2):
     """Adam makes the sign of near-zero gradients decide a +-lr update, so the
     reference is not reproducible across thread counts: oracle(1 or 4 threads)
     vs reference(8 threads) differs by up to 7e-4 on 0.02-0.4 % of elements
-    (measured).  Gate: moments tight, >= 99 % of params within 2e-5, and every
-    param within the largest change two disagreeing Adam steps can make."""
+    (measured).  ReLU masks flip the same way at near-zero pre-activations (GPU vs
+    CPU fp32: a few 1e-3 relative on whole-tensor sums, see tests/test_gpu_train.py).
+    Gate: moments within 5e-3 (m) / 1e-2 (v, squared) relative, >= 99 % of params
+    within 2e-5, and every param within the largest change two disagreeing Adam
+    steps can make."""
     bad = tot = 0
     for n, p in m.net.named_parameters():
         idx = g[f"train/idx/{n}"]
@@ -73,9 +76,9 @@ def check_train_state(m, g, lr=1e-3, steps=2):
         tot += d.size
         st = m.optimizer.state[p]
         ea = st["exp_avg"].reshape(-1).cpu().numpy()[idx]
-        np.testing.assert_allclose(ea, g[f"train/exp_avg/{n}"], atol=2e-5, rtol=1e-3, err_msg=n)
+        np.testing.assert_allclose(ea, g[f"train/exp_avg/{n}"], atol=2e-5, rtol=5e-3, err_msg=n)
         es = st["exp_avg_sq"].reshape(-1).cpu().numpy()[idx]
-        np.testing.assert_allclose(es, g[f"train/exp_avg_sq/{n}"], atol=1e-8, rtol=1e-3, err_msg=n)
+        np.testing.assert_allclose(es, g[f"train/exp_avg_sq/{n}"], atol=1e-8, rtol=1e-2, err_msg=n)
     assert bad <= 0.01 * tot, (bad, tot)
 
 
