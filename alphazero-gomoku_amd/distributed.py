@@ -1,0 +1,101 @@
+"""One process per GPU, torch.distributed over RCCL ("nccl" backend on ROCm) or
+gloo on CPU.  Used in exactly two places:
+
+  * self-play: games are sharded across ranks (independent replicas, no
+    per-move communication);
+  * training: data-parallel step with ONE all-reduce (average) of the flat fp32
+    gradient buffer between backward and clip+Adam, so the clip sees the global
+    gradient; BN running stats are averaged once per iteration; weights and Adam
+    moments are broadcast from rank 0 when replicas must agree.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+def world() -> int:
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def rank() -> int:
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def init_from_env(backend: Optional[str] = None) -> tuple:
+    """Initialise from torchrun env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).
+    Returns (rank, world, local_rank, device)."""
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    r = int(os.environ.get("RANK", "0"))
+    lr = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    device = torch.device("cuda", lr) if use_gpu else torch.device("cpu")
+    if use_gpu:
+        torch.cuda.set_device(device)
+    if ws > 1 and not dist.is_initialized():
+        backend = backend or ("nccl" if use_gpu else "gloo")
+        if backend == "nccl":
+            dist.init_process_group(backend, device_id=device)
+        else:
+            dist.init_process_group(backend)
+    return r, ws, lr, device
+
+
+def allreduce_mean_(t: torch.Tensor) -> torch.Tensor:
+    """In-place average across ranks (SUM then scale: gloo has no AVG)."""
+    n = world()
+    if n > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t.div_(n)
+    return t
+
+
+def allreduce_sum_(t: torch.Tensor) -> torch.Tensor:
+    if world() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t
+
+
+def allreduce_min_int(v: int, device) -> int:
+    if world() == 1:
+        return int(v)
+    t = torch.tensor([int(v)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return int(t.item())
+
+
+def grad_hook():
+    """Hook for PyTorchModel.grad_hook: average the flat gradient buffer."""
+    return allreduce_mean_
+
+
+def broadcast_model(model, src: int = 0) -> None:
+    """Make every replica identical to `src`: params, BN stats and counters, Adam moments."""
+    if world() == 1:
+        return
+    eng = model.engine
+    for t in (eng.flat_params, eng.flat_bn, eng.flat_nbt):
+        dist.broadcast(t, src)
+    opt = model.optimizer
+    dist.broadcast(opt.flat_exp_avg, src)
+    dist.broadcast(opt.flat_exp_avg_sq, src)
+    eng.mark_dirty()
+
+
+def sync_bn_stats(model) -> None:
+    """Average BN running statistics (each rank saw its own local batches)."""
+    if world() > 1:
+        allreduce_mean_(model.engine.flat_bn)
+        model.engine.mark_dirty()
+
+
+def shard(n: int, r: Optional[int] = None, w: Optional[int] = None) -> range:
+    """Contiguous share of n items for rank r (sizes differ by at most one)."""
+    r = rank() if r is None else r
+    w = world() if w is None else w
+    base, extra = divmod(n, w)
+    start = r * base + min(r, extra)
+    return range(start, start + base + (1 if r < extra else 0))

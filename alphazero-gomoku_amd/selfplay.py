@@ -79,20 +79,22 @@ def play_game_and_collect(mcts, game, temp_fn, max_moves=225, use_symmetries=Tru
 class BatchedSelfPlay:
     """Advance many search generators together, one device forward per round.
 
-    ``model`` is a PyTorchModel (HIP engine).  Statistics: ``boards`` (leaf boards
-    evaluated), ``forwards`` (device calls), ``nn_seconds`` (time inside forward,
-    including H2D/D2H)."""
+    ``model`` is a PyTorchModel (HIP engine), or a dict {tag: model} when the
+    generators yield tagged requests (tag, X) -- e.g. evaluation games where two
+    networks play each other; requests are then batched per tag.
+    Statistics: ``boards`` (leaf boards evaluated), ``forwards`` (device calls),
+    ``nn_seconds`` (time inside forward incl. H2D/D2H), ``max_batch``."""
 
     def __init__(self, model):
-        self.model = model
+        self.models = model if isinstance(model, dict) else {None: model}
         self.boards = 0
         self.forwards = 0
         self.nn_seconds = 0.0
         self.max_batch = 0
 
-    def _evaluate(self, X: np.ndarray):
+    def _evaluate(self, tag, X: np.ndarray):
         t0 = time.perf_counter()
-        probs, values = self.model.predict(X)
+        probs, values = self.models[tag].predict(X)
         self.nn_seconds += time.perf_counter() - t0
         self.boards += len(X)
         self.forwards += 1
@@ -100,6 +102,7 @@ class BatchedSelfPlay:
         return probs, values
 
     def run(self, gens: list) -> list:
+        tagged = None not in self.models
         results = [None] * len(gens)
         pending = {}
         for i, g in enumerate(gens):
@@ -108,13 +111,19 @@ class BatchedSelfPlay:
             except StopIteration as stop:
                 results[i] = stop.value
         while pending:
-            order = list(pending)
-            sizes = [len(pending[i]) for i in order]
-            probs, values = self._evaluate(np.concatenate([pending[i] for i in order], axis=0))
-            off = 0
-            for i, n in zip(order, sizes):
-                reply = (probs[off:off + n], values[off:off + n])
-                off += n
+            groups = {}
+            for i, req in pending.items():
+                tag, X = req if tagged else (None, req)
+                groups.setdefault(tag, []).append((i, X))
+            replies = {}
+            for tag, items in groups.items():
+                probs, values = self._evaluate(tag, np.concatenate([X for _, X in items], axis=0))
+                off = 0
+                for i, X in items:
+                    n = len(X)
+                    replies[i] = (probs[off:off + n], values[off:off + n])
+                    off += n
+            for i, reply in replies.items():
                 try:
                     pending[i] = gens[i].send(reply)
                 except StopIteration as stop:

@@ -1,0 +1,97 @@
+"""Multi-process (world_size 2, gloo on CPU) tests of the data-parallel plumbing
+in alphazero-gomoku_amd/distributed.py and of the DP train-step semantics:
+per-rank local batch (own BN batch stats) -> all-reduce(mean) of the flat
+gradient -> global-norm clip -> replicated Adam.  The per-rank gradients come from
+the CPU oracle (no GPU here); the product's GPU path plugs the same helpers in as
+PyTorchModel.grad_hook between azg_pv_train_backward and azg_pv_train_apply."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+import torch.nn.functional as F
+
+from conftest import PKG, REPO
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+    sys.path[:0] = [REPO, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import distributed as D
+    from oracle.boards import encode_batch, synth_positions, synth_targets
+    from oracle.ref_net import RefModel
+
+    torch.set_num_threads(1)
+    r, w, _, dev = D.init_from_env(backend="gloo")
+    assert (r, w, dev.type) == (rank, world, "cpu")
+    # plumbing
+    t = torch.full((5,), float(rank + 1))
+    D.allreduce_mean_(t)
+    assert torch.allclose(t, torch.full((5,), 1.5))
+    assert D.allreduce_min_int(10 + rank, dev) == 10
+    sh = D.shard(7)
+    assert len(sh) == (4 if rank == 0 else 3)
+
+    # DP train step: identical init on all ranks, different local shards
+    torch.manual_seed(0)
+    ref = RefModel(1, 64)
+    params = list(ref.net.parameters())
+    b, p = synth_positions(32, seed=100 + rank)
+    x = torch.from_numpy(encode_batch(b, p))
+    pi, z = (torch.from_numpy(a) for a in synth_targets(32, seed=200 + rank))
+    ref.net.train()
+    logits, v = ref.net(x)
+    loss = F.kl_div(F.log_softmax(logits, 1), pi, reduction="batchmean") + F.mse_loss(v, z)
+    loss.backward()
+    flat = torch.cat([q.grad.reshape(-1) for q in params])
+    np.save(os.path.join(out_dir, f"local_grad{rank}.npy"), flat.numpy())
+    D.allreduce_mean_(flat)                               # the DP exchange
+    o = 0
+    for q in params:
+        q.grad.copy_(flat[o:o + q.numel()].view_as(q))
+        o += q.numel()
+    torch.nn.utils.clip_grad_norm_(params, 3.0)           # clip sees the GLOBAL grad
+    ref.optimizer.step()
+    np.save(os.path.join(out_dir, f"params{rank}.npy"), torch.cat([q.detach().reshape(-1) for q in params]).numpy())
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_dp_step_world2_gloo(tmp_path):
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    p0, p1 = (np.load(tmp_path / f"params{r}.npy") for r in range(2))
+    assert np.array_equal(p0, p1)                          # replicas stay identical
+    # single-process restatement: mean of the two local grads -> clip -> Adam
+    g = (np.load(tmp_path / "local_grad0.npy") + np.load(tmp_path / "local_grad1.npy")) / 2
+    from oracle.ref_net import RefModel
+    torch.manual_seed(0)
+    ref = RefModel(1, 64)
+    params = list(ref.net.parameters())
+    gt = torch.from_numpy(g.astype(np.float32))
+    o = 0
+    for q in params:
+        q.grad = gt[o:o + q.numel()].view_as(q).clone()
+        o += q.numel()
+    torch.nn.utils.clip_grad_norm_(params, 3.0)
+    ref.optimizer.step()
+    want = torch.cat([q.detach().reshape(-1) for q in params]).numpy()
+    np.testing.assert_allclose(p0, want, atol=1e-6, rtol=0)
+
+
+def test_shard_covers_everything():
+    import distributed as D
+    for n in (0, 1, 7, 256):
+        for w in (1, 2, 3, 8):
+            seen = [i for r in range(w) for i in D.shard(n, r, w)]
+            assert seen == list(range(n))

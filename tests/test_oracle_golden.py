@@ -57,7 +57,7 @@ def test_oracle_train_step_matches_reference(tag, blocks, ch):
             np.testing.assert_allclose(sd[k].numpy(), g[f"train/buf/{k}"], atol=1e-4, rtol=1e-3, err_msg=k)
 
 
-def check_train_state(m, g, lr=1e-3, steps=2):
+def check_train_state(m, g, lr=1e-3, steps=2, max_bad_frac=0.01):
     """Adam makes the sign of near-zero gradients decide a +-lr update, so the
     reference is not reproducible across thread counts: oracle(1 or 4 threads)
     vs reference(8 threads) differs by up to 7e-4 on 0.02-0.4 % of elements
@@ -79,7 +79,7 @@ def check_train_state(m, g, lr=1e-3, steps=2):
         np.testing.assert_allclose(ea, g[f"train/exp_avg/{n}"], atol=2e-5, rtol=5e-3, err_msg=n)
         es = st["exp_avg_sq"].reshape(-1).cpu().numpy()[idx]
         np.testing.assert_allclose(es, g[f"train/exp_avg_sq/{n}"], atol=1e-8, rtol=1e-2, err_msg=n)
-    assert bad <= 0.01 * tot, (bad, tot)
+    assert bad <= max_bad_frac * tot, (bad, tot)
 
 
 def test_param_counts():
