@@ -38,6 +38,7 @@ _SIGS = {
                                             _P, _P]),
     "azg_pv_profile_enable": (ctypes.c_int32, [_P, ctypes.c_int32]),
     "azg_pv_profile_read": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
+    "azg_pv_set_tuning": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32]),
     "azg_pv_debug_copy": (ctypes.c_int32, [_P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32, _P]),
 }
 EXPORTS = tuple(_SIGS)

@@ -255,6 +255,8 @@ void free_workspace(azg_pv* h)
         if (h->act[i]) (void)hipFree(h->act[i]);
         h->act[i] = nullptr;
     }
+    if (h->hbuf) (void)hipFree(h->hbuf);
+    h->hbuf = nullptr;
     h->act_cap = 0;
     free_train_workspace(h);
 }
@@ -268,7 +270,13 @@ int32_t ensure_eval_workspace(azg_pv* h, int batch, hipStream_t st)
         if (h->act[i]) (void)hipFree(h->act[i]);
         h->act[i] = nullptr;
     }
+    if (h->hbuf) (void)hipFree(h->hbuf);
+    h->hbuf = nullptr;
     h->act_cap = 0;
+    {
+        hipError_t e = hipMalloc(&h->hbuf, (size_t)cap * 3 * PIX * sizeof(float));
+        if (e != hipSuccess) return fail("ensure_eval_workspace: hipMalloc(head features)", e);
+    }
     const size_t bytes = (size_t)cap * PADPIX * h->C * sizeof(float);
     for (int i = 0; i < 3; ++i) {
         hipError_t e = hipMalloc(&h->act[i], bytes);
@@ -333,7 +341,8 @@ int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* 
     pr = prof_begin(h, AZG_PROF_HEADS, st);
     AZG_TRY(launch_heads_fwd(C, X, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], h->scale + ho, h->shift + ho,
                              h->wpfT, P + h->poff[h->t_pfc_b], h->wv1T, P + h->poff[h->t_vfc1_b],
-                             P + h->poff[h->t_vfc2_w], P + h->poff[h->t_vfc2_b], probs, values, logits, batch, st),
+                             P + h->poff[h->t_vfc2_w], P + h->poff[h->t_vfc2_b], h->hbuf, probs, values, logits,
+                             batch, st),
             "forward: heads");
     prof_end(h, pr, st);
     return 0;

@@ -20,18 +20,24 @@
 //
 // Lane l of an MFMA step s uses K index h*16+s (h = l>>5) for both A and B, so
 // each lane's 16 A values and 16 B values of a chunk are contiguous in LDS.
-#include "pv_common.h"
+#include "pv_internal.h"
+
+#include <map>
+#include <utility>
 
 namespace azg {
 
 // Tile shape: BM = WM*TM*32 pixels x BN channels; 4 waves as WM x WN (WN = 4/WM),
 // each wave TM x TN accumulators of 32x32.  Several shapes are compiled; the host
 // picks the one that balances the tile count over the 256 CUs best (pick_tile).
-template <int C, int BN_, int WM_, int TM_>
+template <int C, int BN_, int WM_, int TM_, int NW_ = 4>
 struct ConvTile {
+    static constexpr int NW = NW_;                // waves per workgroup
+    static constexpr int NT = 64 * NW_;           // threads
+    static constexpr int RPP = NT / 8;            // staging rows per pass (8 x 16 B per row)
     static constexpr int BN = BN_;
     static constexpr int WM = WM_;
-    static constexpr int WN = 4 / WM_;
+    static constexpr int WN = NW_ / WM_;
     static constexpr int TM = TM_;
     static constexpr int TN = BN_ / (WN * 32);
     static constexpr int BM = WM * TM * 32;
@@ -39,19 +45,24 @@ struct ConvTile {
     static constexpr int LDK = BK;          // unpadded rows; XOR-swizzled 16-B chunks
     static constexpr int CG = C / BK;
     static constexpr int NCH = 9 * CG;
-    static constexpr int A_LD = BM * BK / 4 / 256;
-    static constexpr int B_LD = BN * BK / 4 / 256;
+    static constexpr int A_LD = BM * BK / 4 / NT;
+    static constexpr int B_LD = BN * BK / 4 / NT;
     static constexpr int LDS_BYTES = 2 * (BM + BN) * LDK * 4;
     static_assert(TN >= 1 && WN * TN * 32 == BN, "bad tile");
+    static_assert(A_LD >= 1 && B_LD >= 1 && A_LD * NT * 4 == BM * BK && B_LD * NT * 4 == BN * BK, "bad staging");
 };
 
-template <int C, int BN_, int WM_, int TM_, int EPI>
-__global__ __launch_bounds__(256, 2) void conv3x3_mfma(
+// ABL (ablation, timing studies only; 0 in every product launch): bit 1 skips the
+// global loads, bit 2 replaces LDS fragment reads by register values, bit 4 drops
+// the per-chunk barrier.  Results are garbage when ABL != 0.
+template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, int ABL = 0>
+__global__ __launch_bounds__(64 * NW_, NW_ / 2) void conv3x3_mfma(
     const float* __restrict__ in, const float* __restrict__ wp,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ resid, float* __restrict__ out, int M)
 {
-    using T = ConvTile<C, BN_, WM_, TM_>;
+    using T = ConvTile<C, BN_, WM_, TM_, NW_>;
+    constexpr int RPP = T::RPP;
     constexpr int BM = T::BM, BN = T::BN, BK = T::BK, LDK = T::LDK;
     constexpr int CG = T::CG, NCH = T::NCH, WN = T::WN, TM = T::TM, TN = T::TN;
     constexpr int A_LD = T::A_LD, B_LD = T::B_LD;
@@ -66,12 +77,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(
     const int m0 = blockIdx.x * BM;
     const int n0 = blockIdx.y * BN;
 
-    // staging: thread -> (row sr + 32 i, floats sc..sc+3)
+    // staging: thread -> (row sr + RPP i, floats sc..sc+3)
     const int sr = tid >> 3, sc = (tid & 7) * 4;
     int abase[A_LD];
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
-        int m = m0 + sr + 32 * i;
+        int m = m0 + sr + RPP * i;
         m = m < M ? m : M - 1;           // tail rows: clamp to a valid pixel, never stored
         abase[i] = pad_off(m, C) + sc;
     }
@@ -79,6 +90,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(
 
     f32x4 ra[A_LD], rb[B_LD];
     auto gload = [&](int kc) {
+        if (ABL & 1) return;
         const int tap = kc / CG, cg = kc - tap * CG;
         const int ky = tap / 3, kx = tap - ky * 3;
         const int toff = ((ky - 1) * PADW + (kx - 1)) * C + cg * BK;
@@ -86,7 +98,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(
         for (int i = 0; i < A_LD; ++i) ra[i] = *(const f32x4*)(in + abase[i] + toff);
         const float* wk = wsrc + (size_t)kc * C * BK;
 #pragma unroll
-        for (int i = 0; i < B_LD; ++i) rb[i] = *(const f32x4*)(wk + 32 * i * BK);
+        for (int i = 0; i < B_LD; ++i) rb[i] = *(const f32x4*)(wk + RPP * i * BK);
     };
     // 16-B chunk c of LDS row r is stored at chunk c ^ ((r >> 1) & 7): the 16 rows a
     // ds_read_b128 lane group touches land on 16 distinct 4-bank slots.
@@ -95,9 +107,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(
         float* a = As + buf * BM * LDK;
         float* b = Bs + buf * BN * LDK;
 #pragma unroll
-        for (int i = 0; i < A_LD; ++i) *(f32x4*)(a + (sr + 32 * i) * LDK + wchunk) = ra[i];
+        for (int i = 0; i < A_LD; ++i) *(f32x4*)(a + (sr + RPP * i) * LDK + wchunk) = ra[i];
 #pragma unroll
-        for (int i = 0; i < B_LD; ++i) *(f32x4*)(b + (sr + 32 * i) * LDK + wchunk) = rb[i];
+        for (int i = 0; i < B_LD; ++i) *(f32x4*)(b + (sr + RPP * i) * LDK + wchunk) = rb[i];
     };
 
     f32x16 acc[TM][TN];
@@ -142,10 +154,17 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(
             for (int q = 0; q < 4; ++q) {
                 f32x4 a[TM], b[TN];
                 const int rc = ((h * 4 + q) ^ swz) * 4;
+                if (ABL & 2) {
 #pragma unroll
-                for (int i = 0; i < TM; ++i) a[i] = *(const f32x4*)(Ab + arow + i * 32 * LDK + rc);
+                    for (int i = 0; i < TM; ++i) a[i] = f32x4{(float)kc, (float)q, (float)i, 1.f};
 #pragma unroll
-                for (int j = 0; j < TN; ++j) b[j] = *(const f32x4*)(Bb + brow + j * 32 * LDK + rc);
+                    for (int j = 0; j < TN; ++j) b[j] = f32x4{(float)q, (float)kc, 1.f, (float)j};
+                } else {
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) a[i] = *(const f32x4*)(Ab + arow + i * 32 * LDK + rc);
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) b[j] = *(const f32x4*)(Bb + brow + j * 32 * LDK + rc);
+                }
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -155,7 +174,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(
                             at[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], at[i][j], 0, 0, 0);
             }
             if (kc + 1 < NCH) lstore(cur ^ 1);
-            __syncthreads();
+            if (!(ABL & 4)) __syncthreads();
         }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -245,39 +264,50 @@ __global__ __launch_bounds__(256) void stem_conv(
 
 // ---- host launchers ------------------------------------------------------
 
-template <int C, int BN, int WM, int TM, int EPI>
+template <int C, int BN, int WM, int TM, int NW, int EPI>
 static hipError_t launch_conv_t(const float* in, const float* wp, const float* scale, const float* shift,
                                 const float* resid, float* out, int M, hipStream_t st)
 {
-    using T = ConvTile<C, BN, WM, TM>;
+    using T = ConvTile<C, BN, WM, TM, NW>;
     static bool attr_done = false;
     if (!attr_done) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_mfma<C, BN, WM, TM, EPI>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_mfma<C, BN, WM, TM, NW, EPI>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS_BYTES);
         if (e != hipSuccess) return e;
         attr_done = true;
     }
     dim3 grid((M + T::BM - 1) / T::BM, C / T::BN);
-    hipLaunchKernelGGL((conv3x3_mfma<C, BN, WM, TM, EPI>), grid, dim3(256), T::LDS_BYTES, st,
+    hipLaunchKernelGGL((conv3x3_mfma<C, BN, WM, TM, NW, EPI>), grid, dim3(T::NT), T::LDS_BYTES, st,
                        in, wp, scale, shift, resid, out, M);
     return hipGetLastError();
 }
 
-template <int C, int BN, int WM, int TM>
+template <int C, int BN, int WM, int TM, int NW = 4>
 static hipError_t launch_conv_epi(int epi, const float* in, const float* wp, const float* scale, const float* shift,
                                   const float* resid, float* out, int M, hipStream_t st)
 {
     switch (epi) {
-        case EPI_BN_RELU: return launch_conv_t<C, BN, WM, TM, EPI_BN_RELU>(in, wp, scale, shift, resid, out, M, st);
-        case EPI_BN_RES_RELU: return launch_conv_t<C, BN, WM, TM, EPI_BN_RES_RELU>(in, wp, scale, shift, resid, out, M, st);
-        case EPI_ADD: return launch_conv_t<C, BN, WM, TM, EPI_ADD>(in, wp, scale, shift, resid, out, M, st);
-        default: return launch_conv_t<C, BN, WM, TM, EPI_RAW>(in, wp, scale, shift, resid, out, M, st);
+        case EPI_BN_RELU: return launch_conv_t<C, BN, WM, TM, NW, EPI_BN_RELU>(in, wp, scale, shift, resid, out, M, st);
+        case EPI_BN_RES_RELU: return launch_conv_t<C, BN, WM, TM, NW, EPI_BN_RES_RELU>(in, wp, scale, shift, resid, out, M, st);
+        case EPI_ADD: return launch_conv_t<C, BN, WM, TM, NW, EPI_ADD>(in, wp, scale, shift, resid, out, M, st);
+        default: return launch_conv_t<C, BN, WM, TM, NW, EPI_RAW>(in, wp, scale, shift, resid, out, M, st);
     }
 }
 
 // Tile shapes {BM, BN}: index into the switch below.
 struct TileShape { int bm, bn; };
-static const TileShape kShapes[] = {{128, 128}, {96, 128}, {160, 128}, {64, 128}, {128, 64}, {64, 64}};
+// 0-5: 4 waves; 6-9: 8 waves (more waves per SIMD at the same LDS footprint).
+static const TileShape kShapes[] = {{128, 128}, {96, 128}, {160, 128}, {64, 128}, {128, 64}, {64, 64},
+                                    {128, 128}, {128, 128}, {128, 64}, {64, 128}};
+constexpr int kNumShapes = (int)(sizeof(kShapes) / sizeof(kShapes[0]));
+constexpr int kNumAutoShapes = 6;   // heuristic pick_conv_tile only considers 0-5
+
+static bool shape_ok(int shape, int C)
+{
+    if (shape < 0 || shape >= kNumShapes) return false;
+    if (C == 64) return shape == 4 || shape == 5 || shape == 8;
+    return true;
+}
 constexpr int kNumCUs = 256;
 
 // Pick the shape that wastes the fewest workgroup slots: 2 workgroups fit per CU
@@ -287,7 +317,7 @@ int pick_conv_tile(int C, int M)
 {
     int best = -1;
     double best_eff = -1.0;
-    for (int i = 0; i < (int)(sizeof(kShapes) / sizeof(kShapes[0])); ++i) {
+    for (int i = 0; i < kNumAutoShapes; ++i) {
         const int bm = kShapes[i].bm, bn = kShapes[i].bn;
         if (bn > C) continue;
         if (C == 64 && !(bm == 128 || bm == 64)) continue;
@@ -312,6 +342,10 @@ hipError_t launch_conv3x3_shape(int shape, int C, int epi, const float* in, cons
         case 3: return launch_conv_epi<CC, 128, 2, 1>(epi, in, wp, scale, shift, resid, out, M, st);            \
         case 4: return launch_conv_epi<CC, 64, 2, 2>(epi, in, wp, scale, shift, resid, out, M, st);             \
         case 5: return launch_conv_epi<CC, 64, 2, 1>(epi, in, wp, scale, shift, resid, out, M, st);             \
+        case 6: return launch_conv_epi<CC, 128, 2, 2, 8>(epi, in, wp, scale, shift, resid, out, M, st);         \
+        case 7: return launch_conv_epi<CC, 128, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);         \
+        case 8: return launch_conv_epi<CC, 64, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);          \
+        case 9: return launch_conv_epi<CC, 128, 2, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);         \
         default: return hipErrorInvalidValue;                                                                   \
     }
     switch (C) {
@@ -320,6 +354,7 @@ hipError_t launch_conv3x3_shape(int shape, int C, int epi, const float* in, cons
                 case 0: return launch_conv_epi<64, 64, 2, 2>(epi, in, wp, scale, shift, resid, out, M, st);
                 case 5: return launch_conv_epi<64, 64, 2, 1>(epi, in, wp, scale, shift, resid, out, M, st);
                 case 4: return launch_conv_epi<64, 64, 2, 2>(epi, in, wp, scale, shift, resid, out, M, st);
+                case 8: return launch_conv_epi<64, 64, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);
                 default: return hipErrorInvalidValue;
             }
         case 128: AZG_SHAPES(128)
@@ -329,12 +364,102 @@ hipError_t launch_conv3x3_shape(int shape, int C, int epi, const float* in, cons
 #undef AZG_SHAPES
 }
 
+int g_conv_shape_override = -1;
+int g_conv_autotune = 1;
+int g_conv_ablation = 0;
+
+template <int ABL>
+static hipError_t launch_ablation(const float* in, const float* wp, const float* scale, const float* shift,
+                                  const float* resid, float* out, int M, hipStream_t st)
+{
+    using T = ConvTile<128, 128, 1, 5, 4>;
+    (void)hipFuncSetAttribute((const void*)conv3x3_mfma<128, 128, 1, 5, 4, EPI_BN_RELU, ABL>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS_BYTES);
+    dim3 grid((M + T::BM - 1) / T::BM, 1);
+    hipLaunchKernelGGL((conv3x3_mfma<128, 128, 1, 5, 4, EPI_BN_RELU, ABL>), grid, dim3(T::NT), T::LDS_BYTES, st,
+                       in, wp, scale, shift, resid, out, M);
+    return hipGetLastError();
+}
+
+// timing-only: shape 2 (160x128) with ablation mask g_conv_ablation (C = 128 only)
+static hipError_t launch_ablated(const float* in, const float* wp, const float* scale, const float* shift,
+                                 const float* resid, float* out, int M, hipStream_t st)
+{
+    switch (g_conv_ablation) {
+        case 1: return launch_ablation<1>(in, wp, scale, shift, resid, out, M, st);
+        case 2: return launch_ablation<2>(in, wp, scale, shift, resid, out, M, st);
+        case 3: return launch_ablation<3>(in, wp, scale, shift, resid, out, M, st);
+        case 4: return launch_ablation<4>(in, wp, scale, shift, resid, out, M, st);
+        case 7: return launch_ablation<7>(in, wp, scale, shift, resid, out, M, st);
+        default: return launch_ablation<0>(in, wp, scale, shift, resid, out, M, st);
+    }
+}
+
+// Autotune: the first launch for a (C, M) times every valid shape twice on the
+// real operands (each launch fully rewrites `out`, so this is idempotent) and
+// caches the fastest.  All shapes give bitwise-identical results (the K order is
+// shape-independent), so tuning never changes numerics.  Skipped while the
+// stream is being captured into a graph (falls back to pick_conv_tile).
+static std::map<std::pair<int, int>, int>& tune_cache()
+{
+    static std::map<std::pair<int, int>, int> c;
+    return c;
+}
+
+static int autotune_shape(int C, int epi, const float* in, const float* wp, const float* scale, const float* shift,
+                          const float* resid, float* out, int M, hipStream_t st)
+{
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return -1;
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess) return -1;
+    if (hipEventCreate(&e1) != hipSuccess) { (void)hipEventDestroy(e0); return -1; }
+    int best = -1;
+    float best_ms = 1e30f;
+    for (int s = 0; s < kNumShapes; ++s) {
+        if (!shape_ok(s, C)) continue;
+        if (launch_conv3x3_shape(s, C, epi, in, wp, scale, shift, resid, out, M, st) != hipSuccess) continue;
+        (void)hipEventRecord(e0, st);
+        if (launch_conv3x3_shape(s, C, epi, in, wp, scale, shift, resid, out, M, st) != hipSuccess) continue;
+        (void)hipEventRecord(e1, st);
+        if (hipEventSynchronize(e1) != hipSuccess) continue;
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        if (ms < best_ms) { best_ms = ms; best = s; }
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipGetLastError();
+    return best;
+}
+
 hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, const float* scale,
                           const float* shift, const float* resid, float* out, int M, hipStream_t st)
 {
-    int shape = pick_conv_tile(C, M);
-    if (C == 64 && shape == 3) shape = 5;
+    if (g_conv_ablation > 0 && C == 128 && epi == EPI_BN_RELU)
+        return launch_ablated(in, wp, scale, shift, resid, out, M, st);
+    int shape = -1;
+    if (g_conv_shape_override >= 0 && shape_ok(g_conv_shape_override, C)) {
+        shape = g_conv_shape_override;
+    } else {
+        auto key = std::make_pair(C, M);
+        auto it = tune_cache().find(key);
+        if (it != tune_cache().end()) {
+            shape = it->second;
+        } else if (g_conv_autotune) {
+            shape = autotune_shape(C, epi, in, wp, scale, shift, resid, out, M, st);
+            if (shape >= 0) tune_cache()[key] = shape;
+        }
+        if (shape < 0) shape = pick_conv_tile(C, M);
+    }
+    if (C == 64 && !shape_ok(shape, C)) shape = 5;
     return launch_conv3x3_shape(shape, C, epi, in, wp, scale, shift, resid, out, M, st);
+}
+
+int conv_tuned_shape(int C, int M)
+{
+    auto it = tune_cache().find(std::make_pair(C, M));
+    return it == tune_cache().end() ? -1 : it->second;
 }
 
 hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const float* scale,
@@ -355,3 +480,26 @@ hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const fl
 }
 
 }  // namespace azg
+
+extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
+{
+    if (key == 0) {
+        const int prev = azg::g_conv_shape_override;
+        azg::g_conv_shape_override = value;
+        return prev;
+    }
+    if (key == 1) {
+        const int prev = azg::g_conv_autotune;
+        azg::g_conv_autotune = value;
+        return prev;
+    }
+    if (key == 3) {   // ablation mask (timing studies only, C=128 EPI_BN_RELU launches)
+        const int prev = azg::g_conv_ablation;
+        azg::g_conv_ablation = value;
+        return prev;
+    }
+    if (key == 2) {   // query: tuned shape for (C, M) packed as value = M*1024 + C
+        return azg::conv_tuned_shape(value & 1023, value >> 10);
+    }
+    return -1;
+}

@@ -1,32 +1,71 @@
-// Policy + value heads, eval mode, one fused kernel.
+// Policy + value heads (network.py:102-115 + softmax at :180), two kernels.
 //
-// Replaces (network.py:102-115 + :180):
-//   p = relu(policy_bn(policy_conv1x1(h)))  -> view [B,450] (channel-major, NCHW flatten)
-//   logits = policy_fc(p)                    [450 -> 225]
-//   probs = softmax(logits, dim=1)
-//   v = relu(value_bn(value_conv1x1(h)))     -> [B,225]
-//   v = relu(value_fc1(v)); value = tanh(value_fc2(v))
-//
-// HBM-bound: the only large read is the tower output (225*C floats per board);
-// the FC weights (405 KB + 58 KB) are L2-resident and each load is reused for
-// HG boards.  One 256-thread workgroup handles HG boards:
-//   phase 1: one wave per (board, pixel) row: 3 dot products over C with wave
-//            reductions -> folded BN + ReLU -> LDS features;
-//   phase 2: thread j computes logit j for HG boards (transposed weights, coalesced);
-//   phase 3: waves 0..HG-1 softmax one board each; waves HG.. run the value MLP.
-#include "pv_common.h"
+//   heads_project<C, BN>: the three 1x1 projections of the tower output
+//       (policy_conv C->2, value_conv C->1) for every pixel, optionally followed
+//       by the folded eval BatchNorm + ReLU; writes h[b][3][225] (channel-major,
+//       i.e. exactly the NCHW flatten order network.py:105,112 uses).  HBM-bound:
+//       reads 225*C*4 B per board once; 4 consecutive threads cover one pixel's
+//       C channels (coalesced 128-B quarter rows), partial dots reduced by 2 xor
+//       shuffles.  Also used raw (BN = false) by the train step.
+//   heads_fc_eval: per workgroup HB boards: policy_fc 450->225 (+bias), softmax,
+//       value_fc1 225->64 + ReLU, value_fc2 64->1, tanh.  Each transposed weight
+//       load (coalesced, L2-resident) is reused for HB boards.
+#include "pv_internal.h"
 
 namespace azg {
 
-constexpr int HG = 2;   // boards per workgroup
+constexpr int PROJ_ROWS = 64;   // pixels per workgroup in heads_project
+constexpr int HB = 8;           // boards per workgroup in heads_fc_eval
 
-template <int C>
-__global__ __launch_bounds__(256) void heads_fwd(
-    const float* __restrict__ act,
-    const float* __restrict__ wpc,    // policy_conv.weight [2][C]
-    const float* __restrict__ wvc,    // value_conv.weight [C]
-    const float* __restrict__ hscale, // [3] folded BN scale: policy ch0, ch1, value
-    const float* __restrict__ hshift, // [3]
+template <int C, bool BN>
+__global__ __launch_bounds__(256) void heads_project(const float* __restrict__ act, const float* __restrict__ wpc,
+                                                     const float* __restrict__ wvc,
+                                                     const float* __restrict__ hscale,
+                                                     const float* __restrict__ hshift, float* __restrict__ hout,
+                                                     int M)
+{
+    constexpr int Q = C / 4;        // channels per thread
+    __shared__ float w[3][C];
+    for (int i = threadIdx.x; i < 3 * C; i += 256) w[i / C][i % C] = i < 2 * C ? wpc[i] : wvc[i - 2 * C];
+    __syncthreads();
+    const int q = threadIdx.x & 3;
+    const int m = blockIdx.x * PROJ_ROWS + (threadIdx.x >> 2);
+    float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+    if (m < M) {
+        const float* row = act + pad_off(m, C) + q * Q;
+#pragma unroll
+        for (int c = 0; c < Q; c += 4) {
+            const f32x4 a = *(const f32x4*)(row + c);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                d0 = fmaf(a[k], w[0][q * Q + c + k], d0);
+                d1 = fmaf(a[k], w[1][q * Q + c + k], d1);
+                d2 = fmaf(a[k], w[2][q * Q + c + k], d2);
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 1; o < 4; o <<= 1) {
+        d0 += __shfl_xor(d0, o, 64);
+        d1 += __shfl_xor(d1, o, 64);
+        d2 += __shfl_xor(d2, o, 64);
+    }
+    if (m < M && q == 0) {
+        const int b = m / PIX, p = m - b * PIX;
+        float* hb = hout + (size_t)b * 3 * PIX;
+        if (BN) {
+            d0 = fmaxf(d0 * hscale[0] + hshift[0], 0.f);
+            d1 = fmaxf(d1 * hscale[1] + hshift[1], 0.f);
+            d2 = fmaxf(d2 * hscale[2] + hshift[2], 0.f);
+        }
+        hb[p] = d0;
+        hb[PIX + p] = d1;
+        hb[2 * PIX + p] = d2;
+    }
+}
+
+__global__ __launch_bounds__(256) void heads_fc_eval(
+    const float* __restrict__ feat,   // [B][3*225]: policy features 0..449, value features 450..674
     const float* __restrict__ wpfT,   // policy_fc.weight^T [450][225]
     const float* __restrict__ bpf,    // [225]
     const float* __restrict__ wv1T,   // value_fc1.weight^T [225][64]
@@ -35,120 +74,105 @@ __global__ __launch_bounds__(256) void heads_fwd(
     const float* __restrict__ bv2,    // [1]
     float* __restrict__ probs, float* __restrict__ values, float* __restrict__ logits, int B)
 {
-    __shared__ float fp[HG][2 * PIX];
-    __shared__ float fv[HG][PIX];
-    __shared__ float lg[HG][ACTIONS];
-
-    constexpr int CPL = C / 64;   // channels per lane
+    __shared__ float f[HB][3 * PIX];
+    __shared__ float lg[HB][ACTIONS];
+    __shared__ float hid[HB][VHID];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int b0 = blockIdx.x * HG;
-
-    float w0[CPL], w1[CPL], w2[CPL];
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) {
-        w0[q] = wpc[lane * CPL + q];
-        w1[q] = wpc[C + lane * CPL + q];
-        w2[q] = wvc[lane * CPL + q];
-    }
-    const float s0 = hscale[0], s1 = hscale[1], s2 = hscale[2];
-    const float t0 = hshift[0], t1 = hshift[1], t2 = hshift[2];
-
-    for (int task = wid; task < HG * PIX; task += 4) {
-        const int g = task / PIX, p = task - g * PIX;
-        const int b = b0 + g;
-        if (b >= B) break;
-        const float* row = act + pad_off(b * PIX + p, C) + lane * CPL;
-        float d0 = 0.f, d1 = 0.f, d2 = 0.f;
-#pragma unroll
-        for (int q = 0; q < CPL; ++q) {
-            const float a = row[q];
-            d0 = fmaf(a, w0[q], d0);
-            d1 = fmaf(a, w1[q], d1);
-            d2 = fmaf(a, w2[q], d2);
-        }
-        d0 = wave_sum(d0);
-        d1 = wave_sum(d1);
-        d2 = wave_sum(d2);
-        if (lane == 0) {
-            fp[g][p] = fmaxf(d0 * s0 + t0, 0.f);
-            fp[g][PIX + p] = fmaxf(d1 * s1 + t1, 0.f);
-            fv[g][p] = fmaxf(d2 * s2 + t2, 0.f);
-        }
+    const int b0 = blockIdx.x * HB;
+    const int nb = min(HB, B - b0);
+    for (int i = tid; i < HB * 3 * PIX; i += 256) {
+        const int g = i / (3 * PIX);
+        f[g][i - g * 3 * PIX] = g < nb ? feat[(size_t)b0 * 3 * PIX + i] : 0.f;
     }
     __syncthreads();
-
     if (tid < ACTIONS) {
-        float acc[HG];
+        float acc[HB];
 #pragma unroll
-        for (int g = 0; g < HG; ++g) acc[g] = 0.f;
+        for (int g = 0; g < HB; ++g) acc[g] = 0.f;
+#pragma unroll 4
         for (int k = 0; k < 2 * PIX; ++k) {
-            const float w = wpfT[k * ACTIONS + tid];
+            const float wk = wpfT[k * ACTIONS + tid];
 #pragma unroll
-            for (int g = 0; g < HG; ++g) acc[g] = fmaf(w, fp[g][k], acc[g]);
+            for (int g = 0; g < HB; ++g) acc[g] = fmaf(wk, f[g][k], acc[g]);
         }
         const float bias = bpf[tid];
 #pragma unroll
-        for (int g = 0; g < HG; ++g) {
-            const float l = acc[g] + bias;
-            lg[g][tid] = l;
-            if (logits && b0 + g < B) logits[(size_t)(b0 + g) * ACTIONS + tid] = l;
+        for (int g = 0; g < HB; ++g) lg[g][tid] = acc[g] + bias;
+    }
+    {
+        // value hidden layer: thread -> unit i = tid % 64, boards (tid / 64) + 4 j
+        const int i = tid & 63, gq = tid >> 6;
+        constexpr int GPT = HB / 4;
+        float acc[GPT];
+#pragma unroll
+        for (int j = 0; j < GPT; ++j) acc[j] = 0.f;
+#pragma unroll 4
+        for (int k = 0; k < PIX; ++k) {
+            const float wk = wv1T[k * VHID + i];
+#pragma unroll
+            for (int j = 0; j < GPT; ++j) acc[j] = fmaf(wk, f[gq + 4 * j][2 * PIX + k], acc[j]);
         }
+#pragma unroll
+        for (int j = 0; j < GPT; ++j) hid[gq + 4 * j][i] = fmaxf(acc[j] + bv1[i], 0.f);
     }
     __syncthreads();
-
-    if (wid < HG) {
-        const int g = wid, b = b0 + g;
-        if (b < B) {
-            float mx = -INFINITY;
-            for (int j = lane; j < ACTIONS; j += 64) mx = fmaxf(mx, lg[g][j]);
-            mx = wave_max(mx);
-            float e[4];
-            float sum = 0.f;
+    // softmax + value: wave w handles boards w, w+4, ...
+    for (int g = wid; g < nb; g += 4) {
+        const int b = b0 + g;
+        float mx = -INFINITY;
+        for (int j = lane; j < ACTIONS; j += 64) mx = fmaxf(mx, lg[g][j]);
+        mx = wave_max(mx);
+        float e[4];
+        float sum = 0.f;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int j = lane + 64 * q;
-                e[q] = j < ACTIONS ? expf(lg[g][j] - mx) : 0.f;
-                sum += e[q];
-            }
-            sum = wave_sum(sum);
-            const float inv = 1.f / sum;
+        for (int t = 0; t < 4; ++t) {
+            const int j = lane + 64 * t;
+            e[t] = j < ACTIONS ? expf(lg[g][j] - mx) : 0.f;
+            sum += e[t];
+        }
+        sum = wave_sum(sum);
+        const float inv = 1.f / sum;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int j = lane + 64 * q;
-                if (j < ACTIONS) probs[(size_t)b * ACTIONS + j] = e[q] * inv;
+        for (int t = 0; t < 4; ++t) {
+            const int j = lane + 64 * t;
+            if (j < ACTIONS) {
+                probs[(size_t)b * ACTIONS + j] = e[t] * inv;
+                if (logits) logits[(size_t)b * ACTIONS + j] = lg[g][j];
             }
         }
-    } else if (wid < 2 * HG) {
-        const int g = wid - HG, b = b0 + g;
-        if (b < B) {
-            float hsum = bv1[lane];
-            for (int k = 0; k < PIX; ++k) hsum = fmaf(wv1T[k * VHID + lane], fv[g][k], hsum);
-            hsum = fmaxf(hsum, 0.f);
-            float v = wave_sum(hsum * wv2[lane]) + bv2[0];
-            if (lane == 0) values[b] = tanhf(v);
-        }
+        const float v = wave_sum(hid[g][lane] * wv2[lane]) + bv2[0];
+        if (lane == 0) values[b] = tanhf(v);
     }
 }
 
-hipError_t launch_heads_fwd(int C, const float* act, const float* wpc, const float* wvc,
-                            const float* hscale, const float* hshift, const float* wpfT,
-                            const float* bpf, const float* wv1T, const float* bv1,
-                            const float* wv2, const float* bv2, float* probs, float* values,
-                            float* logits, int B, hipStream_t st)
+hipError_t launch_heads_project(int C, bool bn, const float* act, const float* wpc, const float* wvc,
+                                const float* hscale, const float* hshift, float* hout, int M, hipStream_t st)
 {
-    dim3 grid((B + HG - 1) / HG);
-#define AZG_HEADS_CASE(CC)                                                                       \
-    case CC:                                                                                     \
-        hipLaunchKernelGGL((heads_fwd<CC>), grid, dim3(256), 0, st, act, wpc, wvc, hscale, hshift, \
-                           wpfT, bpf, wv1T, bv1, wv2, bv2, probs, values, logits, B);          \
+    dim3 grid((M + PROJ_ROWS - 1) / PROJ_ROWS);
+#define AZG_PROJ_CASE(CC)                                                                                      \
+    case CC:                                                                                                   \
+        if (bn) hipLaunchKernelGGL((heads_project<CC, true>), grid, dim3(256), 0, st, act, wpc, wvc, hscale, hshift, hout, M); \
+        else hipLaunchKernelGGL((heads_project<CC, false>), grid, dim3(256), 0, st, act, wpc, wvc, hscale, hshift, hout, M); \
         return hipGetLastError();
     switch (C) {
-        AZG_HEADS_CASE(64)
-        AZG_HEADS_CASE(128)
-        AZG_HEADS_CASE(256)
+        AZG_PROJ_CASE(64)
+        AZG_PROJ_CASE(128)
+        AZG_PROJ_CASE(256)
         default: return hipErrorInvalidValue;
     }
-#undef AZG_HEADS_CASE
+#undef AZG_PROJ_CASE
+}
+
+hipError_t launch_heads_fwd(int C, const float* act, const float* wpc, const float* wvc, const float* hscale,
+                            const float* hshift, const float* wpfT, const float* bpf, const float* wv1T,
+                            const float* bv1, const float* wv2, const float* bv2, float* hbuf, float* probs,
+                            float* values, float* logits, int B, hipStream_t st)
+{
+    hipError_t e = launch_heads_project(C, true, act, wpc, wvc, hscale, hshift, hbuf, B * PIX, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(heads_fc_eval, dim3((B + HB - 1) / HB), dim3(256), 0, st, hbuf, wpfT, bpf, wv1T, bv1, wv2,
+                       bv2, probs, values, logits, B);
+    return hipGetLastError();
 }
 
 }  // namespace azg

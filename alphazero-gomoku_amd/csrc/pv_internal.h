@@ -27,8 +27,10 @@ hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const fl
 hipError_t launch_heads_fwd(int C, const float* act, const float* wpc, const float* wvc,
                             const float* hscale, const float* hshift, const float* wpfT,
                             const float* bpf, const float* wv1T, const float* bv1,
-                            const float* wv2, const float* bv2, float* probs, float* values,
-                            float* logits, int B, hipStream_t st);
+                            const float* wv2, const float* bv2, float* hbuf, float* probs,
+                            float* values, float* logits, int B, hipStream_t st);
+hipError_t launch_heads_project(int C, bool bn, const float* act, const float* wpc, const float* wvc,
+                                const float* hscale, const float* hshift, float* hout, int M, hipStream_t st);
 hipError_t launch_pack_conv3x3(const float* w, float* wp, int C, hipStream_t st);
 hipError_t launch_pack_dgrad(const float* w, float* wd, int C, hipStream_t st);
 hipError_t launch_pack_stem(const float* w, float* ws, int C, hipStream_t st);
@@ -70,8 +72,9 @@ struct azg_pv {
     float* wpfT = nullptr;    // [450][225]
     float* wv1T = nullptr;    // [225][64]
 
-    // eval activations: 3 padded NHWC buffers
+    // eval activations: 3 padded NHWC buffers + head features [B][3][225]
     float* act[3] = {nullptr, nullptr, nullptr};
+    float* hbuf = nullptr;
     int act_cap = 0;
 
     // train workspace (pv_train.hip)

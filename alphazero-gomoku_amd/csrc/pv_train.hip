@@ -275,44 +275,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     }
 }
 
-// heads: raw 1x1 projections zh[b][ch][p], ch 0,1 = policy_conv, 2 = value_conv
-template <int C>
-__global__ __launch_bounds__(256) void heads_proj_kernel(const float* __restrict__ act,
-                                                         const float* __restrict__ wpc,
-                                                         const float* __restrict__ wvc, float* __restrict__ zh,
-                                                         int M)
-{
-    constexpr int CPL = C / 64;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    float w0[CPL], w1[CPL], w2[CPL];
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) {
-        w0[q] = wpc[lane * CPL + q];
-        w1[q] = wpc[C + lane * CPL + q];
-        w2[q] = wvc[lane * CPL + q];
-    }
-    for (int m = blockIdx.x * 4 + wid; m < M; m += gridDim.x * 4) {
-        const float* row = act + pad_off(m, C) + lane * CPL;
-        float d0 = 0.f, d1 = 0.f, d2 = 0.f;
-#pragma unroll
-        for (int q = 0; q < CPL; ++q) {
-            const float a = row[q];
-            d0 = fmaf(a, w0[q], d0);
-            d1 = fmaf(a, w1[q], d1);
-            d2 = fmaf(a, w2[q], d2);
-        }
-        d0 = wave_sum(d0);
-        d1 = wave_sum(d1);
-        d2 = wave_sum(d2);
-        if (lane == 0) {
-            const int b = m / PIX, p = m - b * PIX;
-            zh[(b * 3 + 0) * PIX + p] = d0;
-            zh[(b * 3 + 1) * PIX + p] = d1;
-            zh[(b * 3 + 2) * PIX + p] = d2;
-        }
-    }
-}
-
 // head BN stats (3 channels over B*225), two-pass in double; one block per channel
 __global__ __launch_bounds__(256) void head_stats_kernel(const float* __restrict__ zh, int B, const BnDesc* desc,
                                                          int pol_layer, int val_layer,
@@ -925,9 +887,9 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     // ---- heads forward + loss + backward to the tower output ----
     {
         int pr = prof_begin(h, AZG_PROF_TRAIN_OTHER, st);
-        hipLaunchKernelGGL((heads_proj_kernel<C>), dim3((M + 15) / 16), dim3(256), 0, st, X,
-                           P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], w->zh, M);
-        AZG_CK(hipGetLastError(), "train: heads_proj");
+        AZG_CK(launch_heads_project(C, false, X, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], nullptr, nullptr,
+                                    w->zh, M, st),
+               "train: heads_project");
         hipLaunchKernelGGL(head_stats_kernel, dim3(3), dim3(256), 0, st, w->zh, B, bdd, h->bn_pol, h->bn_val, P,
                            h->bn, w->bmean, w->binv, w->bscale, w->bshift);
         AZG_CK(hipGetLastError(), "train: head_stats");

@@ -113,6 +113,14 @@ enum {
 int32_t azg_pv_profile_enable(azg_pv* h, int32_t enable);
 int32_t azg_pv_profile_read(azg_pv* h, double* ms, int64_t* launches);
 
+/* Process-wide tuning knobs (benchmarks / A-B tests).  Returns the previous value.
+ *   key 0: force the 3x3-conv tile shape index (-1 = automatic);
+ *   key 1: conv autotuning on/off (default on: the first launch for a (C, M) times
+ *          every tile shape on the real operands and caches the fastest; shapes give
+ *          bitwise-identical results, so this never changes numerics);
+ *   key 2: query the tuned shape for value = M*1024 + C (-1 if not tuned yet). */
+int32_t azg_pv_set_tuning(int32_t key, int32_t value);
+
 /* Debug/test access to train-workspace activations of the last train step:
  * copies the interior [batch][15][15][C] (NHWC) of buffer `which` (block `index`
  * where relevant) into dst (device, batch*225*C floats), stream-ordered.

@@ -1,0 +1,66 @@
+"""Interleaved A/B of 3x3-conv tile shapes in ONE process (6x128, B=512 forward).
+Each round runs every shape for K forwards and reads the conv launches' average
+device time from the engine's hipEvent instrumentation.  Also checks that every
+shape produces bitwise-identical outputs (the K order does not depend on tiling).
+
+    python scripts/conv_ab.py [--shapes 0,6,3] [--rounds 5] [--steps 10] [--batch 512]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "alphazero-gomoku_amd")]
+
+import torch
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default="0,6,3,1")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--blocks", type=int, default=6)
+    ap.add_argument("--channels", type=int, default=128)
+    args = ap.parse_args()
+    from network import PyTorchModel
+    from synth import synth_encoded
+    import _native
+
+    lib = _native.load_library()
+    torch.manual_seed(0)
+    m = PyTorchModel(device="cuda", n_res_blocks=args.blocks, channels=args.channels)
+    eng = m.engine
+    x = torch.from_numpy(synth_encoded(args.batch, seed=5)).cuda()
+    probs = torch.empty((args.batch, 225), device="cuda")
+    values = torch.empty((args.batch, 1), device="cuda")
+    shapes = [int(s) for s in args.shapes.split(",")]
+    ref = None
+    times = {s: [] for s in shapes}
+    for r in range(args.rounds):
+        for s in shapes:
+            lib.azg_pv_set_tuning(0, s)
+            eng.forward_into(x, probs, values)      # warm
+            eng.profile_enable(True)
+            for _ in range(args.steps):
+                eng.forward_into(x, probs, values)
+            prof = eng.profile_read()
+            eng.profile_enable(False)
+            ms, n = prof["conv3x3"]
+            times[s].append(ms / n * 1e3)
+            if ref is None:
+                ref = probs.clone()
+            elif not torch.equal(ref, probs):
+                print(f"shape {s}: outputs differ from shape {shapes[0]} (max {float((ref - probs).abs().max()):.3e})")
+    lib.azg_pv_set_tuning(0, -1)
+    flop = 2 * 225 * args.channels * 9 * args.channels * args.batch
+    out = {s: {"median_us": round(statistics.median(t), 2), "min_us": round(min(t), 2),
+               "tflops": round(flop / (statistics.median(t) * 1e-6) / 1e12, 2)} for s, t in times.items()}
+    print(json.dumps({"batch": args.batch, "net": f"{args.blocks}x{args.channels}", "conv": out}))
+
+
+if __name__ == "__main__":
+    main()

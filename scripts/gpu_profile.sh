@@ -10,7 +10,7 @@ BENCH="bench.py --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline ${BENCH_ARGS}"
 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 $BENCH > $OUT/bench_trace.log 2>&1
 s=$?; echo "trace exit $s"; tail -2 $OUT/bench_trace.log; [ $s -eq 0 ] || exit $s
-for pmc in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES" ${EXTRA_PMC}; do
+for pmc in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES" ${EXTRA_PMC}; do
   name=$(echo $pmc | tr ' ' '_' | cut -c1-40)
   timeout -k 10 300 rocprofv3 --pmc $pmc -f csv -d $OUT/pmc_$name -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > $OUT/pmc_$name.log 2>&1
   s=$?; echo "pmc $pmc exit $s"; [ $s -eq 0 ] || exit $s
