@@ -1,0 +1,136 @@
+"""ctypes binding of libazg_mcts.so (C-ABI declared in include/azg_mcts.h): the
+native multi-game batched-leaf search.  Host code only (no HIP); the library is
+required -- there is no Python fallback behind the native search classes."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("AZG_MCTS_LIB", os.path.join(_HERE, "libazg_mcts.so"))
+
+IDLE, NEED_EVAL, DONE = 0, 1, 2
+
+
+class MctsConfig(ctypes.Structure):
+    _fields_ = [("rules", ctypes.c_int32), ("board", ctypes.c_int32), ("n_simulations", ctypes.c_int32),
+                ("batch_size", ctypes.c_int32), ("apply_dirichlet_n_first_moves", ctypes.c_int32),
+                ("add_dirichlet_noise", ctypes.c_int32), ("cpuct", ctypes.c_double),
+                ("dirichlet_alpha", ctypes.c_double), ("epsilon", ctypes.c_double)]
+
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_SIGS = {
+    "azg_mcts_last_error": (ctypes.c_char_p, []),
+    "azg_mcts_create": (_I32, [ctypes.POINTER(MctsConfig), _I32, ctypes.POINTER(_P)]),
+    "azg_mcts_destroy": (_I32, [_P]),
+    "azg_mcts_set_root": (_I32, [_P, _I32, _P, _I32, _I32, _I32, _I32, _I32, _I32]),
+    "azg_mcts_advance": (_I32, [_P, _P, _P, _P, ctypes.POINTER(_I32), _I32]),
+    "azg_mcts_feed": (_I32, [_P, _P, _P]),
+    "azg_mcts_noise_request": (_I32, [_P, _I32, _P]),
+    "azg_mcts_set_root_prior": (_I32, [_P, _I32, _P]),
+    "azg_mcts_get_pi": (_I32, [_P, _I32, _P]),
+    "azg_mcts_clear": (_I32, [_P, _I32]),
+    "azg_mcts_tree_size": (ctypes.c_int64, [_P, _I32]),
+}
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+
+
+def load_library() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"native MCTS library not found at {LIB_PATH}. Build it with "
+                           "`make -C alphazero-gomoku_amd/csrc` (or __graft_entry__.build()).")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise RuntimeError("libazg_mcts: " + (load_library().azg_mcts_last_error() or b"?").decode())
+
+
+def _addr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+class SearchForest:
+    """One native search tree per game slot.  Thin, allocation-free wrapper: the
+    leaf/pi staging arrays are owned here and reused every round."""
+
+    def __init__(self, n_games: int, n_simulations: int, rules: int = 0, board: int = 15, cpuct: float = 1.0,
+                 batch_size: int = 32, dirichlet_alpha: float = 0.03, epsilon: float = 0.03,
+                 apply_dirichlet_n_first_moves: int = 10, add_dirichlet_noise: bool = True, n_threads: int = 0):
+        self.lib = load_library()
+        self.n_games = int(n_games)
+        self.board = int(board)
+        self.A = self.board * self.board
+        self.batch_size = int(batch_size)
+        self.n_threads = int(n_threads)
+        self.cfg = MctsConfig(int(rules), self.board, int(n_simulations), self.batch_size,
+                              int(apply_dirichlet_n_first_moves), int(bool(add_dirichlet_noise)), float(cpuct),
+                              float(dirichlet_alpha), float(epsilon))
+        self.h = _P()
+        _check(self.lib.azg_mcts_create(ctypes.byref(self.cfg), self.n_games, ctypes.byref(self.h)))
+        self.leaves = np.empty((self.n_games * self.batch_size, 3, self.board, self.board), np.float32)
+        self.counts = np.zeros(self.n_games, np.int32)
+        self.status = np.zeros(self.n_games, np.int32)
+        self._p32 = np.empty(self.A, np.float32)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            self.lib.azg_mcts_destroy(h)
+            self.h = None
+
+    def set_root(self, g: int, game, move_number: int) -> None:
+        board = np.ascontiguousarray(np.asarray(game.board).reshape(-1), dtype=np.int8)
+        last = getattr(game, "last_move", None)
+        lr, lc = (-1, -1) if last is None else (int(last[0]), int(last[1]))
+        caps = getattr(game, "captures", None) or {1: 0, 2: 0}
+        _check(self.lib.azg_mcts_set_root(self.h, g, _addr(board), int(game.current_player), lr, lc,
+                                          int(caps[1]), int(caps[2]), int(move_number)))
+
+    def advance(self) -> int:
+        n = _I32(0)
+        _check(self.lib.azg_mcts_advance(self.h, _addr(self.leaves), _addr(self.counts), _addr(self.status),
+                                         ctypes.byref(n), self.n_threads))
+        return n.value
+
+    def feed(self, probs: np.ndarray, values: np.ndarray) -> None:
+        probs = np.ascontiguousarray(probs, dtype=np.float32)
+        values = np.ascontiguousarray(values, dtype=np.float32)
+        _check(self.lib.azg_mcts_feed(self.h, _addr(probs), _addr(values)))
+
+    def noise_request(self, g: int):
+        r = self.lib.azg_mcts_noise_request(self.h, g, _addr(self._p32))
+        if r < 0:
+            raise RuntimeError("libazg_mcts: bad game index")
+        return self._p32.copy() if r else None
+
+    def set_root_prior(self, g: int, p64: np.ndarray) -> None:
+        p64 = np.ascontiguousarray(p64, dtype=np.float64)
+        _check(self.lib.azg_mcts_set_root_prior(self.h, g, _addr(p64)))
+
+    def get_pi(self, g: int) -> np.ndarray:
+        pi = np.empty(self.A, np.float32)
+        _check(self.lib.azg_mcts_get_pi(self.h, g, _addr(pi)))
+        return pi
+
+    def clear(self, g: int) -> None:
+        _check(self.lib.azg_mcts_clear(self.h, g))
+
+    def tree_size(self, g: int) -> int:
+        return int(self.lib.azg_mcts_tree_size(self.h, g))

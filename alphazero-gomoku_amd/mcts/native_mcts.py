@@ -1,0 +1,260 @@
+"""Native (C++) search behind the reference MCTS interface
+(reference mcts/new_mcts_alpha.py:21-97), and the multi-game self-play engine
+built on it.
+
+``NativeMCTS`` is a drop-in for ``mcts.new_mcts_alpha.MCTS``: same constructor,
+``run(game, move_number) -> pi``, ``run_gen`` (leaf batches as generator yields),
+``clear_tree``, ``symmetries``.  The tree walk, PUCT, backup, leaf queue and
+prior installation run in libazg_mcts.so with the reference's exact float32 /
+float64 arithmetic; only the Dirichlet draw (numpy, same call as the reference)
+and the noise mix stay in Python, so RNG streams are the reference's.
+
+``NativeSelfPlay`` plays many games at once: every round one ``advance`` call runs
+all games' searches in parallel on host threads (OpenMP) up to their next leaf
+flush, one batched forward evaluates every pending leaf, one ``feed`` installs
+them.  Each game owns a ``numpy.random.RandomState`` (Dirichlet noise and move
+sampling), so a game's result does not depend on which other games share its
+batches or on thread scheduling -- it equals that game played alone through the
+reference-semantics Python search with the same RandomState.
+"""
+from __future__ import annotations
+
+import time
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+
+from _native_mcts import DONE, NEED_EVAL, SearchForest
+from mcts.new_mcts_alpha import MCTS as _PyMCTS
+
+
+def _rules_of(game_class) -> int:
+    return 1 if hasattr(game_class(), "captures") else 0
+
+
+def _mix_noise(p32: np.ndarray, rng, alpha: float, eps: float) -> np.ndarray:
+    """new_mcts_alpha.py:176-179 verbatim in numpy: float32 prior, float64 noise."""
+    noise = rng.dirichlet([alpha] * len(p32))
+    p = (1 - eps) * p32 + eps * noise
+    p /= np.sum(p)
+    return p
+
+
+class NativeMCTS:
+    symmetries = _PyMCTS.symmetries
+    drive = _PyMCTS.drive
+
+    def __init__(self, game_class, n_simulations, nn_model, cpuct=1.0, batch_size=32, dirichlet_alpha=0.03,
+                 epsilon=0.03, apply_dirichlet_n_first_moves=10, add_dirichlet_noise=True, rng=None, n_threads=1):
+        self.game_class = game_class
+        self.n_simulations = n_simulations
+        self.nn_model = nn_model
+        self.cpuct = cpuct
+        self.batch_size = batch_size
+        self.dirichlet_alpha = dirichlet_alpha
+        self.epsilon = epsilon
+        self.apply_dirichlet_n_first_moves = apply_dirichlet_n_first_moves
+        self.add_dirichlet_noise = add_dirichlet_noise
+        self.rng = np.random if rng is None else rng
+        g0 = game_class()
+        self.action_size = g0.size ** 2
+        self.forest = SearchForest(1, n_simulations, rules=_rules_of(game_class), board=g0.size, cpuct=cpuct,
+                                   batch_size=batch_size, dirichlet_alpha=dirichlet_alpha, epsilon=epsilon,
+                                   apply_dirichlet_n_first_moves=apply_dirichlet_n_first_moves,
+                                   add_dirichlet_noise=add_dirichlet_noise, n_threads=n_threads)
+
+    def clear_tree(self):
+        self.forest.clear(0)
+
+    def tree_size(self) -> int:
+        return self.forest.tree_size(0)
+
+    def run(self, game_state, move_number):
+        return self.drive(self.run_gen(game_state, move_number))
+
+    def run_gen(self, game_state, move_number):
+        f = self.forest
+        f.set_root(0, game_state, move_number)
+        while True:
+            n = f.advance()
+            if f.status[0] != NEED_EVAL:
+                break
+            probs, values = yield f.leaves[:n].copy()
+            f.feed(probs, values)
+            p32 = f.noise_request(0)
+            if p32 is not None:
+                f.set_root_prior(0, _mix_noise(p32, self.rng, self.dirichlet_alpha, self.epsilon))
+        return f.get_pi(0)
+
+
+class NativeSelfPlay:
+    """Concurrent self-play games over one SearchForest (train.py:360-412 per game).
+
+    ``evaluate(X float32 [n,3,H,W]) -> (probs [n,A], values [n,1])`` is the batched
+    network call (e.g. PyTorchModel.predict).  Statistics: boards, forwards,
+    nn_seconds, search_seconds, max_batch."""
+
+    def __init__(self, evaluate: Callable, game_class, n_games: int, n_simulations: int, cpuct: float = 1.0,
+                 batch_size: int = 32, dirichlet_alpha: float = 0.03, epsilon: float = 0.03,
+                 apply_dirichlet_n_first_moves: int = 10, add_dirichlet_noise: bool = True, n_threads: int = 0):
+        self.evaluate = evaluate
+        self.game_class = game_class
+        self.n_games = n_games
+        self.alpha, self.eps = dirichlet_alpha, epsilon
+        g0 = game_class()
+        self.board = g0.size
+        self.forest = SearchForest(n_games, n_simulations, rules=_rules_of(game_class), board=g0.size, cpuct=cpuct,
+                                   batch_size=batch_size, dirichlet_alpha=dirichlet_alpha, epsilon=epsilon,
+                                   apply_dirichlet_n_first_moves=apply_dirichlet_n_first_moves,
+                                   add_dirichlet_noise=add_dirichlet_noise, n_threads=n_threads)
+        self.boards = self.forwards = self.max_batch = 0
+        self.nn_seconds = self.search_seconds = 0.0
+
+    def play(self, temp_fn: Callable[[int], float], max_moves: int = 225, use_symmetries: bool = True,
+             seeds: Optional[Sequence[int]] = None, games: Optional[list] = None):
+        """Play one game per slot to the end; returns [(examples, winner)] in slot
+        order.  ``seeds`` seed each game's RandomState (default: drawn from numpy's
+        global RNG); ``games`` optionally gives the starting positions."""
+        from selfplay import sample_action_from_pi
+        G = self.n_games
+        if seeds is None:
+            seeds = np.random.randint(0, 2 ** 31 - 1, size=G)
+        rngs = [np.random.RandomState(int(s)) for s in seeds]
+        if games is None:
+            games = []
+            for _ in range(G):
+                g = self.game_class(size=self.board)
+                g.current_player = 1
+                games.append(g)
+        f = self.forest
+        hist: List[list] = [[] for _ in range(G)]
+        moves = [0] * G
+        live = [True] * G
+        results = [None] * G
+
+        for g in range(G):
+            f.clear(g)                  # a fresh tree per game, reused across its moves
+            f.set_root(g, games[g], len(games[g].move_history))
+        n_live = G
+        while n_live:
+            t0 = time.perf_counter()
+            n = f.advance()
+            self.search_seconds += time.perf_counter() - t0
+            # games whose move search finished: sample (per-game RNG), play, restart
+            for g in np.nonzero(f.status == DONE)[0]:
+                g = int(g)
+                game = games[g]
+                pi = f.get_pi(g)
+                state_enc = game.get_encoded_state()
+                action = sample_action_from_pi(pi, temp_fn(moves[g]), rngs[g])
+                if game.get_valid_moves()[action] != 1.0:
+                    action = int(np.argmax(pi))
+                hist[g].append((state_enc, pi.copy(), int(game.current_player)))
+                game.do_move(divmod(action, game.size))
+                moves[g] += 1
+                if game.is_game_over() or moves[g] >= max_moves:
+                    results[g] = self._finish(hist[g], game.get_winner(), use_symmetries)
+                    live[g] = False
+                    n_live -= 1
+                else:
+                    f.set_root(g, game, len(game.move_history))
+            if n:
+                t0 = time.perf_counter()
+                probs, values = self.evaluate(f.leaves[:n])
+                self.nn_seconds += time.perf_counter() - t0
+                self.boards += n
+                self.forwards += 1
+                self.max_batch = max(self.max_batch, n)
+                t0 = time.perf_counter()
+                f.feed(probs, values)
+                for g in np.nonzero(f.status == NEED_EVAL)[0]:
+                    p32 = f.noise_request(int(g))
+                    if p32 is not None:
+                        f.set_root_prior(int(g), _mix_noise(p32, rngs[g], self.alpha, self.eps))
+                self.search_seconds += time.perf_counter() - t0
+        return results
+
+    @staticmethod
+    def _finish(history, winner, use_symmetries):
+        out = []
+        for state_enc, pi_vec, who in history:
+            z = 0.0 if winner == 0 else (1.0 if winner == who else -1.0)
+            if use_symmetries:
+                for s_aug, pi_aug in _PyMCTS.symmetries(None, state_enc, pi_vec):
+                    out.append((s_aug.astype(np.float32), pi_aug.astype(np.float32), z))
+            else:
+                out.append((state_enc.astype(np.float32), pi_vec.astype(np.float32), z))
+        return out, winner
+
+
+class NativeEval:
+    """Evaluation games between two networks (reference train.py:418-487 game body,
+    = train.eval_game_gen): every game keeps one native tree per network; the side to
+    move searches its own tree and plays argmax(pi).  Each round the pending leaves
+    of all games are evaluated with ONE forward per network."""
+
+    def __init__(self, evaluators: dict, game_class, n_games: int, n_simulations: int, cpuct: float = 1.0,
+                 batch_size: int = 32, n_threads: int = 0):
+        self.tags = list(evaluators)
+        self.evaluators = evaluators
+        self.n_games = n_games
+        g0 = game_class()
+        self.forests = {t: SearchForest(n_games, n_simulations, rules=_rules_of(game_class), board=g0.size,
+                                        cpuct=cpuct, batch_size=batch_size, add_dirichlet_noise=False,
+                                        n_threads=n_threads) for t in self.tags}
+        self.boards = self.forwards = self.max_batch = 0
+        self.nn_seconds = self.search_seconds = 0.0
+
+    def play(self, games: list, first_tag: list) -> list:
+        """games[g] already opened; first_tag[g] = tag of the network playing
+        player 1.  Returns the winners (0 draw, 1, 2) in slot order."""
+        G = len(games)
+        assert G == self.n_games and len(first_tag) == G
+        other = {self.tags[0]: self.tags[1], self.tags[1]: self.tags[0]}
+        winners = [None] * G
+        move_no = [1] * G
+        to_move = {}
+
+        def start(g):
+            game = games[g]
+            tag = first_tag[g] if game.current_player == 1 else other[first_tag[g]]
+            to_move[g] = tag
+            self.forests[tag].set_root(g, game, len(game.move_history))
+
+        for f in self.forests.values():
+            for g in range(G):
+                f.clear(g)
+        for g in range(G):
+            if games[g].is_game_over():
+                winners[g] = games[g].get_winner()
+            else:
+                start(g)
+        while to_move:
+            t0 = time.perf_counter()
+            ns = {t: f.advance() for t, f in self.forests.items()}
+            self.search_seconds += time.perf_counter() - t0
+            for g in sorted(to_move):
+                f = self.forests[to_move[g]]
+                if f.status[g] != DONE:
+                    continue
+                game = games[g]
+                action = int(np.argmax(f.get_pi(g)))
+                game.do_move(divmod(action, game.size))
+                move_no[g] += 1
+                if game.is_game_over() or move_no[g] > game.size * game.size:
+                    winners[g] = game.get_winner()
+                    del to_move[g]
+                else:
+                    start(g)
+            for t, n in ns.items():
+                if not n:
+                    continue
+                f = self.forests[t]
+                t0 = time.perf_counter()
+                probs, values = self.evaluators[t](f.leaves[:n])
+                self.nn_seconds += time.perf_counter() - t0
+                self.boards += n
+                self.forwards += 1
+                self.max_batch = max(self.max_batch, n)
+                f.feed(probs, values)
+        return winners

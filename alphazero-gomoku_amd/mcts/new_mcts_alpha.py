@@ -28,8 +28,11 @@ import numpy as np
 
 class MCTS:
     def __init__(self, game_class, n_simulations, nn_model, cpuct=1.0, batch_size=32, dirichlet_alpha=0.03,
-                 epsilon=0.03, apply_dirichlet_n_first_moves=10, add_dirichlet_noise=True):
+                 epsilon=0.03, apply_dirichlet_n_first_moves=10, add_dirichlet_noise=True, rng=None):
         self.game_class = game_class
+        # Dirichlet draws come from numpy's global RandomState (the reference's
+        # np.random.dirichlet) unless a per-search RandomState is given.
+        self.rng = np.random if rng is None else rng
         self.n_simulations = n_simulations
         self.nn_model = nn_model
         self.cpuct = cpuct
@@ -144,7 +147,7 @@ class MCTS:
             if np.sum(p) < 1e-8:
                 p = valid / np.sum(valid)
             if use_noise and key == self.root_key:
-                noise = np.random.dirichlet([self.dirichlet_alpha] * len(p))
+                noise = self.rng.dirichlet([self.dirichlet_alpha] * len(p))
                 p = (1 - self.epsilon) * p + self.epsilon * noise
                 p /= np.sum(p)
             self.P[key] = p

@@ -7,18 +7,22 @@ Kept from the reference on purpose: the side to move is inferred from
 ``turn_number % 2`` (player_alpha.py:65), a list board becomes an int (int64)
 array (player_alpha.py:59-62), the search tree persists across calls, and the
 move is argmax(pi) (first index on ties).
+
+The search is the native one (mcts/native_mcts.py, bit-identical to the reference
+search); ``mcts_class`` selects another implementation with the same interface
+(e.g. the pure-Python mcts.new_mcts_alpha.MCTS).
 """
 from __future__ import annotations
 
 import numpy as np
 
 from games.gomoku import Gomoku
-from mcts.new_mcts_alpha import MCTS
+from mcts.native_mcts import NativeMCTS
 
 
 class AlphaPlayer:
     def __init__(self, rules="gomoku", board_size=15, n_simulations=5000, c_puct=1.0, model_path=None,
-                 nn_model=None, mcts_kwargs=None):
+                 nn_model=None, mcts_kwargs=None, mcts_class=None):
         if nn_model is None:
             from network import PyTorchModel
             nn_model = PyTorchModel
@@ -37,7 +41,8 @@ class AlphaPlayer:
         if self.rules != "gomoku":
             raise ValueError(f"Unsupported rules: {self.rules}. Only 'gomoku' is supported.")
         self.game_class = Gomoku
-        self.mcts = MCTS(game_class=self.game_class, n_simulations=self.n_simulations, nn_model=self.net,
+        mcts_class = mcts_class or NativeMCTS
+        self.mcts = mcts_class(game_class=self.game_class, n_simulations=self.n_simulations, nn_model=self.net,
                          cpuct=self.c_puct, add_dirichlet_noise=False, **(mcts_kwargs or {}))
 
     def play(self, board, turn_number, last_opponent_move):

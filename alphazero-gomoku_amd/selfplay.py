@@ -35,11 +35,11 @@ def softmax_temperature(pi: np.ndarray, temp: float) -> np.ndarray:
     return e / np.sum(e)
 
 
-def sample_action_from_pi(pi: np.ndarray, temp: float) -> int:
+def sample_action_from_pi(pi: np.ndarray, temp: float, rng=None) -> int:
     if temp == 0:
         return int(np.argmax(pi))
     p = softmax_temperature(pi, temp)
-    return int(np.random.choice(len(p), p=p))
+    return int((np.random if rng is None else rng).choice(len(p), p=p))
 
 
 def play_game_gen(mcts, game, temp_fn: Callable[[int], float], max_moves: int = 225,
@@ -52,7 +52,7 @@ def play_game_gen(mcts, game, temp_fn: Callable[[int], float], max_moves: int = 
         state_enc = game.get_encoded_state()
         pi = yield from mcts.run_gen(game, len(game.move_history))
         stored_pi = pi.copy()
-        action = sample_action_from_pi(pi, temp_fn(move_number))
+        action = sample_action_from_pi(pi, temp_fn(move_number), getattr(mcts, "rng", None))
         if game.get_valid_moves()[action] != 1.0:       # safety fallback, train.py:380-383
             action = int(np.argmax(pi))
         history.append((state_enc, stored_pi, int(game.current_player)))
@@ -135,22 +135,39 @@ class BatchedSelfPlay:
 def selfplay_games(model, game_class, n_games: int, n_simulations: int, cpuct: float, temp_fn,
                    dirichlet_alpha: float, dirichlet_epsilon: float, dirichlet_n_moves: int,
                    add_dirichlet_noise: bool = True, max_moves: int = 225, use_symmetries: bool = True,
-                   board_size: int = 15, driver: Optional[BatchedSelfPlay] = None):
+                   board_size: int = 15, driver: Optional[BatchedSelfPlay] = None, native: bool = True,
+                   seeds=None):
     """n_games concurrent self-play games (train.py:671-742 semantics per game).
-    Returns (examples, winners {0,1,2: count}, driver)."""
-    from mcts.new_mcts_alpha import MCTS
-    driver = driver or BatchedSelfPlay(model)
-    gens = []
-    for _ in range(n_games):
-        mcts = MCTS(game_class=game_class, n_simulations=n_simulations, nn_model=model, cpuct=cpuct,
-                    dirichlet_alpha=dirichlet_alpha, epsilon=dirichlet_epsilon,
-                    apply_dirichlet_n_first_moves=dirichlet_n_moves, add_dirichlet_noise=add_dirichlet_noise)
-        game = game_class(size=board_size)
-        game.current_player = 1
-        gens.append(play_game_gen(mcts, game, temp_fn, max_moves=max_moves, use_symmetries=use_symmetries))
+    Returns (examples, winners {0,1,2: count}, driver).
+
+    native=True (default): the C++ search (mcts/native_mcts.NativeSelfPlay), every
+    game with its own RandomState seeded from numpy's global RNG (or ``seeds``).
+    native=False: reference-semantics Python searches advanced by BatchedSelfPlay,
+    drawing from numpy's global RNG."""
     examples: List[Example] = []
     winners = {0: 0, 1: 0, 2: 0}
-    for ex, w in driver.run(gens):
+    if native:
+        from mcts.native_mcts import NativeSelfPlay
+        driver = NativeSelfPlay(model.predict, game_class, n_games, n_simulations, cpuct=cpuct,
+                                dirichlet_alpha=dirichlet_alpha, epsilon=dirichlet_epsilon,
+                                apply_dirichlet_n_first_moves=dirichlet_n_moves,
+                                add_dirichlet_noise=add_dirichlet_noise)
+        games = [game_class(size=board_size) for _ in range(n_games)]
+        results = driver.play(temp_fn, max_moves=max_moves, use_symmetries=use_symmetries, seeds=seeds,
+                              games=games)
+    else:
+        from mcts.new_mcts_alpha import MCTS
+        driver = driver or BatchedSelfPlay(model)
+        gens = []
+        for _ in range(n_games):
+            mcts = MCTS(game_class=game_class, n_simulations=n_simulations, nn_model=model, cpuct=cpuct,
+                        dirichlet_alpha=dirichlet_alpha, epsilon=dirichlet_epsilon,
+                        apply_dirichlet_n_first_moves=dirichlet_n_moves, add_dirichlet_noise=add_dirichlet_noise)
+            game = game_class(size=board_size)
+            game.current_player = 1
+            gens.append(play_game_gen(mcts, game, temp_fn, max_moves=max_moves, use_symmetries=use_symmetries))
+        results = driver.run(gens)
+    for ex, w in results:
         examples.extend(ex)
         winners[w] = winners.get(w, 0) + 1
     return examples, winners, driver

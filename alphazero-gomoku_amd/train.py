@@ -59,23 +59,34 @@ def eval_game_gen(mcts_new, mcts_best, game, new_starts: bool):
 
 
 def evaluate_models(model_new: PyTorchModel, model_best: PyTorchModel, game_name: str = "gomoku",
-                    n_games: int = 20, n_simulations: int = 100, cpuct: float = 1.0) -> Tuple[int, float, int]:
+                    n_games: int = 20, n_simulations: int = 100, cpuct: float = 1.0,
+                    native: bool = True) -> Tuple[int, float, int]:
     """(new_wins, win_rate, draws) over n_games (sharded across ranks), each opened
     by one random move in the centre 9x9 (train.py:440-445), new model first on
-    even game indices."""
+    even game indices.  native=True: both searches in C++ (mcts/native_mcts.NativeEval);
+    native=False: Python searches under BatchedSelfPlay."""
     size = model_new.board_size
     center, radius = size // 2, 4
-    gens, starts = [], []
+    games, starts = [], []
     for i in D.shard(n_games):
         game = GameClass(size=size)
         game.do_move((random.randint(center - radius, center + radius), random.randint(center - radius, center + radius)))
-        new_starts = i % 2 == 0
-        mn = MCTS(GameClass, n_simulations, model_new, cpuct=cpuct, add_dirichlet_noise=False)
-        mb = MCTS(GameClass, n_simulations, model_best, cpuct=cpuct, add_dirichlet_noise=False)
-        gens.append(eval_game_gen(mn, mb, game, new_starts))
-        starts.append(new_starts)
-    driver = BatchedSelfPlay({"new": model_new, "best": model_best})
-    winners = driver.run(gens)
+        games.append(game)
+        starts.append(i % 2 == 0)
+    if not games:
+        winners = []
+    elif native:
+        from mcts.native_mcts import NativeEval
+        arena = NativeEval({"new": model_new.predict, "best": model_best.predict}, GameClass, len(games),
+                           n_simulations, cpuct=cpuct)
+        winners = arena.play(games, ["new" if s else "best" for s in starts])
+    else:
+        gens = []
+        for game, new_starts in zip(games, starts):
+            mn = MCTS(GameClass, n_simulations, model_new, cpuct=cpuct, add_dirichlet_noise=False)
+            mb = MCTS(GameClass, n_simulations, model_best, cpuct=cpuct, add_dirichlet_noise=False)
+            gens.append(eval_game_gen(mn, mb, game, new_starts))
+        winners = BatchedSelfPlay({"new": model_new, "best": model_best}).run(gens)
     new_wins = sum(1 for w, s in zip(winners, starts) if (w == 1 and s) or (w == 2 and not s))
     draws = sum(1 for w in winners if w == 0)
     dev = model_new.engine.device
