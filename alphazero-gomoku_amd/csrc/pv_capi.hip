@@ -90,8 +90,6 @@ int32_t azg_pv_bind(azg_pv* h, float* params, float* grads, float* bn_stats)
         floats += (size_t)2 * h->NB * 9 * C * C;   // wpack
         floats += (size_t)27 * C;                  // wstem
         floats += (size_t)h->nfold * 2;            // scale, shift
-        floats += (size_t)2 * PIX * ACTIONS;       // wpfT
-        floats += (size_t)PIX * VHID;              // wv1T
         float* base = nullptr;
         hipError_t e = hipMalloc(&base, floats * sizeof(float));
         if (e != hipSuccess) return fail("azg_pv_bind: hipMalloc(packed weights)", e);
@@ -100,8 +98,6 @@ int32_t azg_pv_bind(azg_pv* h, float* params, float* grads, float* bn_stats)
         h->wstem = base; base += (size_t)27 * C;
         h->scale = base; base += h->nfold;
         h->shift = base; base += h->nfold;
-        h->wpfT = base; base += (size_t)2 * PIX * ACTIONS;
-        h->wv1T = base; base += (size_t)PIX * VHID;
         e = hipMalloc(&h->bn_desc_dev, sizeof(BnDesc) * h->bn_desc.size());
         if (e == hipSuccess)
             e = hipMemcpy(h->bn_desc_dev, h->bn_desc.data(), sizeof(BnDesc) * h->bn_desc.size(), hipMemcpyHostToDevice);
@@ -274,7 +270,7 @@ int32_t ensure_eval_workspace(azg_pv* h, int batch, hipStream_t st)
     h->hbuf = nullptr;
     h->act_cap = 0;
     {
-        hipError_t e = hipMalloc(&h->hbuf, (size_t)cap * 3 * PIX * sizeof(float));
+        hipError_t e = hipMalloc(&h->hbuf, (size_t)cap * (3 * PIX + ACTIONS + VHID) * sizeof(float));
         if (e != hipSuccess) return fail("ensure_eval_workspace: hipMalloc(head features)", e);
     }
     const size_t bytes = (size_t)cap * PADPIX * h->C * sizeof(float);
@@ -300,8 +296,6 @@ int32_t repack(azg_pv* h, hipStream_t st)
         AZG_TRY(launch_pack_conv3x3(P + h->poff[h->t_blk[i].w2], h->wpack + (size_t)(2 * i + 1) * 9 * C * C, C, st),
                 "repack: conv2");
     }
-    AZG_TRY(launch_transpose(P + h->poff[h->t_pfc_w], h->wpfT, ACTIONS, 2 * PIX, st), "repack: policy_fc^T");
-    AZG_TRY(launch_transpose(P + h->poff[h->t_vfc1_w], h->wv1T, VHID, PIX, st), "repack: value_fc1^T");
     AZG_TRY(launch_fold_bn(P, h->bn, h->bn_desc_dev, (int)h->bn_desc.size(), h->scale, h->shift, st),
             "repack: fold_bn");
     return 0;
@@ -340,7 +334,8 @@ int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* 
     const int ho = bd[h->bn_pol].out_off;   // policy (2) then value (1): contiguous
     pr = prof_begin(h, AZG_PROF_HEADS, st);
     AZG_TRY(launch_heads_fwd(C, X, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], h->scale + ho, h->shift + ho,
-                             h->wpfT, P + h->poff[h->t_pfc_b], h->wv1T, P + h->poff[h->t_vfc1_b],
+                             P + h->poff[h->t_pfc_w], P + h->poff[h->t_pfc_b], P + h->poff[h->t_vfc1_w],
+                             P + h->poff[h->t_vfc1_b],
                              P + h->poff[h->t_vfc2_w], P + h->poff[h->t_vfc2_b], h->hbuf, probs, values, logits,
                              batch, st),
             "forward: heads");

@@ -74,8 +74,16 @@ __global__ __launch_bounds__(64 * NW_, NW_ / 2) void conv3x3_mfma(
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
-    const int m0 = blockIdx.x * BM;
-    const int n0 = blockIdx.y * BN;
+    // XCD-aware tile order: workgroup L is dispatched to XCD L % 8, so give each
+    // XCD a contiguous run of logical tiles (N-halves of one M tile adjacent, then
+    // neighbouring M tiles): the input halo rows and the other N-half's A tile are
+    // then L2 hits on the same XCD instead of fabric re-reads.
+    constexpr int NTN = C / BN;
+    const int L = blockIdx.x, nt = gridDim.x;
+    const int xcd = L & 7, q8 = nt >> 3, r8 = nt & 7;
+    const int t = xcd * q8 + min(xcd, r8) + (L >> 3);
+    const int m0 = (t / NTN) * BM;
+    const int n0 = (t % NTN) * BN;
 
     // staging: thread -> (row sr + RPP i, floats sc..sc+3)
     const int sr = tid >> 3, sc = (tid & 7) * 4;
@@ -276,7 +284,7 @@ static hipError_t launch_conv_t(const float* in, const float* wp, const float* s
         if (e != hipSuccess) return e;
         attr_done = true;
     }
-    dim3 grid((M + T::BM - 1) / T::BM, C / T::BN);
+    dim3 grid(((M + T::BM - 1) / T::BM) * (C / T::BN));
     hipLaunchKernelGGL((conv3x3_mfma<C, BN, WM, TM, NW, EPI>), grid, dim3(T::NT), T::LDS_BYTES, st,
                        in, wp, scale, shift, resid, out, M);
     return hipGetLastError();
@@ -375,7 +383,7 @@ static hipError_t launch_ablation(const float* in, const float* wp, const float*
     using T = ConvTile<128, 128, 1, 5, 4>;
     (void)hipFuncSetAttribute((const void*)conv3x3_mfma<128, 128, 1, 5, 4, EPI_BN_RELU, ABL>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS_BYTES);
-    dim3 grid((M + T::BM - 1) / T::BM, 1);
+    dim3 grid((M + T::BM - 1) / T::BM);
     hipLaunchKernelGGL((conv3x3_mfma<128, 128, 1, 5, 4, EPI_BN_RELU, ABL>), grid, dim3(T::NT), T::LDS_BYTES, st,
                        in, wp, scale, shift, resid, out, M);
     return hipGetLastError();

@@ -7,15 +7,14 @@
 //       reads 225*C*4 B per board once; 4 consecutive threads cover one pixel's
 //       C channels (coalesced 128-B quarter rows), partial dots reduced by 2 xor
 //       shuffles.  Also used raw (BN = false) by the train step.
-//   heads_fc_eval: per workgroup HB boards: policy_fc 450->225 (+bias), softmax,
-//       value_fc1 225->64 + ReLU, value_fc2 64->1, tanh.  Each transposed weight
-//       load (coalesced, L2-resident) is reused for HB boards.
+//   small_gemm (pv_gemm.hip) + heads_finalize: policy_fc 450->225 and value_fc1
+//       225->64 as one two-problem fp32-MFMA GEMM launch, then bias, softmax, ReLU,
+//       value_fc2 64->1 and tanh, one wave per board.
 #include "pv_internal.h"
 
 namespace azg {
 
 constexpr int PROJ_ROWS = 64;   // pixels per workgroup in heads_project
-constexpr int HB = 8;           // boards per workgroup in heads_fc_eval
 
 template <int C, bool BN>
 __global__ __launch_bounds__(256) void heads_project(const float* __restrict__ act, const float* __restrict__ wpc,
@@ -64,85 +63,47 @@ __global__ __launch_bounds__(256) void heads_project(const float* __restrict__ a
     }
 }
 
-__global__ __launch_bounds__(256) void heads_fc_eval(
-    const float* __restrict__ feat,   // [B][3*225]: policy features 0..449, value features 450..674
-    const float* __restrict__ wpfT,   // policy_fc.weight^T [450][225]
-    const float* __restrict__ bpf,    // [225]
-    const float* __restrict__ wv1T,   // value_fc1.weight^T [225][64]
-    const float* __restrict__ bv1,    // [64]
-    const float* __restrict__ wv2,    // [64]
-    const float* __restrict__ bv2,    // [1]
-    float* __restrict__ probs, float* __restrict__ values, float* __restrict__ logits, int B)
+constexpr int FC_OUT = ACTIONS + VHID;           // pre[b] = [policy logits (225) | value hidden (64)]
+
+// Per board (one wave): logits = pre + bias, softmax; value = tanh(relu(pre_v + b1) . w2 + b2).
+__global__ __launch_bounds__(256) void heads_finalize(const float* __restrict__ pre, const float* __restrict__ bpf,
+                                                      const float* __restrict__ bv1, const float* __restrict__ wv2,
+                                                      const float* __restrict__ bv2, float* __restrict__ probs,
+                                                      float* __restrict__ values, float* __restrict__ logits, int B)
 {
-    __shared__ float f[HB][3 * PIX];
-    __shared__ float lg[HB][ACTIONS];
-    __shared__ float hid[HB][VHID];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int b0 = blockIdx.x * HB;
-    const int nb = min(HB, B - b0);
-    for (int i = tid; i < HB * 3 * PIX; i += 256) {
-        const int g = i / (3 * PIX);
-        f[g][i - g * 3 * PIX] = g < nb ? feat[(size_t)b0 * 3 * PIX + i] : 0.f;
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= B) return;
+    const float* pb = pre + (size_t)b * FC_OUT;
+    float lg[4];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int j = lane + 64 * t;
+        lg[t] = j < ACTIONS ? pb[j] + bpf[j] : -INFINITY;
+        mx = fmaxf(mx, lg[t]);
     }
-    __syncthreads();
-    if (tid < ACTIONS) {
-        float acc[HB];
+    mx = wave_max(mx);
+    float e[4], sum = 0.f;
 #pragma unroll
-        for (int g = 0; g < HB; ++g) acc[g] = 0.f;
-#pragma unroll 4
-        for (int k = 0; k < 2 * PIX; ++k) {
-            const float wk = wpfT[k * ACTIONS + tid];
-#pragma unroll
-            for (int g = 0; g < HB; ++g) acc[g] = fmaf(wk, f[g][k], acc[g]);
-        }
-        const float bias = bpf[tid];
-#pragma unroll
-        for (int g = 0; g < HB; ++g) lg[g][tid] = acc[g] + bias;
+    for (int t = 0; t < 4; ++t) {
+        const int j = lane + 64 * t;
+        e[t] = j < ACTIONS ? expf(lg[t] - mx) : 0.f;
+        sum += e[t];
     }
-    {
-        // value hidden layer: thread -> unit i = tid % 64, boards (tid / 64) + 4 j
-        const int i = tid & 63, gq = tid >> 6;
-        constexpr int GPT = HB / 4;
-        float acc[GPT];
+    sum = wave_sum(sum);
+    const float inv = 1.f / sum;
 #pragma unroll
-        for (int j = 0; j < GPT; ++j) acc[j] = 0.f;
-#pragma unroll 4
-        for (int k = 0; k < PIX; ++k) {
-            const float wk = wv1T[k * VHID + i];
-#pragma unroll
-            for (int j = 0; j < GPT; ++j) acc[j] = fmaf(wk, f[gq + 4 * j][2 * PIX + k], acc[j]);
+    for (int t = 0; t < 4; ++t) {
+        const int j = lane + 64 * t;
+        if (j < ACTIONS) {
+            probs[(size_t)b * ACTIONS + j] = e[t] * inv;
+            if (logits) logits[(size_t)b * ACTIONS + j] = lg[t];
         }
-#pragma unroll
-        for (int j = 0; j < GPT; ++j) hid[gq + 4 * j][i] = fmaxf(acc[j] + bv1[i], 0.f);
     }
-    __syncthreads();
-    // softmax + value: wave w handles boards w, w+4, ...
-    for (int g = wid; g < nb; g += 4) {
-        const int b = b0 + g;
-        float mx = -INFINITY;
-        for (int j = lane; j < ACTIONS; j += 64) mx = fmaxf(mx, lg[g][j]);
-        mx = wave_max(mx);
-        float e[4];
-        float sum = 0.f;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int j = lane + 64 * t;
-            e[t] = j < ACTIONS ? expf(lg[g][j] - mx) : 0.f;
-            sum += e[t];
-        }
-        sum = wave_sum(sum);
-        const float inv = 1.f / sum;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int j = lane + 64 * t;
-            if (j < ACTIONS) {
-                probs[(size_t)b * ACTIONS + j] = e[t] * inv;
-                if (logits) logits[(size_t)b * ACTIONS + j] = lg[g][j];
-            }
-        }
-        const float v = wave_sum(hid[g][lane] * wv2[lane]) + bv2[0];
-        if (lane == 0) values[b] = tanhf(v);
-    }
+    const float hid = fmaxf(pb[ACTIONS + lane] + bv1[lane], 0.f);
+    const float v = wave_sum(hid * wv2[lane]) + bv2[0];
+    if (lane == 0) values[b] = tanhf(v);
 }
 
 hipError_t launch_heads_project(int C, bool bn, const float* act, const float* wpc, const float* wvc,
@@ -164,14 +125,20 @@ hipError_t launch_heads_project(int C, bool bn, const float* act, const float* w
 }
 
 hipError_t launch_heads_fwd(int C, const float* act, const float* wpc, const float* wvc, const float* hscale,
-                            const float* hshift, const float* wpfT, const float* bpf, const float* wv1T,
+                            const float* hshift, const float* wpf, const float* bpf, const float* wv1,
                             const float* bv1, const float* wv2, const float* bv2, float* hbuf, float* probs,
                             float* values, float* logits, int B, hipStream_t st)
 {
     hipError_t e = launch_heads_project(C, true, act, wpc, wvc, hscale, hshift, hbuf, B * PIX, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(heads_fc_eval, dim3((B + HB - 1) / HB), dim3(256), 0, st, hbuf, wpfT, bpf, wv1T, bv1, wv2,
-                       bv2, probs, values, logits, B);
+    float* pre = hbuf + (size_t)B * 3 * PIX;
+    // policy_fc: pre[b][j] = sum_k feat[b][k] wpf[j][k] (k < 450); value_fc1 on feat[b][450..674]
+    GemmProb gp{hbuf, 3 * PIX, 1, wpf, 1, 2 * PIX, pre, FC_OUT, 1, nullptr, 0, 0, B, ACTIONS, 2 * PIX};
+    GemmProb gv{hbuf + 2 * PIX, 3 * PIX, 1, wv1, 1, PIX, pre + ACTIONS, FC_OUT, 1, nullptr, 0, 0, B, VHID, PIX};
+    e = launch_small_gemm(gp, &gv, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(heads_finalize, dim3((B + 3) / 4), dim3(256), 0, st, pre, bpf, bv1, wv2, bv2, probs, values,
+                       logits, B);
     return hipGetLastError();
 }
 

@@ -17,6 +17,17 @@ struct BnDesc {
 };
 
 struct BlockTensors { int w1, g1, b1, w2, g2, b2; };
+
+// strided fp32 GEMM problem (pv_gemm.hip): C(i,j) = sum_k A(i,k) B(k,j), optionally
+// zeroed where mask(i,j) <= 0
+struct GemmProb {
+    const float* A; int sai, sak;
+    const float* B; int sbk, sbj;
+    float* C; int sci, scj;
+    const float* mask; int smi, smj;
+    int M, N, K;
+};
+struct GemmPair { GemmProb p[2]; int ntn0; };
 struct BlockBn { int first, second; };
 
 // kernel launchers (pv_conv.hip, pv_heads.hip, pv_pack.hip, pv_train.hip)
@@ -25,12 +36,13 @@ hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, cons
 hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const float* scale,
                        const float* shift, float* out, int B, hipStream_t st);
 hipError_t launch_heads_fwd(int C, const float* act, const float* wpc, const float* wvc,
-                            const float* hscale, const float* hshift, const float* wpfT,
-                            const float* bpf, const float* wv1T, const float* bv1,
+                            const float* hscale, const float* hshift, const float* wpf,
+                            const float* bpf, const float* wv1, const float* bv1,
                             const float* wv2, const float* bv2, float* hbuf, float* probs,
                             float* values, float* logits, int B, hipStream_t st);
 hipError_t launch_heads_project(int C, bool bn, const float* act, const float* wpc, const float* wvc,
                                 const float* hscale, const float* hshift, float* hout, int M, hipStream_t st);
+hipError_t launch_small_gemm(const GemmProb& p0, const GemmProb* p1, hipStream_t st);
 hipError_t launch_pack_conv3x3(const float* w, float* wp, int C, hipStream_t st);
 hipError_t launch_pack_dgrad(const float* w, float* wd, int C, hipStream_t st);
 hipError_t launch_pack_stem(const float* w, float* ws, int C, hipStream_t st);
@@ -69,8 +81,6 @@ struct azg_pv {
     float* wstem = nullptr;   // [27][C]
     float* scale = nullptr;   // folded BN (eval)
     float* shift = nullptr;
-    float* wpfT = nullptr;    // [450][225]
-    float* wv1T = nullptr;    // [225][64]
 
     // eval activations: 3 padded NHWC buffers + head features [B][3][225]
     float* act[3] = {nullptr, nullptr, nullptr};

@@ -25,7 +25,8 @@ namespace azg {
 hipError_t launch_wgrad(int C, const float* dz, const float* x, float* slab, float* dw, int M, int S, int rps,
                         hipStream_t st);
 
-constexpr int TROWS = 128;   // rows per statistics tile
+constexpr int TROWS = 64;    // rows per statistics tile (BN stats / BN backward partials)
+constexpr int HROWS = 128;   // rows per tile of the head-projection backward partials
 
 struct TrainWS {
     int cap = 0;
@@ -47,6 +48,8 @@ struct TrainWS {
     // heads
     float *zh = nullptr, *fp = nullptr, *fv = nullptr, *hv = nullptr, *dpre = nullptr;
     float *dlogits = nullptr, *dfp = nullptr, *dfv = nullptr, *dhv = nullptr, *dzh = nullptr, *lossb = nullptr;
+    float *lpre = nullptr, *hpre = nullptr, *hbw = nullptr;   // FC pre-activations, head BN bwd coefficients
+    double* hspart = nullptr;                                 // head BN (channel, chunk) partials
     // optimizer
     double* npart = nullptr;     // grad sq-sum partials
     float* scal = nullptr;       // [0] total norm, [1] clip coef
@@ -83,36 +86,52 @@ __device__ __forceinline__ double block_sum_d(double v, double* red)
     return s;
 }
 
-// per-tile column (mean, M2) of a padded NHWC tensor (two passes over the tile)
+// per-tile column (mean, M2) of a padded NHWC tensor.  Thread = 4 consecutive
+// channels (f32x4) x RPT rows held in registers: one HBM read, two passes from
+// registers (exact two-pass M2 per tile), fixed-order LDS reduction.
 template <int C>
 __global__ __launch_bounds__(256) void col_stats_kernel(const float* __restrict__ z, float* __restrict__ pmean,
                                                         float* __restrict__ pm2, int M)
 {
-    constexpr int TPC = 256 / C;
-    __shared__ float red[256];
-    const int c = threadIdx.x % C, rg = threadIdx.x / C;
+    constexpr int Q = C / 4, RG = 256 / Q, RPT = TROWS / RG;
+    __shared__ f32x4 red[RG][Q];
+    const int q = threadIdx.x % Q, rg = threadIdx.x / Q;
     const int m0 = blockIdx.x * TROWS;
     const int rows = min(TROWS, M - m0);
-    float s = 0.f;
-    for (int r = rg; r < rows; r += TPC) s += z[pad_off(m0 + r, C) + c];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    float tot = 0.f;
-    for (int g = 0; g < TPC; ++g) tot += red[g * C + c];
-    const float mean = tot / (float)rows;
-    __syncthreads();
-    float q = 0.f;
-    for (int r = rg; r < rows; r += TPC) {
-        const float d = z[pad_off(m0 + r, C) + c] - mean;
-        q = fmaf(d, d, q);
+    f32x4 v[RPT];
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+        const int r = rg + RG * i;
+        v[i] = r < rows ? *(const f32x4*)(z + pad_off(m0 + r, C) + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+        s += v[i];
     }
-    red[threadIdx.x] = q;
+    red[rg][q] = s;
+    __syncthreads();
+    f32x4 tot = red[0][q];
+    for (int g = 1; g < RG; ++g) tot += red[g][q];
+    f32x4 mean;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) mean[k] = tot[k] / (float)rows;
+    __syncthreads();
+    f32x4 m2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+        if (rg + RG * i < rows) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float d = v[i][k] - mean[k];
+                m2[k] = fmaf(d, d, m2[k]);
+            }
+        }
+    }
+    red[rg][q] = m2;
     __syncthreads();
     if (rg == 0) {
-        float m2 = 0.f;
-        for (int g = 0; g < TPC; ++g) m2 += red[g * C + c];
-        pmean[blockIdx.x * C + c] = mean;
-        pm2[blockIdx.x * C + c] = m2;
+        f32x4 t = red[0][q];
+        for (int g = 1; g < RG; ++g) t += red[g][q];
+        *(f32x4*)(pmean + (size_t)blockIdx.x * C + 4 * q) = mean;
+        *(f32x4*)(pm2 + (size_t)blockIdx.x * C + 4 * q) = t;
     }
 }
 
@@ -184,7 +203,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
     }
 }
 
-// BN backward partial sums per tile: dy = g * (act > 0); S dy, S (z-mean) dy
+// BN backward partial sums per tile: dy = g * (act > 0); S dy, S (z-mean) dy.
+// Same thread layout as col_stats_kernel (f32x4 channels, fixed-order reduction).
 template <int C>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ g,
                                                             const float* __restrict__ act,
@@ -192,30 +212,40 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
                                                             const float* __restrict__ mean, float* __restrict__ pa,
                                                             float* __restrict__ pb, int M)
 {
-    constexpr int TPC = 256 / C;
-    __shared__ float red[2][256];
-    const int c = threadIdx.x % C, rg = threadIdx.x / C;
+    constexpr int Q = C / 4, RG = 256 / Q, RPT = TROWS / RG;
+    __shared__ f32x4 red[2][RG][Q];
+    const int q = threadIdx.x % Q, rg = threadIdx.x / Q;
     const int m0 = blockIdx.x * TROWS;
     const int rows = min(TROWS, M - m0);
-    const float mu = mean[c];
-    float s = 0.f, q = 0.f;
-    for (int r = rg; r < rows; r += TPC) {
-        const int o = pad_off(m0 + r, C) + c;
-        const float dy = act[o] > 0.f ? g[o] : 0.f;
-        s += dy;
-        q = fmaf(z[o] - mu, dy, q);
+    const f32x4 mu = *(const f32x4*)(mean + 4 * q);
+    f32x4 s = {0.f, 0.f, 0.f, 0.f}, d2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+        const int r = rg + RG * i;
+        if (r < rows) {
+            const int o = pad_off(m0 + r, C) + 4 * q;
+            const f32x4 gv = *(const f32x4*)(g + o);
+            const f32x4 av = *(const f32x4*)(act + o);
+            const f32x4 zv = *(const f32x4*)(z + o);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float dy = av[k] > 0.f ? gv[k] : 0.f;
+                s[k] += dy;
+                d2[k] = fmaf(zv[k] - mu[k], dy, d2[k]);
+            }
+        }
     }
-    red[0][threadIdx.x] = s;
-    red[1][threadIdx.x] = q;
+    red[0][rg][q] = s;
+    red[1][rg][q] = d2;
     __syncthreads();
     if (rg == 0) {
-        float a = 0.f, b = 0.f;
-        for (int k = 0; k < TPC; ++k) {
-            a += red[0][k * C + c];
-            b += red[1][k * C + c];
+        f32x4 a = red[0][0][q], b = red[1][0][q];
+        for (int k = 1; k < RG; ++k) {
+            a += red[0][k][q];
+            b += red[1][k][q];
         }
-        pa[blockIdx.x * C + c] = a;
-        pb[blockIdx.x * C + c] = b;
+        *(f32x4*)(pa + (size_t)blockIdx.x * C + 4 * q) = a;
+        *(f32x4*)(pb + (size_t)blockIdx.x * C + 4 * q) = b;
     }
 }
 
@@ -275,268 +305,267 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     }
 }
 
-// head BN stats (3 channels over B*225), two-pass in double; one block per channel
-__global__ __launch_bounds__(256) void head_stats_kernel(const float* __restrict__ zh, int B, const BnDesc* desc,
-                                                         int pol_layer, int val_layer,
-                                                         const float* __restrict__ params,
-                                                         float* __restrict__ stats, float* __restrict__ bmean,
-                                                         float* __restrict__ binv, float* __restrict__ bscale,
-                                                         float* __restrict__ bshift)
+// ---- heads (policy_conv/value_conv 1x1 -> BN -> ReLU -> FCs), train mode ----
+constexpr int HSC = 32;   // chunks per head channel for the head BN reductions
+
+__device__ __forceinline__ double wave_sum_d(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// per (channel, chunk): S z, S z^2 in double over the chunk of the B*225 pixels
+__global__ __launch_bounds__(256) void head_stats_partial_kernel(const float* __restrict__ zh, int B,
+                                                                 double* __restrict__ part)
 {
     __shared__ double red[8];
-    const int ch = blockIdx.x;
-    const BnDesc d = desc[ch < 2 ? pol_layer : val_layer];
-    const int c = ch < 2 ? ch : 0;
+    const int ch = blockIdx.x, chunk = blockIdx.y;
     const int N = B * PIX;
-    double s = 0.0;
-    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    const int i0 = (int)((int64_t)chunk * N / HSC), i1 = (int)((int64_t)(chunk + 1) * N / HSC);
+    double s = 0.0, ss = 0.0;
+    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
         const int b = i / PIX, p = i - b * PIX;
-        s += (double)zh[(b * 3 + ch) * PIX + p];
+        const double v = (double)zh[(b * 3 + ch) * PIX + p];
+        s += v;
+        ss += v * v;
     }
     s = block_sum_d(s, red);
-    const double mean = s / (double)N;
-    double q = 0.0;
-    for (int i = threadIdx.x; i < N; i += blockDim.x) {
-        const int b = i / PIX, p = i - b * PIX;
-        const double dd = (double)zh[(b * 3 + ch) * PIX + p] - mean;
-        q += dd * dd;
-    }
-    q = block_sum_d(q, red);
+    ss = block_sum_d(ss, red);
     if (threadIdx.x == 0) {
-        const double var = q / (double)N;
-        const float mean_f = (float)mean;
-        const float inv_f = (float)(1.0 / sqrt(var + (double)BN_EPS));
-        const float alpha = inv_f * params[d.gamma_off + c];
-        bmean[d.out_off + c] = mean_f;
-        binv[d.out_off + c] = inv_f;
-        bscale[d.out_off + c] = alpha;
-        bshift[d.out_off + c] = params[d.beta_off + c] - mean_f * alpha;
-        const double unb = N > 1 ? q / (double)(N - 1) : var;
-        float* rm = stats + d.stat_off;
-        float* rv = stats + d.stat_off + d.c;
-        rm[c] = (float)((double)BN_MOMENTUM * mean + (1.0 - (double)BN_MOMENTUM) * (double)rm[c]);
-        rv[c] = (float)((double)BN_MOMENTUM * unb + (1.0 - (double)BN_MOMENTUM) * (double)rv[c]);
+        part[(ch * HSC + chunk) * 2 + 0] = s;
+        part[(ch * HSC + chunk) * 2 + 1] = ss;
     }
 }
 
-struct HeadsArgs {
-    const float* zh;
-    const float* hscale;   // [3]: policy ch0, ch1, value (folded train BN)
-    const float* hshift;
-    const float* wpf;      // policy_fc.weight [225][450]
-    const float* wpfT;     // [450][225]
-    const float* bpf;
-    const float* wv1;      // value_fc1.weight [64][225]
-    const float* wv1T;     // [225][64]
-    const float* bv1;
-    const float* wv2;      // [64]
-    const float* bv2;
-    const float* pis;      // [B][225]
-    const float* zs;       // [B]
-    float* fp;
-    float* fv;
-    float* hv;
-    float* dpre;
-    float* dlogits;
-    float* dfp;
-    float* dfv;
-    float* dhv;
-    float* lossb;          // [B][2]
-    int B;
-};
-
-// per board: head forward (train BN), loss terms, and the backward down to the
-// (masked) post-BN head features.  One 256-thread workgroup per board.
-__global__ __launch_bounds__(256) void heads_train_kernel(HeadsArgs a)
+// batch stats of the 3 head BN channels -> folded coefficients + running stats
+__global__ void head_stats_finalize_kernel(const double* __restrict__ part, int B, const BnDesc* desc, int pol_layer,
+                                           int val_layer, const float* __restrict__ params,
+                                           float* __restrict__ stats, float* __restrict__ bmean,
+                                           float* __restrict__ binv, float* __restrict__ bscale,
+                                           float* __restrict__ bshift)
 {
-    __shared__ float sfp[2 * PIX];
-    __shared__ float sfv[PIX];
-    __shared__ float slog[ACTIONS];
-    __shared__ float sdl[ACTIONS];
-    __shared__ float shv[VHID];
-    __shared__ float sdhv[VHID];
-    __shared__ float red[8];
-    __shared__ float sv;
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const float* zb = a.zh + (size_t)b * 3 * PIX;
-    for (int k = tid; k < 3 * PIX; k += 256) {
-        const int ch = k / PIX;
-        const float y = fmaxf(zb[k] * a.hscale[ch] + a.hshift[ch], 0.f);
-        if (ch < 2) {
-            sfp[k] = y;
-            a.fp[(size_t)b * 2 * PIX + k] = y;
-        } else {
-            sfv[k - 2 * PIX] = y;
-            a.fv[(size_t)b * PIX + k - 2 * PIX] = y;
-        }
+    const int ch = threadIdx.x;
+    if (ch >= 3) return;
+    const BnDesc d = desc[ch < 2 ? pol_layer : val_layer];
+    const int c = ch < 2 ? ch : 0;
+    const double N = (double)B * PIX;
+    double s = 0.0, ss = 0.0;
+    for (int k = 0; k < HSC; ++k) {
+        s += part[(ch * HSC + k) * 2 + 0];
+        ss += part[(ch * HSC + k) * 2 + 1];
     }
-    __syncthreads();
-    // logits (threads < 225) and value hidden layer (threads < 64)
-    if (tid < ACTIONS) {
-        float acc = 0.f;
-        for (int k = 0; k < 2 * PIX; ++k) acc = fmaf(a.wpfT[k * ACTIONS + tid], sfp[k], acc);
-        slog[tid] = acc + a.bpf[tid];
-    }
-    if (tid < VHID) {
-        float acc = 0.f;
-        for (int k = 0; k < PIX; ++k) acc = fmaf(a.wv1T[k * VHID + tid], sfv[k], acc);
-        shv[tid] = fmaxf(acc + a.bv1[tid], 0.f);
-    }
-    __syncthreads();
-    if (wid == 0) {
-        // log_softmax, KL term, dlogits
-        float mx = -INFINITY;
-        for (int j = lane; j < ACTIONS; j += 64) mx = fmaxf(mx, slog[j]);
-        mx = wave_max(mx);
-        float se = 0.f;
-        for (int j = lane; j < ACTIONS; j += 64) se += expf(slog[j] - mx);
-        se = wave_sum(se);
-        const float lse = logf(se);
-        const float* t = a.pis + (size_t)b * ACTIONS;
-        float kl = 0.f, st = 0.f;
-        for (int j = lane; j < ACTIONS; j += 64) {
-            const float tj = t[j];
-            const float lp = (slog[j] - mx) - lse;
-            if (tj > 0.f) kl += tj * (logf(tj) - lp);
-            st += tj;
-        }
-        kl = wave_sum(kl);
-        st = wave_sum(st);
-        const float invB = 1.f / (float)a.B;
-        for (int j = lane; j < ACTIONS; j += 64) {
-            const float lp = (slog[j] - mx) - lse;
-            const float d = (expf(lp) * st - t[j]) * invB;
-            sdl[j] = d;
-            a.dlogits[(size_t)b * ACTIONS + j] = d;
-        }
-        if (lane == 0) a.lossb[b * 2 + 0] = kl;
-    } else if (wid == 1) {
-        // value: v = tanh(w2.hv + b2); (v-z)^2; dpre = 2(v-z)/B (1-v^2)
-        float pre = wave_sum(a.wv2[lane] * shv[lane]) + a.bv2[0];
-        const float v = tanhf(pre);
-        const float z = a.zs[b];
-        const float dv = 2.f * (v - z) / (float)a.B;
-        const float dp = dv * (1.f - v * v);
-        const float dh = shv[lane] > 0.f ? dp * a.wv2[lane] : 0.f;
-        sdhv[lane] = dh;
-        a.dhv[(size_t)b * VHID + lane] = dh;
-        a.hv[(size_t)b * VHID + lane] = shv[lane];
-        if (lane == 0) {
-            a.lossb[b * 2 + 1] = (v - z) * (v - z);
-            a.dpre[b] = dp;
-            sv = v;
-        }
-    }
-    __syncthreads();
-    // dfp[k] = (S_j Wpf[j][k] dl_j) * (fp>0);  dfv[k] = (S_i Wv1[i][k] dhv_i) * (fv>0)
-    for (int k = tid; k < 2 * PIX; k += 256) {
-        float acc = 0.f;
-        for (int j = 0; j < ACTIONS; ++j) acc = fmaf(a.wpf[j * 2 * PIX + k], sdl[j], acc);
-        a.dfp[(size_t)b * 2 * PIX + k] = sfp[k] > 0.f ? acc : 0.f;
-    }
-    for (int k = tid; k < PIX; k += 256) {
-        float acc = 0.f;
-        for (int i = 0; i < VHID; ++i) acc = fmaf(a.wv1[i * PIX + k], sdhv[i], acc);
-        a.dfv[(size_t)b * PIX + k] = sfv[k] > 0.f ? acc : 0.f;
-    }
-    (void)red;
-    (void)sv;
+    const double mean = s / N;
+    double q = ss - s * mean;              // S (z - mean)^2
+    q = q > 0.0 ? q : 0.0;
+    const double var = q / N;
+    const float mean_f = (float)mean;
+    const float inv_f = (float)(1.0 / sqrt(var + (double)BN_EPS));
+    const float alpha = inv_f * params[d.gamma_off + c];
+    bmean[d.out_off + c] = mean_f;
+    binv[d.out_off + c] = inv_f;
+    bscale[d.out_off + c] = alpha;
+    bshift[d.out_off + c] = params[d.beta_off + c] - mean_f * alpha;
+    const double unb = N > 1 ? q / (N - 1.0) : var;
+    float* rm = stats + d.stat_off;
+    float* rv = stats + d.stat_off + d.c;
+    rm[c] = (float)((double)BN_MOMENTUM * mean + (1.0 - (double)BN_MOMENTUM) * (double)rm[c]);
+    rv[c] = (float)((double)BN_MOMENTUM * unb + (1.0 - (double)BN_MOMENTUM) * (double)rv[c]);
 }
 
-// FC weight/bias grads of the heads + the loss means.
-__global__ __launch_bounds__(256) void heads_wgrad_kernel(const float* __restrict__ dlogits,
-                                                          const float* __restrict__ fp,
-                                                          const float* __restrict__ dhv,
-                                                          const float* __restrict__ fv,
-                                                          const float* __restrict__ dpre,
-                                                          const float* __restrict__ hv,
-                                                          const float* __restrict__ lossb, int B,
-                                                          float* __restrict__ g_pfw, float* __restrict__ g_pfb,
-                                                          float* __restrict__ g_v1w, float* __restrict__ g_v1b,
-                                                          float* __restrict__ g_v2w, float* __restrict__ g_v2b,
-                                                          float* __restrict__ losses)
+// fp[b][0..449] = relu(BN(zh policy)), fv[b][0..224] = relu(BN(zh value))
+__global__ __launch_bounds__(256) void head_bn_apply_kernel(const float* __restrict__ zh,
+                                                            const float* __restrict__ hscale,
+                                                            const float* __restrict__ hshift, float* __restrict__ fp,
+                                                            float* __restrict__ fv, int B)
 {
-    const int n_pfw = ACTIONS * 2 * PIX, n_v1w = VHID * PIX;
-    const int total = n_pfw + ACTIONS + n_v1w + VHID + VHID + 1;
+    const int total = B * 3 * PIX;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-        float s = 0.f;
-        if (i < n_pfw) {
-            const int j = i / (2 * PIX), k = i - j * 2 * PIX;
-            for (int b = 0; b < B; ++b) s = fmaf(dlogits[b * ACTIONS + j], fp[b * 2 * PIX + k], s);
-            g_pfw[i] = s;
-        } else if (i < n_pfw + ACTIONS) {
-            const int j = i - n_pfw;
-            for (int b = 0; b < B; ++b) s += dlogits[b * ACTIONS + j];
-            g_pfb[j] = s;
-        } else if (i < n_pfw + ACTIONS + n_v1w) {
-            const int r = i - n_pfw - ACTIONS;
-            const int u = r / PIX, k = r - u * PIX;
-            for (int b = 0; b < B; ++b) s = fmaf(dhv[b * VHID + u], fv[b * PIX + k], s);
-            g_v1w[r] = s;
-        } else if (i < n_pfw + ACTIONS + n_v1w + VHID) {
-            const int u = i - n_pfw - ACTIONS - n_v1w;
-            for (int b = 0; b < B; ++b) s += dhv[b * VHID + u];
-            g_v1b[u] = s;
-        } else if (i < n_pfw + ACTIONS + n_v1w + 2 * VHID) {
-            const int u = i - n_pfw - ACTIONS - n_v1w - VHID;
-            for (int b = 0; b < B; ++b) s = fmaf(dpre[b], hv[b * VHID + u], s);
-            g_v2w[u] = s;
-        } else {
-            for (int b = 0; b < B; ++b) s += dpre[b];
-            g_v2b[0] = s;
-            double pl = 0.0, vl = 0.0;
-            for (int b = 0; b < B; ++b) {
-                pl += (double)lossb[2 * b];
-                vl += (double)lossb[2 * b + 1];
-            }
+        const int b = i / (3 * PIX), k = i - b * 3 * PIX;
+        const int ch = k / PIX;
+        const float y = fmaxf(zh[i] * hscale[ch] + hshift[ch], 0.f);
+        if (ch < 2) fp[(size_t)b * 2 * PIX + k] = y;
+        else fv[(size_t)b * PIX + k - 2 * PIX] = y;
+    }
+}
+
+// per board (one wave): log_softmax, KL term and dlogits; value head tail, (v-z)^2,
+// dpre = 2(v-z)/B (1-v^2) and the masked value-hidden gradient.
+__global__ __launch_bounds__(256) void heads_loss_kernel(
+    const float* __restrict__ lpre, const float* __restrict__ bpf, const float* __restrict__ hpre,
+    const float* __restrict__ bv1, const float* __restrict__ wv2, const float* __restrict__ bv2,
+    const float* __restrict__ pis, const float* __restrict__ zs, float* __restrict__ dlogits,
+    float* __restrict__ hv, float* __restrict__ dhv, float* __restrict__ dpre, float* __restrict__ lossb, int B)
+{
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= B) return;
+    float lg[4];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int j = lane + 64 * t;
+        lg[t] = j < ACTIONS ? lpre[(size_t)b * ACTIONS + j] + bpf[j] : -INFINITY;
+        mx = fmaxf(mx, lg[t]);
+    }
+    mx = wave_max(mx);
+    float se = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        if (lane + 64 * t < ACTIONS) se += expf(lg[t] - mx);
+    se = wave_sum(se);
+    const float lse = logf(se);
+    const float* tp = pis + (size_t)b * ACTIONS;
+    float kl = 0.f, st = 0.f, tv[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int j = lane + 64 * t;
+        tv[t] = j < ACTIONS ? tp[j] : 0.f;
+        if (j < ACTIONS) {
+            const float lp = (lg[t] - mx) - lse;
+            if (tv[t] > 0.f) kl += tv[t] * (logf(tv[t]) - lp);
+            st += tv[t];
+        }
+    }
+    kl = wave_sum(kl);
+    st = wave_sum(st);
+    const float invB = 1.f / (float)B;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int j = lane + 64 * t;
+        if (j < ACTIONS) {
+            const float lp = (lg[t] - mx) - lse;
+            dlogits[(size_t)b * ACTIONS + j] = (expf(lp) * st - tv[t]) * invB;
+        }
+    }
+    const float hid = fmaxf(hpre[(size_t)b * VHID + lane] + bv1[lane], 0.f);
+    const float pre = wave_sum(wv2[lane] * hid) + bv2[0];
+    const float v = tanhf(pre);
+    const float z = zs[b];
+    const float dv = 2.f * (v - z) / (float)B;
+    const float dp = dv * (1.f - v * v);
+    hv[(size_t)b * VHID + lane] = hid;
+    dhv[(size_t)b * VHID + lane] = hid > 0.f ? dp * wv2[lane] : 0.f;
+    if (lane == 0) {
+        lossb[b * 2 + 0] = kl;
+        lossb[b * 2 + 1] = (v - z) * (v - z);
+        dpre[b] = dp;
+    }
+}
+
+// bias / value_fc2 gradients and the loss means: one wave per output (fixed order)
+constexpr int HSG_OUT = ACTIONS + VHID + VHID + 2;
+__global__ __launch_bounds__(256) void heads_small_grads_kernel(
+    const float* __restrict__ dlogits, const float* __restrict__ dhv, const float* __restrict__ dpre,
+    const float* __restrict__ hv, const float* __restrict__ lossb, int B, float* __restrict__ g_pfb,
+    float* __restrict__ g_v1b, float* __restrict__ g_v2w, float* __restrict__ g_v2b, float* __restrict__ losses)
+{
+    const int lane = threadIdx.x & 63;
+    const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (o >= HSG_OUT) return;
+    if (o == HSG_OUT - 1) {
+        double pl = 0.0, vl = 0.0;
+        for (int b = lane; b < B; b += 64) {
+            pl += (double)lossb[2 * b];
+            vl += (double)lossb[2 * b + 1];
+        }
+        pl = wave_sum_d(pl);
+        vl = wave_sum_d(vl);
+        if (lane == 0) {
             const float plf = (float)(pl / (double)B), vlf = (float)(vl / (double)B);
             losses[0] = plf;
             losses[1] = vlf;
             losses[2] = plf + vlf;
         }
+        return;
+    }
+    float s = 0.f;
+    if (o < ACTIONS) {
+        for (int b = lane; b < B; b += 64) s += dlogits[(size_t)b * ACTIONS + o];
+    } else if (o < ACTIONS + VHID) {
+        const int u = o - ACTIONS;
+        for (int b = lane; b < B; b += 64) s += dhv[(size_t)b * VHID + u];
+    } else if (o < ACTIONS + 2 * VHID) {
+        const int u = o - ACTIONS - VHID;
+        for (int b = lane; b < B; b += 64) s = fmaf(dpre[b], hv[(size_t)b * VHID + u], s);
+    } else {
+        for (int b = lane; b < B; b += 64) s += dpre[b];
+    }
+    s = wave_sum(s);
+    if (lane == 0) {
+        if (o < ACTIONS) g_pfb[o] = s;
+        else if (o < ACTIONS + VHID) g_v1b[o - ACTIONS] = s;
+        else if (o < ACTIONS + 2 * VHID) g_v2w[o - ACTIONS - VHID] = s;
+        else g_v2b[0] = s;
     }
 }
 
-// head BN backward (3 channels): grads of gamma/beta and dzh.  One block per channel.
-__global__ __launch_bounds__(256) void head_bn_bwd_kernel(const float* __restrict__ zh,
-                                                          const float* __restrict__ dfp,
-                                                          const float* __restrict__ dfv, int B,
-                                                          const BnDesc* desc, int pol_layer, int val_layer,
-                                                          const float* __restrict__ params,
-                                                          float* __restrict__ grads, const float* __restrict__ bmean,
-                                                          const float* __restrict__ binv, float* __restrict__ dzh)
+// head BN backward, (channel, chunk) partials: S dy, S (z-mean) dy in double
+__global__ __launch_bounds__(256) void head_bn_bwd_partial_kernel(const float* __restrict__ zh,
+                                                                  const float* __restrict__ dfp,
+                                                                  const float* __restrict__ dfv, int B,
+                                                                  const float* __restrict__ hmean,
+                                                                  double* __restrict__ part)
 {
     __shared__ double red[8];
-    const int ch = blockIdx.x;
-    const BnDesc d = desc[ch < 2 ? pol_layer : val_layer];
-    const int c = ch < 2 ? ch : 0;
+    const int ch = blockIdx.x, chunk = blockIdx.y;
     const int N = B * PIX;
-    const float mu = bmean[d.out_off + c], inv = binv[d.out_off + c];
-    auto dy_at = [&](int b, int p) {
-        return ch < 2 ? dfp[(size_t)b * 2 * PIX + ch * PIX + p] : dfv[(size_t)b * PIX + p];
-    };
+    const int i0 = (int)((int64_t)chunk * N / HSC), i1 = (int)((int64_t)(chunk + 1) * N / HSC);
+    const double mu = (double)hmean[ch];
     double s = 0.0, q = 0.0;
-    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
         const int b = i / PIX, p = i - b * PIX;
-        const double dy = (double)dy_at(b, p);
+        const double dy = ch < 2 ? (double)dfp[(size_t)b * 2 * PIX + ch * PIX + p] : (double)dfv[(size_t)b * PIX + p];
         s += dy;
-        q += ((double)zh[(b * 3 + ch) * PIX + p] - (double)mu) * dy;
+        q += ((double)zh[(b * 3 + ch) * PIX + p] - mu) * dy;
     }
     s = block_sum_d(s, red);
     q = block_sum_d(q, red);
-    const double invd = (double)inv;
     if (threadIdx.x == 0) {
-        grads[d.gamma_off + c] = (float)(q * invd);
-        grads[d.beta_off + c] = (float)s;
+        part[(ch * HSC + chunk) * 2 + 0] = s;
+        part[(ch * HSC + chunk) * 2 + 1] = q;
     }
-    const float gm = (float)(s / (double)N);
-    const float kk = (float)(q * invd * invd / (double)N);
-    const float iw = inv * params[d.gamma_off + c];
-    for (int i = threadIdx.x; i < N; i += blockDim.x) {
-        const int b = i / PIX, p = i - b * PIX;
-        const float dy = dy_at(b, p);
-        const float zz = zh[(b * 3 + ch) * PIX + p];
-        dzh[(b * 3 + ch) * PIX + p] = ((dy - gm) - (zz - mu) * kk) * iw;
+}
+
+// gamma/beta grads of the head BNs and the per-channel backward coefficients
+// hb[ch][0..2] = (S dy / N, S(z-mean)dy invstd^2 / N, invstd*gamma)
+__global__ void head_bn_bwd_finalize_kernel(const double* __restrict__ part, int B, const BnDesc* desc,
+                                            int pol_layer, int val_layer, const float* __restrict__ params,
+                                            float* __restrict__ grads, const float* __restrict__ binv,
+                                            float* __restrict__ hb)
+{
+    const int ch = threadIdx.x;
+    if (ch >= 3) return;
+    const BnDesc d = desc[ch < 2 ? pol_layer : val_layer];
+    const int c = ch < 2 ? ch : 0;
+    const double N = (double)B * PIX;
+    double s = 0.0, q = 0.0;
+    for (int k = 0; k < HSC; ++k) {
+        s += part[(ch * HSC + k) * 2 + 0];
+        q += part[(ch * HSC + k) * 2 + 1];
+    }
+    const float inv = binv[d.out_off + c];
+    const double invd = (double)inv;
+    grads[d.gamma_off + c] = (float)(q * invd);
+    grads[d.beta_off + c] = (float)s;
+    hb[ch * 3 + 0] = (float)(s / N);
+    hb[ch * 3 + 1] = (float)(q * invd * invd / N);
+    hb[ch * 3 + 2] = inv * params[d.gamma_off + c];
+}
+
+__global__ __launch_bounds__(256) void head_bn_bwd_apply_kernel(const float* __restrict__ zh,
+                                                                const float* __restrict__ dfp,
+                                                                const float* __restrict__ dfv,
+                                                                const float* __restrict__ hmean,
+                                                                const float* __restrict__ hb, float* __restrict__ dzh,
+                                                                int B)
+{
+    const int total = B * 3 * PIX;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const int b = i / (3 * PIX), k = i - b * 3 * PIX;
+        const int ch = k / PIX, p = k - ch * PIX;
+        const float dy = ch < 2 ? dfp[(size_t)b * 2 * PIX + k] : dfv[(size_t)b * PIX + p];
+        dzh[i] = ((dy - hb[ch * 3 + 0]) - (zh[i] - hmean[ch]) * hb[ch * 3 + 1]) * hb[ch * 3 + 2];
     }
 }
 
@@ -552,8 +581,8 @@ __global__ __launch_bounds__(256) void heads_bwd_proj_kernel(const float* __rest
     constexpr int TPC = 256 / C;
     __shared__ float red[3][256];
     const int c = threadIdx.x % C, rg = threadIdx.x / C;
-    const int m0 = blockIdx.x * TROWS;
-    const int rows = min(TROWS, M - m0);
+    const int m0 = blockIdx.x * HROWS;
+    const int rows = min(HROWS, M - m0);
     const float w0 = wpc[c], w1 = wpc[C + c], w2 = wvc[c];
     float s0 = 0.f, s1 = 0.f, s2 = 0.f;
     for (int r = rg; r < rows; r += TPC) {
@@ -586,15 +615,30 @@ __global__ __launch_bounds__(256) void heads_bwd_proj_kernel(const float* __rest
     }
 }
 
-// out[j] = S_t part[t][j] for j < n (fixed order)
-__global__ void sum_partials_kernel(const float* __restrict__ part, int ntile, int n, float* __restrict__ out0,
-                                    float* __restrict__ out1, int split)
+// out[j] = S_t part[t][j]: 64 outputs x 4 interleaved t-groups per workgroup,
+// groups combined in fixed order.  mode 0: j < split -> out0[j], else out1[j-split];
+// mode 1 (stem partials [t][k][c], j = k*C + c): out0[c*27 + k].
+__global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ part, int T, int n,
+                                                              float* __restrict__ out0, float* __restrict__ out1,
+                                                              int split, int mode, int C)
 {
-    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-        float s = 0.f;
-        for (int t = 0; t < ntile; ++t) s += part[(size_t)t * n + j];
-        if (j < split) out0[j] = s;
-        else out1[j - split] = s;
+    __shared__ float red[4][64];
+    const int jl = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int j = blockIdx.x * 64 + jl;
+    float s = 0.f;
+    if (j < n)
+        for (int t = g; t < T; t += 4) s += part[(size_t)t * n + j];
+    red[g][jl] = s;
+    __syncthreads();
+    if (g == 0 && j < n) {
+        const float v = ((red[0][jl] + red[1][jl]) + red[2][jl]) + red[3][jl];
+        if (mode == 0) {
+            if (j < split) out0[j] = v;
+            else out1[j - split] = v;
+        } else {
+            const int k = j / C, c = j - k * C;
+            out0[c * 27 + k] = v;
+        }
     }
 }
 
@@ -643,18 +687,6 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const float* __restrict
                 spart[((size_t)b * 27 + k) * C + c] = s;
             }
         }
-    }
-}
-
-// sum stem partials over boards -> grads[c*27 + k]
-__global__ void stem_wgrad_reduce_kernel(const float* __restrict__ spart, int B, int C, float* __restrict__ g)
-{
-    const int total = 27 * C;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-        const int k = i / C, c = i - k * C;
-        float s = 0.f;
-        for (int b = 0; b < B; ++b) s += spart[((size_t)b * 27 + k) * C + c];
-        g[c * 27 + k] = s;
     }
 }
 
@@ -764,7 +796,7 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     A(w->bgm, nf, true); A(w->bk, nf, true); A(w->biw, nf, true);
     A(w->part_a, (size_t)ntile * C, false);
     A(w->part_b, (size_t)ntile * C, false);
-    A(w->hpart, (size_t)ntile * 3 * C, false);
+    A(w->hpart, (size_t)((M + HROWS - 1) / HROWS) * 3 * C, false);
     A(w->spart, (size_t)cap * 27 * C, false);
     // split-K for wgrad: ~512 rows per split
     w->rps = 512;
@@ -781,6 +813,14 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     A(w->dhv, (size_t)cap * VHID, false);
     A(w->dzh, (size_t)cap * 3 * PIX, false);
     A(w->lossb, (size_t)cap * 2, false);
+    A(w->lpre, (size_t)cap * ACTIONS, false);
+    A(w->hpre, (size_t)cap * VHID, false);
+    A(w->hbw, 16, false);
+    {
+        float* hp = nullptr;
+        A(hp, 3 * HSC * 2 * 2, false);
+        w->hspart = (double*)hp;
+    }
     float* np = nullptr;
     A(np, 2 * 1024, false);
     w->npart = (double*)np;
@@ -890,44 +930,59 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         AZG_CK(launch_heads_project(C, false, X, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], nullptr, nullptr,
                                     w->zh, M, st),
                "train: heads_project");
-        hipLaunchKernelGGL(head_stats_kernel, dim3(3), dim3(256), 0, st, w->zh, B, bdd, h->bn_pol, h->bn_val, P,
-                           h->bn, w->bmean, w->binv, w->bscale, w->bshift);
-        AZG_CK(hipGetLastError(), "train: head_stats");
-        const int ho = bd[h->bn_pol].out_off;
-        HeadsArgs ha;
-        ha.zh = w->zh;
-        ha.hscale = w->bscale + ho;
-        ha.hshift = w->bshift + ho;
-        ha.wpf = P + h->poff[h->t_pfc_w];
-        ha.wpfT = h->wpfT;
-        ha.bpf = P + h->poff[h->t_pfc_b];
-        ha.wv1 = P + h->poff[h->t_vfc1_w];
-        ha.wv1T = h->wv1T;
-        ha.bv1 = P + h->poff[h->t_vfc1_b];
-        ha.wv2 = P + h->poff[h->t_vfc2_w];
-        ha.bv2 = P + h->poff[h->t_vfc2_b];
-        ha.pis = pis;
-        ha.zs = zs;
-        ha.fp = w->fp; ha.fv = w->fv; ha.hv = w->hv; ha.dpre = w->dpre; ha.dlogits = w->dlogits;
-        ha.dfp = w->dfp; ha.dfv = w->dfv; ha.dhv = w->dhv; ha.lossb = w->lossb;
-        ha.B = B;
-        hipLaunchKernelGGL(heads_train_kernel, dim3(B), dim3(256), 0, st, ha);
-        AZG_CK(hipGetLastError(), "train: heads_train");
-        const int64_t nw = (int64_t)ACTIONS * 2 * PIX + ACTIONS + VHID * PIX + 2 * VHID + 1;
-        hipLaunchKernelGGL(heads_wgrad_kernel, dim3(grid_for(nw)), dim3(256), 0, st, w->dlogits, w->fp, w->dhv,
-                           w->fv, w->dpre, w->hv, w->lossb, B, G + h->poff[h->t_pfc_w], G + h->poff[h->t_pfc_b],
-                           G + h->poff[h->t_vfc1_w], G + h->poff[h->t_vfc1_b], G + h->poff[h->t_vfc2_w],
-                           G + h->poff[h->t_vfc2_b], losses);
-        AZG_CK(hipGetLastError(), "train: heads_wgrad");
-        hipLaunchKernelGGL(head_bn_bwd_kernel, dim3(3), dim3(256), 0, st, w->zh, w->dfp, w->dfv, B, bdd, h->bn_pol,
-                           h->bn_val, P, G, w->bmean, w->binv, w->dzh);
-        AZG_CK(hipGetLastError(), "train: head_bn_bwd");
-        hipLaunchKernelGGL((heads_bwd_proj_kernel<C>), dim3(ntile), dim3(256), 0, st, X, w->dzh,
+        hipLaunchKernelGGL(head_stats_partial_kernel, dim3(3, HSC), dim3(256), 0, st, w->zh, B, w->hspart);
+        AZG_CK(hipGetLastError(), "train: head_stats_partial");
+        hipLaunchKernelGGL(head_stats_finalize_kernel, dim3(1), dim3(64), 0, st, w->hspart, B, bdd, h->bn_pol,
+                           h->bn_val, P, h->bn, w->bmean, w->binv, w->bscale, w->bshift);
+        AZG_CK(hipGetLastError(), "train: head_stats_finalize");
+        const int ho = bd[h->bn_pol].out_off;   // policy ch0, ch1, value: contiguous
+        const int gH = grid_for((int64_t)B * 3 * PIX);
+        hipLaunchKernelGGL(head_bn_apply_kernel, dim3(gH), dim3(256), 0, st, w->zh, w->bscale + ho, w->bshift + ho,
+                           w->fp, w->fv, B);
+        AZG_CK(hipGetLastError(), "train: head_bn_apply");
+        const float* wpf = P + h->poff[h->t_pfc_w];
+        const float* wv1 = P + h->poff[h->t_vfc1_w];
+        {   // logits / value hidden pre-activations
+            GemmProb a{w->fp, 2 * PIX, 1, wpf, 1, 2 * PIX, w->lpre, ACTIONS, 1, nullptr, 0, 0, B, ACTIONS, 2 * PIX};
+            GemmProb b{w->fv, PIX, 1, wv1, 1, PIX, w->hpre, VHID, 1, nullptr, 0, 0, B, VHID, PIX};
+            AZG_CK(launch_small_gemm(a, &b, st), "train: head fc fwd");
+        }
+        hipLaunchKernelGGL(heads_loss_kernel, dim3((B + 3) / 4), dim3(256), 0, st, w->lpre, P + h->poff[h->t_pfc_b],
+                           w->hpre, P + h->poff[h->t_vfc1_b], P + h->poff[h->t_vfc2_w], P + h->poff[h->t_vfc2_b],
+                           pis, zs, w->dlogits, w->hv, w->dhv, w->dpre, w->lossb, B);
+        AZG_CK(hipGetLastError(), "train: heads_loss");
+        {   // dfp = (dlogits . Wpf) * (fp > 0), dfv = (dhv . Wv1) * (fv > 0)
+            GemmProb a{w->dlogits, ACTIONS, 1, wpf, 2 * PIX, 1, w->dfp, 2 * PIX, 1, w->fp, 2 * PIX, 1, B, 2 * PIX,
+                       ACTIONS};
+            GemmProb b{w->dhv, VHID, 1, wv1, PIX, 1, w->dfv, PIX, 1, w->fv, PIX, 1, B, PIX, VHID};
+            AZG_CK(launch_small_gemm(a, &b, st), "train: head fc dgrad");
+        }
+        {   // weight grads: dWpf = dlogits^T . fp, dWv1 = dhv^T . fv
+            GemmProb a{w->dlogits, 1, ACTIONS, w->fp, 2 * PIX, 1, G + h->poff[h->t_pfc_w], 2 * PIX, 1, nullptr, 0, 0,
+                       ACTIONS, 2 * PIX, B};
+            GemmProb b{w->dhv, 1, VHID, w->fv, PIX, 1, G + h->poff[h->t_vfc1_w], PIX, 1, nullptr, 0, 0, VHID, PIX, B};
+            AZG_CK(launch_small_gemm(a, &b, st), "train: head fc wgrad");
+        }
+        hipLaunchKernelGGL(heads_small_grads_kernel, dim3((HSG_OUT + 3) / 4), dim3(256), 0, st, w->dlogits, w->dhv,
+                           w->dpre, w->hv, w->lossb, B, G + h->poff[h->t_pfc_b], G + h->poff[h->t_vfc1_b],
+                           G + h->poff[h->t_vfc2_w], G + h->poff[h->t_vfc2_b], losses);
+        AZG_CK(hipGetLastError(), "train: heads_small_grads");
+        hipLaunchKernelGGL(head_bn_bwd_partial_kernel, dim3(3, HSC), dim3(256), 0, st, w->zh, w->dfp, w->dfv, B,
+                           w->bmean + ho, w->hspart);
+        AZG_CK(hipGetLastError(), "train: head_bn_bwd_partial");
+        hipLaunchKernelGGL(head_bn_bwd_finalize_kernel, dim3(1), dim3(64), 0, st, w->hspart, B, bdd, h->bn_pol,
+                           h->bn_val, P, G, w->binv, w->hbw);
+        AZG_CK(hipGetLastError(), "train: head_bn_bwd_finalize");
+        hipLaunchKernelGGL(head_bn_bwd_apply_kernel, dim3(gH), dim3(256), 0, st, w->zh, w->dfp, w->dfv, w->bmean + ho,
+                           w->hbw, w->dzh, B);
+        AZG_CK(hipGetLastError(), "train: head_bn_bwd_apply");
+        const int hntile = (M + HROWS - 1) / HROWS;
+        hipLaunchKernelGGL((heads_bwd_proj_kernel<C>), dim3(hntile), dim3(256), 0, st, X, w->dzh,
                            P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], w->gX, w->hpart, M);
         AZG_CK(hipGetLastError(), "train: heads_bwd_proj");
         // policy_conv.weight [2][C] then value_conv.weight [C]: partial layout [t][3][C]
-        hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(3 * C)), dim3(256), 0, st, w->hpart, ntile, 3 * C,
-                           G + h->poff[h->t_pc_w], G + h->poff[h->t_vc_w], 2 * C);
+        hipLaunchKernelGGL(reduce_partials_kernel, dim3((3 * C + 63) / 64), dim3(256), 0, st, w->hpart, hntile, 3 * C,
+                           G + h->poff[h->t_pc_w], G + h->poff[h->t_vc_w], 2 * C, 0, C);
         AZG_CK(hipGetLastError(), "train: heads proj wgrad");
         prof_end(h, pr, st);
     }
@@ -953,8 +1008,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     R(bwd_bn(w->gX, w->a0, w->z0, h->bn_stem, w->DZ, nullptr));
     hipLaunchKernelGGL((stem_wgrad_kernel<C>), dim3(B), dim3(256), 0, st, x, w->DZ, w->spart);
     AZG_CK(hipGetLastError(), "train: stem_wgrad");
-    hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(grid_for(27 * C)), dim3(256), 0, st, w->spart, B, C,
-                       G + h->poff[h->t_stem_w]);
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3((27 * C + 63) / 64), dim3(256), 0, st, w->spart, B, 27 * C,
+                       G + h->poff[h->t_stem_w], nullptr, 27 * C, 1, C);
     AZG_CK(hipGetLastError(), "train: stem_wgrad_reduce");
 #undef R
     return 0;

@@ -239,19 +239,27 @@ class PyTorchModel:
         z = torch.from_numpy(np.ascontiguousarray(target_vs, dtype=np.float32).reshape(-1, 1)).to(dev)
         return self.train_batch_device(s, t, z, epochs)
 
-    def train_batch_device(self, s: torch.Tensor, t: torch.Tensor, z: torch.Tensor, epochs: int = 1) -> dict:
+    def train_batch_device(self, s: torch.Tensor, t: torch.Tensor, z: torch.Tensor, epochs: int = 1,
+                           return_tensor: bool = False):
+        """train_batch on device-resident tensors.  return_tensor=True returns the
+        mean losses as a float32 [3] device tensor (policy, value, total) without a
+        host sync, so consecutive steps pipeline on the stream."""
         self.net.train()
         eng = self.engine
-        acc = torch.zeros(3, dtype=torch.float64, device=eng.device)
         losses = torch.empty(3, dtype=torch.float32, device=eng.device)
+        acc = None
         for _ in range(epochs):
             eng.train_backward(s, t, z, losses)
             if self.grad_hook is not None:
                 self.grad_hook(eng.flat_grads)
             self.optimizer.hip_step(self.max_grad_norm)
             eng.flat_nbt.add_(1)
-            acc += losses
-        vals = (acc / float(epochs)).tolist()
+            if epochs > 1:
+                acc = losses.double() if acc is None else acc + losses
+        mean = losses if epochs == 1 else (acc / float(epochs)).float()
+        if return_tensor:
+            return mean
+        vals = (mean.double() if epochs == 1 else acc / float(epochs)).tolist()
         return {"policy_loss": vals[0], "value_loss": vals[1], "total_loss": vals[2]}
 
     train_step = train_batch

@@ -87,3 +87,32 @@ def test_train_alphazero_smoke(tmp_path):
     files = os.listdir(tmp_path)
     assert any(f.startswith("snapshot_iter1_") for f in files) and "replay_buffer_latest.pkl" in files
     assert best.engine is not None
+
+
+def test_native_selfplay_on_gpu_matches_python_search():
+    """The C++ multi-game search fed by the HIP forward gives, per game, exactly the
+    reference-semantics Python search run alone on the same model (noise + sampling
+    from the game's own RandomState)."""
+    from games.gomoku import Gomoku
+    from mcts.native_mcts import NativeSelfPlay
+    from mcts.new_mcts_alpha import MCTS
+    from network import PyTorchModel
+    import selfplay
+
+    g = load_golden("3x64")
+    m = PyTorchModel(device="cuda")
+    m.net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in golden_state(g).items()})
+    temp = lambda n: 1.0 if n < 4 else 0.0
+    seeds = [101, 202, 303, 404, 505, 606, 707, 808]
+    sp = NativeSelfPlay(m.predict, Gomoku, len(seeds), 48, cpuct=1.2, dirichlet_alpha=0.3, epsilon=0.25,
+                        apply_dirichlet_n_first_moves=3)
+    together = sp.play(temp, max_moves=8, use_symmetries=False, seeds=seeds)
+    assert sp.max_batch > 32
+    for i in (0, 7):
+        mc = MCTS(Gomoku, 48, m, cpuct=1.2, dirichlet_alpha=0.3, epsilon=0.25, apply_dirichlet_n_first_moves=3,
+                  rng=np.random.RandomState(seeds[i]))
+        ea, wa = selfplay.play_game_and_collect(mc, Gomoku(15), temp, max_moves=8, use_symmetries=False)
+        eb, wb = together[i]
+        assert wa == wb and len(ea) == len(eb)
+        for x, y in zip(ea, eb):
+            assert np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1]) and x[2] == y[2]
