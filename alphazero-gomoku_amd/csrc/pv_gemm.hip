@@ -17,6 +17,7 @@
 namespace azg {
 
 constexpr int GK = 256;                       // K chunk
+constexpr int GU = 8;                         // loads in flight per thread while staging
 constexpr int GLDK_MAX = GK + 2;
 constexpr int G_LDS = 2 * 32 * GLDK_MAX * 4;  // 66,048 B
 
@@ -45,31 +46,42 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(GemmPair gp)
         const int kc = min(GK, P.K - k0);
         const int ldk = gemm_ldk(kc);
         float* Bs = smem + 32 * ldk;
-        // stage A tile [32][ldk] and B^T tile [32][ldk], zero outside the problem
-        if (P.sak == 1) {
-            for (int e = tid; e < 32 * ldk; e += 256) {
-                const int r = e / ldk, k = e - r * ldk;
+        // stage A tile [32][ldk] and B^T tile [32][ldk], zero outside the problem.
+        // Batches of GU independent loads per thread are issued before their LDS
+        // stores (the loads would otherwise serialise on L2 latency).
+        const int tot = 32 * ldk;
+        const float inv_ldk = 1.f / (float)ldk;
+        auto split = [&](int e, int& r, int& k) {   // e = r*ldk + k, exact for e < 2^20
+            r = (int)((float)e * inv_ldk);
+            k = e - r * ldk;
+            if (k < 0) { --r; k += ldk; }
+            else if (k >= ldk) { ++r; k -= ldk; }
+        };
+        for (int e0 = 0; e0 < tot; e0 += 256 * GU) {
+            float va[GU], vb[GU];
+#pragma unroll
+            for (int u = 0; u < GU; ++u) {
+                const int e = e0 + u * 256 + tid;
+                int r, k;
+                if (P.sak == 1) split(e, r, k); else { k = e >> 5; r = e & 31; }
                 const int i = i0 + r;
-                As[e] = (k < kc && i < P.M) ? P.A[(size_t)i * P.sai + (k0 + k)] : 0.f;
-            }
-        } else {
-            for (int e = tid; e < 32 * ldk; e += 256) {
-                const int k = e >> 5, r = e & 31;
-                const int i = i0 + r;
-                As[r * ldk + k] = (k < kc && i < P.M) ? P.A[(size_t)i * P.sai + (size_t)(k0 + k) * P.sak] : 0.f;
-            }
-        }
-        if (P.sbk == 1) {
-            for (int e = tid; e < 32 * ldk; e += 256) {
-                const int c = e / ldk, k = e - c * ldk;
+                va[u] = (e < tot && k < kc && i < P.M) ? P.A[(size_t)i * P.sai + (size_t)(k0 + k) * P.sak] : 0.f;
+                int c, kb;
+                if (P.sbk == 1) split(e, c, kb); else { kb = e >> 5; c = e & 31; }
                 const int j = j0 + c;
-                Bs[e] = (k < kc && j < P.N) ? P.B[(size_t)j * P.sbj + (k0 + k)] : 0.f;
+                vb[u] = (e < tot && kb < kc && j < P.N) ? P.B[(size_t)(k0 + kb) * P.sbk + (size_t)j * P.sbj] : 0.f;
             }
-        } else {
-            for (int e = tid; e < 32 * ldk; e += 256) {
-                const int k = e >> 5, c = e & 31;
-                const int j = j0 + c;
-                Bs[c * ldk + k] = (k < kc && j < P.N) ? P.B[(size_t)(k0 + k) * P.sbk + (size_t)j * P.sbj] : 0.f;
+#pragma unroll
+            for (int u = 0; u < GU; ++u) {
+                const int e = e0 + u * 256 + tid;
+                if (e < tot) {
+                    int r, k;
+                    if (P.sak == 1) split(e, r, k); else { k = e >> 5; r = e & 31; }
+                    As[r * ldk + k] = va[u];
+                    int c, kb;
+                    if (P.sbk == 1) split(e, c, kb); else { kb = e >> 5; c = e & 31; }
+                    Bs[c * ldk + kb] = vb[u];
+                }
             }
         }
         __syncthreads();

@@ -1,6 +1,6 @@
 """End-to-end self-play throughput (BASELINE configs[2] shape, scaled down by
-flags): G concurrent games x S simulations/move through the reference-semantics
-Python MCTS + batched HIP forward.  Reports leaf boards/s (NN-evaluated boards
+flags): G concurrent games x S simulations/move through the native C++ search
+(default) or the reference-semantics Python MCTS (--python) + batched HIP forward.  Reports leaf boards/s (NN-evaluated boards
 per second), moves/s and the share of wall time inside the forward.
 
     python scripts/bench_selfplay.py --games 64 --sims 100 --moves 6 [--blocks 6 --channels 128]
@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--moves", type=int, default=6, help="moves per game (max_moves)")
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--channels", type=int, default=128)
+    ap.add_argument("--python", action="store_true", help="Python search instead of the native one")
     args = ap.parse_args()
     from games.gomoku import Gomoku
     from network import PyTorchModel
@@ -36,14 +37,16 @@ def main():
     m.predict(np.zeros((8, 3, 15, 15), np.float32))
     t0 = time.perf_counter()
     ex, winners, drv = selfplay.selfplay_games(m, Gomoku, args.games, args.sims, 1.0, lambda n: 1.0, 0.05, 0.15, 10,
-                                               max_moves=args.moves)
+                                               max_moves=args.moves, native=not args.python)
     dt = time.perf_counter() - t0
     moves = len(ex) // 8
     print(json.dumps({"games": args.games, "sims": args.sims, "net": f"{args.blocks}x{args.channels}",
                       "leaf_boards": drv.boards, "forwards": drv.forwards, "max_batch": drv.max_batch,
                       "seconds": round(dt, 2), "boards_per_s": round(drv.boards / dt, 1),
                       "moves_per_s": round(moves / dt, 2), "nn_share": round(drv.nn_seconds / dt, 3),
-                      "mean_batch": round(drv.boards / max(drv.forwards, 1), 1)}))
+                      "mean_batch": round(drv.boards / max(drv.forwards, 1), 1),
+                      "search": "python" if args.python else "native",
+                      "search_share": round(getattr(drv, "search_seconds", 0.0) / dt, 3)}))
 
 
 if __name__ == "__main__":

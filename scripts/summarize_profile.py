@@ -1,0 +1,138 @@
+"""Condense a rocprofv3 run of bench.py (scripts/gpu_profile.sh output under
+gpurun_out/prof_<TAG>/) into the committed evidence under profiles/:
+
+  profiles/<TAG>_kernel_stats.csv   the --kernel-trace --stats summary, verbatim
+  profiles/<TAG>_pmc.csv            per-kernel averages of every PMC pass
+  profiles/<TAG>_summary.md         top kernels + the dominant conv kernel's HBM bytes
+                                    (FETCH_SIZE x2 and WRITE_SIZE, KiB -> bytes, per the
+                                    MI355X guide's gfx950 correction), MFMA busy and clock
+  profiles/conv_traffic.json        per-launch HBM bytes of the tuned conv, read by bench.py
+
+    python scripts/summarize_profile.py gpurun_out/prof_r1 r1 [--train gpurun_out/prof_r1_train]
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF = os.path.join(REPO, "profiles")
+BATCH, BLOCKS, CHANNELS = 512, 6, 128
+FLOP_CONV = 2 * 225 * CHANNELS * 9 * CHANNELS   # per board per conv
+
+
+def read_csv(path):
+    with open(path, newline="") as f:
+        return list(csv.DictReader(f))
+
+
+def short(name, n=70):
+    return name if len(name) <= n else name[:n] + "..."
+
+
+def pmc_table(prof_dir):
+    """{kernel_name: {counter: (mean, n)}} over all PMC passes."""
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for path in glob.glob(os.path.join(prof_dir, "pmc_*", "run_counter_collection.csv")):
+        for row in read_csv(path):
+            acc[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return {k: {c: (sum(v) / len(v), len(v)) for c, v in d.items()} for k, d in acc.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prof_dir")
+    ap.add_argument("tag")
+    ap.add_argument("--train", default=None)
+    args = ap.parse_args()
+    os.makedirs(PROF, exist_ok=True)
+    stats_path = os.path.join(args.prof_dir, "trace", "run_kernel_stats.csv")
+    stats = read_csv(stats_path)
+    shutil.copy(stats_path, os.path.join(PROF, f"{args.tag}_kernel_stats.csv"))
+    pmc = pmc_table(args.prof_dir)
+    with open(os.path.join(PROF, f"{args.tag}_pmc.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "counter", "mean_per_dispatch", "dispatches"])
+        for k in sorted(pmc):
+            for c, (m, n) in sorted(pmc[k].items()):
+                w.writerow([k, c, m, n])
+
+    # dominant conv: the product-path conv kernels are the most-called conv3x3 names
+    # (autotuning dispatches every candidate shape only twice)
+    convs = [r for r in stats if "conv3x3_mfma" in r["Name"]]
+    convs.sort(key=lambda r: int(r["Calls"]), reverse=True)
+    top_calls = int(convs[0]["Calls"]) if convs else 0
+    tuned = [r for r in convs if int(r["Calls"]) >= top_calls // 2]
+    calls = sum(int(r["Calls"]) for r in tuned)
+    avg_ns = sum(float(r["TotalDurationNs"]) for r in tuned) / max(calls, 1)
+    fetch = write = mfma = grbm = 0.0
+    nk = 0
+    for r in tuned:
+        d = pmc.get(r["Name"], {})
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            wgt = int(r["Calls"])
+            fetch += d["FETCH_SIZE"][0] * wgt
+            write += d["WRITE_SIZE"][0] * wgt
+            mfma += d.get("SQ_VALU_MFMA_BUSY_CYCLES", (0, 0))[0] * wgt
+            grbm += d.get("GRBM_GUI_ACTIVE", (0, 0))[0] * wgt
+            nk += wgt
+    lines = [f"# rocprofv3 summary `{args.tag}` (bench.py: 6x128, B={BATCH} forward)", ""]
+    lines.append("Source: `rocprofv3 --kernel-trace --stats` + separate `--pmc` passes "
+                 "(scripts/gpu_profile.sh); raw files in this directory.")
+    lines.append("")
+    lines.append("| kernel | calls | avg us | total ms | % |")
+    lines.append("|---|---|---|---|---|")
+    for r in sorted(stats, key=lambda r: float(r["TotalDurationNs"]), reverse=True)[:14]:
+        lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
+                     f"{float(r['TotalDurationNs']) / 1e6:.2f} | {float(r['Percentage']):.1f} |")
+    lines.append("")
+    traffic = None
+    if nk:
+        fetch_b = fetch / nk * 1024 * 2      # KiB, gfx950 streaming-read correction x2
+        write_b = write / nk * 1024
+        traffic = fetch_b + write_b
+        in_b = BATCH * 289 * CHANNELS * 4 + 9 * CHANNELS * CHANNELS * 4
+        out_b = BATCH * 225 * CHANNELS * 4
+        alg = in_b + out_b + 0.5 * out_b     # conv2 of each block also reads the residual
+        clk = grbm / nk / 8 / (avg_ns * 1e-9) / 1e9 if avg_ns else 0.0
+        busy = mfma / nk / (4 * 256) / (grbm / nk / 8) if grbm else 0.0
+        tflops = FLOP_CONV * BATCH / (avg_ns * 1e-9) / 1e12
+        lines += [
+            "## Dominant kernel: 3x3 conv (tuned shape)",
+            "",
+            f"* kernels: {', '.join('`' + short(r['Name'], 60) + '`' for r in tuned)}",
+            f"* dispatches: {calls}, average duration {avg_ns / 1e3:.1f} us -> {tflops:.1f} TFLOP/s "
+            f"({tflops / 157.3 * 100:.1f} % of the 157.3 TFLOP/s dense fp32 MFMA peak)",
+            f"* HBM-side bytes per launch: FETCH_SIZE x2 = {fetch_b / 1e6:.1f} MB, WRITE_SIZE = {write_b / 1e6:.1f} MB, "
+            f"total {traffic / 1e6:.1f} MB (algorithmic {alg / 1e6:.1f} MB: padded input once + weights + "
+            "output, + residual on every second launch)",
+            f"* SQ_VALU_MFMA_BUSY_CYCLES / (4 SIMD x 256 CU x GRBM_GUI_ACTIVE/8) = {busy * 100:.1f} %, "
+            f"clock ~ {clk:.2f} GHz",
+            "",
+        ]
+        with open(os.path.join(PROF, "conv_traffic.json"), "w") as f:
+            json.dump({"config": f"{BLOCKS}x{CHANNELS}_B{BATCH}", "tag": args.tag,
+                       "hbm_bytes_per_launch": round(traffic), "fetch_bytes": round(fetch_b),
+                       "write_bytes": round(write_b), "algorithmic_bytes": round(alg),
+                       "avg_launch_us": round(avg_ns / 1e3, 2)}, f, indent=1)
+    if args.train:
+        tpath = os.path.join(args.train, "trace", "run_kernel_stats.csv")
+        if os.path.exists(tpath):
+            shutil.copy(tpath, os.path.join(PROF, f"{args.tag}_train_kernel_stats.csv"))
+            ts = read_csv(tpath)
+            lines += ["## Train step (scripts/bench_train.py: 6x128, B=128)", "",
+                      "| kernel | calls | avg us | total ms | % |", "|---|---|---|---|---|"]
+            for r in sorted(ts, key=lambda r: float(r["TotalDurationNs"]), reverse=True)[:16]:
+                lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
+                             f"{float(r['TotalDurationNs']) / 1e6:.2f} | {float(r['Percentage']):.1f} |")
+            lines.append("")
+    with open(os.path.join(PROF, f"{args.tag}_summary.md"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
