@@ -32,6 +32,7 @@ _SIGS = {
     "azg_pv_bind": (ctypes.c_int32, [_P, _P, _P, _P]),
     "azg_pv_mark_dirty": (ctypes.c_int32, [_P]),
     "azg_pv_forward": (ctypes.c_int32, [_P, _P, ctypes.c_int32, _P, _P, _P, _P]),
+    "azg_pv_forward_boards": (ctypes.c_int32, [_P, _P, _P, ctypes.c_int32, _P, _P, _P, _P]),
     "azg_pv_train_backward": (ctypes.c_int32, [_P, _P, _P, _P, ctypes.c_int32, _P, _P]),
     "azg_pv_train_apply": (ctypes.c_int32, [_P, _P, _P, ctypes.c_int64, ctypes.c_float, ctypes.c_float,
                                             ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,

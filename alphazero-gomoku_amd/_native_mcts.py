@@ -29,6 +29,7 @@ _SIGS = {
     "azg_mcts_destroy": (_I32, [_P]),
     "azg_mcts_set_root": (_I32, [_P, _I32, _P, _I32, _I32, _I32, _I32, _I32, _I32]),
     "azg_mcts_advance": (_I32, [_P, _P, _P, _P, ctypes.POINTER(_I32), _I32]),
+    "azg_mcts_advance_boards": (_I32, [_P, _P, _P, _P, _P, ctypes.POINTER(_I32), _I32]),
     "azg_mcts_feed": (_I32, [_P, _P, _P]),
     "azg_mcts_noise_request": (_I32, [_P, _I32, _P]),
     "azg_mcts_set_root_prior": (_I32, [_P, _I32, _P]),
@@ -84,10 +85,17 @@ class SearchForest:
                               float(dirichlet_alpha), float(epsilon))
         self.h = _P()
         _check(self.lib.azg_mcts_create(ctypes.byref(self.cfg), self.n_games, ctypes.byref(self.h)))
-        self.leaves = np.empty((self.n_games * self.batch_size, 3, self.board, self.board), np.float32)
+        self._leaves = None
         self.counts = np.zeros(self.n_games, np.int32)
         self.status = np.zeros(self.n_games, np.int32)
         self._p32 = np.empty(self.A, np.float32)
+
+    @property
+    def leaves(self) -> np.ndarray:
+        """float32 [n_games*batch_size, 3, H, W] staging for advance() (allocated on first use)."""
+        if self._leaves is None:
+            self._leaves = np.empty((self.n_games * self.batch_size, 3, self.board, self.board), np.float32)
+        return self._leaves
 
     def __del__(self):
         h = getattr(self, "h", None)
@@ -107,6 +115,18 @@ class SearchForest:
         n = _I32(0)
         _check(self.lib.azg_mcts_advance(self.h, _addr(self.leaves), _addr(self.counts), _addr(self.status),
                                          ctypes.byref(n), self.n_threads))
+        return n.value
+
+    def advance_boards(self, boards: np.ndarray, players: np.ndarray) -> int:
+        """advance() with the leaves written as int8 boards [n,225] + side to move [n]
+        into the given C-contiguous int8 arrays (capacity n_games*batch_size), e.g.
+        numpy views of pinned host tensors."""
+        assert boards.dtype == np.int8 and players.dtype == np.int8
+        assert boards.flags.c_contiguous and players.flags.c_contiguous
+        assert boards.size >= self.n_games * self.batch_size * self.A and players.size >= self.n_games * self.batch_size
+        n = _I32(0)
+        _check(self.lib.azg_mcts_advance_boards(self.h, _addr(boards), _addr(players), _addr(self.counts),
+                                                _addr(self.status), ctypes.byref(n), self.n_threads))
         return n.value
 
     def feed(self, probs: np.ndarray, values: np.ndarray) -> None:

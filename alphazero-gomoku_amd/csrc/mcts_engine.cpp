@@ -200,8 +200,6 @@ struct GameSearch {
     // noise hand-off
     bool noise_pending = false;
     int32_t noise_node = -1;
-    // emitted leaves for this round
-    std::vector<float> out;
 
     int32_t node_for(const Key& k) const
     {
@@ -310,7 +308,6 @@ void install_uniform(GameSearch& gs, const Key& k, const State& st, int A)
 void run_game(const azg_mcts* h, GameSearch& gs)
 {
     const int A = h->A, bs = h->cfg.batch_size;
-    gs.out.clear();
     if (!gs.active) { gs.status = AZG_MCTS_IDLE; return; }
     for (;;) {
         if (!gs.in_sim) {
@@ -368,11 +365,56 @@ void run_game(const azg_mcts* h, GameSearch& gs)
         }
         if (emitted) break;
     }
-    // emit the queue
-    gs.status = AZG_MCTS_NEED_EVAL;
-    const size_t per = (size_t)3 * A;
-    gs.out.resize(gs.queue.size() * per);
-    for (size_t i = 0; i < gs.queue.size(); ++i) gs.queue[i].st.encode(gs.out.data() + i * per);
+    gs.status = AZG_MCTS_NEED_EVAL;   // the queue is emitted by the caller (advance_impl)
+}
+
+// Run all games (parallel), then write the pending leaves of every game, in game
+// order, either as float32 planes or as int8 boards + side to move (parallel copy
+// at prefix offsets).
+int32_t advance_impl(azg_mcts* h, float* leaves, int8_t* boards, int8_t* players, int32_t* counts,
+                     int32_t* status, int32_t* n_out, int32_t n_threads)
+{
+    const int G = (int)h->games.size();
+    for (int g = 0; g < G; ++g)
+        if (h->games[g].noise_pending) return fail("azg_mcts_advance: a root prior awaits azg_mcts_set_root_prior");
+    const int nt = n_threads > 0 ? n_threads : omp_get_max_threads();
+    std::vector<size_t> off(G + 1, 0);
+#pragma omp parallel num_threads(nt)
+    {
+#pragma omp for schedule(dynamic, 1)
+        for (int g = 0; g < G; ++g) {
+            GameSearch& gs = h->games[g];
+            if (gs.status == AZG_MCTS_NEED_EVAL) continue;   // not fed yet: re-emit the same leaves
+            run_game(h, gs);
+        }
+#pragma omp single
+        {
+            for (int g = 0; g < G; ++g) {
+                const GameSearch& gs = h->games[g];
+                status[g] = gs.status;
+                const int n = gs.status == AZG_MCTS_NEED_EVAL ? (int)gs.queue.size() : 0;
+                counts[g] = n;
+                off[g + 1] = off[g] + n;
+            }
+        }
+        const int A = h->A;
+#pragma omp for schedule(dynamic, 4)
+        for (int g = 0; g < G; ++g) {
+            const GameSearch& gs = h->games[g];
+            const size_t n = off[g + 1] - off[g];
+            for (size_t i = 0; i < n; ++i) {
+                const size_t row = off[g] + i;
+                const State& st = gs.queue[i].st;
+                if (leaves) st.encode(leaves + row * 3 * A);
+                if (boards) {
+                    std::memcpy(boards + row * A, st.board.data(), A);
+                    players[row] = (int8_t)st.player;
+                }
+            }
+        }
+    }
+    *n_out = (int32_t)off[G];
+    return 0;
 }
 
 }  // namespace
@@ -434,28 +476,14 @@ int32_t azg_mcts_advance(azg_mcts* h, float* leaves, int32_t* counts, int32_t* s
                          int32_t n_threads)
 {
     if (!h || !leaves || !counts || !status || !n_out) return fail("azg_mcts_advance: null argument");
-    const int G = (int)h->games.size();
-    for (int g = 0; g < G; ++g)
-        if (h->games[g].noise_pending) return fail("azg_mcts_advance: a root prior awaits azg_mcts_set_root_prior");
-    const int nt = n_threads > 0 ? n_threads : omp_get_max_threads();
-#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
-    for (int g = 0; g < G; ++g) {
-        GameSearch& gs = h->games[g];
-        if (gs.status == AZG_MCTS_NEED_EVAL) continue;   // fed? (no: still waiting) -- caller error guard
-        run_game(h, gs);
-    }
-    const size_t per = (size_t)3 * h->A;
-    size_t off = 0;
-    for (int g = 0; g < G; ++g) {
-        GameSearch& gs = h->games[g];
-        status[g] = gs.status;
-        const int n = gs.status == AZG_MCTS_NEED_EVAL ? (int)gs.queue.size() : 0;
-        counts[g] = n;
-        if (n) std::memcpy(leaves + off * per, gs.out.data(), (size_t)n * per * sizeof(float));
-        off += n;
-    }
-    *n_out = (int32_t)off;
-    return 0;
+    return advance_impl(h, leaves, nullptr, nullptr, counts, status, n_out, n_threads);
+}
+
+int32_t azg_mcts_advance_boards(azg_mcts* h, int8_t* boards, int8_t* players, int32_t* counts, int32_t* status,
+                                int32_t* n_out, int32_t n_threads)
+{
+    if (!h || !boards || !players || !counts || !status || !n_out) return fail("azg_mcts_advance_boards: null argument");
+    return advance_impl(h, nullptr, boards, players, counts, status, n_out, n_threads);
 }
 
 int32_t azg_mcts_feed(azg_mcts* h, const float* probs, const float* values)

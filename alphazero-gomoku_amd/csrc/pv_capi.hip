@@ -129,7 +129,23 @@ int32_t azg_pv_forward(azg_pv* h, const float* x, int32_t batch, float* probs, f
         if (int32_t r = repack(h, st)) return r;
         h->dirty = false;
     }
-    return forward_eval(h, x, batch, probs, values, logits, st);
+    return forward_eval(h, x, batch, probs, values, logits, st, nullptr, nullptr, nullptr);
+}
+
+int32_t azg_pv_forward_boards(azg_pv* h, const int8_t* boards, const int8_t* players, int32_t batch, float* probs,
+                              float* values, float* priors, void* stream)
+{
+    if (!h || !h->params) return fail("azg_pv_forward_boards: handle not bound (azg_pv_bind)");
+    if (!boards || !players || !probs || !values) return fail("azg_pv_forward_boards: null boards/players/probs/values");
+    if (h->cfg.board != BOARD || h->cfg.in_ch != 3) return fail("azg_pv_forward_boards: needs a 15x15, 3-plane net");
+    if (batch <= 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (int32_t r = ensure_eval_workspace(h, batch, st)) return r;
+    if (h->dirty) {
+        if (int32_t r = repack(h, st)) return r;
+        h->dirty = false;
+    }
+    return forward_eval(h, nullptr, batch, probs, values, nullptr, st, boards, players, priors);
 }
 
 int32_t azg_pv_profile_enable(azg_pv* h, int32_t enable)
@@ -302,7 +318,7 @@ int32_t repack(azg_pv* h, hipStream_t st)
 }
 
 int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* values, float* logits,
-                     hipStream_t st)
+                     hipStream_t st, const int8_t* boards, const int8_t* players, float* priors)
 {
     const int C = h->C;
     const int M = batch * PIX;
@@ -310,7 +326,7 @@ int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* 
     const BnDesc* bd = h->bn_desc.data();
     int pr = prof_begin(h, AZG_PROF_STEM, st);
     AZG_TRY(launch_stem(C, EPI_BN_RELU, x, h->wstem, h->scale + bd[h->bn_stem].out_off,
-                        h->shift + bd[h->bn_stem].out_off, h->act[0], batch, st),
+                        h->shift + bd[h->bn_stem].out_off, h->act[0], batch, st, boards, players),
             "forward: stem");
     prof_end(h, pr, st);
     float* X = h->act[0];
@@ -337,7 +353,7 @@ int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* 
                              P + h->poff[h->t_pfc_w], P + h->poff[h->t_pfc_b], P + h->poff[h->t_vfc1_w],
                              P + h->poff[h->t_vfc1_b],
                              P + h->poff[h->t_vfc2_w], P + h->poff[h->t_vfc2_b], h->hbuf, probs, values, logits,
-                             batch, st),
+                             batch, st, boards, priors),
             "forward: heads");
     prof_end(h, pr, st);
     return 0;

@@ -222,21 +222,36 @@ __global__ __launch_bounds__(64 * NW_, NW_ / 2) void conv3x3_mfma(
 // workgroup per board; the board's 3 input planes are staged into LDS with a
 // zero halo; each thread owns one output channel (27 weights in registers) and a
 // strided set of pixels.  Weight layout ws[k][c], k = ci*9 + ky*3 + kx.
-template <int C, int EPI>
+//
+// BOARDS: the input is the int8 game board [B][225] (0 empty, 1, 2) + side to move
+// [B]; the reference encoding (games/gomoku.py:130-150: planes board==player,
+// board==opponent, ones) is built straight into the LDS patch (on-GPU encode, no
+// float planes in HBM).
+template <int C, int EPI, bool BOARDS = false>
 __global__ __launch_bounds__(256) void stem_conv(
-    const float* __restrict__ x, const float* __restrict__ ws,
-    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ x, const int8_t* __restrict__ boards, const int8_t* __restrict__ players,
+    const float* __restrict__ ws, const float* __restrict__ scale, const float* __restrict__ shift,
     float* __restrict__ out)
 {
     __shared__ float xs[3 * PADPIX];
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
     const float* xb = x + (size_t)b * 3 * PIX;
+    const int8_t* bb = boards + (size_t)b * PIX;
+    const int me = BOARDS ? (int)players[b] : 0;
     for (int i = tid; i < 3 * PADPIX; i += 256) {
         const int ci = i / PADPIX, rem = i - ci * PADPIX;
         const int yy = rem / PADW, xx = rem - yy * PADW;
         float v = 0.f;
-        if (yy >= 1 && yy <= BOARD && xx >= 1 && xx <= BOARD) v = xb[ci * PIX + (yy - 1) * BOARD + (xx - 1)];
+        if (yy >= 1 && yy <= BOARD && xx >= 1 && xx <= BOARD) {
+            const int p = (yy - 1) * BOARD + (xx - 1);
+            if (BOARDS) {
+                const int c = bb[p];
+                v = ci == 0 ? (c == me ? 1.f : 0.f) : ci == 1 ? (c == 3 - me ? 1.f : 0.f) : 1.f;
+            } else {
+                v = xb[ci * PIX + p];
+            }
+        }
         xs[i] = v;
     }
     __syncthreads();
@@ -471,12 +486,14 @@ int conv_tuned_shape(int C, int M)
 }
 
 hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const float* scale,
-                       const float* shift, float* out, int B, hipStream_t st)
+                       const float* shift, float* out, int B, hipStream_t st, const int8_t* boards,
+                       const int8_t* players)
 {
 #define AZG_STEM_CASE(CC)                                                                              \
     case CC:                                                                                           \
-        if (epi == EPI_RAW) hipLaunchKernelGGL((stem_conv<CC, EPI_RAW>), dim3(B), dim3(256), 0, st, x, ws, scale, shift, out); \
-        else hipLaunchKernelGGL((stem_conv<CC, EPI_BN_RELU>), dim3(B), dim3(256), 0, st, x, ws, scale, shift, out); \
+        if (boards) hipLaunchKernelGGL((stem_conv<CC, EPI_BN_RELU, true>), dim3(B), dim3(256), 0, st, x, boards, players, ws, scale, shift, out); \
+        else if (epi == EPI_RAW) hipLaunchKernelGGL((stem_conv<CC, EPI_RAW>), dim3(B), dim3(256), 0, st, x, boards, players, ws, scale, shift, out); \
+        else hipLaunchKernelGGL((stem_conv<CC, EPI_BN_RELU>), dim3(B), dim3(256), 0, st, x, boards, players, ws, scale, shift, out); \
         return hipGetLastError();
     switch (C) {
         AZG_STEM_CASE(64)

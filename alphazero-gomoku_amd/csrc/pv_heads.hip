@@ -66,10 +66,13 @@ __global__ __launch_bounds__(256) void heads_project(const float* __restrict__ a
 constexpr int FC_OUT = ACTIONS + VHID;           // pre[b] = [policy logits (225) | value hidden (64)]
 
 // Per board (one wave): logits = pre + bias, softmax; value = tanh(relu(pre_v + b1) . w2 + b2).
+// priors (optional, with boards): probs * (board == 0), the reference's masked
+// prior p * valid (mcts/new_mcts_alpha.py:166) -- float32 multiply by 1.0 / 0.0.
 __global__ __launch_bounds__(256) void heads_finalize(const float* __restrict__ pre, const float* __restrict__ bpf,
                                                       const float* __restrict__ bv1, const float* __restrict__ wv2,
                                                       const float* __restrict__ bv2, float* __restrict__ probs,
-                                                      float* __restrict__ values, float* __restrict__ logits, int B)
+                                                      float* __restrict__ values, float* __restrict__ logits, int B,
+                                                      const int8_t* __restrict__ boards, float* __restrict__ priors)
 {
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -97,8 +100,10 @@ __global__ __launch_bounds__(256) void heads_finalize(const float* __restrict__ 
     for (int t = 0; t < 4; ++t) {
         const int j = lane + 64 * t;
         if (j < ACTIONS) {
-            probs[(size_t)b * ACTIONS + j] = e[t] * inv;
+            const float pj = e[t] * inv;
+            probs[(size_t)b * ACTIONS + j] = pj;
             if (logits) logits[(size_t)b * ACTIONS + j] = lg[t];
+            if (priors) priors[(size_t)b * ACTIONS + j] = pj * (boards[(size_t)b * PIX + j] == 0 ? 1.f : 0.f);
         }
     }
     const float hid = fmaxf(pb[ACTIONS + lane] + bv1[lane], 0.f);
@@ -127,7 +132,8 @@ hipError_t launch_heads_project(int C, bool bn, const float* act, const float* w
 hipError_t launch_heads_fwd(int C, const float* act, const float* wpc, const float* wvc, const float* hscale,
                             const float* hshift, const float* wpf, const float* bpf, const float* wv1,
                             const float* bv1, const float* wv2, const float* bv2, float* hbuf, float* probs,
-                            float* values, float* logits, int B, hipStream_t st)
+                            float* values, float* logits, int B, hipStream_t st, const int8_t* boards,
+                            float* priors)
 {
     hipError_t e = launch_heads_project(C, true, act, wpc, wvc, hscale, hshift, hbuf, B * PIX, st);
     if (e != hipSuccess) return e;
@@ -138,7 +144,7 @@ hipError_t launch_heads_fwd(int C, const float* act, const float* wpc, const flo
     e = launch_small_gemm(gp, &gv, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(heads_finalize, dim3((B + 3) / 4), dim3(256), 0, st, pre, bpf, bv1, wv2, bv2, probs, values,
-                       logits, B);
+                       logits, B, boards, priors);
     return hipGetLastError();
 }
 

@@ -34,12 +34,14 @@ struct BlockBn { int first, second; };
 hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, const float* scale,
                           const float* shift, const float* resid, float* out, int M, hipStream_t st);
 hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const float* scale,
-                       const float* shift, float* out, int B, hipStream_t st);
+                       const float* shift, float* out, int B, hipStream_t st, const int8_t* boards = nullptr,
+                       const int8_t* players = nullptr);
 hipError_t launch_heads_fwd(int C, const float* act, const float* wpc, const float* wvc,
                             const float* hscale, const float* hshift, const float* wpf,
                             const float* bpf, const float* wv1, const float* bv1,
                             const float* wv2, const float* bv2, float* hbuf, float* probs,
-                            float* values, float* logits, int B, hipStream_t st);
+                            float* values, float* logits, int B, hipStream_t st,
+                            const int8_t* boards = nullptr, float* priors = nullptr);
 hipError_t launch_heads_project(int C, bool bn, const float* act, const float* wpc, const float* wvc,
                                 const float* hscale, const float* hshift, float* hout, int M, hipStream_t st);
 hipError_t launch_small_gemm(const GemmProb& p0, const GemmProb* p1, hipStream_t st);
@@ -109,5 +111,5 @@ int32_t repack(azg_pv* h, hipStream_t st);
 int prof_begin(azg_pv* h, int cls, hipStream_t st);   // returns pair index or -1
 void prof_end(azg_pv* h, int pair, hipStream_t st);
 int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* values, float* logits,
-                     hipStream_t st);
+                     hipStream_t st, const int8_t* boards, const int8_t* players, float* priors);
 }  // namespace azg

@@ -128,6 +128,13 @@ class PolicyValueEngine:
         check(self.lib.azg_pv_forward(self.h, ptr(x), int(x.shape[0]), ptr(probs), ptr(values), ptr(logits),
                                       _stream(self.device)), self.lib)
 
+    def forward_boards_into(self, boards, players, probs, values, priors=None):
+        """Eval forward from device int8 boards [B,225] + players [B] (on-GPU encode);
+        priors (optional) = probs * (board == 0)."""
+        self.sync_dirty()
+        check(self.lib.azg_pv_forward_boards(self.h, ptr(boards), ptr(players), int(boards.shape[0]), ptr(probs),
+                                             ptr(values), ptr(priors), _stream(self.device)), self.lib)
+
     def train_backward(self, x, pis, zs, losses):
         self.sync_dirty()
         check(self.lib.azg_pv_train_backward(self.h, ptr(x), ptr(pis), ptr(zs), int(x.shape[0]), ptr(losses),

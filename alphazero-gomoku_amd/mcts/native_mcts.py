@@ -87,26 +87,79 @@ class NativeMCTS:
         return f.get_pi(0)
 
 
+class PlanesEvaluator:
+    """Synchronous adapter: the search emits float32 planes, ``evaluate(X)`` returns
+    (probs, values) -- e.g. PyTorchModel.predict or a test double."""
+
+    def __init__(self, evaluate: Callable, forest: SearchForest):
+        self.evaluate, self.forest, self.result = evaluate, forest, None
+
+    def advance(self) -> int:
+        return self.forest.advance()
+
+    def submit(self, n: int) -> None:
+        self.result = self.evaluate(self.forest.leaves[:n])
+
+    def wait(self):
+        return self.result
+
+
+class _BoardsAdapter:
+    """Board-mode adapter around an evaluator with pinned ``boards``/``players``
+    staging and asynchronous ``submit(n)`` / ``wait()`` (network.BoardEvaluator)."""
+
+    def __init__(self, ev, forest: SearchForest):
+        self.ev, self.forest = ev, forest
+
+    def advance(self) -> int:
+        return self.forest.advance_boards(self.ev.boards, self.ev.players)
+
+    def submit(self, n: int) -> None:
+        self.ev.submit(n)
+
+    def wait(self):
+        return self.ev.wait()
+
+
 class NativeSelfPlay:
-    """Concurrent self-play games over one SearchForest (train.py:360-412 per game).
+    """Concurrent self-play games over native search forests (train.py:360-412 per game).
 
-    ``evaluate(X float32 [n,3,H,W]) -> (probs [n,A], values [n,1])`` is the batched
-    network call (e.g. PyTorchModel.predict).  Statistics: boards, forwards,
-    nn_seconds, search_seconds, max_batch."""
+    Evaluation, one of:
+      * ``evaluate(X float32 [n,3,H,W]) -> (probs, values)``: synchronous, one forest;
+      * ``evaluator_factory(capacity) -> evaluator`` with pinned ``boards``/``players``
+        staging and async ``submit(n)``/``wait()`` (PyTorchModel.board_evaluator): the
+        games are split into ``groups`` forests and the host searches one group while
+        the GPU evaluates another (leaves cross PCIe as int8 boards, encoded on the GPU).
+    Every game draws from its own RandomState, so results are identical in both modes
+    and for any grouping.  Statistics: boards, forwards, nn_seconds (host time waiting
+    for / inside evaluation), search_seconds, max_batch."""
 
-    def __init__(self, evaluate: Callable, game_class, n_games: int, n_simulations: int, cpuct: float = 1.0,
-                 batch_size: int = 32, dirichlet_alpha: float = 0.03, epsilon: float = 0.03,
-                 apply_dirichlet_n_first_moves: int = 10, add_dirichlet_noise: bool = True, n_threads: int = 0):
-        self.evaluate = evaluate
+    def __init__(self, evaluate: Optional[Callable], game_class, n_games: int, n_simulations: int,
+                 cpuct: float = 1.0, batch_size: int = 32, dirichlet_alpha: float = 0.03, epsilon: float = 0.03,
+                 apply_dirichlet_n_first_moves: int = 10, add_dirichlet_noise: bool = True, n_threads: int = 0,
+                 evaluator_factory: Optional[Callable] = None, groups: int = 2):
+        if (evaluate is None) == (evaluator_factory is None):
+            raise ValueError("give exactly one of evaluate / evaluator_factory")
         self.game_class = game_class
         self.n_games = n_games
         self.alpha, self.eps = dirichlet_alpha, epsilon
         g0 = game_class()
         self.board = g0.size
-        self.forest = SearchForest(n_games, n_simulations, rules=_rules_of(game_class), board=g0.size, cpuct=cpuct,
-                                   batch_size=batch_size, dirichlet_alpha=dirichlet_alpha, epsilon=epsilon,
-                                   apply_dirichlet_n_first_moves=apply_dirichlet_n_first_moves,
-                                   add_dirichlet_noise=add_dirichlet_noise, n_threads=n_threads)
+        K = 1 if evaluate is not None else max(1, min(groups, n_games))
+        bounds = [n_games * k // K for k in range(K + 1)]
+        self.slices = [(bounds[k], bounds[k + 1]) for k in range(K)]
+        self.forests, self.evals = [], []
+        for lo, hi in self.slices:
+            f = SearchForest(hi - lo, n_simulations, rules=_rules_of(game_class), board=g0.size, cpuct=cpuct,
+                             batch_size=batch_size, dirichlet_alpha=dirichlet_alpha, epsilon=epsilon,
+                             apply_dirichlet_n_first_moves=apply_dirichlet_n_first_moves,
+                             add_dirichlet_noise=add_dirichlet_noise, n_threads=n_threads)
+            self.forests.append(f)
+            if evaluate is not None:
+                self.evals.append(PlanesEvaluator(evaluate, f))
+            else:
+                self.evals.append(_BoardsAdapter(evaluator_factory((hi - lo) * batch_size), f))
+        self.forest = self.forests[0]
         self.boards = self.forwards = self.max_batch = 0
         self.nn_seconds = self.search_seconds = 0.0
 
@@ -126,52 +179,63 @@ class NativeSelfPlay:
                 g = self.game_class(size=self.board)
                 g.current_player = 1
                 games.append(g)
-        f = self.forest
         hist: List[list] = [[] for _ in range(G)]
         moves = [0] * G
-        live = [True] * G
         results = [None] * G
-
-        for g in range(G):
-            f.clear(g)                  # a fresh tree per game, reused across its moves
-            f.set_root(g, games[g], len(games[g].move_history))
-        n_live = G
-        while n_live:
-            t0 = time.perf_counter()
-            n = f.advance()
-            self.search_seconds += time.perf_counter() - t0
-            # games whose move search finished: sample (per-game RNG), play, restart
-            for g in np.nonzero(f.status == DONE)[0]:
-                g = int(g)
-                game = games[g]
-                pi = f.get_pi(g)
-                state_enc = game.get_encoded_state()
-                action = sample_action_from_pi(pi, temp_fn(moves[g]), rngs[g])
-                if game.get_valid_moves()[action] != 1.0:
-                    action = int(np.argmax(pi))
-                hist[g].append((state_enc, pi.copy(), int(game.current_player)))
-                game.do_move(divmod(action, game.size))
-                moves[g] += 1
-                if game.is_game_over() or moves[g] >= max_moves:
-                    results[g] = self._finish(hist[g], game.get_winner(), use_symmetries)
-                    live[g] = False
-                    n_live -= 1
-                else:
-                    f.set_root(g, game, len(game.move_history))
-            if n:
+        live = [0] * len(self.forests)
+        for k, (lo, hi) in enumerate(self.slices):
+            f = self.forests[k]
+            for g in range(lo, hi):
+                f.clear(g - lo)          # a fresh tree per game, reused across its moves
+                f.set_root(g - lo, games[g], len(games[g].move_history))
+            live[k] = hi - lo
+        pending = [False] * len(self.forests)
+        while any(live) or any(pending):
+            for k, (lo, hi) in enumerate(self.slices):
+                f, ev = self.forests[k], self.evals[k]
                 t0 = time.perf_counter()
-                probs, values = self.evaluate(f.leaves[:n])
-                self.nn_seconds += time.perf_counter() - t0
-                self.boards += n
-                self.forwards += 1
-                self.max_batch = max(self.max_batch, n)
-                t0 = time.perf_counter()
-                f.feed(probs, values)
-                for g in np.nonzero(f.status == NEED_EVAL)[0]:
-                    p32 = f.noise_request(int(g))
-                    if p32 is not None:
-                        f.set_root_prior(int(g), _mix_noise(p32, rngs[g], self.alpha, self.eps))
+                if pending[k]:
+                    probs, values = ev.wait()
+                    t1 = time.perf_counter()
+                    self.nn_seconds += t1 - t0
+                    t0 = t1
+                    f.feed(probs, values)
+                    for i in np.nonzero(f.status == NEED_EVAL)[0]:
+                        p32 = f.noise_request(int(i))
+                        if p32 is not None:
+                            f.set_root_prior(int(i), _mix_noise(p32, rngs[lo + i], self.alpha, self.eps))
+                    pending[k] = False
+                if not live[k]:
+                    self.search_seconds += time.perf_counter() - t0
+                    continue
+                n = ev.advance()
+                # games whose move search finished: sample (per-game RNG), play, restart
+                for i in np.nonzero(f.status == DONE)[0]:
+                    i = int(i)
+                    g = lo + i
+                    game = games[g]
+                    pi = f.get_pi(i)
+                    state_enc = game.get_encoded_state()
+                    action = sample_action_from_pi(pi, temp_fn(moves[g]), rngs[g])
+                    if game.get_valid_moves()[action] != 1.0:
+                        action = int(np.argmax(pi))
+                    hist[g].append((state_enc, pi.copy(), int(game.current_player)))
+                    game.do_move(divmod(action, game.size))
+                    moves[g] += 1
+                    if game.is_game_over() or moves[g] >= max_moves:
+                        results[g] = self._finish(hist[g], game.get_winner(), use_symmetries)
+                        live[k] -= 1
+                    else:
+                        f.set_root(i, game, len(game.move_history))
                 self.search_seconds += time.perf_counter() - t0
+                if n:
+                    t0 = time.perf_counter()
+                    ev.submit(n)
+                    self.nn_seconds += time.perf_counter() - t0
+                    pending[k] = True
+                    self.boards += n
+                    self.forwards += 1
+                    self.max_batch = max(self.max_batch, n)
         return results
 
     @staticmethod

@@ -178,6 +178,50 @@ class HipAdam(torch.optim.Adam):
         return loss
 
 
+class BoardEvaluator:
+    """Asynchronous leaf evaluation for the native search: pinned host staging
+    (the search writes int8 boards straight into it), non-blocking H2D, the
+    board-input forward, non-blocking D2H of the masked priors and values, and an
+    event to wait on.  Two evaluators let the host search one half of the games
+    while the GPU evaluates the other."""
+
+    def __init__(self, model: "PyTorchModel", capacity: int):
+        self.model = model
+        dev = model.engine.device
+        self.capacity = int(capacity)
+        self.h_boards = torch.empty((capacity, 225), dtype=torch.int8).pin_memory()
+        self.h_players = torch.empty((capacity,), dtype=torch.int8).pin_memory()
+        self.h_priors = torch.empty((capacity, 225), dtype=torch.float32).pin_memory()
+        self.h_values = torch.empty((capacity, 1), dtype=torch.float32).pin_memory()
+        self.d_boards = torch.empty((capacity, 225), dtype=torch.int8, device=dev)
+        self.d_players = torch.empty((capacity,), dtype=torch.int8, device=dev)
+        self.d_probs = torch.empty((capacity, 225), dtype=torch.float32, device=dev)
+        self.d_priors = torch.empty((capacity, 225), dtype=torch.float32, device=dev)
+        self.d_values = torch.empty((capacity, 1), dtype=torch.float32, device=dev)
+        self.boards = self.h_boards.numpy()      # views the search writes into
+        self.players = self.h_players.numpy()
+        self.event = torch.cuda.Event()
+        self.n = 0
+
+    def submit(self, n: int) -> None:
+        self.n = n
+        if n == 0:
+            return
+        self.d_boards[:n].copy_(self.h_boards[:n], non_blocking=True)
+        self.d_players[:n].copy_(self.h_players[:n], non_blocking=True)
+        self.model.engine.forward_boards_into(self.d_boards[:n], self.d_players[:n], self.d_probs[:n],
+                                              self.d_values[:n], self.d_priors[:n])
+        self.h_priors[:n].copy_(self.d_priors[:n], non_blocking=True)
+        self.h_values[:n].copy_(self.d_values[:n], non_blocking=True)
+        self.event.record()
+
+    def wait(self):
+        """-> (priors [n,225], values [n,1]) numpy views of the pinned buffers."""
+        if self.n:
+            self.event.synchronize()
+        return self.h_priors.numpy()[:self.n], self.h_values.numpy()[:self.n]
+
+
 class PyTorchModel:
     """Reference network.py:132-265 surface over the HIP engine."""
 
@@ -223,6 +267,23 @@ class PyTorchModel:
         return probs, values
 
     policy_value = predict
+
+    def predict_boards(self, boards: np.ndarray, players: np.ndarray, masked: bool = True):
+        """Leaf evaluation from int8 boards [B,15,15] or [B,225] and the side to move
+        [B]: the encoding (games/gomoku.py:130-150) runs inside the stem kernel.
+        Returns (priors = probs * valid if masked else probs, values [B,1]) as numpy."""
+        eng = self.engine
+        b = torch.from_numpy(np.ascontiguousarray(boards, dtype=np.int8).reshape(len(boards), -1)).to(eng.device)
+        pl = torch.from_numpy(np.ascontiguousarray(players, dtype=np.int8).reshape(-1)).to(eng.device)
+        B = int(b.shape[0])
+        probs = torch.empty((B, 225), dtype=torch.float32, device=eng.device)
+        values = torch.empty((B, 1), dtype=torch.float32, device=eng.device)
+        priors = torch.empty_like(probs) if masked else None
+        eng.forward_boards_into(b, pl, probs, values, priors)
+        return (priors if masked else probs).cpu().numpy(), values.cpu().numpy()
+
+    def board_evaluator(self, capacity: int) -> "BoardEvaluator":
+        return BoardEvaluator(self, capacity)
 
     def predict_batch(self, states_list: list) -> Tuple[np.ndarray, np.ndarray]:
         return self.predict(self.make_batch_from_states(states_list))

@@ -148,10 +148,13 @@ def selfplay_games(model, game_class, n_games: int, n_simulations: int, cpuct: f
     winners = {0: 0, 1: 0, 2: 0}
     if native:
         from mcts.native_mcts import NativeSelfPlay
-        driver = NativeSelfPlay(model.predict, game_class, n_games, n_simulations, cpuct=cpuct,
-                                dirichlet_alpha=dirichlet_alpha, epsilon=dirichlet_epsilon,
-                                apply_dirichlet_n_first_moves=dirichlet_n_moves,
-                                add_dirichlet_noise=add_dirichlet_noise)
+        kw = dict(cpuct=cpuct, dirichlet_alpha=dirichlet_alpha, epsilon=dirichlet_epsilon,
+                  apply_dirichlet_n_first_moves=dirichlet_n_moves, add_dirichlet_noise=add_dirichlet_noise)
+        if hasattr(model, "board_evaluator"):      # HIP model: int8 leaves, GPU encode, pipelined groups
+            driver = NativeSelfPlay(None, game_class, n_games, n_simulations,
+                                    evaluator_factory=model.board_evaluator, groups=2 if n_games > 1 else 1, **kw)
+        else:
+            driver = NativeSelfPlay(model.predict, game_class, n_games, n_simulations, **kw)
         games = [game_class(size=board_size) for _ in range(n_games)]
         results = driver.play(temp_fn, max_moves=max_moves, use_symmetries=use_symmetries, seeds=seeds,
                               games=games)

@@ -68,6 +68,12 @@ int32_t azg_mcts_set_root(azg_mcts* h, int32_t g, const int8_t* board, int32_t p
 int32_t azg_mcts_advance(azg_mcts* h, float* leaves, int32_t* counts, int32_t* status, int32_t* n_out,
                          int32_t n_threads);
 
+/* Same as azg_mcts_advance, but the leaves are written as int8 boards [n][size*size]
+ * (0 empty, 1, 2) and the side to move [n] (1|2), for the on-GPU encoding of
+ * azg_pv_forward_boards (capacity n_games*batch_size boards). */
+int32_t azg_mcts_advance_boards(azg_mcts* h, int8_t* boards, int8_t* players, int32_t* counts, int32_t* status,
+                                int32_t* n_out, int32_t n_threads);
+
 /* Install the evaluation of the last emitted leaves (same order): probs
  * float32 [n][size*size], values float32 [n] (stored, unused by the search,
  * as in the reference). */

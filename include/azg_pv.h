@@ -9,6 +9,9 @@
  *   azg_pv_forward        <- PyTorchModel.predict            (network.py:168-183)
  *                            = AlphaZeroNet.forward in eval mode (network.py:85-117)
  *                              + F.softmax(dim=1) (network.py:180)
+ *   azg_pv_forward_boards <- Gomoku.get_encoded_state (games/gomoku.py:130-150) on every
+ *                            queued leaf + predict + p * valid (mcts/new_mcts_alpha.py:
+ *                            158-166), from int8 boards
  *   azg_pv_train_backward <- train_batch: zero_grad, train-mode forward, log_softmax,
  *                            KLDiv(batchmean) + MSE, loss.backward()  (network.py:213-222)
  *   azg_pv_train_apply    <- clip_grad_norm_(params, 3.0) + Adam.step()
@@ -77,6 +80,14 @@ int32_t azg_pv_mark_dirty(azg_pv* h);
  * [batch,225] (NULL to skip). */
 int32_t azg_pv_forward(azg_pv* h, const float* x, int32_t batch,
                        float* probs, float* values, float* logits, void* stream);
+
+/* Eval-mode forward from int8 boards: boards [batch,225] (0 empty, 1, 2), players
+ * [batch] (side to move, 1|2), both device.  The reference encoding (planes
+ * board==player, board==3-player, ones) is built inside the stem kernel.  probs /
+ * values as azg_pv_forward; priors (optional, NULL to skip): probs * (board == 0),
+ * the reference's masked prior, bitwise equal to numpy's p * valid. */
+int32_t azg_pv_forward_boards(azg_pv* h, const int8_t* boards, const int8_t* players, int32_t batch,
+                              float* probs, float* values, float* priors, void* stream);
 
 /* Train-mode forward + loss + backward on the local batch (reference
  * network.py:213-222).  Writes d(loss)/d(param) into the bound grad buffer

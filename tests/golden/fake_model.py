@@ -35,3 +35,28 @@ class FakeModel:
         v = np.tanh(np.array([row @ self.wv for row in X]) - 0.5)
         self.calls.append(len(X))
         return p.astype(np.float32), v.reshape(-1, 1).astype(np.float32)
+
+
+class FakeBoardEvaluator:
+    """Test double of network.BoardEvaluator: int8 board staging, deferred
+    evaluation, masked priors (probs * valid) -- drives the pipelined native
+    self-play on CPU."""
+
+    def __init__(self, model, capacity, board_size=15):
+        self.model = model
+        self.boards = np.zeros((capacity, board_size * board_size), np.int8)
+        self.players = np.zeros((capacity,), np.int8)
+        self.n = 0
+        self.out = None
+
+    def submit(self, n):
+        self.n = n
+        b = self.boards[:n].astype(np.int64)
+        pl = self.players[:n].astype(np.int64)[:, None]
+        x = np.stack([(b == pl), (b == 3 - pl), np.ones_like(b, dtype=bool)], axis=1).astype(np.float32)
+        x = x.reshape(n, 3, int(np.sqrt(b.shape[1])), -1)
+        probs, values = self.model.predict(x)
+        self.out = (probs * (self.boards[:n] == 0).astype(np.float32), values)
+
+    def wait(self):
+        return self.out

@@ -134,3 +134,32 @@ def test_load_state_dict_invalidates_packed_weights():
     q1, _ = other.predict(x)
     assert not np.array_equal(p0, p1)
     assert np.array_equal(p1, q1)
+
+
+@pytest.mark.parametrize("blocks,ch,B", [(3, 64, 37), (6, 128, 300)])
+def test_forward_boards_is_encode_then_forward(blocks, ch, B):
+    """azg_pv_forward_boards (int8 boards encoded inside the stem kernel) is bitwise
+    the float-plane forward of the reference encoding; priors are bitwise
+    probs * valid (mcts/new_mcts_alpha.py:166)."""
+    m = make_model(blocks, ch, seed=5)
+    boards, players = synth_positions(B, seed=17)
+    x = encode_batch(boards, players)
+    p_ref, v_ref = m.predict(x)
+    pri, v = m.predict_boards(np.asarray(boards, np.int8), np.asarray(players, np.int8))
+    probs, v2 = m.predict_boards(np.asarray(boards, np.int8), np.asarray(players, np.int8), masked=False)
+    assert np.array_equal(probs, p_ref) and np.array_equal(v, v_ref) and np.array_equal(v2, v_ref)
+    masks = np.stack([valid_mask(b) for b in boards]).astype(np.float32)
+    assert np.array_equal(pri, p_ref * masks)
+
+
+def test_board_evaluator_async_matches_predict():
+    m = make_model(3, 64, seed=6)
+    boards, players = synth_positions(200, seed=23)
+    ev = m.board_evaluator(256)
+    ev.boards[:200] = np.asarray(boards, np.int8).reshape(200, -1)
+    ev.players[:200] = np.asarray(players, np.int8)
+    ev.submit(200)
+    pri, v = ev.wait()
+    p_ref, v_ref = m.predict(encode_batch(boards, players))
+    masks = np.stack([valid_mask(b) for b in boards]).astype(np.float32)
+    assert np.array_equal(pri, p_ref * masks) and np.array_equal(v, v_ref)

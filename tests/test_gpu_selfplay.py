@@ -104,10 +104,17 @@ def test_native_selfplay_on_gpu_matches_python_search():
     m.net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in golden_state(g).items()})
     temp = lambda n: 1.0 if n < 4 else 0.0
     seeds = [101, 202, 303, 404, 505, 606, 707, 808]
-    sp = NativeSelfPlay(m.predict, Gomoku, len(seeds), 48, cpuct=1.2, dirichlet_alpha=0.3, epsilon=0.25,
-                        apply_dirichlet_n_first_moves=3)
+    kw = dict(cpuct=1.2, dirichlet_alpha=0.3, epsilon=0.25, apply_dirichlet_n_first_moves=3)
+    sp = NativeSelfPlay(m.predict, Gomoku, len(seeds), 48, **kw)
     together = sp.play(temp, max_moves=8, use_symmetries=False, seeds=seeds)
     assert sp.max_batch > 32
+    # int8 leaves + on-GPU encode + pinned async evaluation in 2 pipelined groups
+    pipe = NativeSelfPlay(None, Gomoku, len(seeds), 48, evaluator_factory=m.board_evaluator, groups=2, **kw)
+    piped = pipe.play(temp, max_moves=8, use_symmetries=False, seeds=seeds)
+    for (ea, wa), (eb, wb) in zip(together, piped):
+        assert wa == wb and len(ea) == len(eb)
+        for x, y in zip(ea, eb):
+            assert np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1]) and x[2] == y[2]
     for i in (0, 7):
         mc = MCTS(Gomoku, 48, m, cpuct=1.2, dirichlet_alpha=0.3, epsilon=0.25, apply_dirichlet_n_first_moves=3,
                   rng=np.random.RandomState(seeds[i]))

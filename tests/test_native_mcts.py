@@ -14,7 +14,7 @@ import pytest
 from conftest import GOLDEN, REPO
 
 sys.path.insert(0, GOLDEN)
-from fake_model import FakeModel  # noqa: E402
+from fake_model import FakeBoardEvaluator, FakeModel  # noqa: E402
 
 import _native_mcts  # noqa: E402
 import selfplay  # noqa: E402
@@ -215,3 +215,48 @@ def test_errors_are_loud():
         f2.advance()
     f2.set_root_prior(0, p32.astype(np.float64))
     f2.advance()
+
+
+@pytest.mark.parametrize("groups", [1, 2, 3])
+def test_pipelined_board_selfplay_equals_sync(groups):
+    """Board-mode leaves (int8 + side to move), masked priors and the grouped
+    search/evaluate pipeline give exactly the synchronous planes-mode games."""
+    G = 7
+    seeds = [31 + i for i in range(G)]
+    temp = lambda n: 1.0 if n < 5 else 0.0
+    kw = dict(cpuct=1.1, dirichlet_alpha=0.3, epsilon=0.25, apply_dirichlet_n_first_moves=4)
+    sync = NativeSelfPlay(FakeModel(seed=12).predict, Gomoku, G, 36, **kw).play(temp, max_moves=14, seeds=seeds)
+    m = FakeModel(seed=12)
+    pipe = NativeSelfPlay(None, Gomoku, G, 36, evaluator_factory=lambda cap: FakeBoardEvaluator(m, cap),
+                          groups=groups, **kw)
+    out = pipe.play(temp, max_moves=14, seeds=seeds)
+    assert len(pipe.forests) == groups
+    for (ea, wa), (eb, wb) in zip(sync, out):
+        assert wa == wb and same_examples(ea, eb)
+
+
+def test_advance_boards_matches_planes():
+    """The int8 leaves encode to exactly the float planes advance() emits."""
+    fa = _native_mcts.SearchForest(3, 40, add_dirichlet_noise=False)
+    fb = _native_mcts.SearchForest(3, 40, add_dirichlet_noise=False)
+    m = FakeModel(seed=2)
+    for g in range(3):
+        game = Gomoku(15)
+        game.do_move((g, 2 * g))
+        fa.set_root(g, game, 1)
+        fb.set_root(g, game, 1)
+    boards = np.zeros((3 * 32, 225), np.int8)
+    players = np.zeros(3 * 32, np.int8)
+    for _ in range(4):
+        na = fa.advance()
+        nb = fb.advance_boards(boards, players)
+        assert na == nb and np.array_equal(fa.counts, fb.counts) and np.array_equal(fa.status, fb.status)
+        if na == 0:
+            break
+        b = boards[:nb].astype(np.int64)
+        pl = players[:nb].astype(np.int64)[:, None]
+        x = np.stack([(b == pl), (b == 3 - pl), np.ones_like(b, dtype=bool)], axis=1).astype(np.float32)
+        assert np.array_equal(x.reshape(nb, 3, 15, 15), fa.leaves[:na])
+        p, v = m.predict(fa.leaves[:na])
+        fa.feed(p, v)
+        fb.feed(p * (boards[:nb] == 0), v)      # pre-masked priors install identically
