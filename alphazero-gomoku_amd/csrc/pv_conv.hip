@@ -30,7 +30,7 @@ namespace azg {
 // Tile shape: BM = WM*TM*32 pixels x BN channels; 4 waves as WM x WN (WN = 4/WM),
 // each wave TM x TN accumulators of 32x32.  Several shapes are compiled; the host
 // picks the one that balances the tile count over the 256 CUs best (pick_tile).
-template <int C, int BN_, int WM_, int TM_, int NW_ = 4>
+template <int C, int BN_, int WM_, int TM_, int NW_ = 4, int SB_ = 0>
 struct ConvTile {
     static constexpr int NW = NW_;                // waves per workgroup
     static constexpr int NT = 64 * NW_;           // threads
@@ -47,7 +47,9 @@ struct ConvTile {
     static constexpr int NCH = 9 * CG;
     static constexpr int A_LD = BM * BK / 4 / NT;
     static constexpr int B_LD = BN * BK / 4 / NT;
-    static constexpr int LDS_BYTES = 2 * (BM + BN) * LDK * 4;
+    // SB_: single LDS buffer (the next chunk waits in registers; two barriers per
+    // chunk) -- half the LDS per workgroup, twice the resident workgroups.
+    static constexpr int LDS_BYTES = (SB_ ? 1 : 2) * (BM + BN) * LDK * 4;
     static_assert(TN >= 1 && WN * TN * 32 == BN, "bad tile");
     static_assert(A_LD >= 1 && B_LD >= 1 && A_LD * NT * 4 == BM * BK && B_LD * NT * 4 == BN * BK, "bad staging");
 };
@@ -55,13 +57,13 @@ struct ConvTile {
 // ABL (ablation, timing studies only; 0 in every product launch): bit 1 skips the
 // global loads, bit 2 replaces LDS fragment reads by register values, bit 4 drops
 // the per-chunk barrier.  Results are garbage when ABL != 0.
-template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, int ABL = 0>
+template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, int ABL = 0, int SB = 0>
 __global__ __launch_bounds__(64 * NW_, NW_ / 2) void conv3x3_mfma(
     const float* __restrict__ in, const float* __restrict__ wp,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ resid, float* __restrict__ out, int M)
 {
-    using T = ConvTile<C, BN_, WM_, TM_, NW_>;
+    using T = ConvTile<C, BN_, WM_, TM_, NW_, SB>;
     constexpr int RPP = T::RPP;
     constexpr int BM = T::BM, BN = T::BN, BK = T::BK, LDK = T::LDK;
     constexpr int CG = T::CG, NCH = T::NCH, WN = T::WN, TM = T::TM, TN = T::TN;
@@ -69,7 +71,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ / 2) void conv3x3_mfma(
 
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* As = smem;                    // [2][BM][LDK]
-    float* Bs = smem + 2 * BM * LDK;     // [2][BN][LDK]
+    float* Bs = smem + (SB ? 1 : 2) * BM * LDK;   // [2 or 1][BN][LDK]
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
@@ -151,7 +153,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ / 2) void conv3x3_mfma(
 #pragma unroll
         for (int cg = 0; cg < CG; ++cg) {
             const int kc = tap * CG + cg;
-            const int cur = kc & 1;
+            const int cur = SB ? 0 : (kc & 1);
             if (kc + 1 < NCH) gload(kc + 1);
             // keep the next chunk's global loads at the top of the chunk: without this
             // fence hipcc sinks them to just before their vmcnt wait (latency exposed)
@@ -181,7 +183,10 @@ __global__ __launch_bounds__(64 * NW_, NW_ / 2) void conv3x3_mfma(
                         for (int j = 0; j < TN; ++j)
                             at[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], at[i][j], 0, 0, 0);
             }
-            if (kc + 1 < NCH) lstore(cur ^ 1);
+            if (kc + 1 < NCH) {
+                if (SB) __syncthreads();   // every wave is done reading the buffer
+                lstore(SB ? 0 : cur ^ 1);
+            }
             if (!(ABL & 4)) __syncthreads();
         }
 #pragma unroll
@@ -287,48 +292,51 @@ __global__ __launch_bounds__(256) void stem_conv(
 
 // ---- host launchers ------------------------------------------------------
 
-template <int C, int BN, int WM, int TM, int NW, int EPI>
+template <int C, int BN, int WM, int TM, int NW, int EPI, int SB = 0>
 static hipError_t launch_conv_t(const float* in, const float* wp, const float* scale, const float* shift,
                                 const float* resid, float* out, int M, hipStream_t st)
 {
-    using T = ConvTile<C, BN, WM, TM, NW>;
+    using T = ConvTile<C, BN, WM, TM, NW, SB>;
     static bool attr_done = false;
     if (!attr_done) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_mfma<C, BN, WM, TM, NW, EPI>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_mfma<C, BN, WM, TM, NW, EPI, 0, SB>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS_BYTES);
         if (e != hipSuccess) return e;
         attr_done = true;
     }
     dim3 grid(((M + T::BM - 1) / T::BM) * (C / T::BN));
-    hipLaunchKernelGGL((conv3x3_mfma<C, BN, WM, TM, NW, EPI>), grid, dim3(T::NT), T::LDS_BYTES, st,
+    hipLaunchKernelGGL((conv3x3_mfma<C, BN, WM, TM, NW, EPI, 0, SB>), grid, dim3(T::NT), T::LDS_BYTES, st,
                        in, wp, scale, shift, resid, out, M);
     return hipGetLastError();
 }
 
-template <int C, int BN, int WM, int TM, int NW = 4>
+template <int C, int BN, int WM, int TM, int NW = 4, int SB = 0>
 static hipError_t launch_conv_epi(int epi, const float* in, const float* wp, const float* scale, const float* shift,
                                   const float* resid, float* out, int M, hipStream_t st)
 {
     switch (epi) {
-        case EPI_BN_RELU: return launch_conv_t<C, BN, WM, TM, NW, EPI_BN_RELU>(in, wp, scale, shift, resid, out, M, st);
-        case EPI_BN_RES_RELU: return launch_conv_t<C, BN, WM, TM, NW, EPI_BN_RES_RELU>(in, wp, scale, shift, resid, out, M, st);
-        case EPI_ADD: return launch_conv_t<C, BN, WM, TM, NW, EPI_ADD>(in, wp, scale, shift, resid, out, M, st);
-        default: return launch_conv_t<C, BN, WM, TM, NW, EPI_RAW>(in, wp, scale, shift, resid, out, M, st);
+        case EPI_BN_RELU: return launch_conv_t<C, BN, WM, TM, NW, EPI_BN_RELU, SB>(in, wp, scale, shift, resid, out, M, st);
+        case EPI_BN_RES_RELU: return launch_conv_t<C, BN, WM, TM, NW, EPI_BN_RES_RELU, SB>(in, wp, scale, shift, resid, out, M, st);
+        case EPI_ADD: return launch_conv_t<C, BN, WM, TM, NW, EPI_ADD, SB>(in, wp, scale, shift, resid, out, M, st);
+        default: return launch_conv_t<C, BN, WM, TM, NW, EPI_RAW, SB>(in, wp, scale, shift, resid, out, M, st);
     }
 }
 
 // Tile shapes {BM, BN}: index into the switch below.
 struct TileShape { int bm, bn; };
 // 0-5: 4 waves; 6-9: 8 waves (more waves per SIMD at the same LDS footprint).
+// 10-12: single LDS buffer (64x64, 128x64, 64x128; 4 waves).
 static const TileShape kShapes[] = {{128, 128}, {96, 128}, {160, 128}, {64, 128}, {128, 64}, {64, 64},
-                                    {128, 128}, {128, 128}, {128, 64}, {64, 128}};
+                                    {128, 128}, {128, 128}, {128, 64}, {64, 128},
+                                    {64, 64}, {128, 64}, {64, 128}};
 constexpr int kNumShapes = (int)(sizeof(kShapes) / sizeof(kShapes[0]));
 constexpr int kNumAutoShapes = 6;   // heuristic pick_conv_tile only considers 0-5
+constexpr int kNumTunedShapes = 10; // autotuning times 0-9 (the single-buffer 10-12 measured slower everywhere)
 
 static bool shape_ok(int shape, int C)
 {
     if (shape < 0 || shape >= kNumShapes) return false;
-    if (C == 64) return shape == 4 || shape == 5 || shape == 8;
+    if (C == 64) return shape == 4 || shape == 5 || shape == 8 || shape == 10 || shape == 11;
     return true;
 }
 constexpr int kNumCUs = 256;
@@ -369,6 +377,9 @@ hipError_t launch_conv3x3_shape(int shape, int C, int epi, const float* in, cons
         case 7: return launch_conv_epi<CC, 128, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);         \
         case 8: return launch_conv_epi<CC, 64, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);          \
         case 9: return launch_conv_epi<CC, 128, 2, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);         \
+        case 10: return launch_conv_epi<CC, 64, 2, 1, 4, 1>(epi, in, wp, scale, shift, resid, out, M, st);      \
+        case 11: return launch_conv_epi<CC, 64, 2, 2, 4, 1>(epi, in, wp, scale, shift, resid, out, M, st);      \
+        case 12: return launch_conv_epi<CC, 128, 2, 1, 4, 1>(epi, in, wp, scale, shift, resid, out, M, st);     \
         default: return hipErrorInvalidValue;                                                                   \
     }
     switch (C) {
@@ -378,6 +389,8 @@ hipError_t launch_conv3x3_shape(int shape, int C, int epi, const float* in, cons
                 case 5: return launch_conv_epi<64, 64, 2, 1>(epi, in, wp, scale, shift, resid, out, M, st);
                 case 4: return launch_conv_epi<64, 64, 2, 2>(epi, in, wp, scale, shift, resid, out, M, st);
                 case 8: return launch_conv_epi<64, 64, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);
+                case 10: return launch_conv_epi<64, 64, 2, 1, 4, 1>(epi, in, wp, scale, shift, resid, out, M, st);
+                case 11: return launch_conv_epi<64, 64, 2, 2, 4, 1>(epi, in, wp, scale, shift, resid, out, M, st);
                 default: return hipErrorInvalidValue;
             }
         case 128: AZG_SHAPES(128)
@@ -429,6 +442,19 @@ static std::map<std::pair<int, int>, int>& tune_cache()
     return c;
 }
 
+// Autotuning is cached per (C, batch bucket): exact batch up to 256 boards (rounded
+// up to 16), then 1/8-octave buckets -- self-play batches vary every round and must
+// not re-tune (each tuning synchronises the stream).
+static int tune_bucket(int M)
+{
+    const int b = (M + PIX - 1) / PIX;
+    if (b <= 256) return (b + 15) / 16 * 16;
+    int p = 256;
+    while (p * 2 <= b) p *= 2;
+    const int q = p / 8;
+    return (b + q - 1) / q * q;
+}
+
 static int autotune_shape(int C, int epi, const float* in, const float* wp, const float* scale, const float* shift,
                           const float* resid, float* out, int M, hipStream_t st)
 {
@@ -440,7 +466,7 @@ static int autotune_shape(int C, int epi, const float* in, const float* wp, cons
     int best = -1;
     float best_ms = 1e30f;
     for (int s = 0; s < kNumShapes; ++s) {
-        if (!shape_ok(s, C)) continue;
+        if (!shape_ok(s, C) || s >= kNumTunedShapes) continue;
         if (launch_conv3x3_shape(s, C, epi, in, wp, scale, shift, resid, out, M, st) != hipSuccess) continue;
         (void)hipEventRecord(e0, st);
         if (launch_conv3x3_shape(s, C, epi, in, wp, scale, shift, resid, out, M, st) != hipSuccess) continue;
@@ -465,7 +491,7 @@ hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, cons
     if (g_conv_shape_override >= 0 && shape_ok(g_conv_shape_override, C)) {
         shape = g_conv_shape_override;
     } else {
-        auto key = std::make_pair(C, M);
+        auto key = std::make_pair(C, tune_bucket(M));
         auto it = tune_cache().find(key);
         if (it != tune_cache().end()) {
             shape = it->second;
@@ -481,7 +507,7 @@ hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, cons
 
 int conv_tuned_shape(int C, int M)
 {
-    auto it = tune_cache().find(std::make_pair(C, M));
+    auto it = tune_cache().find(std::make_pair(C, tune_bucket(M)));
     return it == tune_cache().end() ? -1 : it->second;
 }
 

@@ -7,7 +7,7 @@
 // Every head GEMM is tiny (M <= a few thousand, N <= 450, K <= 450 or the batch),
 // so one launch carries up to two problems side by side (grid.y = column tiles of
 // problem 0 then problem 1).  A workgroup owns one 32x32 output tile: K is staged
-// through LDS in chunks of <= 256 (row stride LDK with LDK/2 odd: conflict-free
+// through LDS in chunks of <= 512 (row stride LDK with LDK/2 odd: conflict-free
 // column reads and transposed writes), the 4 waves take contiguous quarters of a
 // chunk's v_mfma_f32_32x32x2_f32 steps and the 4 partial tiles are summed in fixed
 // wave order.  Deterministic, and each output row depends only on its own A row
@@ -16,10 +16,10 @@
 
 namespace azg {
 
-constexpr int GK = 256;                       // K chunk
-constexpr int GU = 8;                         // loads in flight per thread while staging
+constexpr int GK = 512;                       // K chunk (one chunk for every head GEMM up to B = 512)
+constexpr int GU = 32;                        // loads in flight per thread while staging
 constexpr int GLDK_MAX = GK + 2;
-constexpr int G_LDS = 2 * 32 * GLDK_MAX * 4;  // 66,048 B
+constexpr int G_LDS = 2 * 32 * GLDK_MAX * 4;  // 131,584 B
 
 __device__ __forceinline__ int gemm_ldk(int kc)
 {

@@ -24,6 +24,7 @@ namespace azg {
 
 hipError_t launch_wgrad(int C, const float* dz, const float* x, float* slab, float* dw, int M, int S, int rps,
                         hipStream_t st);
+int wgrad_rows_per_split(int C, int M);
 
 constexpr int TROWS = 64;    // rows per statistics tile (BN stats / BN backward partials)
 constexpr int HROWS = 128;   // rows per tile of the head-projection backward partials
@@ -799,7 +800,7 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     A(w->hpart, (size_t)((M + HROWS - 1) / HROWS) * 3 * C, false);
     A(w->spart, (size_t)cap * 27 * C, false);
     // split-K for wgrad: ~512 rows per split
-    w->rps = 512;
+    w->rps = 256;                         // smallest split wgrad_rows_per_split picks
     w->S = (M + w->rps - 1) / w->rps;
     A(w->slab, (size_t)w->S * 9 * C * C, false);
     A(w->zh, (size_t)cap * 3 * PIX, false);
@@ -902,7 +903,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     };
     auto wgrad = [&](const float* dz, const float* xin, int tensor) -> int32_t {
         int pr = prof_begin(h, AZG_PROF_TRAIN_WGRAD, st);
-        AZG_CK(launch_wgrad(C, dz, xin, w->slab, G + h->poff[tensor], M, (M + w->rps - 1) / w->rps, w->rps, st),
+        const int rps = wgrad_rows_per_split(C, M);
+        AZG_CK(launch_wgrad(C, dz, xin, w->slab, G + h->poff[tensor], M, (M + rps - 1) / rps, rps, st),
                "train: wgrad");
         prof_end(h, pr, st);
         return 0;

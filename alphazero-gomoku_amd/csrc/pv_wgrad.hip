@@ -169,7 +169,30 @@ static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, f
     return hipGetLastError();
 }
 
-// rows_per_split chosen by the caller (wgrad_splits); slab must hold S*9*C*C floats.
+// Rows per split (multiple of 32, >= 256): minimise rounds-of-workgroups x chunks
+// per workgroup + the slab reduction (S slabs of 9*C*C floats re-read once).  The
+// old fixed 512 gave 57 x 9 = 513 workgroups at B = 128 on 512 slots: one extra round.
+int wgrad_rows_per_split(int C, int M)
+{
+    const int bt = C < 128 ? C : 128;
+    const int tiles = 9 * (C / bt) * (C / bt);
+    const int lds = 2 * 2 * 32 * (bt + 4) * 4;
+    const int slots = 256 * (160 * 1024 / lds);
+    const double chunk_us = 5.4 * (bt / 128.0) * (bt / 128.0) * (160.0 * 1024 / lds) / 2.0;
+    const double red_us = 9.0 * C * C * 4 / 4.0e6;     // one slab at ~4 TB/s
+    int best = 512;
+    double best_cost = 1e30;
+    for (int rps = 256; rps <= 4096; rps += 32) {
+        const int S = (M + rps - 1) / rps;
+        const int rounds = (S * tiles + slots - 1) / slots;
+        const double cost = rounds * (rps / 32) * chunk_us + S * red_us;
+        if (cost < best_cost - 1e-9) { best_cost = cost; best = rps; }
+        if (S == 1) break;
+    }
+    return best;
+}
+
+// slab must hold S*9*C*C floats, S = ceil(M / rps).
 hipError_t launch_wgrad(int C, const float* dz, const float* x, float* slab, float* dw, int M, int S, int rps,
                         hipStream_t st)
 {

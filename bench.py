@@ -10,6 +10,12 @@ boards already resident in HBM.  Prints ONE JSON line on rank 0 with a live
 `roofline` for the dominant kernel (the fused 3x3 conv, timed by hipEvents on its
 own stream over the timed region) and a bounded `cpu_baseline` (the CPU oracle,
 i.e. the reference's PyTorch-CPU algorithm, timed on this host).
+
+After the timed forward loop, a `selfplay` object reports BASELINE configs[2] end to
+end on every rank: 256 concurrent games x 400 simulations/move through the native
+C++ search (int8 leaves, on-GPU encoding, search of one half of the games overlapped
+with the forward of the other), for --sp-moves moves per game; leaf boards summed over
+ranks / max wall time over ranks (weak scaling, no collective inside).
 """
 from __future__ import annotations
 
@@ -89,6 +95,38 @@ def load_traffic():
     return None
 
 
+def selfplay_leg(model, args, rank, dist, dev, local):
+    """BASELINE configs[2]: G games x S sims/move on this rank (native search +
+    pipelined board evaluator); returns aggregate leaf boards/s over ranks."""
+    from games.gomoku import Gomoku
+    from mcts.native_mcts import NativeSelfPlay
+    G, S = args.sp_games, args.sp_sims
+    sp = NativeSelfPlay(None, Gomoku, G, S, cpuct=1.0, dirichlet_alpha=0.03, epsilon=0.25,
+                        apply_dirichlet_n_first_moves=10, evaluator_factory=model.board_evaluator, groups=2)
+    warm = NativeSelfPlay(None, Gomoku, 8, 64, evaluator_factory=model.board_evaluator, groups=2)
+    warm.play(lambda n: 1.0, max_moves=1, use_symmetries=False, seeds=list(range(8)))
+    barrier_sync(dist, local)
+    t0 = time.perf_counter()
+    sp.play(lambda n: 1.0, max_moves=args.sp_moves, use_symmetries=False,
+            seeds=[1000 * rank + i for i in range(G)])
+    barrier_sync(dist, local)
+    dt = time.perf_counter() - t0
+    v = torch.tensor([float(sp.boards), dt], dtype=torch.float64, device=dev)
+    if dist is not None:
+        b = v[:1].clone()
+        dist.all_reduce(b)
+        m = v[1:].clone()
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        v = torch.cat([b, m])
+    boards, dt = float(v[0]), float(v[1])
+    return {"config": f"configs[2]: {G} concurrent games/GPU x {S} sims/move, {args.sp_moves} moves/game, "
+                      f"native C++ search + batched HIP forward (6x128)",
+            "boards_per_s": round(boards / dt, 1), "leaf_boards": int(boards), "seconds": round(dt, 3),
+            "moves_per_s": round(G * args.sp_moves * (dist.get_world_size() if dist else 1) / dt, 1),
+            "nn_share_rank0": round(sp.nn_seconds / dt, 3), "search_share_rank0": round(sp.search_seconds / dt, 3),
+            "mean_batch": round(sp.boards / max(sp.forwards, 1), 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -97,6 +135,9 @@ def main():
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--sp-games", type=int, default=256)
+    ap.add_argument("--sp-sims", type=int, default=400)
+    ap.add_argument("--sp-moves", type=int, default=2, help="moves per game in the self-play leg (0: skip)")
     args = ap.parse_args()
 
     rank, world, local, dist = dist_setup(args.gpus)
@@ -135,6 +176,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
+    selfplay = None
+    if args.sp_moves > 0:
+        selfplay = selfplay_leg(model, args, rank, dist, dev, local)
+
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -169,6 +214,7 @@ def main():
         "roofline": roof,
         "whole_forward_mfma_frac": round(value / world * FLOP_BOARD / PEAK_F32_MFMA, 4),
         "kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in prof.items()},
+        "selfplay": selfplay,
     }
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
