@@ -45,11 +45,15 @@ def init_from_env(backend: Optional[str] = None) -> tuple:
 
 
 def allreduce_mean_(t: torch.Tensor) -> torch.Tensor:
-    """In-place average across ranks (SUM then scale: gloo has no AVG)."""
+    """In-place average across ranks: RCCL's AVG (one pass over xGMI, no extra
+    kernel) on GPU tensors, SUM then scale on gloo (no AVG there)."""
     n = world()
     if n > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        t.div_(n)
+        if t.is_cuda and dist.get_backend() == "nccl":
+            dist.all_reduce(t, op=dist.ReduceOp.AVG)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            t.div_(n)
     return t
 
 

@@ -127,6 +127,37 @@ def selfplay_leg(model, args, rank, dist, dev, local):
             "mean_batch": round(sp.boards / max(sp.forwards, 1), 1)}
 
 
+def train_leg(model, args, rank, world, dist, dev, local):
+    """BASELINE configs[3] train half: PyTorchModel.train_batch_device on 128 samples
+    per GPU (global 128 x N) with the flat-gradient all-reduce over RCCL between
+    backward and clip+Adam (distributed.grad_hook); max step time over ranks."""
+    import distributed as D
+    from synth import synth_encoded
+    B, K = 128, args.train_steps
+    rng = np.random.default_rng(77 + rank)
+    x = torch.from_numpy(synth_encoded(B, seed=77 + rank)).to(dev)
+    pi = rng.random((B, 225)).astype(np.float32)
+    pi /= pi.sum(1, keepdims=True)
+    pi = torch.from_numpy(pi).to(dev)
+    z = torch.from_numpy(rng.integers(-1, 2, (B, 1)).astype(np.float32)).to(dev)
+    model.grad_hook = D.grad_hook() if world > 1 else None
+    for _ in range(3):
+        model.train_batch_device(x, pi, z, return_tensor=True)
+    barrier_sync(dist, local)
+    t0 = time.perf_counter()
+    for _ in range(K):
+        losses = model.train_batch_device(x, pi, z, return_tensor=True)
+    barrier_sync(dist, local)
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    dt = float(dt.item())
+    assert torch.isfinite(losses).all()
+    return {"config": f"configs[3] train step: 6x128, {B} samples/GPU (global {B * world}), "
+                      f"{'RCCL all-reduce of the flat fp32 gradient (7.57 MB) + ' if world > 1 else ''}clip 3.0 + Adam",
+            "samples_per_s": round(B * K * world / dt, 1), "ms_per_step": round(dt / K * 1e3, 3), "steps": K}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -138,6 +169,7 @@ def main():
     ap.add_argument("--sp-games", type=int, default=256)
     ap.add_argument("--sp-sims", type=int, default=400)
     ap.add_argument("--sp-moves", type=int, default=2, help="moves per game in the self-play leg (0: skip)")
+    ap.add_argument("--train-steps", type=int, default=20, help="steps of the data-parallel train leg (0: skip)")
     args = ap.parse_args()
 
     rank, world, local, dist = dist_setup(args.gpus)
@@ -179,6 +211,9 @@ def main():
     selfplay = None
     if args.sp_moves > 0:
         selfplay = selfplay_leg(model, args, rank, dist, dev, local)
+    train = None
+    if args.train_steps > 0:
+        train = train_leg(model, args, rank, world, dist, dev, local)
 
     if rank != 0:
         dist.destroy_process_group()
@@ -215,6 +250,7 @@ def main():
         "whole_forward_mfma_frac": round(value / world * FLOP_BOARD / PEAK_F32_MFMA, 4),
         "kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in prof.items()},
         "selfplay": selfplay,
+        "train": train,
     }
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
