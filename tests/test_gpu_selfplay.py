@@ -123,3 +123,28 @@ def test_native_selfplay_on_gpu_matches_python_search():
         assert wa == wb and len(ea) == len(eb)
         for x, y in zip(ea, eb):
             assert np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1]) and x[2] == y[2]
+
+
+def test_native_pente_10x256_selfplay_on_gpu():
+    """BASELINE configs[4] shape at toy scale: Pente rules (captures) in the native
+    search, 10-block/256-filter net on the GPU, pipelined int8-board evaluation ==
+    the Python search played alone."""
+    from games.pente import Pente
+    from mcts.native_mcts import NativeSelfPlay
+    from mcts.new_mcts_alpha import MCTS
+    from network import PyTorchModel
+    import selfplay
+
+    torch.manual_seed(3)
+    m = PyTorchModel(device="cuda", n_res_blocks=10, channels=256)
+    temp = lambda n: 1.0 if n < 3 else 0.0
+    seeds = [5, 6, 7, 8]
+    kw = dict(cpuct=1.0, dirichlet_alpha=0.3, epsilon=0.25, apply_dirichlet_n_first_moves=2)
+    sp = NativeSelfPlay(None, Pente, len(seeds), 40, evaluator_factory=m.board_evaluator, groups=2, **kw)
+    out = sp.play(temp, max_moves=6, use_symmetries=False, seeds=seeds)
+    mc = MCTS(Pente, 40, m, rng=np.random.RandomState(seeds[1]), **kw)
+    ea, wa = selfplay.play_game_and_collect(mc, Pente(15), temp, max_moves=6, use_symmetries=False)
+    eb, wb = out[1]
+    assert wa == wb and len(ea) == len(eb)
+    for x, y in zip(ea, eb):
+        assert np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1]) and x[2] == y[2]
