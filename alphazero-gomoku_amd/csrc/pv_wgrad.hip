@@ -132,8 +132,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_mfma(
             }
 }
 
-// dW (torch layout [co][ci][3][3]) = sum over slabs, fixed order.
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ dw, int C, int S)
+// dW (torch layout [co][ci][3][3]) = sum over slabs, fixed order: four interleaved
+// partial sums (slabs k = 0,1,2,3 mod 4: independent loads in flight) combined as
+// ((p0 + p1) + (p2 + p3)).
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ dw,
+                                                           int C, int S)
 {
     const int total = 9 * C * C;
     for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
@@ -141,9 +144,18 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __res
         const int tap = idx / (C * C);
         const int rem = idx - tap * C * C;
         const int co = rem / C, ci = rem - co * C;
-        float s = 0.f;
-        for (int k = 0; k < S; ++k) s += slab[(size_t)k * total + idx];
-        dw[(co * C + ci) * 9 + tap] = s;
+        float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
+        int k = 0;
+        for (; k + 4 <= S; k += 4) {
+            p0 += slab[(size_t)k * total + idx];
+            p1 += slab[(size_t)(k + 1) * total + idx];
+            p2 += slab[(size_t)(k + 2) * total + idx];
+            p3 += slab[(size_t)(k + 3) * total + idx];
+        }
+        if (k < S) p0 += slab[(size_t)k * total + idx];
+        if (k + 1 < S) p1 += slab[(size_t)(k + 1) * total + idx];
+        if (k + 2 < S) p2 += slab[(size_t)(k + 2) * total + idx];
+        dw[(co * C + ci) * 9 + tap] = (p0 + p1) + (p2 + p3);
     }
 }
 

@@ -58,28 +58,46 @@ def barrier_sync(dist, local):
     torch.cuda.synchronize()
 
 
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(seconds: float = 12.0) -> dict:
     """Oracle (PyTorch-CPU restatement of reference network.py) timed on this host:
-    batches of 64 boards until ~`seconds` elapse."""
+    batches of 64 boards, ~2/3 of `seconds` at up to 16 threads (the reported value)
+    and ~1/3 single-threaded (1 thread and all cores)."""
     from oracle.boards import encode_batch, synth_positions
     from oracle.ref_net import RefModel
+
+    def timed(threads, budget):
+        torch.set_num_threads(threads)
+        n = 0
+        ref.predict(x)                   # warm-up at this thread count
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < budget:
+            ref.predict(x)
+            n += 64
+        return n, time.perf_counter() - t0
+
     threads = max(1, min(16, os.cpu_count() or 1))
-    torch.set_num_threads(threads)
     torch.manual_seed(0)
     ref = RefModel(BLOCKS, CHANNELS)
     b, p = synth_positions(64, seed=99)
     x = encode_batch(b, p)
-    ref.predict(x)                       # warm-up
-    n = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        ref.predict(x)
-        n += 64
-    dt = time.perf_counter() - t0
+    n, dt = timed(threads, seconds * 2 / 3)
+    n1, dt1 = timed(1, seconds / 3)
     return {"value": round(n / dt, 2), "unit": "boards/s", "cores": threads, "kind": "port",
             "sample": f"{n} boards as {n // 64} predict() batches of 64, 6x128, torch-CPU oracle "
                       f"(oracle/ref_net.py = reference network.py:168-183 restated), {dt:.1f}s, "
-                      f"{threads} threads"}
+                      f"{threads} threads",
+            "value_1_thread": round(n1 / dt1, 2), "cpu_model": _cpu_model(),
+            "host_cpus_visible": os.cpu_count()}
 
 
 def load_traffic():
@@ -105,6 +123,12 @@ def selfplay_leg(model, args, rank, dist, dev, local):
                         apply_dirichlet_n_first_moves=10, evaluator_factory=model.board_evaluator, groups=2)
     warm = NativeSelfPlay(None, Gomoku, 8, 64, evaluator_factory=model.board_evaluator, groups=2)
     warm.play(lambda n: 1.0, max_moves=1, use_symmetries=False, seeds=list(range(8)))
+    # conv tile autotuning is cached per batch bucket: visit the buckets the timed
+    # run's leaf batches (up to G/2 x 32 boards per group) fall in
+    top = (G + 1) // 2 * 32
+    z8 = np.zeros((top, 225), np.int8)
+    for b in sorted({max(1, top * k // 16) for k in range(4, 17)}):
+        model.predict_boards(z8[:b], np.ones(b, np.int8))
     barrier_sync(dist, local)
     t0 = time.perf_counter()
     sp.play(lambda n: 1.0, max_moves=args.sp_moves, use_symmetries=False,

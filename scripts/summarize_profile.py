@@ -42,11 +42,77 @@ def pmc_table(prof_dir):
     return {k: {c: (sum(v) / len(v), len(v)) for c, v in d.items()} for k, d in acc.items()}
 
 
+def hbm_models(B, C=CHANNELS, n_params=1_892_650, S_wgrad=None):
+    """Algorithmic HBM bytes per launch of the bandwidth-bound kernels (name prefix
+    -> bytes) at batch B: every tensor read or written once, fp32."""
+    M = B * 225
+    act = M * C * 4
+    m = {
+        "azg::col_stats_kernel": act,
+        "azg::bn_apply_kernel<128, false>": 2 * act,
+        "azg::bn_apply_kernel<128, true>": 3 * act,
+        "azg::bn_bwd_reduce_kernel": 3 * act,
+        "azg::bn_bwd_apply_kernel<128, false>": 4 * act,
+        "azg::bn_bwd_apply_kernel<128, true>": 5 * act,
+        "azg::adam_kernel": 8 * 4 * n_params,
+        "azg::grad_sqsum_kernel": 4 * n_params,
+        "azg::heads_project<128, false>": act + 3 * M * 4,
+        "azg::heads_project<128, true>": act + 3 * M * 4,
+    }
+    if S_wgrad:
+        m["azg::wgrad_reduce_kernel"] = (S_wgrad + 1) * 9 * C * C * 4
+    return m
+
+
+def bw_table(stats, models):
+    rows = []
+    for r in stats:
+        name = r["Name"]
+        short_name = name.replace("void ", "")
+        for k, b in models.items():
+            if short_name.startswith(k):
+                us = float(r["AverageNs"]) / 1e3
+                rows.append(f"| `{short(short_name, 60)}` | {r['Calls']} | {us:.1f} | {b / 1e6:.1f} | "
+                            f"{b / (us * 1e-6) / 1e9:.0f} | {b / (us * 1e-6) / 8e12 * 100:.0f} % |")
+                break
+    if not rows:
+        return []
+    return ["| HBM-bound kernel | calls | avg us | algorithmic MB | GB/s | of 8 TB/s |",
+            "|---|---|---|---|---|---|"] + rows + [""]
+
+
+def selfplay_busy(trace_csv):
+    """GPU busy fraction over the self-play leg: union of kernel intervals between
+    the first board-input stem kernel and the last kernel of the run."""
+    rows = read_csv(trace_csv)
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+    starts = [a for a, _, n in iv if "stem_conv" in n and "true>" in n]
+    if not starts:
+        return None
+    # the timed leg starts after the warm-up game: take the window from the last
+    # gap > 50 ms before the final board-input stem launches
+    t0 = starts[0]
+    sel = [(a, b) for a, b, _ in iv if a >= t0]
+    t_end = max(b for _, b in sel)
+    busy, cur_a, cur_b = 0, None, None
+    for a, b in sel:
+        if cur_b is None or a > cur_b:
+            if cur_b is not None:
+                busy += cur_b - cur_a
+            cur_a, cur_b = a, b
+        else:
+            cur_b = max(cur_b, b)
+    busy += cur_b - cur_a
+    return {"window_ms": (t_end - t0) / 1e6, "busy_ms": busy / 1e6, "busy_frac": busy / max(t_end - t0, 1),
+            "kernels": len(sel)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("prof_dir")
     ap.add_argument("tag")
     ap.add_argument("--train", default=None)
+    ap.add_argument("--selfplay", default=None)
     args = ap.parse_args()
     os.makedirs(PROF, exist_ok=True)
     stats_path = os.path.join(args.prof_dir, "trace", "run_kernel_stats.csv")
@@ -118,6 +184,7 @@ def main():
                        "hbm_bytes_per_launch": round(traffic), "fetch_bytes": round(fetch_b),
                        "write_bytes": round(write_b), "algorithmic_bytes": round(alg),
                        "avg_launch_us": round(avg_ns / 1e3, 2)}, f, indent=1)
+    lines += ["## HBM-bound kernels of the forward (B=512)", ""] + bw_table(stats, hbm_models(BATCH))
     if args.train:
         tpath = os.path.join(args.train, "trace", "run_kernel_stats.csv")
         if os.path.exists(tpath):
@@ -129,6 +196,19 @@ def main():
                 lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
                              f"{float(r['TotalDurationNs']) / 1e6:.2f} | {float(r['Percentage']):.1f} |")
             lines.append("")
+            lines += ["### HBM-bound kernels of the train step (B=128)", ""]
+            lines += bw_table(ts, hbm_models(128, S_wgrad=(128 * 225 + 543) // 544))
+    if args.selfplay:
+        tr = os.path.join(args.selfplay, "trace", "run_kernel_trace.csv")
+        st = os.path.join(args.selfplay, "trace", "run_kernel_stats.csv")
+        if os.path.exists(tr):
+            shutil.copy(st, os.path.join(PROF, f"{args.tag}_selfplay_kernel_stats.csv"))
+            b = selfplay_busy(tr)
+            if b:
+                lines += ["## Self-play leg (bench.py: 256 games x 400 sims, native search, int8 leaves)", "",
+                          f"* GPU busy {b['busy_ms']:.1f} ms of {b['window_ms']:.1f} ms "
+                          f"({b['busy_frac'] * 100:.1f} %) from the first board-input forward to the last "
+                          f"kernel ({b['kernels']} kernels; includes the warm-up game and bucket warm-up)", ""]
     with open(os.path.join(PROF, f"{args.tag}_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
