@@ -62,6 +62,7 @@ int32_t azg_pv_destroy(azg_pv* h)
     free_workspace(h);
     if (h->wbase) (void)hipFree(h->wbase);
     if (h->bn_desc_dev) (void)hipFree(h->bn_desc_dev);
+    if (h->conv_off_dev) (void)hipFree(h->conv_off_dev);
     for (auto& e : h->prof_ev) (void)hipEventDestroy(e);
     delete h;
     return 0;
@@ -102,6 +103,15 @@ int32_t azg_pv_bind(azg_pv* h, float* params, float* grads, float* bn_stats)
         if (e == hipSuccess)
             e = hipMemcpy(h->bn_desc_dev, h->bn_desc.data(), sizeof(BnDesc) * h->bn_desc.size(), hipMemcpyHostToDevice);
         if (e != hipSuccess) return fail("azg_pv_bind: bn descriptor upload", e);
+        std::vector<int64_t> offs(2 * h->NB > 0 ? 2 * h->NB : 1, 0);
+        for (int i = 0; i < h->NB; ++i) {
+            offs[2 * i] = h->poff[h->t_blk[i].w1];
+            offs[2 * i + 1] = h->poff[h->t_blk[i].w2];
+        }
+        e = hipMalloc(&h->conv_off_dev, sizeof(int64_t) * offs.size());
+        if (e == hipSuccess)
+            e = hipMemcpy(h->conv_off_dev, offs.data(), sizeof(int64_t) * offs.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) return fail("azg_pv_bind: conv offset upload", e);
     }
     h->params = params;
     h->grads = grads;
@@ -301,17 +311,13 @@ int32_t ensure_eval_workspace(azg_pv* h, int batch, hipStream_t st)
     return 0;
 }
 
-int32_t repack(azg_pv* h, hipStream_t st)
+int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst)
 {
     const int C = h->C;
     const float* P = h->params;
     AZG_TRY(launch_pack_stem(P + h->poff[h->t_stem_w], h->wstem, C, st), "repack: stem");
-    for (int i = 0; i < h->NB; ++i) {
-        AZG_TRY(launch_pack_conv3x3(P + h->poff[h->t_blk[i].w1], h->wpack + (size_t)(2 * i) * 9 * C * C, C, st),
-                "repack: conv1");
-        AZG_TRY(launch_pack_conv3x3(P + h->poff[h->t_blk[i].w2], h->wpack + (size_t)(2 * i + 1) * 9 * C * C, C, st),
-                "repack: conv2");
-    }
+    if (h->NB > 0)   // every residual conv in one launch (and its dgrad packing when training)
+        AZG_TRY(launch_pack_convs(P, h->conv_off_dev, 2 * h->NB, h->wpack, dgrad_dst, C, st), "repack: convs");
     AZG_TRY(launch_fold_bn(P, h->bn, h->bn_desc_dev, (int)h->bn_desc.size(), h->scale, h->shift, st),
             "repack: fold_bn");
     return 0;

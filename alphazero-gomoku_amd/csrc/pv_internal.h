@@ -45,8 +45,8 @@ hipError_t launch_heads_fwd(int C, const float* act, const float* wpc, const flo
 hipError_t launch_heads_project(int C, bool bn, const float* act, const float* wpc, const float* wvc,
                                 const float* hscale, const float* hshift, float* hout, int M, hipStream_t st);
 hipError_t launch_small_gemm(const GemmProb& p0, const GemmProb* p1, hipStream_t st);
-hipError_t launch_pack_conv3x3(const float* w, float* wp, int C, hipStream_t st);
-hipError_t launch_pack_dgrad(const float* w, float* wd, int C, hipStream_t st);
+hipError_t launch_pack_convs(const float* params, const int64_t* offs, int nl, float* wp, float* wd, int C,
+                             hipStream_t st);
 hipError_t launch_pack_stem(const float* w, float* ws, int C, hipStream_t st);
 hipError_t launch_transpose(const float* src, float* dst, int R, int Cc, hipStream_t st);
 hipError_t launch_fold_bn(const float* params, const float* stats, const void* desc, int nlayers,
@@ -70,6 +70,7 @@ struct azg_pv {
     int bn_stem = 0, bn_pol = 0, bn_val = 0;
     std::vector<azg::BlockBn> bn_blk;
     void* bn_desc_dev = nullptr;
+    int64_t* conv_off_dev = nullptr;   // flat-param offset of each 3x3 conv weight (2*NB, block order)
 
     // bound torch-owned buffers
     float* params = nullptr;
@@ -107,7 +108,7 @@ void build_layout(azg_pv* h);
 void free_workspace(azg_pv* h);
 void free_train_workspace(azg_pv* h);
 int32_t ensure_eval_workspace(azg_pv* h, int batch, hipStream_t st);
-int32_t repack(azg_pv* h, hipStream_t st);
+int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst = nullptr);   // dgrad_dst: also pack dgrad weights
 int prof_begin(azg_pv* h, int cls, hipStream_t st);   // returns pair index or -1
 void prof_end(azg_pv* h, int pair, hipStream_t st);
 int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* values, float* logits,

@@ -3,7 +3,8 @@
 // Torch layouts in (network.py:41-73): conv [Cout][Cin][3][3], linear [out][in].
 // Packed layouts out:
 //   res conv  -> wp[kc][n][32], kc = tap*(C/32) + cin/32, tap = ky*3 + kx
-//   dgrad     -> wd[kc][n=cin][32 of cout] for the flipped tap (transpose conv)
+//   dgrad     -> wd[kc][n=cin][32 of cout] for the flipped tap 8 - tap (transpose
+//                conv: dX[ci] at q = sum over taps and cout of dY[co] at q + off(t') W[co][ci][2-ky'][2-kx'])
 //   stem      -> ws[k][c], k = cin*9 + ky*3 + kx
 //   FC        -> W^T [in][out]
 // Eval-mode BN fold, as ATen's CPU inference path (alpha = invstd*gamma,
@@ -14,34 +15,25 @@
 namespace azg {
 
 
-__global__ void pack_conv3x3_kernel(const float* __restrict__ w, float* __restrict__ wp, int C)
+// All residual convs at once: layer l = blockIdx.y reads params + offs[l] and
+// writes the forward packing to wp + l*9*C*C and, when wd is given, the dgrad
+// packing to wd + l*9*C*C (one launch instead of 2 per layer).
+__global__ void pack_convs_kernel(const float* __restrict__ params, const int64_t* __restrict__ offs,
+                                  float* __restrict__ wp, float* __restrict__ wd, int C)
 {
     const int total = 9 * C * C;
     const int cg_n = C / 32;
+    const float* w = params + offs[blockIdx.y];
+    float* wpl = wp + (size_t)blockIdx.y * total;
+    float* wdl = wd ? wd + (size_t)blockIdx.y * total : nullptr;
     for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
         const int k = idx & 31;
         const int n = (idx >> 5) % C;
         const int kc = idx / (32 * C);
         const int tap = kc / cg_n, cg = kc - tap * cg_n;
-        const int ci = cg * 32 + k;
-        wp[idx] = w[(n * C + ci) * 9 + tap];
-    }
-}
-
-// transpose-conv packing for dgrad: dX[ci] at pixel q = sum over taps t' and
-// cout of dY[co] at q + off(t') * W[co][ci][2-ky'][2-kx'] where t' = (ky',kx').
-__global__ void pack_dgrad_kernel(const float* __restrict__ w, float* __restrict__ wd, int C)
-{
-    const int total = 9 * C * C;
-    const int cg_n = C / 32;
-    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
-        const int k = idx & 31;              // cout within chunk
-        const int n = (idx >> 5) % C;        // cin (output of dgrad)
-        const int kc = idx / (32 * C);
-        const int tap = kc / cg_n, cg = kc - tap * cg_n;
-        const int co = cg * 32 + k;
-        const int ftap = 8 - tap;            // (2-ky)*3 + (2-kx)
-        wd[idx] = w[(co * C + n) * 9 + ftap];
+        const int c2 = cg * 32 + k;
+        wpl[idx] = w[(n * C + c2) * 9 + tap];                 // = pack_conv3x3_kernel
+        if (wdl) wdl[idx] = w[(c2 * C + n) * 9 + (8 - tap)];  // = pack_dgrad_kernel
     }
 }
 
@@ -78,15 +70,12 @@ __global__ void fold_bn_kernel(const float* __restrict__ params, const float* __
 
 static inline int nblk(int total) { int b = (total + 255) / 256; return b > 4096 ? 4096 : b; }
 
-hipError_t launch_pack_conv3x3(const float* w, float* wp, int C, hipStream_t st)
+hipError_t launch_pack_convs(const float* params, const int64_t* offs, int nl, float* wp, float* wd, int C,
+                             hipStream_t st)
 {
-    hipLaunchKernelGGL(pack_conv3x3_kernel, dim3(nblk(9 * C * C)), dim3(256), 0, st, w, wp, C);
-    return hipGetLastError();
-}
-
-hipError_t launch_pack_dgrad(const float* w, float* wd, int C, hipStream_t st)
-{
-    hipLaunchKernelGGL(pack_dgrad_kernel, dim3(nblk(9 * C * C)), dim3(256), 0, st, w, wd, C);
+    int nb = nblk(9 * C * C);
+    nb = nb > 256 ? 256 : nb;
+    hipLaunchKernelGGL(pack_convs_kernel, dim3(nb, nl), dim3(256), 0, st, params, offs, wp, wd, C);
     return hipGetLastError();
 }
 

@@ -56,6 +56,13 @@ struct TrainWS {
     float* scal = nullptr;       // [0] total norm, [1] clip coef
     // debug snapshots of gX (AZG_DEBUG_SNAP=1): after heads, after each block
     std::vector<float*> snap;
+    // tower backward: the weight gradient of each conv runs on `side`, concurrently
+    // with the data gradient on the caller's stream (both only read dZ); dZ
+    // alternates between DZ and DZ2 so the next BN backward never overwrites a dZ a
+    // pending wgrad still reads (ev_ready: dZ written; ev_done: its wgrad finished)
+    float* DZ2 = nullptr;
+    hipStream_t side = nullptr;
+    hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
 };
 
 static TrainWS* ws_of(azg_pv* h) { return (TrainWS*)h->train; }
@@ -64,7 +71,13 @@ void free_train_workspace(azg_pv* h)
 {
     TrainWS* w = ws_of(h);
     if (!w) return;
+    if (w->side) (void)hipStreamSynchronize(w->side);
     for (float* p : w->allocs) (void)hipFree(p);
+    for (int i = 0; i < 2; ++i) {
+        if (w->ev_ready[i]) (void)hipEventDestroy(w->ev_ready[i]);
+        if (w->ev_done[i]) (void)hipEventDestroy(w->ev_done[i]);
+    }
+    if (w->side) (void)hipStreamDestroy(w->side);
     delete w;
     h->train = nullptr;
 }
@@ -791,6 +804,15 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     A(w->DZ, act, true);
     A(w->DH, act, true);
     A(w->GR, act, true);
+    A(w->DZ2, act, true);
+    {
+        hipError_t e = hipStreamCreateWithFlags(&w->side, hipStreamNonBlocking);
+        for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+            e = hipEventCreateWithFlags(&w->ev_ready[i], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&w->ev_done[i], hipEventDisableTiming);
+        }
+        if (e != hipSuccess) return set_error("train: side stream / events", e);
+    }
     A(w->wdpack, (size_t)(2 * NB > 0 ? 2 * NB : 1) * 9 * C * C, false);
     const size_t nf = h->nfold;
     A(w->bmean, nf, true); A(w->binv, nf, true); A(w->bscale, nf, true); A(w->bshift, nf, true);
@@ -901,12 +923,27 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         AZG_CK(hipGetLastError(), "train: bn_bwd_apply");
         return 0;
     };
-    auto wgrad = [&](const float* dz, const float* xin, int tensor) -> int32_t {
-        int pr = prof_begin(h, AZG_PROF_TRAIN_WGRAD, st);
+    // weight gradient of one conv on the side stream, after dZ (slot) is ready
+    bool pending[2] = {false, false};
+    float* dzbuf[2] = {w->DZ, w->DZ2};
+    auto wgrad = [&](int slot, const float* xin, int tensor) -> int32_t {
+        AZG_CK(hipEventRecord(w->ev_ready[slot], st), "train: event record");
+        AZG_CK(hipStreamWaitEvent(w->side, w->ev_ready[slot], 0), "train: stream wait");
+        int pr = prof_begin(h, AZG_PROF_TRAIN_WGRAD, w->side);
         const int rps = wgrad_rows_per_split(C, M);
-        AZG_CK(launch_wgrad(C, dz, xin, w->slab, G + h->poff[tensor], M, (M + rps - 1) / rps, rps, st),
+        AZG_CK(launch_wgrad(C, dzbuf[slot], xin, w->slab, G + h->poff[tensor], M, (M + rps - 1) / rps, rps, w->side),
                "train: wgrad");
-        prof_end(h, pr, st);
+        prof_end(h, pr, w->side);
+        AZG_CK(hipEventRecord(w->ev_done[slot], w->side), "train: event record");
+        pending[slot] = true;
+        return 0;
+    };
+    // the caller's stream may overwrite dZ (slot) only after its wgrad has read it
+    auto reuse = [&](int slot) -> int32_t {
+        if (pending[slot]) {
+            AZG_CK(hipStreamWaitEvent(st, w->ev_done[slot], 0), "train: stream wait");
+            pending[slot] = false;
+        }
         return 0;
     };
     int32_t r;
@@ -998,15 +1035,19 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     // ---- tower backward ----
     for (int i = NB - 1; i >= 0; --i) {
         const float* Xin = i == 0 ? w->a0 : w->xo[i - 1];
-        R(bwd_bn(w->gX, w->xo[i], w->z2[i], h->bn_blk[i].second, w->DZ, w->GR));
-        R(wgrad(w->DZ, w->hh[i], h->t_blk[i].w2));
-        R(conv(EPI_RAW, w->DZ, w->wdpack + (size_t)(2 * i + 1) * 9 * C * C, nullptr, w->DH));
-        R(bwd_bn(w->DH, w->hh[i], w->z1[i], h->bn_blk[i].first, w->DZ, nullptr));
-        R(wgrad(w->DZ, Xin, h->t_blk[i].w1));
-        R(conv(EPI_ADD, w->DZ, w->wdpack + (size_t)(2 * i) * 9 * C * C, w->GR, w->gX));
+        R(reuse(0));
+        R(bwd_bn(w->gX, w->xo[i], w->z2[i], h->bn_blk[i].second, dzbuf[0], w->GR));
+        R(wgrad(0, w->hh[i], h->t_blk[i].w2));
+        R(conv(EPI_RAW, dzbuf[0], w->wdpack + (size_t)(2 * i + 1) * 9 * C * C, nullptr, w->DH));
+        R(reuse(1));
+        R(bwd_bn(w->DH, w->hh[i], w->z1[i], h->bn_blk[i].first, dzbuf[1], nullptr));
+        R(wgrad(1, Xin, h->t_blk[i].w1));
+        R(conv(EPI_ADD, dzbuf[1], w->wdpack + (size_t)(2 * i) * 9 * C * C, w->GR, w->gX));
         R(snap(NB - i));
     }
     // ---- stem backward ----
+    R(reuse(0));
+    R(reuse(1));                 // joins the side stream: every conv weight grad is done
     R(bwd_bn(w->gX, w->a0, w->z0, h->bn_stem, w->DZ, nullptr));
     hipLaunchKernelGGL((stem_wgrad_kernel<C>), dim3(B), dim3(256), 0, st, x, w->DZ, w->spart);
     AZG_CK(hipGetLastError(), "train: stem_wgrad");
@@ -1021,15 +1062,9 @@ int32_t train_backward(azg_pv* h, const float* x, const float* pis, const float*
                        hipStream_t st)
 {
     if (int32_t r = ensure_train_ws(h, B, st)) return r;
-    if (int32_t r = repack(h, st)) return r;
     TrainWS* w = ws_of(h);
+    if (int32_t r = repack(h, st, w->wdpack)) return r;
     const int C = h->C;
-    for (int i = 0; i < 2 * h->NB; ++i) {
-        const int blk = i / 2;
-        const int t = (i & 1) ? h->t_blk[blk].w2 : h->t_blk[blk].w1;
-        hipError_t e = launch_pack_dgrad(h->params + h->poff[t], w->wdpack + (size_t)i * 9 * C * C, C, st);
-        if (e != hipSuccess) return set_error("train: pack_dgrad", e);
-    }
     int32_t r;
     switch (C) {
         case 64: r = train_backward_t<64>(h, x, pis, zs, B, losses, st); break;
