@@ -131,8 +131,9 @@ int32_t azg_pv_forward(azg_pv* h, const float* x, int32_t batch, float* probs, f
                        float* logits, void* stream)
 {
     if (!h || !h->params) return fail("azg_pv_forward: handle not bound (azg_pv_bind)");
+    if (batch < 0) return fail("azg_pv_forward: negative batch");
+    if (batch == 0) return 0;            // empty batch: nothing to do (empty tensors have null data)
     if (!x || !probs || !values) return fail("azg_pv_forward: null x/probs/values");
-    if (batch <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     if (int32_t r = ensure_eval_workspace(h, batch, st)) return r;
     if (h->dirty) {
@@ -146,9 +147,10 @@ int32_t azg_pv_forward_boards(azg_pv* h, const int8_t* boards, const int8_t* pla
                               float* values, float* priors, void* stream)
 {
     if (!h || !h->params) return fail("azg_pv_forward_boards: handle not bound (azg_pv_bind)");
-    if (!boards || !players || !probs || !values) return fail("azg_pv_forward_boards: null boards/players/probs/values");
     if (h->cfg.board != BOARD || h->cfg.in_ch != 3) return fail("azg_pv_forward_boards: needs a 15x15, 3-plane net");
-    if (batch <= 0) return 0;
+    if (batch < 0) return fail("azg_pv_forward_boards: negative batch");
+    if (batch == 0) return 0;
+    if (!boards || !players || !probs || !values) return fail("azg_pv_forward_boards: null boards/players/probs/values");
     hipStream_t st = (hipStream_t)stream;
     if (int32_t r = ensure_eval_workspace(h, batch, st)) return r;
     if (h->dirty) {

@@ -163,3 +163,36 @@ def test_board_evaluator_async_matches_predict():
     p_ref, v_ref = m.predict(encode_batch(boards, players))
     masks = np.stack([valid_mask(b) for b in boards]).astype(np.float32)
     assert np.array_equal(pri, p_ref * masks) and np.array_equal(v, v_ref)
+
+
+def test_full_size_batches_properties():
+    """At the self-play batch size (configs[2]: up to 8192 boards, 6x128) through the
+    board-input path: every row equals the same board evaluated alone at B=1 and in
+    a B=512 batch (bitwise), probs are a distribution, priors vanish on occupied
+    points, values lie in [-1, 1]."""
+    m = make_model(6, 128, seed=2)
+    B = 8192
+    boards, players = synth_positions(B, seed=31)
+    bi8 = np.asarray(boards, np.int8)
+    pl8 = np.asarray(players, np.int8)
+    pri, v = m.predict_boards(bi8, pl8)
+    probs, v2 = m.predict_boards(bi8, pl8, masked=False)
+    assert np.array_equal(v, v2)
+    assert np.allclose(probs.sum(1), 1.0, atol=2e-5) and np.all(np.abs(v) <= 1.0)
+    occ = bi8.reshape(B, -1) != 0
+    assert np.all(pri[occ] == 0) and np.array_equal(pri[~occ], probs[~occ])
+    rows = np.random.default_rng(5).choice(B, 24, replace=False)
+    for i in rows[:8]:
+        p1, v1 = m.predict_boards(bi8[i:i + 1], pl8[i:i + 1], masked=False)
+        assert np.array_equal(p1[0], probs[i]) and np.array_equal(v1[0], v[i])
+    p512, v512 = m.predict_boards(bi8[rows[8]:rows[8] + 512], pl8[rows[8]:rows[8] + 512], masked=False)
+    n = min(512, B - rows[8])
+    assert np.array_equal(p512[:n], probs[rows[8]:rows[8] + n]) and np.array_equal(v512[:n], v[rows[8]:rows[8] + n])
+
+
+def test_empty_batch():
+    m = make_model(3, 64)
+    p, v = m.predict(np.zeros((0, 3, 15, 15), np.float32))
+    assert p.shape == (0, 225) and v.shape == (0, 1)
+    p, v = m.predict_boards(np.zeros((0, 225), np.int8), np.zeros(0, np.int8))
+    assert p.shape == (0, 225) and v.shape == (0, 1)
