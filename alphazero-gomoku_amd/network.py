@@ -273,7 +273,7 @@ class PyTorchModel:
         [B]: the encoding (games/gomoku.py:130-150) runs inside the stem kernel.
         Returns (priors = probs * valid if masked else probs, values [B,1]) as numpy."""
         eng = self.engine
-        b = torch.from_numpy(np.ascontiguousarray(boards, dtype=np.int8).reshape(len(boards), -1)).to(eng.device)
+        b = torch.from_numpy(np.ascontiguousarray(boards, dtype=np.int8).reshape(len(boards), 225)).to(eng.device)
         pl = torch.from_numpy(np.ascontiguousarray(players, dtype=np.int8).reshape(-1)).to(eng.device)
         B = int(b.shape[0])
         probs = torch.empty((B, 225), dtype=torch.float32, device=eng.device)
