@@ -56,7 +56,8 @@ struct ConvTile {
 
 // ABL (ablation, timing studies only; 0 in every product launch): bit 1 skips the
 // global loads, bit 2 replaces LDS fragment reads by register values, bit 4 drops
-// the per-chunk barrier.  Results are garbage when ABL != 0.
+// the per-chunk barrier, bit 8 skips the epilogue stores (kept live by a never-true
+// compare).  Results are garbage when ABL != 0.
 template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, int ABL = 0, int SB = 0>
 __global__ __launch_bounds__(64 * NW_, NW_ / 2) void conv3x3_mfma(
     const float* __restrict__ in, const float* __restrict__ wp,
@@ -206,6 +207,205 @@ __global__ __launch_bounds__(64 * NW_, NW_ / 2) void conv3x3_mfma(
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m < M && (!(ABL & 8) || acc[i][j][r] == 1234.5f)) {
+                    const int o = pad_off(m, C) + col;
+                    float v = acc[i][j][r];
+                    if (EPI == EPI_BN_RELU) {
+                        v = fmaxf(v * s_ + t_, 0.f);
+                    } else if (EPI == EPI_BN_RES_RELU) {
+                        v = fmaxf(v * s_ + t_ + resid[o], 0.f);
+                    } else if (EPI == EPI_ADD) {
+                        v = v + resid[o];
+                    }
+                    out[o] = v;
+                }
+            }
+        }
+    }
+}
+
+// ---- halo-staged variant ---------------------------------------------------
+//
+// Padded-pixel ("row") index of interior pixel m; a 3x3 tap is the constant row
+// shift (ky-1)*17 + (kx-1).  Padded rows are contiguous across boards, so the
+// input rows every tap of a BM-pixel tile reads form ONE contiguous range
+// [row(m0) - 18, row(m0+BM-1) + 18]: the tile's halo.
+__host__ __device__ constexpr int pad_row(int m)
+{
+    return (m / PIX) * PADPIX + ((m % PIX) / BOARD + 1) * PADW + (m % BOARD) + 1;
+}
+// largest halo (rows) over every tile position: m0 mod 225 repeats after 225 tiles
+constexpr int halo_span(int BM)
+{
+    int mx = 0;
+    for (int t = 0; t < PIX; ++t) {
+        const int m0 = t * BM;
+        const int s = pad_row(m0 + BM - 1) - pad_row(m0) + 2 * (PADW + 1) + 1;
+        mx = s > mx ? s : mx;
+    }
+    return mx;
+}
+
+// Same GEMM as conv3x3_mfma, K ordered input-channel-group major: for each 32-wide
+// channel group cg the tile's halo slice [rows][32] is staged into LDS ONCE and all
+// 9 taps read their shifted A fragments from it (9x fewer A loads from L2 than
+// staging one A tile per (tap, cg) chunk); the weights still stream per chunk
+// through a double-buffered LDS tile.  Accumulation: one MFMA chain per channel
+// group over its 9 taps x 32 channels (288 terms), group sums added in cg order
+// -- error growth chain(288) + C/32, cf. chain(9C) for a single chain.  The K
+// order is per output element and the same for every tile shape and position
+// (tuning never changes numerics; the forward stays batch-independent).
+// Halo rows are staged through registers (loads issued over the first taps of the
+// previous group) into a single LDS buffer, swapped behind one extra barrier per
+// group.
+template <int C, int BN_, int WM_, int TM_, int NW_, int EPI>
+__global__ __launch_bounds__(64 * NW_, 2) void conv3x3_halo(
+    const float* __restrict__ in, const float* __restrict__ wp,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ resid, float* __restrict__ out, int M)
+{
+    using T = ConvTile<C, BN_, WM_, TM_, NW_>;
+    constexpr int RPP = T::RPP;
+    constexpr int BM = T::BM, BN = T::BN, BK = T::BK;
+    constexpr int CG = T::CG, WN = T::WN, TM = T::TM, TN = T::TN;
+    constexpr int B_LD = T::B_LD;
+    constexpr int HS = halo_span(BM);
+    constexpr int H_LD = (HS + RPP - 1) / RPP;
+    constexpr int HR = H_LD * RPP;
+    static_assert(RPP % 16 == 0, "halo staging rows must keep the row swizzle");
+    static_assert(H_LD <= 9, "halo loads are spread over the 9 taps");
+
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* Ah = smem;                 // [HR][32]
+    float* Bs = smem + HR * BK;       // [2][BN][32]
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    constexpr int NTN = C / BN;
+    const int L = blockIdx.x, nt = gridDim.x;
+    const int xcd = L & 7, q8 = nt >> 3, r8 = nt & 7;
+    const int t = xcd * q8 + min(xcd, r8) + (L >> 3);
+    const int m0 = (t / NTN) * BM;
+    const int n0 = (t % NTN) * BN;
+    const int mlast = min(m0 + BM, M) - 1;
+    const int hbase = pad_row(m0) - (PADW + 1);
+    const int hmax = pad_row(mlast) + (PADW + 1);
+
+    const int sr = tid >> 3, sc = (tid & 7) * 4;
+    int hsrc[H_LD];
+#pragma unroll
+    for (int i = 0; i < H_LD; ++i) {
+        const int r = min(hbase + sr + RPP * i, hmax);   // rows past the tile's need: any valid row
+        hsrc[i] = r * C + sc;
+    }
+    const float* wsrc = wp + (size_t)(n0 + sr) * BK + sc;
+
+    f32x4 rh[H_LD], rb[B_LD];
+    auto hload = [&](int cg, int i) { rh[i] = *(const f32x4*)(in + hsrc[i] + cg * BK); };
+    auto bload = [&](int kc) {
+        const float* wk = wsrc + (size_t)kc * C * BK;
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) rb[i] = *(const f32x4*)(wk + RPP * i * BK);
+    };
+    const int wchunk = ((tid & 7) ^ ((sr >> 1) & 7)) * 4;
+    auto hstore = [&]() {
+#pragma unroll
+        for (int i = 0; i < H_LD; ++i) *(f32x4*)(Ah + (sr + RPP * i) * BK + wchunk) = rh[i];
+    };
+    auto bstore = [&](int buf) {
+        float* b = Bs + buf * BN * BK;
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) *(f32x4*)(b + (sr + RPP * i) * BK + wchunk) = rb[i];
+    };
+
+    const int r32 = lane & 31, h = lane >> 5;
+    // halo row of each fragment pixel (tail pixels clamp to the last valid one)
+    int hrow[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) hrow[i] = pad_row(min(m0 + wm * TM * 32 + i * 32 + r32, M - 1)) - hbase;
+    const int bswz = (r32 >> 1) & 7;
+    const int brow = (wn * TN * 32 + r32) * BK;
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+#pragma unroll
+    for (int i = 0; i < H_LD; ++i) hload(0, i);
+    bload(0);
+    hstore();
+    bstore(0);
+    __syncthreads();
+
+    for (int cg = 0; cg < CG; ++cg) {
+        f32x16 at[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) at[i][j][r] = 0.f;
+        const bool more = cg + 1 < CG;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int cur = (cg + tap) & 1;        // chunk index cg*9 + tap, parity
+            if (tap < 8) bload((tap + 1) * CG + cg);
+            else if (more) bload(cg + 1);
+            if (more && tap < H_LD) hload(cg + 1, tap);
+            __builtin_amdgcn_sched_barrier(0);
+            const int d = (tap / 3 - 1) * PADW + (tap % 3 - 1);
+            int arow[TM], aswz[TM];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int r = hrow[i] + d;
+                arow[i] = r * BK;
+                aswz[i] = (r >> 1) & 7;
+            }
+            const float* Bb = Bs + cur * BN * BK;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                f32x4 a[TM], b[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) a[i] = *(const f32x4*)(Ah + arow[i] + (((h * 4 + q) ^ aswz[i]) * 4));
+                const int rc = ((h * 4 + q) ^ bswz) * 4;
+#pragma unroll
+                for (int j = 0; j < TN; ++j) b[j] = *(const f32x4*)(Bb + brow + j * 32 * BK + rc);
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            at[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], at[i][j], 0, 0, 0);
+            }
+            if (tap < 8 || more) bstore(cur ^ 1);
+            __syncthreads();
+            if (tap == 8 && more) {
+                hstore();            // every wave is past its last read of this group's halo
+                __syncthreads();
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] += at[i][j];
+    }
+
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * TN * 32 + j * 32 + r32;
+        float s_ = 1.f, t_ = 0.f;
+        if (EPI == EPI_BN_RELU || EPI == EPI_BN_RES_RELU) { s_ = scale[col]; t_ = shift[col]; }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (m < M) {
                     const int o = pad_off(m, C) + col;
                     float v = acc[i][j][r];
@@ -221,6 +421,13 @@ __global__ __launch_bounds__(64 * NW_, NW_ / 2) void conv3x3_mfma(
             }
         }
     }
+}
+
+template <int C, int BN, int WM, int TM, int NW>
+constexpr int halo_lds_bytes()
+{
+    using T = ConvTile<C, BN, WM, TM, NW>;
+    return ((halo_span(T::BM) + T::RPP - 1) / T::RPP * T::RPP + 2 * BN) * T::BK * 4;
 }
 
 // Stem conv 3->C (K = 27) on the VALU: 0.2 % of the forward FLOPs.  One
@@ -310,10 +517,39 @@ static hipError_t launch_conv_t(const float* in, const float* wp, const float* s
     return hipGetLastError();
 }
 
+template <int C, int BN, int WM, int TM, int NW, int EPI>
+static hipError_t launch_halo_t(const float* in, const float* wp, const float* scale, const float* shift,
+                                const float* resid, float* out, int M, hipStream_t st)
+{
+    using T = ConvTile<C, BN, WM, TM, NW>;
+    constexpr int lds = halo_lds_bytes<C, BN, WM, TM, NW>();
+    static bool attr_done = false;
+    if (!attr_done) {
+        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_halo<C, BN, WM, TM, NW, EPI>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return e;
+        attr_done = true;
+    }
+    dim3 grid(((M + T::BM - 1) / T::BM) * (C / T::BN));
+    hipLaunchKernelGGL((conv3x3_halo<C, BN, WM, TM, NW, EPI>), grid, dim3(T::NT), lds, st, in, wp, scale, shift,
+                       resid, out, M);
+    return hipGetLastError();
+}
+
+int g_conv_variant = 1;   // 1: halo-staged (product); 0: per-chunk A staging (timing studies)
+
 template <int C, int BN, int WM, int TM, int NW = 4, int SB = 0>
 static hipError_t launch_conv_epi(int epi, const float* in, const float* wp, const float* scale, const float* shift,
                                   const float* resid, float* out, int M, hipStream_t st)
 {
+    if (g_conv_variant == 1 && SB == 0) {
+        switch (epi) {
+            case EPI_BN_RELU: return launch_halo_t<C, BN, WM, TM, NW, EPI_BN_RELU>(in, wp, scale, shift, resid, out, M, st);
+            case EPI_BN_RES_RELU: return launch_halo_t<C, BN, WM, TM, NW, EPI_BN_RES_RELU>(in, wp, scale, shift, resid, out, M, st);
+            case EPI_ADD: return launch_halo_t<C, BN, WM, TM, NW, EPI_ADD>(in, wp, scale, shift, resid, out, M, st);
+            default: return launch_halo_t<C, BN, WM, TM, NW, EPI_RAW>(in, wp, scale, shift, resid, out, M, st);
+        }
+    }
     switch (epi) {
         case EPI_BN_RELU: return launch_conv_t<C, BN, WM, TM, NW, EPI_BN_RELU, SB>(in, wp, scale, shift, resid, out, M, st);
         case EPI_BN_RES_RELU: return launch_conv_t<C, BN, WM, TM, NW, EPI_BN_RES_RELU, SB>(in, wp, scale, shift, resid, out, M, st);
@@ -408,16 +644,16 @@ template <int ABL>
 static hipError_t launch_ablation(const float* in, const float* wp, const float* scale, const float* shift,
                                   const float* resid, float* out, int M, hipStream_t st)
 {
-    using T = ConvTile<128, 128, 1, 5, 4>;
-    (void)hipFuncSetAttribute((const void*)conv3x3_mfma<128, 128, 1, 5, 4, EPI_BN_RELU, ABL>,
+    using T = ConvTile<128, 64, 2, 1, 4>;
+    (void)hipFuncSetAttribute((const void*)conv3x3_mfma<128, 64, 2, 1, 4, EPI_BN_RELU, ABL>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS_BYTES);
-    dim3 grid((M + T::BM - 1) / T::BM);
-    hipLaunchKernelGGL((conv3x3_mfma<128, 128, 1, 5, 4, EPI_BN_RELU, ABL>), grid, dim3(T::NT), T::LDS_BYTES, st,
+    dim3 grid(((M + T::BM - 1) / T::BM) * 2);
+    hipLaunchKernelGGL((conv3x3_mfma<128, 64, 2, 1, 4, EPI_BN_RELU, ABL>), grid, dim3(T::NT), T::LDS_BYTES, st,
                        in, wp, scale, shift, resid, out, M);
     return hipGetLastError();
 }
 
-// timing-only: shape 2 (160x128) with ablation mask g_conv_ablation (C = 128 only)
+// timing-only: shape 5 (64x64) with ablation mask g_conv_ablation (C = 128 only)
 static hipError_t launch_ablated(const float* in, const float* wp, const float* scale, const float* shift,
                                  const float* resid, float* out, int M, hipStream_t st)
 {
@@ -427,6 +663,8 @@ static hipError_t launch_ablated(const float* in, const float* wp, const float* 
         case 3: return launch_ablation<3>(in, wp, scale, shift, resid, out, M, st);
         case 4: return launch_ablation<4>(in, wp, scale, shift, resid, out, M, st);
         case 7: return launch_ablation<7>(in, wp, scale, shift, resid, out, M, st);
+        case 8: return launch_ablation<8>(in, wp, scale, shift, resid, out, M, st);
+        case 15: return launch_ablation<15>(in, wp, scale, shift, resid, out, M, st);
         default: return launch_ablation<0>(in, wp, scale, shift, resid, out, M, st);
     }
 }
@@ -568,6 +806,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     if (key == 3) {   // ablation mask (timing studies only, C=128 EPI_BN_RELU launches)
         const int prev = azg::g_conv_ablation;
         azg::g_conv_ablation = value;
+        return prev;
+    }
+    if (key == 4) {   // conv kernel variant (1 halo-staged, 0 per-chunk staging; timing studies)
+        const int prev = azg::g_conv_variant;
+        azg::g_conv_variant = value;
         return prev;
     }
     if (key == 2) {   // query: tuned shape for (C, M) packed as value = M*1024 + C

@@ -250,7 +250,7 @@ def main():
     achieved = FLOP_CONV * B / conv_avg_s
     roof = {"bound": "mfma", "achieved": round(achieved / 1e12, 3), "peak": PEAK_F32_MFMA / 1e12,
             "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA, 4), "traffic": load_traffic(),
-            "kernel": "azg::conv3x3_mfma<128,*> (fused 3x3 conv + BN + residual + ReLU)",
+            "kernel": "azg::conv3x3_halo<128,*> (fused 3x3 conv + BN + residual + ReLU, halo-staged)",
             "avg_launch_us": round(conv_avg_s * 1e6, 2), "launches": conv_n,
             "flop_per_launch": FLOP_CONV * B}
     out = {

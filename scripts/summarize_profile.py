@@ -128,7 +128,7 @@ def main():
 
     # dominant conv: the product-path conv kernels are the most-called conv3x3 names
     # (autotuning dispatches every candidate shape only twice)
-    convs = [r for r in stats if "conv3x3_mfma" in r["Name"]]
+    convs = [r for r in stats if "conv3x3_halo" in r["Name"] or "conv3x3_mfma" in r["Name"]]
     convs.sort(key=lambda r: int(r["Calls"]), reverse=True)
     top_calls = int(convs[0]["Calls"]) if convs else 0
     tuned = [r for r in convs if int(r["Calls"]) >= top_calls // 2]
