@@ -40,10 +40,11 @@ _SIGS = {
     "azg_pv_profile_enable": (ctypes.c_int32, [_P, ctypes.c_int32]),
     "azg_pv_profile_read": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     "azg_pv_set_tuning": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32]),
+    "azg_pv_tower_status": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_void_p]),
     "azg_pv_debug_copy": (ctypes.c_int32, [_P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32, _P]),
 }
 EXPORTS = tuple(_SIGS)
-PROF_CLASSES = ("conv3x3", "stem", "heads", "train_conv", "train_wgrad", "train_other", "r6", "r7")
+PROF_CLASSES = ("conv3x3", "stem", "heads", "train_conv", "train_wgrad", "train_other", "tower", "r7")
 ABI_VERSION = 1
 
 _lib = None

@@ -4,6 +4,9 @@
 #include "../../include/azg_pv.h"
 #include "pv_internal.h"
 
+#include <map>
+#include <tuple>
+
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -190,6 +193,17 @@ int32_t azg_pv_profile_read(azg_pv* h, double* ms, int64_t* launches)
     return 0;
 }
 
+int32_t azg_pv_tower_status(azg_pv* h, void* stream)
+{
+    if (!h) return fail("azg_pv_tower_status: null handle");
+    if (!h->tower_sync) return 0;
+    unsigned w[2] = {0, 0};
+    hipStream_t st = (hipStream_t)stream;
+    AZG_TRY(hipMemcpyAsync(w, h->tower_sync, sizeof(w), hipMemcpyDeviceToHost, st), "azg_pv_tower_status: copy");
+    AZG_TRY(hipStreamSynchronize(st), "azg_pv_tower_status: sync");
+    return (int32_t)w[1];
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------
@@ -281,6 +295,8 @@ void free_workspace(azg_pv* h)
     }
     if (h->hbuf) (void)hipFree(h->hbuf);
     h->hbuf = nullptr;
+    if (h->tower_sync) (void)hipFree(h->tower_sync);
+    h->tower_sync = nullptr;
     h->act_cap = 0;
     free_train_workspace(h);
 }
@@ -296,7 +312,13 @@ int32_t ensure_eval_workspace(azg_pv* h, int batch, hipStream_t st)
     }
     if (h->hbuf) (void)hipFree(h->hbuf);
     h->hbuf = nullptr;
+    if (h->tower_sync) (void)hipFree(h->tower_sync);
+    h->tower_sync = nullptr;
     h->act_cap = 0;
+    {
+        hipError_t e = hipMalloc(&h->tower_sync, tower_sync_bytes(2 * h->NB, cap * PIX));
+        if (e != hipSuccess) return fail("ensure_eval_workspace: hipMalloc(tower sync)", e);
+    }
     {
         hipError_t e = hipMalloc(&h->hbuf, (size_t)cap * (3 * PIX + ACTIONS + VHID) * sizeof(float));
         if (e != hipSuccess) return fail("ensure_eval_workspace: hipMalloc(head features)", e);
@@ -325,12 +347,13 @@ int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst)
     return 0;
 }
 
-int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* values, float* logits,
-                     hipStream_t st, const int8_t* boards, const int8_t* players, float* priors)
+// Stem + residual tower.  variant 0: one launch per conv; 5 / 8: the persistent
+// tower (pv_tower.hip) with 64x64 / 128x64 tiles.  All bitwise identical.
+static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch, hipStream_t st,
+                              const int8_t* boards, const int8_t* players, float** out)
 {
     const int C = h->C;
     const int M = batch * PIX;
-    const float* P = h->params;
     const BnDesc* bd = h->bn_desc.data();
     int pr = prof_begin(h, AZG_PROF_STEM, st);
     AZG_TRY(launch_stem(C, EPI_BN_RELU, x, h->wstem, h->scale + bd[h->bn_stem].out_off,
@@ -340,6 +363,21 @@ int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* 
     float* X = h->act[0];
     float* H = h->act[1];
     float* Y = h->act[2];
+    if (variant != 0 && h->NB > 0) {
+        // the whole residual tower in one persistent launch
+        int out_off[2 * kTowerMaxBlocks];
+        for (int i = 0; i < h->NB; ++i) {
+            out_off[2 * i] = bd[h->bn_blk[i].first].out_off;
+            out_off[2 * i + 1] = bd[h->bn_blk[i].second].out_off;
+        }
+        pr = prof_begin(h, AZG_PROF_TOWER, st);
+        AZG_TRY(launch_tower(C, h->NB, variant, h->act, h->wpack, h->scale, h->shift, out_off, M, h->tower_sync,
+                             st, &X),
+                "forward: tower");
+        prof_end(h, pr, st);
+        *out = X;
+        return 0;
+    }
     for (int i = 0; i < h->NB; ++i) {
         const BnDesc& b1 = bd[h->bn_blk[i].first];
         const BnDesc& b2 = bd[h->bn_blk[i].second];
@@ -355,8 +393,75 @@ int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* 
         prof_end(h, pr, st);
         float* t = X; X = Y; Y = t;
     }
+    *out = X;
+    return 0;
+}
+
+// Tower variant per (C, blocks, batch bucket): g_tower_mode 0 = per-layer launches,
+// 1 = persistent tower with shape g_tower_shape, 2 = timed on first use of the
+// bucket (stem + tower, every variant, best of 2 after a warm pass; the persistent
+// tower wins from ~128 boards, per-layer launches below and at the largest
+// batches).  While the stream is being captured the untuned default is used.
+static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, const int8_t* boards,
+                         const int8_t* players)
+{
+    if (h->NB == 0 || h->NB > kTowerMaxBlocks) return 0;
+    if ((size_t)batch * PADPIX * h->C * sizeof(float) >= (size_t)INT32_MAX) return 0;
+    if (g_tower_mode == 0) return 0;
+    if (g_tower_mode == 1) return g_tower_shape;
+    const int bucket = conv_batch_bucket(batch * PIX);
+    static std::map<std::tuple<int, int, int>, int> cache;
+    const auto key = std::make_tuple(h->C, h->NB, bucket);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    const int fallback = batch >= 128 ? 8 : 0;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return fallback;
+    const bool prof = h->prof_on;
+    h->prof_on = false;
+    const int cand[3] = {0, 5, 8};
+    float best_ms[3] = {1e30f, 1e30f, 1e30f};
+    hipEvent_t e0, e1;
+    int choice = fallback;
+    if (hipEventCreate(&e0) == hipSuccess) {
+        if (hipEventCreate(&e1) == hipSuccess) {
+            bool ok = true;
+            float* out = nullptr;
+            for (int r = 0; r < 3 && ok; ++r)
+                for (int c = 0; c < 3 && ok; ++c) {
+                    ok = hipEventRecord(e0, st) == hipSuccess &&
+                         stem_and_tower(h, cand[c], x, batch, st, boards, players, &out) == 0 &&
+                         hipEventRecord(e1, st) == hipSuccess && hipEventSynchronize(e1) == hipSuccess;
+                    float ms = 0.f;
+                    if (ok && r > 0 && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms < best_ms[c]) best_ms[c] = ms;
+                }
+            if (ok) {
+                int b = 0;
+                for (int c = 1; c < 3; ++c)
+                    if (best_ms[c] < best_ms[b]) b = c;
+                choice = cand[b];
+            }
+            (void)hipEventDestroy(e1);
+        }
+        (void)hipEventDestroy(e0);
+    }
+    (void)hipGetLastError();
+    h->prof_on = prof;
+    cache[key] = choice;
+    return choice;
+}
+
+int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* values, float* logits,
+                     hipStream_t st, const int8_t* boards, const int8_t* players, float* priors)
+{
+    const int C = h->C;
+    const float* P = h->params;
+    const BnDesc* bd = h->bn_desc.data();
+    const int variant = tower_variant(h, x, batch, st, boards, players);
+    float* X = nullptr;
+    if (int32_t r = stem_and_tower(h, variant, x, batch, st, boards, players, &X)) return r;
     const int ho = bd[h->bn_pol].out_off;   // policy (2) then value (1): contiguous
-    pr = prof_begin(h, AZG_PROF_HEADS, st);
+    int pr = prof_begin(h, AZG_PROF_HEADS, st);
     AZG_TRY(launch_heads_fwd(C, X, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], h->scale + ho, h->shift + ho,
                              P + h->poff[h->t_pfc_w], P + h->poff[h->t_pfc_b], P + h->poff[h->t_vfc1_w],
                              P + h->poff[h->t_vfc1_b],

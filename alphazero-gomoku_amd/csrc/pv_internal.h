@@ -33,6 +33,14 @@ struct BlockBn { int first, second; };
 // kernel launchers (pv_conv.hip, pv_heads.hip, pv_pack.hip, pv_train.hip)
 hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, const float* scale,
                           const float* shift, const float* resid, float* out, int M, hipStream_t st);
+extern int g_tower_mode;
+extern int g_tower_shape;
+constexpr int kTowerMaxBlocks = 32;
+int conv_batch_bucket(int M);
+size_t tower_sync_bytes(int nlayers, int M);
+hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const float* wpack, const float* scale,
+                        const float* shift, const int* out_off, int M, unsigned* sync, hipStream_t st,
+                        float** result);
 hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const float* scale,
                        const float* shift, float* out, int B, hipStream_t st, const int8_t* boards = nullptr,
                        const int8_t* players = nullptr);
@@ -88,6 +96,7 @@ struct azg_pv {
     // eval activations: 3 padded NHWC buffers + head features [B][3][225]
     float* act[3] = {nullptr, nullptr, nullptr};
     float* hbuf = nullptr;
+    unsigned* tower_sync = nullptr;   // persistent tower: work counter, error word, tile counters
     int act_cap = 0;
 
     // train workspace (pv_train.hip)

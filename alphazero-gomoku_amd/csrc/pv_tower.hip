@@ -1,0 +1,187 @@
+// Persistent residual-tower kernel: every 3x3 conv of the eval forward's tower
+// (network.py:98-99, ResidualBlock network.py:9-26) in ONE launch.
+//
+// Why: a per-layer launch ends with a partial round of tiles (at B = 512, 3600
+// 64x64 tiles on 1024 resident slots) and every layer waits for the previous one
+// to drain.  Here workgroups stay resident and claim tiles (layer-major, then M
+// tile, then N tile) from one atomic counter; tile (l, mt) starts as soon as the
+// three layer-(l-1) M tiles whose rows its halo reads (mt-1, mt, mt+1) are done, so
+// the tail of one layer overlaps the head of the next.
+//
+// Tile body: halo_tile (pv_halo.h), identical arithmetic to the per-layer kernel
+// (results are bitwise equal to the per-layer path).
+//
+// Hand-off protocol (cdna_hip_programming.md Guideline 16, R1 + acquire):
+//  * producer: every output element is stored write-through (buffer_store sc1);
+//    each wave drains (s_waitcnt vmcnt(0)); workgroup barrier; one lane adds 1 to
+//    the (layer, M tile) counter with an agent-scope atomic;
+//  * consumer: one lane polls the (up to) three counters with relaxed agent-scope
+//    loads until each equals the number of N tiles, then ONE agent-scope acquire
+//    (L1 invalidate), s_waitcnt vmcnt(0), workgroup barrier, then plain loads.
+// Deadlock freedom: a tile waits only on tiles claimed before it (all of layer
+// l-1 precedes layer l in claim order), and a claimed tile is always executed by a
+// running workgroup, so the oldest unfinished tile can always finish.  Spins are
+// bounded; a timeout sets the error word (read by azg_pv_tower_status) and the
+// workgroup proceeds so the grid always drains.
+//
+// Buffer reuse (WAR): with X -> H -> Y(+X) -> H -> X(+Y) ..., a tile overwrites
+// rows whose readers are exactly (or transitively) the tiles it waits on.
+#include "pv_internal.h"
+#include "pv_halo.h"
+
+namespace azg {
+
+constexpr int kTowerMaxLayers = 2 * kTowerMaxBlocks;
+
+struct TowerLayer {
+    const float* wp;
+    const float* scale;
+    const float* shift;
+    const float* in;
+    const float* resid;    // nullptr for the first conv of a block
+    float* out;
+};
+
+struct TowerArgs {
+    TowerLayer L[kTowerMaxLayers];
+    int nlayers;
+    int M;
+    int act_bytes;       // bytes of one activation buffer (buffer descriptor range)
+    unsigned* sync;      // [0] work counter, [1] error word, [4..] per-(layer, M tile) counters
+};
+
+constexpr unsigned kSpinLimit = 1u << 22;    // x s_sleep(2): seconds, far above any tile time
+
+template <int C, int BN_, int WM_, int TM_, int NW_>
+__global__ __launch_bounds__(64 * NW_, 4) void conv_tower(const TowerArgs a)
+{
+    using T = ConvTile<C, BN_, WM_, TM_, NW_>;
+    constexpr int NTN = C / T::BN;
+    constexpr int LDS_FLOATS = halo_lds_bytes<C, BN_, WM_, TM_, NW_>() / 4;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    int* s_claim = (int*)(smem + LDS_FLOATS);
+
+    const int tid = threadIdx.x;
+    const int mtiles = (a.M + T::BM - 1) / T::BM;
+    const int tpl = mtiles * NTN;
+    const int total = tpl * a.nlayers;
+    unsigned* work = a.sync;
+    unsigned* err = a.sync + 1;
+    unsigned* cnt = a.sync + 4;
+
+    if (tid == 0) s_claim[0] = (int)__hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    int w = s_claim[0];
+    while (w < total) {
+        const int l = w / tpl, t = w - l * tpl;
+        const int mt = t / NTN, nt = t - mt * NTN;
+        __syncthreads();                          // every wave has read s_claim
+        if (tid == 0) {
+            // next claim now: its latency overlaps this tile (read after the tile)
+            s_claim[0] = (int)__hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (l > 0) {
+                const unsigned* c = cnt + (size_t)(l - 1) * mtiles;
+                const int j0 = max(mt - 1, 0), j1 = min(mt + 1, mtiles - 1);
+                for (int j = j0; j <= j1; ++j) {
+                    unsigned spins = 0;
+                    while (__hip_atomic_load(c + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)NTN) {
+                        if (++spins > kSpinLimit) {
+                            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(2);
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        __syncthreads();
+        const TowerLayer& Ly = a.L[l];
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Ly.out, (short)0, a.act_bytes, 0x00020000);
+        halo_tile<C, BN_, WM_, TM_, NW_, EPI_BN_OPTRES_RELU, true>(Ly.in, Ly.wp, Ly.scale, Ly.shift, Ly.resid, Ly.out,
+                                                                  rs, a.M, mt * T::BM, nt * T::BN, smem);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(cnt + (size_t)l * mtiles + mt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        w = s_claim[0];
+    }
+}
+
+template <int C, int BN, int WM, int TM, int NW>
+static hipError_t launch_tower_t(const TowerArgs& a, hipStream_t st, int* grid_out)
+{
+    constexpr int lds = halo_lds_bytes<C, BN, WM, TM, NW>() + 16;
+    static int grid = 0;
+    if (grid == 0) {
+        hipError_t e = hipFuncSetAttribute((const void*)conv_tower<C, BN, WM, TM, NW>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return e;
+        int per_cu = 0, dev = 0, cus = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)conv_tower<C, BN, WM, TM, NW>,
+                                                         64 * NW, lds);
+        if (e != hipSuccess) return e;
+        if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+        if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+        grid = max(1, per_cu) * cus;
+    }
+    if (grid_out) *grid_out = grid;
+    hipLaunchKernelGGL((conv_tower<C, BN, WM, TM, NW>), dim3(grid), dim3(64 * NW), lds, st, a);
+    return hipGetLastError();
+}
+
+int g_tower_shape = 8;   // forced shape when g_tower_mode == 1: 5 = 64x64 (4 waves), 8 = 128x64 (8 waves)
+
+size_t tower_sync_bytes(int nlayers, int M)
+{
+    const int mtiles = (M + 63) / 64;   // the smallest BM (64) has the most M tiles
+    return ((size_t)(4 + nlayers * mtiles) * sizeof(unsigned) + 15) / 16 * 16;
+}
+
+// Eval residual tower in one launch: NB blocks, conv1 X -> H (BN, ReLU), conv2
+// H -> Y (BN, + X, ReLU), X <-> Y.  `act` are the three padded NHWC buffers
+// (act[0] holds the stem output; the result ends in act[0] or act[2], returned in
+// *result).  `sync` must hold tower_sync_bytes(2*NB, M) bytes.
+hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const float* wpack, const float* scale,
+                        const float* shift, const int* out_off, int M, unsigned* sync, hipStream_t st,
+                        float** result)
+{
+    if (2 * NB > kTowerMaxLayers) return hipErrorInvalidValue;
+    const size_t act_bytes = (size_t)(M / PIX) * PADPIX * C * sizeof(float);
+    if (act_bytes >= (size_t)INT32_MAX) return hipErrorInvalidValue;
+    TowerArgs a{};
+    a.nlayers = 2 * NB;
+    a.M = M;
+    a.act_bytes = (int)act_bytes;
+    a.sync = sync;
+    float* X = act[0];
+    float* H = act[1];
+    float* Y = act[2];
+    for (int i = 0; i < NB; ++i) {
+        TowerLayer& c1 = a.L[2 * i];
+        c1 = TowerLayer{wpack + (size_t)(2 * i) * 9 * C * C, scale + out_off[2 * i], shift + out_off[2 * i], X,
+                        nullptr, H};
+        TowerLayer& c2 = a.L[2 * i + 1];
+        c2 = TowerLayer{wpack + (size_t)(2 * i + 1) * 9 * C * C, scale + out_off[2 * i + 1],
+                        shift + out_off[2 * i + 1], H, X, Y};
+        float* t = X;
+        X = Y;
+        Y = t;
+    }
+    *result = X;
+    hipError_t e = hipMemsetAsync(sync, 0, tower_sync_bytes(2 * NB, M), st);
+    if (e != hipSuccess) return e;
+#define AZG_TOWER_C(CC)                                                                    \
+    case CC:                                                                               \
+        if (shape == 8) return launch_tower_t<CC, 64, 4, 1, 8>(a, st, nullptr);    \
+        return launch_tower_t<CC, 64, 2, 1, 4>(a, st, nullptr);
+    switch (C) {
+        AZG_TOWER_C(64)
+        AZG_TOWER_C(128)
+        AZG_TOWER_C(256)
+        default: return hipErrorInvalidValue;
+    }
+#undef AZG_TOWER_C
+}
+
+}  // namespace azg

@@ -119,6 +119,7 @@ enum {
     AZG_PROF_TRAIN_CONV = 3, /* train-mode 3x3 conv fwd + dgrad        */
     AZG_PROF_TRAIN_WGRAD = 4,
     AZG_PROF_TRAIN_OTHER = 5,
+    AZG_PROF_TOWER = 6,      /* persistent residual tower (all 2*NB convs, one launch) */
     AZG_PROF_NCLASS = 8
 };
 int32_t azg_pv_profile_enable(azg_pv* h, int32_t enable);
@@ -129,8 +130,18 @@ int32_t azg_pv_profile_read(azg_pv* h, double* ms, int64_t* launches);
  *   key 1: conv autotuning on/off (default on: the first launch for a (C, M) times
  *          every tile shape on the real operands and caches the fastest; shapes give
  *          bitwise-identical results, so this never changes numerics);
- *   key 2: query the tuned shape for value = M*1024 + C (-1 if not tuned yet). */
+ *   key 2: query the tuned shape for value = M*1024 + C (-1 if not tuned yet);
+ *   key 4: conv kernel variant (1 halo-staged, default; 0 per-chunk staging, timing only);
+ *   key 5: eval residual tower: 0 one launch per conv, 1 one persistent launch
+ *          (shape from key 6), 2 (default) chosen per (C, blocks, batch bucket) by
+ *          timing every variant on first use -- all bitwise identical;
+ *   key 6: persistent-tower tile shape for key 5 = 1 (8: 128x64 / 8 waves, default;
+ *          5: 64x64 / 4 waves). */
 int32_t azg_pv_set_tuning(int32_t key, int32_t value);
+
+/* Persistent-tower health: 0, or nonzero if a tile of the last eval forward on
+ * this handle timed out waiting for its inputs (synchronises `stream`). */
+int32_t azg_pv_tower_status(azg_pv* h, void* stream);
 
 /* Debug/test access to train-workspace activations of the last train step:
  * copies the interior [batch][15][15][C] (NHWC) of buffer `which` (block `index`

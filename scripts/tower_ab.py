@@ -1,0 +1,68 @@
+"""Per-layer conv launches vs the persistent residual tower (one launch), 6x128
+eval forward: residual-tower device time per forward (hipEvents) and whole-forward
+wall time, per batch size and tower tile shape.
+
+    python scripts/tower_ab.py [--batches 128,512,4096] [--steps 10]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "alphazero-gomoku_amd")]
+
+import torch
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batches", default="32,128,256,512,1024,4096")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--blocks", type=int, default=6)
+    ap.add_argument("--channels", type=int, default=128)
+    args = ap.parse_args()
+    from network import PyTorchModel
+    from synth import synth_encoded
+    import _native
+
+    lib = _native.load_library()
+    torch.manual_seed(0)
+    m = PyTorchModel(device="cuda", n_res_blocks=args.blocks, channels=args.channels)
+    eng = m.engine
+    C = args.channels
+    for B in map(int, args.batches.split(",")):
+        x = torch.from_numpy(synth_encoded(B, seed=5)).cuda()
+        probs = torch.empty((B, 225), device="cuda")
+        values = torch.empty((B, 1), device="cuda")
+        flop = 2 * 225 * C * 9 * C * B * 2 * args.blocks
+        row = {"batch": B}
+        for name, mode, shape in (("layers", 0, 5), ("tower64", 1, 5), ("tower128", 1, 8)):
+            lib.azg_pv_set_tuning(5, mode)
+            lib.azg_pv_set_tuning(6, shape)
+            for _ in range(2):
+                eng.forward_into(x, probs, values)
+            best_dev, best_wall = None, None
+            for _ in range(3):
+                eng.profile_enable(True)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(args.steps):
+                    eng.forward_into(x, probs, values)
+                torch.cuda.synchronize()
+                wall = (time.perf_counter() - t0) / args.steps
+                prof = eng.profile_read()
+                eng.profile_enable(False)
+                dev = (prof.get("tower", (0.0, 0))[0] + prof.get("conv3x3", (0.0, 0))[0]) / args.steps
+                best_dev = dev if best_dev is None else min(best_dev, dev)
+                best_wall = wall if best_wall is None else min(best_wall, wall)
+            row[name] = {"tower_ms": round(best_dev, 4), "frac": round(flop / (best_dev * 1e-3) / 157.3e12, 4),
+                         "fwd_ms": round(best_wall * 1e3, 4), "boards_per_s": round(B / best_wall)}
+        print(json.dumps(row), flush=True)
+    lib.azg_pv_set_tuning(5, 2)
+    lib.azg_pv_set_tuning(6, 8)
+
+
+if __name__ == "__main__":
+    main()

@@ -196,3 +196,60 @@ def test_empty_batch():
     assert p.shape == (0, 225) and v.shape == (0, 1)
     p, v = m.predict_boards(np.zeros((0, 225), np.int8), np.zeros(0, np.int8))
     assert p.shape == (0, 225) and v.shape == (0, 1)
+
+
+@pytest.mark.parametrize("blocks,ch,batches", [(6, 128, (512, 1, 37, 256, 2048)), (3, 64, (300, 5)),
+                                               (10, 256, (96, 513))])
+def test_persistent_tower_bitwise_equals_per_layer_launches(blocks, ch, batches):
+    """The persistent residual tower (one launch, tiles handed between workgroups
+    through counters + acquire) computes exactly the per-layer kernels' arithmetic:
+    outputs must be BITWISE equal.  Repeated runs (stale-line hazards show up
+    intermittently), with each tile shape, and the timeout word must stay 0."""
+    import _native
+    from synth import synth_encoded
+    lib = _native.load_library()
+    m = make_model(blocks, ch, seed=3)
+    eng = m.engine
+    stream = torch.cuda.current_stream().cuda_stream
+    prev_mode = lib.azg_pv_set_tuning(5, 1)
+    try:
+        for B in batches:
+            x = torch.from_numpy(synth_encoded(B, seed=B)).cuda()
+            lib.azg_pv_set_tuning(5, 0)
+            p0, v0, l0 = eng.forward(x, want_logits=True)
+            lib.azg_pv_set_tuning(5, 1)
+            for shape in (5, 8):
+                lib.azg_pv_set_tuning(6, shape)
+                for rep in range(3):
+                    p1, v1, l1 = eng.forward(x, want_logits=True)
+                    assert lib.azg_pv_tower_status(eng.h, stream) == 0
+                    assert torch.equal(l0, l1), (B, shape, rep, float((l0 - l1).abs().max()))
+                    assert torch.equal(p0, p1) and torch.equal(v0, v1), (B, shape, rep)
+    finally:
+        lib.azg_pv_set_tuning(6, 5)
+        lib.azg_pv_set_tuning(5, prev_mode)
+
+
+def test_persistent_tower_under_concurrent_load():
+    """Tower forwards on two streams at once (uneven load: a per-layer forward and
+    a tower forward of another model share the GPU) stay bitwise reproducible."""
+    import _native
+    from synth import synth_encoded
+    lib = _native.load_library()
+    m1 = make_model(6, 128, seed=4)
+    m2 = make_model(6, 128, seed=5)
+    x1 = torch.from_numpy(synth_encoded(512, seed=11)).cuda()
+    x2 = torch.from_numpy(synth_encoded(1024, seed=12)).cuda()
+    prev_mode = lib.azg_pv_set_tuning(5, 1)
+    r1 = m1.engine.forward(x1)[0].clone()
+    r2 = m2.engine.forward(x2)[0].clone()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for _ in range(4):
+        with torch.cuda.stream(s1):
+            a = m1.engine.forward(x1)[0]
+        with torch.cuda.stream(s2):
+            b = m2.engine.forward(x2)[0]
+        torch.cuda.synchronize()
+        assert torch.equal(a, r1) and torch.equal(b, r2)
+    lib.azg_pv_set_tuning(5, prev_mode)
