@@ -202,7 +202,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ / 2) void conv3x3_mfma(
 // workgroup L is dispatched to XCD L % 8, so each XCD gets a contiguous run of
 // logical tiles (the N-tiles of one M tile adjacent, then neighbouring M tiles) and
 // the halo rows they share are L2 hits on that XCD.
-template <int C, int BN_, int WM_, int TM_, int NW_, int EPI>
+template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, int ABL = 0>
 __global__ __launch_bounds__(64 * NW_, 2) void conv3x3_halo(
     const float* __restrict__ in, const float* __restrict__ wp,
     const float* __restrict__ scale, const float* __restrict__ shift,
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(64 * NW_, 2) void conv3x3_halo(
     const int L = blockIdx.x, nt = gridDim.x;
     const int xcd = L & 7, q8 = nt >> 3, r8 = nt & 7;
     const int t = xcd * q8 + min(xcd, r8) + (L >> 3);
-    halo_tile<C, BN_, WM_, TM_, NW_, EPI>(in, wp, scale, shift, resid, out,
+    halo_tile<C, BN_, WM_, TM_, NW_, EPI, false, ABL>(in, wp, scale, shift, resid, out,
                                           __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0, 0x00020000), M,
                                           (t / NTN) * T::BM, (t % NTN) * T::BN, smem);
 }
@@ -429,31 +429,39 @@ int g_conv_shape_override = -1;
 int g_conv_autotune = 1;
 int g_conv_ablation = 0;
 
+// timing-only ablations of the product tile (halo kernel, 64x64 4 waves or
+// 128x64 8 waves per g_ablation_shape; C = 128, EPI_BN_RELU launches only)
+int g_ablation_shape = 5;
+
+template <int ABL, int BN, int WM, int TM, int NW>
+static hipError_t launch_ablation_s(const float* in, const float* wp, const float* scale, const float* shift,
+                                    const float* resid, float* out, int M, hipStream_t st)
+{
+    using T = ConvTile<128, BN, WM, TM, NW>;
+    constexpr int lds = halo_lds_bytes<128, BN, WM, TM, NW>();
+    (void)hipFuncSetAttribute((const void*)conv3x3_halo<128, BN, WM, TM, NW, EPI_BN_RELU, ABL>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    dim3 grid(((M + T::BM - 1) / T::BM) * (128 / BN));
+    hipLaunchKernelGGL((conv3x3_halo<128, BN, WM, TM, NW, EPI_BN_RELU, ABL>), grid, dim3(T::NT), lds, st, in, wp,
+                       scale, shift, resid, out, M);
+    return hipGetLastError();
+}
+
 template <int ABL>
 static hipError_t launch_ablation(const float* in, const float* wp, const float* scale, const float* shift,
                                   const float* resid, float* out, int M, hipStream_t st)
 {
-    using T = ConvTile<128, 64, 2, 1, 4>;
-    (void)hipFuncSetAttribute((const void*)conv3x3_mfma<128, 64, 2, 1, 4, EPI_BN_RELU, ABL>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS_BYTES);
-    dim3 grid(((M + T::BM - 1) / T::BM) * 2);
-    hipLaunchKernelGGL((conv3x3_mfma<128, 64, 2, 1, 4, EPI_BN_RELU, ABL>), grid, dim3(T::NT), T::LDS_BYTES, st,
-                       in, wp, scale, shift, resid, out, M);
-    return hipGetLastError();
+    if (g_ablation_shape == 8) return launch_ablation_s<ABL, 64, 4, 1, 8>(in, wp, scale, shift, resid, out, M, st);
+    return launch_ablation_s<ABL, 64, 2, 1, 4>(in, wp, scale, shift, resid, out, M, st);
 }
 
-// timing-only: shape 5 (64x64) with ablation mask g_conv_ablation (C = 128 only)
 static hipError_t launch_ablated(const float* in, const float* wp, const float* scale, const float* shift,
                                  const float* resid, float* out, int M, hipStream_t st)
 {
     switch (g_conv_ablation) {
-        case 1: return launch_ablation<1>(in, wp, scale, shift, resid, out, M, st);
-        case 2: return launch_ablation<2>(in, wp, scale, shift, resid, out, M, st);
-        case 3: return launch_ablation<3>(in, wp, scale, shift, resid, out, M, st);
-        case 4: return launch_ablation<4>(in, wp, scale, shift, resid, out, M, st);
-        case 7: return launch_ablation<7>(in, wp, scale, shift, resid, out, M, st);
-        case 8: return launch_ablation<8>(in, wp, scale, shift, resid, out, M, st);
-        case 15: return launch_ablation<15>(in, wp, scale, shift, resid, out, M, st);
+#define AZG_ABL(k) case k: return launch_ablation<k>(in, wp, scale, shift, resid, out, M, st);
+        AZG_ABL(1) AZG_ABL(2) AZG_ABL(3) AZG_ABL(4) AZG_ABL(8) AZG_ABL(16) AZG_ABL(7) AZG_ABL(31)
+#undef AZG_ABL
         default: return launch_ablation<0>(in, wp, scale, shift, resid, out, M, st);
     }
 }
@@ -595,6 +603,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     if (key == 3) {   // ablation mask (timing studies only, C=128 EPI_BN_RELU launches)
         const int prev = azg::g_conv_ablation;
         azg::g_conv_ablation = value;
+        return prev;
+    }
+    if (key == 7) {   // ablation tile shape (5 or 8)
+        const int prev = azg::g_ablation_shape;
+        azg::g_ablation_shape = value;
         return prev;
     }
     if (key == 5) {   // persistent residual tower on/off

@@ -60,11 +60,15 @@ constexpr int halo_span(int BM)
     return mx;
 }
 
+// LDS: halo rows [HR][32] + two weight chunks [2][BN][32]; the epilogue reuses it
+// as a [BM][BN+8] tile.
 template <int C, int BN, int WM, int TM, int NW>
 constexpr int halo_lds_bytes()
 {
     using T = ConvTile<C, BN, WM, TM, NW>;
-    return ((halo_span(T::BM) + T::RPP - 1) / T::RPP * T::RPP + 2 * BN) * T::BK * 4;
+    const int staging = ((halo_span(T::BM) + T::RPP - 1) / T::RPP * T::RPP + 2 * BN) * T::BK * 4;
+    const int epilogue = T::BM * (BN + 8) * 4;
+    return staging > epilogue ? staging : epilogue;
 }
 
 // Tower epilogue: BN scale/shift, residual added when `resid` is non-null, ReLU
@@ -86,7 +90,12 @@ constexpr int EPI_BN_OPTRES_RELU = 4;
 // SC1: outputs are stored write-through (buffer_store ... sc1 via `out_rs`) so a
 // consumer workgroup of the same launch can read them after its acquire
 // (cdna_hip_programming.md Guideline 16, R1).
-template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1 = false>
+//
+// ABL (timing studies only, 0 in every product launch; results are garbage when
+// set): bit 1 skips the weight loads, bit 2 the halo loads, bit 4 the per-chunk
+// barriers, bit 8 replaces LDS fragment reads by register values, bit 16 skips the
+// epilogue stores (kept live by a never-true compare).
+template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1 = false, int ABL = 0>
 __device__ __forceinline__ void halo_tile(
     const float* __restrict__ in, const float* __restrict__ wp,
     const float* __restrict__ scale, const float* __restrict__ shift,
@@ -124,8 +133,12 @@ __device__ __forceinline__ void halo_tile(
     const float* wsrc = wp + (size_t)(n0 + sr) * BK + sc;
 
     f32x4 rh[H_LD], rb[B_LD];
-    auto hload = [&](int cg, int i) { rh[i] = *(const f32x4*)(in + hsrc[i] + cg * BK); };
+    auto hload = [&](int cg, int i) {
+        if (ABL & 2) return;
+        rh[i] = *(const f32x4*)(in + hsrc[i] + cg * BK);
+    };
     auto bload = [&](int kc) {
+        if (ABL & 1) return;
         const float* wk = wsrc + (size_t)kc * C * BK;
 #pragma unroll
         for (int i = 0; i < B_LD; ++i) rb[i] = *(const f32x4*)(wk + RPP * i * BK);
@@ -198,11 +211,18 @@ __device__ __forceinline__ void halo_tile(
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 f32x4 a[TM], b[TN];
+                if (ABL & 8) {
 #pragma unroll
-                for (int i = 0; i < TM; ++i) a[i] = *(const f32x4*)(Ah + arow[i] + (((h * 4 + q) ^ aswz[i]) * 4));
-                const int rc = ((h * 4 + q) ^ bswz) * 4;
+                    for (int i = 0; i < TM; ++i) a[i] = f32x4{(float)cg, (float)q, (float)i, (float)tap};
 #pragma unroll
-                for (int j = 0; j < TN; ++j) b[j] = *(const f32x4*)(Bb + brow + j * 32 * BK + rc);
+                    for (int j = 0; j < TN; ++j) b[j] = f32x4{(float)q, (float)cg, 1.f, (float)j};
+                } else {
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) a[i] = *(const f32x4*)(Ah + arow[i] + (((h * 4 + q) ^ aswz[i]) * 4));
+                    const int rc = ((h * 4 + q) ^ bswz) * 4;
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) b[j] = *(const f32x4*)(Bb + brow + j * 32 * BK + rc);
+                }
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -212,7 +232,7 @@ __device__ __forceinline__ void halo_tile(
                             at[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], at[i][j], 0, 0, 0);
             }
             if (tap < 8 || more) bstore(cur ^ 1);
-            __syncthreads();
+            if (!(ABL & 4)) __syncthreads();
             if (tap == 8 && more) {
                 hstore();            // every wave is past its last read of this group's halo
                 __syncthreads();
@@ -224,38 +244,64 @@ __device__ __forceinline__ void halo_tile(
             for (int j = 0; j < TN; ++j) acc[i][j] += at[i][j];
     }
 
-    // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+    // Epilogue through LDS: the accumulators (C/D map of the 32x32 MFMA: col =
+    // lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)) are written to an LDS tile
+    // [BM][BN+8] (the +8 puts rows 4 apart on opposite bank halves: conflict-free),
+    // then every thread finishes 16-B runs of 4 channels of one pixel: one pad_off,
+    // float4 scale/shift/residual, one 16-B store per run -- instead of 16 scalar
+    // stores (and 16 pad_off divisions) per fragment.  Same per-element arithmetic.
+    constexpr int ELD = BN + 8;
+    float* Es = smem;   // the last chunk ended with a barrier: staging buffers are free
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int col = n0 + wn * TN * 32 + j * 32 + r32;
-        float s_ = 1.f, t_ = 0.f;
-        if (EPI == EPI_BN_RELU || EPI == EPI_BN_RES_RELU || EPI == EPI_BN_OPTRES_RELU) {
-            s_ = scale[col];
-            t_ = shift[col];
-        }
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m < M) {
-                    const int o = pad_off(m, C) + col;
-                    float v = acc[i][j][r];
-                    if (EPI == EPI_BN_RELU) {
-                        v = fmaxf(v * s_ + t_, 0.f);
-                    } else if (EPI == EPI_BN_RES_RELU) {
-                        v = fmaxf(v * s_ + t_ + resid[o], 0.f);
-                    } else if (EPI == EPI_BN_OPTRES_RELU) {
-                        v = resid ? fmaxf(v * s_ + t_ + resid[o], 0.f) : fmaxf(v * s_ + t_, 0.f);
-                    } else if (EPI == EPI_ADD) {
-                        v = v + resid[o];
-                    }
-                    if constexpr (SC1) {
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), out_rs, o * 4, 0, 16);
-                    } else {
-                        out[o] = v;
-                    }
+                const int row = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                Es[row * ELD + wn * TN * 32 + j * 32 + r32] = acc[i][j][r];
+            }
+    __syncthreads();
+    constexpr int CPR = BN / 4;            // 16-B runs per pixel row
+    constexpr int RPI = T::NT / CPR;       // pixel rows per pass
+    static_assert(BM % RPI == 0, "epilogue passes");
+    const int ec = (tid % CPR) * 4;
+    const int er = tid / CPR;
+    const int col = n0 + ec;
+    f32x4 s4 = {1.f, 1.f, 1.f, 1.f}, t4 = {0.f, 0.f, 0.f, 0.f};
+    if (EPI == EPI_BN_RELU || EPI == EPI_BN_RES_RELU || EPI == EPI_BN_OPTRES_RELU) {
+        s4 = *(const f32x4*)(scale + col);
+        t4 = *(const f32x4*)(shift + col);
+    }
+#pragma unroll
+    for (int p = 0; p < BM / RPI; ++p) {
+        const int row = er + p * RPI;
+        const int m = m0 + row;
+        f32x4 v = *(const f32x4*)(Es + row * ELD + ec);
+        if (m < M && (!(ABL & 16) || v[0] == 1234.5f)) {
+            const int o = pad_off(m, C) + col;
+            f32x4 rv = {0.f, 0.f, 0.f, 0.f};
+            const bool has_res = EPI == EPI_BN_RES_RELU || EPI == EPI_ADD || (EPI == EPI_BN_OPTRES_RELU && resid);
+            if (has_res) rv = *(const f32x4*)(resid + o);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float x = v[e];
+                if (EPI == EPI_BN_RELU) {
+                    x = fmaxf(x * s4[e] + t4[e], 0.f);
+                } else if (EPI == EPI_BN_RES_RELU) {
+                    x = fmaxf(x * s4[e] + t4[e] + rv[e], 0.f);
+                } else if (EPI == EPI_BN_OPTRES_RELU) {
+                    x = has_res ? fmaxf(x * s4[e] + t4[e] + rv[e], 0.f) : fmaxf(x * s4[e] + t4[e], 0.f);
+                } else if (EPI == EPI_ADD) {
+                    x = x + rv[e];
                 }
+                v[e] = x;
+            }
+            if constexpr (SC1) {
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), out_rs, o * 4, 0, 16);
+            } else {
+                *(f32x4*)(out + o) = v;
             }
         }
     }

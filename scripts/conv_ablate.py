@@ -1,5 +1,7 @@
-"""Ablation timing of the 3x3 conv main loop (shape 64x64, C=128, B from argv, default 512):
-mask bit 1 = no global loads, 2 = no LDS fragment reads, 4 = no barrier, 8 = no epilogue stores.
+"""Ablation timing of the halo-staged 3x3 conv tile (C=128; argv: batch [default 512],
+tile shape 5 = 64x64 / 8 = 128x64 [default 5]), per-layer launches:
+mask bit 1 = no weight loads, 2 = no halo loads, 4 = no per-chunk barrier,
+8 = no LDS fragment reads, 16 = no epilogue stores.
 Only conv1 launches (EPI_BN_RELU) are ablated; we time those."""
 import os, sys, json, statistics
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -16,11 +18,15 @@ def main():
     m = PyTorchModel(device="cuda", n_res_blocks=6, channels=128)
     eng = m.engine
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+    shape = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    lib.azg_pv_set_tuning(5, 0)        # per-layer launches (ablations apply there)
+    lib.azg_pv_set_tuning(0, shape)    # un-ablated conv2 launches use the same shape
+    lib.azg_pv_set_tuning(7, shape)
     x = torch.from_numpy(synth_encoded(B, seed=5)).cuda()
     probs = torch.empty((B, 225), device="cuda"); values = torch.empty((B, 1), device="cuda")
     res = {}
     for rnd in range(3):
-        for mask in (0, 1, 2, 3, 4, 7, 8, 15):
+        for mask in (0, 1, 2, 3, 4, 8, 16, 7, 31):
             lib.azg_pv_set_tuning(3, mask)
             eng.forward_into(x, probs, values)
             eng.profile_enable(True)
@@ -32,7 +38,7 @@ def main():
     lib.azg_pv_set_tuning(3, 0)
     med = {k: statistics.median(v) for k, v in res.items()}
     normal = med[0]
-    print(json.dumps({"batch": B, "avg_us": {str(k): round(v, 1) for k, v in med.items()},
+    print(json.dumps({"batch": B, "shape": shape, "avg_us": {str(k): round(v, 1) for k, v in med.items()},
                       "ablated_conv1_us": {str(k): round(2 * v - normal, 1) for k, v in med.items()}}))
     print("note: mixes ablated conv1 (6/step) with normal conv2 (6/step); ablated time = 2*avg - normal")
 
