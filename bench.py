@@ -100,13 +100,15 @@ def cpu_baseline(seconds: float = 12.0) -> dict:
             "host_cpus_visible": os.cpu_count()}
 
 
-def load_traffic():
+def load_traffic(kernel):
+    """HBM bytes per launch of `kernel` ("tower" or "conv3x3") from the committed PMC
+    pass (profiles/conv_traffic.json, scripts/summarize_profile.py), or None."""
     path = os.path.join(REPO, "profiles", "conv_traffic.json")
     if not os.path.exists(path):
         return None
     try:
         d = json.load(open(path))
-        if d.get("config") == f"{BLOCKS}x{CHANNELS}_B{BATCH}":
+        if d.get("config") == f"{BLOCKS}x{CHANNELS}_B{BATCH}" and d.get("kernel", "conv3x3") == kernel:
             return d.get("hbm_bytes_per_launch")
     except Exception:
         pass
@@ -245,7 +247,8 @@ def main():
 
     boards = B * args.steps * world
     value = boards / elapsed
-    if prof.get("tower", (0.0, 0))[1]:
+    tower = bool(prof.get("tower", (0.0, 0))[1])
+    if tower:
         # persistent residual tower: one launch runs all 2*BLOCKS convs
         conv_ms, conv_n = prof["tower"]
         flop_launch = FLOP_CONV * B * 2 * BLOCKS
@@ -258,7 +261,8 @@ def main():
     conv_avg_s = conv_ms / 1e3 / max(conv_n, 1)
     achieved = flop_launch / conv_avg_s
     roof = {"bound": "mfma", "achieved": round(achieved / 1e12, 3), "peak": PEAK_F32_MFMA / 1e12,
-            "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA, 4), "traffic": load_traffic(),
+            "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA, 4),
+            "traffic": load_traffic("tower" if tower else "conv3x3"),
             "kernel": kname, "avg_launch_us": round(conv_avg_s * 1e6, 2), "launches": conv_n,
             "flop_per_launch": flop_launch}
     out = {

@@ -126,12 +126,20 @@ def main():
             for c, (m, n) in sorted(pmc[k].items()):
                 w.writerow([k, c, m, n])
 
-    # dominant conv: the product-path conv kernels are the most-called conv3x3 names
-    # (autotuning dispatches every candidate shape only twice)
-    convs = [r for r in stats if "conv3x3_halo" in r["Name"] or "conv3x3_mfma" in r["Name"]]
-    convs.sort(key=lambda r: int(r["Calls"]), reverse=True)
-    top_calls = int(convs[0]["Calls"]) if convs else 0
-    tuned = [r for r in convs if int(r["Calls"]) >= top_calls // 2]
+    # dominant conv: the persistent residual tower when the forward used it (one
+    # launch = all 2*BLOCKS convs), else the product-path per-layer conv kernels (the
+    # most-called conv3x3 names: autotuning dispatches every candidate shape only twice)
+    towers = [r for r in stats if "conv_tower" in r["Name"]]
+    if towers:
+        towers.sort(key=lambda r: int(r["Calls"]), reverse=True)
+        tuned = towers[:1]
+        convs_per_launch = 2 * BLOCKS
+    else:
+        convs = [r for r in stats if "conv3x3_halo" in r["Name"] or "conv3x3_mfma" in r["Name"]]
+        convs.sort(key=lambda r: int(r["Calls"]), reverse=True)
+        top_calls = int(convs[0]["Calls"]) if convs else 0
+        tuned = [r for r in convs if int(r["Calls"]) >= top_calls // 2]
+        convs_per_launch = 1
     calls = sum(int(r["Calls"]) for r in tuned)
     avg_ns = sum(float(r["TotalDurationNs"]) for r in tuned) / max(calls, 1)
     fetch = write = mfma = grbm = 0.0
@@ -162,25 +170,30 @@ def main():
         traffic = fetch_b + write_b
         in_b = BATCH * 289 * CHANNELS * 4 + 9 * CHANNELS * CHANNELS * 4
         out_b = BATCH * 225 * CHANNELS * 4
-        alg = in_b + out_b + 0.5 * out_b     # conv2 of each block also reads the residual
+        # per conv: padded input once + weights + output; conv2 of each block also
+        # reads the residual
+        alg = convs_per_launch * (in_b + out_b + 0.5 * out_b)
         clk = grbm / nk / 8 / (avg_ns * 1e-9) / 1e9 if avg_ns else 0.0
         busy = mfma / nk / (4 * 256) / (grbm / nk / 8) if grbm else 0.0
-        tflops = FLOP_CONV * BATCH / (avg_ns * 1e-9) / 1e12
+        tflops = FLOP_CONV * BATCH * convs_per_launch / (avg_ns * 1e-9) / 1e12
+        what = (f"persistent residual tower ({convs_per_launch} convs per launch)" if towers
+                else "3x3 conv (tuned shape)")
         lines += [
-            "## Dominant kernel: 3x3 conv (tuned shape)",
+            f"## Dominant kernel: {what}",
             "",
             f"* kernels: {', '.join('`' + short(r['Name'], 60) + '`' for r in tuned)}",
             f"* dispatches: {calls}, average duration {avg_ns / 1e3:.1f} us -> {tflops:.1f} TFLOP/s "
             f"({tflops / 157.3 * 100:.1f} % of the 157.3 TFLOP/s dense fp32 MFMA peak)",
             f"* HBM-side bytes per launch: FETCH_SIZE x2 = {fetch_b / 1e6:.1f} MB, WRITE_SIZE = {write_b / 1e6:.1f} MB, "
-            f"total {traffic / 1e6:.1f} MB (algorithmic {alg / 1e6:.1f} MB: padded input once + weights + "
-            "output, + residual on every second launch)",
+            f"total {traffic / 1e6:.1f} MB (algorithmic {alg / 1e6:.1f} MB: per conv padded input once + "
+            "weights + output, + residual on every second conv)",
             f"* SQ_VALU_MFMA_BUSY_CYCLES / (4 SIMD x 256 CU x GRBM_GUI_ACTIVE/8) = {busy * 100:.1f} %, "
             f"clock ~ {clk:.2f} GHz",
             "",
         ]
         with open(os.path.join(PROF, "conv_traffic.json"), "w") as f:
             json.dump({"config": f"{BLOCKS}x{CHANNELS}_B{BATCH}", "tag": args.tag,
+                       "kernel": "tower" if towers else "conv3x3", "convs_per_launch": convs_per_launch,
                        "hbm_bytes_per_launch": round(traffic), "fetch_bytes": round(fetch_b),
                        "write_bytes": round(write_b), "algorithmic_bytes": round(alg),
                        "avg_launch_us": round(avg_ns / 1e3, 2)}, f, indent=1)
