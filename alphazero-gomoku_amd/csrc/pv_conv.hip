@@ -605,6 +605,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         azg::g_conv_ablation = value;
         return prev;
     }
+    if (key == 8) {   // persistent-tower ablation mask (timing studies only)
+        const int prev = azg::g_tower_ablation;
+        azg::g_tower_ablation = value;
+        return prev;
+    }
     if (key == 7) {   // ablation tile shape (5 or 8)
         const int prev = azg::g_ablation_shape;
         azg::g_ablation_shape = value;

@@ -35,6 +35,7 @@ hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, cons
                           const float* shift, const float* resid, float* out, int M, hipStream_t st);
 extern int g_tower_mode;
 extern int g_tower_shape;
+extern int g_tower_ablation;
 constexpr int kTowerMaxBlocks = 32;
 int conv_batch_bucket(int M);
 size_t tower_sync_bytes(int nlayers, int M);

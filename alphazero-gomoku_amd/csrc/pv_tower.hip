@@ -48,6 +48,8 @@ struct TowerArgs {
     int M;
     int act_bytes;       // bytes of one activation buffer (buffer descriptor range)
     unsigned* sync;      // [0] work counter, [1] error word, [4..] per-(layer, M tile) counters
+    int abl;             // timing studies only (0 in the product; results not valid otherwise):
+                         // bit 1 skips the dependency wait + acquire, bit 2 the publish drain
 };
 
 constexpr unsigned kSpinLimit = 1u << 22;    // x s_sleep(2): seconds, far above any tile time
@@ -79,7 +81,7 @@ __global__ __launch_bounds__(64 * NW_, 4) void conv_tower(const TowerArgs a)
         if (tid == 0) {
             // next claim now: its latency overlaps this tile (read after the tile)
             s_claim[0] = (int)__hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (l > 0) {
+            if (l > 0 && !(a.abl & 1)) {
                 const unsigned* c = cnt + (size_t)(l - 1) * mtiles;
                 const int j0 = max(mt - 1, 0), j1 = min(mt + 1, mtiles - 1);
                 for (int j = j0; j <= j1; ++j) {
@@ -101,8 +103,10 @@ __global__ __launch_bounds__(64 * NW_, 4) void conv_tower(const TowerArgs a)
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Ly.out, (short)0, a.act_bytes, 0x00020000);
         halo_tile<C, BN_, WM_, TM_, NW_, EPI_BN_OPTRES_RELU, true>(Ly.in, Ly.wp, Ly.scale, Ly.shift, Ly.resid, Ly.out,
                                                                   rs, a.M, mt * T::BM, nt * T::BN, smem);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
-        __syncthreads();
+        if (!(a.abl & 2)) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
+            __syncthreads();
+        }
         if (tid == 0) __hip_atomic_fetch_add(cnt + (size_t)l * mtiles + mt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         w = s_claim[0];
     }
@@ -130,6 +134,7 @@ static hipError_t launch_tower_t(const TowerArgs& a, hipStream_t st, int* grid_o
     return hipGetLastError();
 }
 
+int g_tower_ablation = 0;
 int g_tower_shape = 8;   // forced shape when g_tower_mode == 1: 5 = 64x64 (4 waves), 8 = 128x64 (8 waves)
 
 size_t tower_sync_bytes(int nlayers, int M)
@@ -154,6 +159,7 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     a.M = M;
     a.act_bytes = (int)act_bytes;
     a.sync = sync;
+    a.abl = g_tower_ablation;
     float* X = act[0];
     float* H = act[1];
     float* Y = act[2];
