@@ -605,6 +605,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         azg::g_conv_ablation = value;
         return prev;
     }
+    if (key == 10) {  // persistent-tower tile body variant (A/B studies, bitwise identical)
+        const int prev = azg::g_tower_var;
+        if (value >= 0 && value <= 5) azg::g_tower_var = value;
+        return prev;
+    }
     if (key == 8) {   // persistent-tower ablation mask (timing studies only)
         const int prev = azg::g_tower_ablation;
         azg::g_tower_ablation = value;

@@ -60,13 +60,16 @@ constexpr int halo_span(int BM)
     return mx;
 }
 
-// LDS: halo rows [HR][32] + two weight chunks [2][BN][32]; the epilogue reuses it
-// as a [BM][BN+8] tile.
-template <int C, int BN, int WM, int TM, int NW>
+// LDS: halo rows [HR][32] + two weight chunks [2][BN][32] (register staging), or
+// two halo buffers [2][HRG][32] + [2][BN][32] (LDS-DMA staging, VAR bit 4); the
+// epilogue reuses it as a [BM][ELD] tile.
+template <int C, int BN, int WM, int TM, int NW, int VAR = 0>
 constexpr int halo_lds_bytes()
 {
     using T = ConvTile<C, BN, WM, TM, NW>;
-    const int staging = ((halo_span(T::BM) + T::RPP - 1) / T::RPP * T::RPP + 2 * BN) * T::BK * 4;
+    const int hrg = (halo_span(T::BM) + 7) / 8 * 8;
+    const int staging = (VAR & 4) ? (2 * hrg + 2 * BN) * T::BK * 4
+                                  : ((halo_span(T::BM) + T::RPP - 1) / T::RPP * T::RPP + 2 * BN) * T::BK * 4;
     const int epilogue = T::BM * (BN + 8) * 4;
     return staging > epilogue ? staging : epilogue;
 }
@@ -75,183 +78,35 @@ constexpr int halo_lds_bytes()
 // (EPI_BN_RELU / EPI_BN_RES_RELU chosen at run time, same arithmetic).
 constexpr int EPI_BN_OPTRES_RELU = 4;
 
-// One BM x BN output tile at (m0, n0).  K is ordered input-channel-group major:
-// for each 32-wide channel group cg the tile's halo slice [rows][32] is staged into
-// LDS ONCE and all 9 taps read their shifted A fragments from it (9x fewer A loads
-// from L2 than staging an A tile per (tap, cg) chunk); the weights stream per chunk
-// through a double-buffered LDS tile.  Accumulation: one MFMA chain per channel
-// group over its 9 taps x 32 channels (288 terms), group sums added in cg order --
-// error growth chain(288) + C/32, cf. chain(9C) for a single chain.  The K order
-// is per output element and the same for every tile shape and position, so tuning
-// never changes numerics and the forward is batch-independent.  Halo rows are
-// staged through registers (loads issued over the first taps of the previous
-// group) into a single LDS buffer, swapped behind one extra barrier per group.
-//
-// SC1: outputs are stored write-through (buffer_store ... sc1 via `out_rs`) so a
-// consumer workgroup of the same launch can read them after its acquire
-// (cdna_hip_programming.md Guideline 16, R1).
-//
-// ABL (timing studies only, 0 in every product launch; results are garbage when
-// set): bit 1 skips the weight loads, bit 2 the halo loads, bit 4 the per-chunk
-// barriers, bit 8 replaces LDS fragment reads by register values, bit 16 skips the
-// epilogue stores (kept live by a never-true compare).
-template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1 = false, int ABL = 0>
-__device__ __forceinline__ void halo_tile(
-    const float* __restrict__ in, const float* __restrict__ wp,
-    const float* __restrict__ scale, const float* __restrict__ shift,
-    const float* __restrict__ resid, float* __restrict__ out, __amdgpu_buffer_rsrc_t out_rs,
-    int M, int m0, int n0, float* smem)
+// key of the 16-B slot swizzle of halo row `row` (padded-pixel index): the padded
+// board position v = yy*15 + xx (see halo_tile)
+__device__ __forceinline__ int halo_vkey(int row)
+{
+    const int rb = row % PADPIX;
+    return (rb / PADW) * BOARD + rb % PADW;
+}
+
+// Epilogue through LDS: the accumulators (C/D map of the 32x32 MFMA: col =
+// lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)) are written to an LDS tile
+// [BM][ELD] (ELD = BN: the ds_write_b32 halves and the ds_read_b128 lane groups
+// are conflict-free on unpadded rows; BN+8 conflicts on the reads), then every
+// thread finishes 16-B runs of 4 channels of one pixel: one pad_off, float4
+// scale/shift/residual, one 16-B store per run -- instead of 16 scalar stores (and
+// 16 pad_off divisions) per fragment.  Same per-element arithmetic.  The caller
+// guarantees every wave is past its last staging-buffer access (barrier).
+template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1, int ABL, int ELD>
+__device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<C, BN_, WM_, TM_, NW_>::TN],
+                                              const float* __restrict__ scale, const float* __restrict__ shift,
+                                              const float* __restrict__ resid, float* __restrict__ out,
+                                              __amdgpu_buffer_rsrc_t out_rs, int M, int m0, int n0, float* smem)
 {
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
-    constexpr int RPP = T::RPP;
-    constexpr int BM = T::BM, BN = T::BN, BK = T::BK;
-    constexpr int CG = T::CG, WN = T::WN, TM = T::TM, TN = T::TN;
-    constexpr int B_LD = T::B_LD;
-    constexpr int HS = halo_span(BM);
-    constexpr int H_LD = (HS + RPP - 1) / RPP;
-    constexpr int HR = H_LD * RPP;
-    static_assert(RPP % 16 == 0, "halo staging rows must keep the row swizzle");
-    static_assert(H_LD <= 9, "halo loads are spread over the 9 taps");
-
-    float* Ah = smem;                 // [HR][32]
-    float* Bs = smem + HR * BK;       // [2][BN][32]
-
+    constexpr int BM = T::BM, BN = T::BN, WN = T::WN, TM = T::TM, TN = T::TN;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
-    const int mlast = min(m0 + BM, M) - 1;
-    const int hbase = pad_row(m0) - (PADW + 1);
-    const int hmax = pad_row(mlast) + (PADW + 1);
-
-    const int sr = tid >> 3, sc = (tid & 7) * 4;
-    int hsrc[H_LD];
-#pragma unroll
-    for (int i = 0; i < H_LD; ++i) {
-        const int r = min(hbase + sr + RPP * i, hmax);   // rows past the tile's need: any valid row
-        hsrc[i] = r * C + sc;
-    }
-    const float* wsrc = wp + (size_t)(n0 + sr) * BK + sc;
-
-    f32x4 rh[H_LD], rb[B_LD];
-    auto hload = [&](int cg, int i) {
-        if (ABL & 2) return;
-        rh[i] = *(const f32x4*)(in + hsrc[i] + cg * BK);
-    };
-    auto bload = [&](int kc) {
-        if (ABL & 1) return;
-        const float* wk = wsrc + (size_t)kc * C * BK;
-#pragma unroll
-        for (int i = 0; i < B_LD; ++i) rb[i] = *(const f32x4*)(wk + RPP * i * BK);
-    };
-    // 16-B chunk c of LDS row r is stored at chunk c ^ ((r >> 1) & 7): any 16
-    // consecutive rows a ds_read_b128 lane group touches land on distinct slots.
-    const int wchunk = ((tid & 7) ^ ((sr >> 1) & 7)) * 4;
-    auto hstore = [&]() {
-#pragma unroll
-        for (int i = 0; i < H_LD; ++i) *(f32x4*)(Ah + (sr + RPP * i) * BK + wchunk) = rh[i];
-    };
-    auto bstore = [&](int buf) {
-        float* b = Bs + buf * BN * BK;
-#pragma unroll
-        for (int i = 0; i < B_LD; ++i) *(f32x4*)(b + (sr + RPP * i) * BK + wchunk) = rb[i];
-    };
-
-    // Lane l of an MFMA step s uses K index h*16+s (h = l>>5) for both A and B, so
-    // each lane's 16 A values and 16 B values of a chunk are contiguous in LDS.
     const int r32 = lane & 31, h = lane >> 5;
-    // halo row of each fragment pixel (tail pixels clamp to the last valid one)
-    int hrow[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) hrow[i] = pad_row(min(m0 + wm * TM * 32 + i * 32 + r32, M - 1)) - hbase;
-    const int bswz = (r32 >> 1) & 7;
-    const int brow = (wn * TN * 32 + r32) * BK;
-
-    f32x16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-#pragma unroll
-    for (int i = 0; i < H_LD; ++i) hload(0, i);
-    bload(0);
-    hstore();
-    bstore(0);
-    __syncthreads();
-
-    for (int cg = 0; cg < CG; ++cg) {
-        f32x16 at[TM][TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) at[i][j][r] = 0.f;
-        const bool more = cg + 1 < CG;
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-            const int cur = (cg + tap) & 1;        // chunk index cg*9 + tap, parity
-            if (tap < 8) bload((tap + 1) * CG + cg);
-            else if (more) bload(cg + 1);
-            if (more && tap < H_LD) hload(cg + 1, tap);
-            // keep the next chunk's global loads at the top of the chunk: without this
-            // fence hipcc sinks them to just before their vmcnt wait (latency exposed)
-            __builtin_amdgcn_sched_barrier(0);
-            const int d = (tap / 3 - 1) * PADW + (tap % 3 - 1);
-            int arow[TM], aswz[TM];
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const int r = hrow[i] + d;
-                arow[i] = r * BK;
-                aswz[i] = (r >> 1) & 7;
-            }
-            const float* Bb = Bs + cur * BN * BK;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                f32x4 a[TM], b[TN];
-                if (ABL & 8) {
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) a[i] = f32x4{(float)cg, (float)q, (float)i, (float)tap};
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) b[j] = f32x4{(float)q, (float)cg, 1.f, (float)j};
-                } else {
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) a[i] = *(const f32x4*)(Ah + arow[i] + (((h * 4 + q) ^ aswz[i]) * 4));
-                    const int rc = ((h * 4 + q) ^ bswz) * 4;
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) b[j] = *(const f32x4*)(Bb + brow + j * 32 * BK + rc);
-                }
-#pragma unroll
-                for (int s = 0; s < 4; ++s)
-#pragma unroll
-                    for (int i = 0; i < TM; ++i)
-#pragma unroll
-                        for (int j = 0; j < TN; ++j)
-                            at[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], at[i][j], 0, 0, 0);
-            }
-            if (tap < 8 || more) bstore(cur ^ 1);
-            if (!(ABL & 4)) __syncthreads();
-            if (tap == 8 && more) {
-                hstore();            // every wave is past its last read of this group's halo
-                __syncthreads();
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] += at[i][j];
-    }
-
-    // Epilogue through LDS: the accumulators (C/D map of the 32x32 MFMA: col =
-    // lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)) are written to an LDS tile
-    // [BM][BN+8] (the +8 puts rows 4 apart on opposite bank halves: conflict-free),
-    // then every thread finishes 16-B runs of 4 channels of one pixel: one pad_off,
-    // float4 scale/shift/residual, one 16-B store per run -- instead of 16 scalar
-    // stores (and 16 pad_off divisions) per fragment.  Same per-element arithmetic.
-    constexpr int ELD = BN + 8;
-    float* Es = smem;   // the last chunk ended with a barrier: staging buffers are free
+    float* Es = smem;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -305,6 +160,381 @@ __device__ __forceinline__ void halo_tile(
             }
         }
     }
+}
+
+// Main loop with LDS-DMA staging (VAR bit 4): every operand reaches LDS through
+// global_load_lds_dwordx4 (one wave-instruction = 1 KiB = 8 rows of 128 B, written
+// lane-linearly; the slot swizzle is applied to each lane's SOURCE address, and the
+// fragment reads use the same swizzle -- cdna_hip_programming.md §5.4 rule 21), so
+// no VGPR holds staged data and no ds_write is issued.  The halo is double-buffered
+// (group g+1's pieces are issued over the first taps of group g), so the extra
+// per-group barrier of the register path disappears; weights of chunk j+1 are issued
+// at the top of chunk j.  Ordering: every chunk ends with __syncthreads (its fence
+// waits vmcnt(0), retiring that chunk's DMAs before the barrier), data is read one
+// chunk after the barrier that retired it, and a buffer is refilled one chunk after
+// the barrier that ended its last read.  Same K order and chains as halo_tile.
+template <int C, int BN_, int WM_, int TM_, int NW_, int VAR>
+__device__ __forceinline__ void halo_mainloop_glds(const float* __restrict__ in, const float* __restrict__ wp,
+                                                   int M, int m0, int n0, float* smem,
+                                                   f32x16 (&acc)[TM_][ConvTile<C, BN_, WM_, TM_, NW_>::TN])
+{
+    using T = ConvTile<C, BN_, WM_, TM_, NW_>;
+    constexpr int BM = T::BM, BN = T::BN, BK = T::BK;
+    constexpr int CG = T::CG, WN = T::WN, TM = T::TM, TN = T::TN, NW = T::NW;
+    constexpr int HS = halo_span(BM);
+    constexpr int NP = (HS + 7) / 8;          // halo pieces (8 rows each)
+    constexpr int HRG = NP * 8;
+    constexpr int NPW = (NP + NW - 1) / NW;   // halo pieces per wave
+    constexpr int NBP = BN / 8;               // weight pieces per chunk
+    constexpr int NBW = (NBP + NW - 1) / NW;
+    constexpr int NCHK = 9 * CG;
+    constexpr bool VSWZ = (VAR & 1) != 0;
+    static_assert(NPW <= 9, "halo pieces are spread over the 9 taps");
+    static_assert(BN % 8 == 0, "weight pieces");
+
+    float* Ah = smem;                  // [2][HRG][32]
+    float* Bs = smem + 2 * HRG * BK;   // [2][BN][32]
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid / WN, wn = wid % WN;
+    const int mlast = min(m0 + BM, M) - 1;
+    const int hbase = pad_row(m0) - (PADW + 1);
+    const int hmax = pad_row(mlast) + (PADW + 1);
+    const int lr = lane >> 3, ls = lane & 7;   // row in piece, LDS slot of this lane
+
+    int hoff[NPW];
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) {
+        const int l = 8 * (wid + NW * i) + lr;            // LDS halo row
+        const int key = VSWZ ? (halo_vkey(hbase + l) >> 1) & 7 : (l >> 1) & 7;
+        hoff[i] = min(hbase + l, hmax) * C + ((ls ^ key) * 4);
+    }
+    int woff[NBW];
+#pragma unroll
+    for (int i = 0; i < NBW; ++i) {
+        const int n = 8 * (wid + NW * i) + lr;
+        woff[i] = (n0 + n) * BK + ((ls ^ ((n >> 1) & 7)) * 4);
+    }
+    auto glds = [](const float* src, float* dst) {
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    };
+    auto hpiece = [&](int g, int i) {
+        const int p = wid + NW * i;
+        if (p < NP) glds(in + g * BK + hoff[i], Ah + (g & 1) * HRG * BK + p * 8 * BK);
+    };
+    auto bchunk = [&](int j) {
+        const float* wk = wp + (size_t)((j % 9) * CG + j / 9) * C * BK;
+#pragma unroll
+        for (int i = 0; i < NBW; ++i) {
+            const int p = wid + NW * i;
+            if (p < NBP) glds(wk + woff[i], Bs + (j & 1) * BN * BK + p * 8 * BK);
+        }
+    };
+
+    const int r32 = lane & 31, h = lane >> 5;
+    int hrow[TM], vpix[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int pr = pad_row(min(m0 + wm * TM * 32 + i * 32 + r32, M - 1));
+        hrow[i] = pr - hbase;
+        vpix[i] = halo_vkey(pr);
+    }
+    const int bswz = (r32 >> 1) & 7;
+    const int brow = (wn * TN * 32 + r32) * BK;
+
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) hpiece(0, i);
+    bchunk(0);
+    __syncthreads();
+
+#pragma unroll
+    for (int cg = 0; cg < CG; ++cg) {
+        f32x16 at[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) at[i][j][r] = 0.f;
+        const float* Ab = Ah + (cg & 1) * HRG * BK;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int j = cg * 9 + tap;
+            if (j + 1 < NCHK) bchunk(j + 1);
+            if (cg + 1 < CG && tap < NPW) hpiece(cg + 1, tap);
+            __builtin_amdgcn_sched_barrier(0);
+            const int d = (tap / 3 - 1) * PADW + (tap % 3 - 1);
+            const int vd = (tap / 3 - 1) * BOARD + (tap % 3 - 1);
+            int arow[TM], aswz[TM];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int r = hrow[i] + d;
+                arow[i] = r * BK;
+                aswz[i] = VSWZ ? ((vpix[i] + vd) >> 1) & 7 : (r >> 1) & 7;
+            }
+            const float* Bb = Bs + (j & 1) * BN * BK;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                f32x4 a[TM], b[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) a[i] = *(const f32x4*)(Ab + arow[i] + (((h * 4 + q) ^ aswz[i]) * 4));
+                const int rc = ((h * 4 + q) ^ bswz) * 4;
+#pragma unroll
+                for (int jn = 0; jn < TN; ++jn) b[jn] = *(const f32x4*)(Bb + brow + jn * 32 * BK + rc);
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int jn = 0; jn < TN; ++jn)
+                            at[i][jn] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[jn][s], at[i][jn], 0, 0, 0);
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] += at[i][j];
+    }
+}
+
+// One BM x BN output tile at (m0, n0).  K is ordered input-channel-group major:
+// for each 32-wide channel group cg the tile's halo slice [rows][32] is staged into
+// LDS ONCE and all 9 taps read their shifted A fragments from it (9x fewer A loads
+// from L2 than staging an A tile per (tap, cg) chunk); the weights stream per chunk
+// through a double-buffered LDS tile.  Accumulation: one MFMA chain per channel
+// group over its 9 taps x 32 channels (288 terms), group sums added in cg order --
+// error growth chain(288) + C/32, cf. chain(9C) for a single chain.  The K order
+// is per output element and the same for every tile shape and position, so tuning
+// never changes numerics and the forward is batch-independent.  Halo rows are
+// staged through registers (loads issued over the first taps of the previous
+// group) into a single LDS buffer, swapped behind one extra barrier per group.
+//
+// SC1: outputs are stored write-through (buffer_store ... sc1 via `out_rs`) so a
+// consumer workgroup of the same launch can read them after its acquire
+// (cdna_hip_programming.md Guideline 16, R1).
+//
+// ABL (timing studies only, 0 in every product launch; results are garbage when
+// set): bit 1 skips the weight loads, bit 2 the halo loads, bit 4 the per-chunk
+// barriers, bit 8 replaces LDS fragment reads by register values, bit 16 skips the
+// epilogue stores (kept live by a never-true compare).
+template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1 = false, int ABL = 0, int VAR = 0>
+__device__ __forceinline__ void halo_tile(
+    const float* __restrict__ in, const float* __restrict__ wp,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ resid, float* __restrict__ out, __amdgpu_buffer_rsrc_t out_rs,
+    int M, int m0, int n0, float* smem)
+{
+    using T = ConvTile<C, BN_, WM_, TM_, NW_>;
+    if constexpr ((VAR & 4) != 0) {   // LDS-DMA staging
+        f32x16 acc[TM_][T::TN];
+        halo_mainloop_glds<C, BN_, WM_, TM_, NW_, VAR>(in, wp, M, m0, n0, smem, acc);
+        halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, T::BN>(acc, scale, shift, resid, out, out_rs, M, m0, n0,
+                                                                   smem);
+        return;
+    }
+    constexpr int RPP = T::RPP;
+    constexpr int BM = T::BM, BN = T::BN, BK = T::BK;
+    constexpr int CG = T::CG, WN = T::WN, TM = T::TM, TN = T::TN;
+    constexpr int B_LD = T::B_LD;
+    constexpr int HS = halo_span(BM);
+    constexpr int H_LD = (HS + RPP - 1) / RPP;
+    constexpr int HR = H_LD * RPP;
+    static_assert(RPP % 16 == 0, "halo staging rows must keep the row swizzle");
+    static_assert(H_LD <= 9, "halo loads are spread over the 9 taps");
+    // VAR (A/B studies; the product uses 0, measured fastest): bit 1 = halo rows
+    // swizzled on the padded board position (conflict-free fragment reads) and an
+    // unpadded epilogue tile; bit 2 = weights staged two chunks ahead; bit 4 = LDS-DMA
+    // staging (halo_mainloop_glds).  Every VAR computes bitwise-identical results.
+    constexpr bool VSWZ = (VAR & 1) != 0;
+    constexpr bool BPF2 = (VAR & 2) != 0;
+    constexpr int NCHK = 9 * CG;
+
+    float* Ah = smem;                 // [HR][32]
+    float* Bs = smem + HR * BK;       // [2][BN][32]
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int mlast = min(m0 + BM, M) - 1;
+    const int hbase = pad_row(m0) - (PADW + 1);
+    const int hmax = pad_row(mlast) + (PADW + 1);
+
+    const int sr = tid >> 3, sc = (tid & 7) * 4;
+    int hsrc[H_LD];
+#pragma unroll
+    for (int i = 0; i < H_LD; ++i) {
+        const int r = min(hbase + sr + RPP * i, hmax);   // rows past the tile's need: any valid row
+        hsrc[i] = r * C + sc;
+    }
+    const float* wsrc = wp + (size_t)(n0 + sr) * BK + sc;
+
+    // weights: rb1 holds chunk j+1 (stored to LDS at the end of chunk j); with BPF2,
+    // rb2 receives chunk j+2 at the top of chunk j, so a load has a whole chunk plus
+    // the next chunk's MFMAs to land before the ds_write that waits on it (the loops
+    // are fully unrolled: the rb1 = rb2 hand-over is a register renaming, not a move)
+    f32x4 rh[H_LD], rb1[B_LD], rb2[B_LD];
+    auto hload = [&](int cg, int i) {
+        if (ABL & 2) return;
+        rh[i] = *(const f32x4*)(in + hsrc[i] + cg * BK);
+    };
+    auto bload = [&](f32x4 (&rb)[B_LD], int kc) {
+        if (ABL & 1) return;
+        const float* wk = wsrc + (size_t)kc * C * BK;
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) rb[i] = *(const f32x4*)(wk + RPP * i * BK);
+    };
+    // K chunk j (0 .. 9*CG-1) = tap j%9 of channel group j/9 -> packed weight chunk
+    auto kchunk = [](int j) { return (j % 9) * CG + j / 9; };
+    // LDS swizzles.  ds_read_b128 serves a wave in 4 lane groups of 16 (e.g. lanes
+    // {0-3, 12-15, 20-27}); a group is conflict-free iff its 16 reads hit distinct
+    // (row parity, 16-B slot) pairs.  Weight rows: chunk c of row r sits at slot
+    // c ^ ((r >> 1) & 7) -- consecutive rows, conflict-free.  Halo rows: a fragment's
+    // 32 lanes read the rows of 32 consecutive pixels, which jump by 3 padded rows at
+    // each board-row end, so a row-keyed slot conflicts there (113 M conflict cycles
+    // per tower launch, PMC).  VSWZ keys halo rows on v = yy*15 + xx of the padded
+    // position (yy, xx): for every tap, consecutive pixels read consecutive v (across
+    // row ends too) and the row parity alternates with v (row steps are 1 or 3), so
+    // slot c ^ ((v >> 1) & 7) is conflict-free for every lane group inside a board.
+    const int wchunk = ((tid & 7) ^ ((sr >> 1) & 7)) * 4;
+    auto vkey = [](int row) { return halo_vkey(row); };
+    int hwchunk[H_LD];
+#pragma unroll
+    for (int i = 0; i < H_LD; ++i)
+        hwchunk[i] = VSWZ ? ((tid & 7) ^ ((vkey(hbase + sr + RPP * i) >> 1) & 7)) * 4 : wchunk;
+    auto hstore = [&]() {
+#pragma unroll
+        for (int i = 0; i < H_LD; ++i) *(f32x4*)(Ah + (sr + RPP * i) * BK + hwchunk[i]) = rh[i];
+    };
+    auto bstore = [&](const f32x4 (&rb)[B_LD], int buf) {
+        float* b = Bs + buf * BN * BK;
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) *(f32x4*)(b + (sr + RPP * i) * BK + wchunk) = rb[i];
+    };
+
+    // Lane l of an MFMA step s uses K index h*16+s (h = l>>5) for both A and B, so
+    // each lane's 16 A values and 16 B values of a chunk are contiguous in LDS.
+    const int r32 = lane & 31, h = lane >> 5;
+    // halo row of each fragment pixel (tail pixels clamp to the last valid one)
+    int hrow[TM], vpix[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int pr = pad_row(min(m0 + wm * TM * 32 + i * 32 + r32, M - 1));
+        hrow[i] = pr - hbase;
+        vpix[i] = vkey(pr);
+    }
+    const int bswz = (r32 >> 1) & 7;
+    const int brow = (wn * TN * 32 + r32) * BK;
+    const f32x4 rfix = {(float)r32, (float)h, 1.f, 2.f};   // ABL & 8 operands (timing only)
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+#pragma unroll
+    for (int i = 0; i < H_LD; ++i) hload(0, i);
+    if (BPF2) {
+        bload(rb2, kchunk(0));
+        bload(rb1, kchunk(1));
+    } else {
+        bload(rb1, kchunk(0));
+    }
+    hstore();
+    if (BPF2) bstore(rb2, 0);
+    else bstore(rb1, 0);
+    __syncthreads();
+
+#pragma unroll
+    for (int cg = 0; cg < CG; ++cg) {
+        f32x16 at[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) at[i][j][r] = 0.f;
+        const bool more = cg + 1 < CG;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int j = cg * 9 + tap;            // chunk index
+            const int cur = j & 1;
+            if (BPF2) {
+                if (j + 2 < NCHK) bload(rb2, kchunk(j + 2));
+            } else {
+                if (j + 1 < NCHK) bload(rb1, kchunk(j + 1));
+            }
+            if (more && tap < H_LD) hload(cg + 1, tap);
+            // keep the next chunk's global loads at the top of the chunk: without this
+            // fence hipcc sinks them to just before their vmcnt wait (latency exposed)
+            __builtin_amdgcn_sched_barrier(0);
+            const int d = (tap / 3 - 1) * PADW + (tap % 3 - 1);
+            const int vd = (tap / 3 - 1) * BOARD + (tap % 3 - 1);
+            int arow[TM], aswz[TM];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int r = hrow[i] + d;
+                arow[i] = r * BK;
+                aswz[i] = VSWZ ? ((vpix[i] + vd) >> 1) & 7 : (r >> 1) & 7;
+            }
+            const float* Bb = Bs + cur * BN * BK;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                f32x4 a[TM], b[TN];
+                if (ABL & 8) {
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) a[i] = rfix;
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) b[j] = rfix;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) a[i] = *(const f32x4*)(Ah + arow[i] + (((h * 4 + q) ^ aswz[i]) * 4));
+                    const int rc = ((h * 4 + q) ^ bswz) * 4;
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) b[j] = *(const f32x4*)(Bb + brow + j * 32 * BK + rc);
+                }
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            at[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], at[i][j], 0, 0, 0);
+            }
+            if (j + 1 < NCHK) {
+                bstore(rb1, cur ^ 1);
+                if (BPF2) {
+#pragma unroll
+                    for (int i = 0; i < B_LD; ++i) rb1[i] = rb2[i];
+                }
+            }
+            if (!(ABL & 4)) __syncthreads();
+            if (tap == 8 && more) {
+                hstore();            // every wave is past its last read of this group's halo
+                __syncthreads();
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] += at[i][j];
+    }
+
+    // the last chunk ended with a barrier: the staging buffers are free
+    halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, (VSWZ ? BN : BN + 8)>(acc, scale, shift, resid, out, out_rs, M,
+                                                                             m0, n0, smem);
 }
 
 }  // namespace azg

@@ -36,6 +36,7 @@ hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, cons
 extern int g_tower_mode;
 extern int g_tower_shape;
 extern int g_tower_ablation;
+extern int g_tower_var;
 constexpr int kTowerMaxBlocks = 32;
 int conv_batch_bucket(int M);
 size_t tower_sync_bytes(int nlayers, int M);

@@ -54,12 +54,12 @@ struct TowerArgs {
 
 constexpr unsigned kSpinLimit = 1u << 22;    // x s_sleep(2): seconds, far above any tile time
 
-template <int C, int BN_, int WM_, int TM_, int NW_>
+template <int C, int BN_, int WM_, int TM_, int NW_, int VAR = 0>
 __global__ __launch_bounds__(64 * NW_, 4) void conv_tower(const TowerArgs a)
 {
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
     constexpr int NTN = C / T::BN;
-    constexpr int LDS_FLOATS = halo_lds_bytes<C, BN_, WM_, TM_, NW_>() / 4;
+    constexpr int LDS_FLOATS = halo_lds_bytes<C, BN_, WM_, TM_, NW_, VAR>() / 4;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     int* s_claim = (int*)(smem + LDS_FLOATS);
 
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(64 * NW_, 4) void conv_tower(const TowerArgs a)
         __syncthreads();
         const TowerLayer& Ly = a.L[l];
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Ly.out, (short)0, a.act_bytes, 0x00020000);
-        halo_tile<C, BN_, WM_, TM_, NW_, EPI_BN_OPTRES_RELU, true>(Ly.in, Ly.wp, Ly.scale, Ly.shift, Ly.resid, Ly.out,
+        halo_tile<C, BN_, WM_, TM_, NW_, EPI_BN_OPTRES_RELU, true, 0, VAR>(Ly.in, Ly.wp, Ly.scale, Ly.shift, Ly.resid, Ly.out,
                                                                   rs, a.M, mt * T::BM, nt * T::BN, smem);
         if (!(a.abl & 2)) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
@@ -112,17 +112,17 @@ __global__ __launch_bounds__(64 * NW_, 4) void conv_tower(const TowerArgs a)
     }
 }
 
-template <int C, int BN, int WM, int TM, int NW>
+template <int C, int BN, int WM, int TM, int NW, int VAR = 0>
 static hipError_t launch_tower_t(const TowerArgs& a, hipStream_t st, int* grid_out)
 {
-    constexpr int lds = halo_lds_bytes<C, BN, WM, TM, NW>() + 16;
+    constexpr int lds = halo_lds_bytes<C, BN, WM, TM, NW, VAR>() + 16;
     static int grid = 0;
     if (grid == 0) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv_tower<C, BN, WM, TM, NW>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv_tower<C, BN, WM, TM, NW, VAR>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
         int per_cu = 0, dev = 0, cus = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)conv_tower<C, BN, WM, TM, NW>,
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)conv_tower<C, BN, WM, TM, NW, VAR>,
                                                          64 * NW, lds);
         if (e != hipSuccess) return e;
         if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
@@ -130,11 +130,12 @@ static hipError_t launch_tower_t(const TowerArgs& a, hipStream_t st, int* grid_o
         grid = max(1, per_cu) * cus;
     }
     if (grid_out) *grid_out = grid;
-    hipLaunchKernelGGL((conv_tower<C, BN, WM, TM, NW>), dim3(grid), dim3(64 * NW), lds, st, a);
+    hipLaunchKernelGGL((conv_tower<C, BN, WM, TM, NW, VAR>), dim3(grid), dim3(64 * NW), lds, st, a);
     return hipGetLastError();
 }
 
 int g_tower_ablation = 0;
+int g_tower_var = 0;     // halo_tile VAR of the 128x64 C=128 tower (0 = product; 1..5 A/B studies)
 int g_tower_shape = 8;   // forced shape when g_tower_mode == 1: 5 = 64x64 (4 waves), 8 = 128x64 (8 waves)
 
 size_t tower_sync_bytes(int nlayers, int M)
@@ -181,6 +182,13 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     case CC:                                                                               \
         if (shape == 8) return launch_tower_t<CC, 64, 4, 1, 8>(a, st, nullptr);    \
         return launch_tower_t<CC, 64, 2, 1, 4>(a, st, nullptr);
+    if (C == 128 && shape == 8 && g_tower_var != 0) {   // A/B variants (bitwise identical)
+        if (g_tower_var == 3) return launch_tower_t<128, 64, 4, 1, 8, 3>(a, st, nullptr);
+        if (g_tower_var == 1) return launch_tower_t<128, 64, 4, 1, 8, 1>(a, st, nullptr);
+        if (g_tower_var == 2) return launch_tower_t<128, 64, 4, 1, 8, 2>(a, st, nullptr);
+        if (g_tower_var == 4) return launch_tower_t<128, 64, 4, 1, 8, 4>(a, st, nullptr);
+        if (g_tower_var == 5) return launch_tower_t<128, 64, 4, 1, 8, 5>(a, st, nullptr);
+    }
     switch (C) {
         AZG_TOWER_C(64)
         AZG_TOWER_C(128)

@@ -136,7 +136,11 @@ int32_t azg_pv_profile_read(azg_pv* h, double* ms, int64_t* launches);
  *          (shape from key 6), 2 (default) chosen per (C, blocks, batch bucket) by
  *          timing every variant on first use -- all bitwise identical;
  *   key 6: persistent-tower tile shape for key 5 = 1 (8: 128x64 / 8 waves, default;
- *          5: 64x64 / 4 waves). */
+ *          5: 64x64 / 4 waves);
+ *   keys 3, 7, 8: timing-only ablation switches (results invalid while set);
+ *   key 10: tile-body variant of the C=128 128x64 persistent tower (0 = default;
+ *          1..5 = swizzle / prefetch / LDS-DMA staging variants for A/B timing, all
+ *          bitwise identical to 0).  Every call returns the previous value. */
 int32_t azg_pv_set_tuning(int32_t key, int32_t value);
 
 /* Persistent-tower health: 0, or nonzero if a tile of the last eval forward on

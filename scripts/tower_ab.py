@@ -23,7 +23,8 @@ def main():
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--channels", type=int, default=128)
     ap.add_argument("--ablations", default="", help="comma list of tower ablation masks to time too")
-    ap.add_argument("--shapes", default="", help="extra tower tile shapes (C=128: 4, 6, 7, 9)")
+    ap.add_argument("--shapes", default="", help="extra tower tile shapes")
+    ap.add_argument("--vars", default="", help="tower tile-body variants (C=128, 128x64 tiles): 0..5")
     args = ap.parse_args()
     from network import PyTorchModel
     from synth import synth_encoded
@@ -40,13 +41,15 @@ def main():
         values = torch.empty((B, 1), device="cuda")
         flop = 2 * 225 * C * 9 * C * B * 2 * args.blocks
         row = {"batch": B}
-        variants = [("layers", 0, 5, 0), ("tower64", 1, 5, 0), ("tower128", 1, 8, 0)]
-        variants += [(f"tower128_abl{a}", 1, 8, int(a)) for a in args.ablations.split(",") if a]
-        variants += [(f"tower_s{t}", 1, int(t), 0) for t in args.shapes.split(",") if t]
-        for name, mode, shape, abl in variants:
+        variants = [("layers", 0, 5, 0, 0), ("tower64", 1, 5, 0, 0), ("tower128", 1, 8, 0, 0)]
+        variants += [(f"tower128_abl{a}", 1, 8, int(a), 0) for a in args.ablations.split(",") if a]
+        variants += [(f"tower_s{t}", 1, int(t), 0, 0) for t in args.shapes.split(",") if t]
+        variants += [(f"tower128_v{v}", 1, 8, 0, int(v)) for v in args.vars.split(",") if v]
+        for name, mode, shape, abl, var in variants:
             lib.azg_pv_set_tuning(5, mode)
             lib.azg_pv_set_tuning(6, shape)
             lib.azg_pv_set_tuning(8, abl)
+            lib.azg_pv_set_tuning(10, var)
             for _ in range(2):
                 eng.forward_into(x, probs, values)
             best_dev, best_wall = None, None
@@ -69,6 +72,7 @@ def main():
     lib.azg_pv_set_tuning(5, 2)
     lib.azg_pv_set_tuning(6, 8)
     lib.azg_pv_set_tuning(8, 0)
+    lib.azg_pv_set_tuning(10, 0)
 
 
 if __name__ == "__main__":
