@@ -93,6 +93,7 @@ int32_t azg_pv_bind(azg_pv* h, float* params, float* grads, float* bn_stats)
         size_t floats = 0;
         floats += (size_t)2 * h->NB * 9 * C * C;   // wpack
         floats += (size_t)27 * C;                  // wstem
+        floats += (size_t)FC_OUT * FC_KP;          // wfc
         floats += (size_t)h->nfold * 2;            // scale, shift
         float* base = nullptr;
         hipError_t e = hipMalloc(&base, floats * sizeof(float));
@@ -100,6 +101,7 @@ int32_t azg_pv_bind(azg_pv* h, float* params, float* grads, float* bn_stats)
         h->wbase = base;
         h->wpack = base; base += (size_t)2 * h->NB * 9 * C * C;
         h->wstem = base; base += (size_t)27 * C;
+        h->wfc = base; base += (size_t)FC_OUT * FC_KP;
         h->scale = base; base += h->nfold;
         h->shift = base; base += h->nfold;
         e = hipMalloc(&h->bn_desc_dev, sizeof(BnDesc) * h->bn_desc.size());
@@ -320,8 +322,11 @@ int32_t ensure_eval_workspace(azg_pv* h, int batch, hipStream_t st)
         if (e != hipSuccess) return fail("ensure_eval_workspace: hipMalloc(tower sync)", e);
     }
     {
-        hipError_t e = hipMalloc(&h->hbuf, (size_t)cap * (3 * PIX + ACTIONS + VHID) * sizeof(float));
+        const size_t hb = (size_t)cap * (FC_FS + FC_OUT) * sizeof(float);
+        hipError_t e = hipMalloc(&h->hbuf, hb);
         if (e != hipSuccess) return fail("ensure_eval_workspace: hipMalloc(head features)", e);
+        e = hipMemsetAsync(h->hbuf, 0, hb, st);   // feature pads: zero, never written
+        if (e != hipSuccess) return fail("ensure_eval_workspace: hipMemsetAsync(head features)", e);
     }
     const size_t bytes = (size_t)cap * PADPIX * h->C * sizeof(float);
     for (int i = 0; i < 3; ++i) {
@@ -340,6 +345,7 @@ int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst)
     const int C = h->C;
     const float* P = h->params;
     AZG_TRY(launch_pack_stem(P + h->poff[h->t_stem_w], h->wstem, C, st), "repack: stem");
+    AZG_TRY(launch_pack_fc(P + h->poff[h->t_pfc_w], P + h->poff[h->t_vfc1_w], h->wfc, st), "repack: head fc");
     if (h->NB > 0)   // every residual conv in one launch (and its dgrad packing when training)
         AZG_TRY(launch_pack_convs(P, h->conv_off_dev, 2 * h->NB, h->wpack, dgrad_dst, C, st), "repack: convs");
     AZG_TRY(launch_fold_bn(P, h->bn, h->bn_desc_dev, (int)h->bn_desc.size(), h->scale, h->shift, st),
@@ -463,8 +469,7 @@ int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* 
     const int ho = bd[h->bn_pol].out_off;   // policy (2) then value (1): contiguous
     int pr = prof_begin(h, AZG_PROF_HEADS, st);
     AZG_TRY(launch_heads_fwd(C, X, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], h->scale + ho, h->shift + ho,
-                             P + h->poff[h->t_pfc_w], P + h->poff[h->t_pfc_b], P + h->poff[h->t_vfc1_w],
-                             P + h->poff[h->t_vfc1_b],
+                             h->wfc, P + h->poff[h->t_pfc_b], P + h->poff[h->t_vfc1_b],
                              P + h->poff[h->t_vfc2_w], P + h->poff[h->t_vfc2_b], h->hbuf, probs, values, logits,
                              batch, st, boards, priors),
             "forward: heads");

@@ -16,6 +16,14 @@ constexpr int PADW = BOARD + 2;           // 17
 constexpr int PADPIX = PADW * PADW;       // 289
 constexpr int ACTIONS = PIX;              // 225
 constexpr int VHID = 64;                  // value_fc1 width (network.py:70)
+// eval head features, per board (16-B aligned rows): policy planes (450, padded to
+// FC_KP = 456) then the value plane (225, padded to FC_KV = 232); packed head FC
+// weights wfc[FC_OUT][FC_KP]: rows 0..224 policy_fc (K = 450), 225..288 value_fc1
+// (K = 225), zero-padded.  The pads are zero and never written.
+constexpr int FC_KP = 456;
+constexpr int FC_KV = 232;
+constexpr int FC_FS = FC_KP + FC_KV;      // 688 floats per board
+constexpr int FC_OUT = ACTIONS + VHID;    // 289: pre[b] = [policy logits | value hidden]
 constexpr float BN_EPS = 1e-5f;           // nn.BatchNorm2d default
 constexpr float BN_MOMENTUM = 0.1f;       // nn.BatchNorm2d default
 

@@ -285,6 +285,137 @@ __global__ __launch_bounds__(256) void stem_conv(
     }
 }
 
+// Stem conv 3->C on fp32 MFMA (the product stem; stem_conv above is kept as the
+// bitwise reference, tuning key 9).  The stem is an M x C x K=27 GEMM (K padded to
+// 28): each wave owns 32 pixels x CW channels (CW = min(C, 128), NJ = CW/32
+// accumulators of v_mfma_f32_32x32x2_f32).  Both operands are built straight in
+// registers -- no LDS: lane (r, h) holds A[pixel r][k = 2s + h] for the 14 steps s,
+// computed from the 3x3 neighbourhood of its pixel (BOARDS: the int8 board cells,
+// encoded as games/gomoku.py:130-150 does: board == player, board == opponent,
+// ones inside the board; zero padding outside), and B[k][channel] = ws[k][c].  K
+// order k = ci*9 + ky*3 + kx, step s = k 2s then 2s+1: the MFMA's exact fmaf chain
+// (MI355X_MICROARCH.md: "exact f32 (= fmaf chain, bitwise)") in stem_conv's order, so
+// the two stems are bitwise equal (tested).  The epilogue (BN + ReLU) writes 128-B
+// runs of channels per pixel row straight from the accumulators.
+constexpr int STEM_CW = 64;   // channels per wave (2 accumulators): twice the waves of 128
+// ABL (timing studies only, results invalid when set): 1 no stores, 2 no input
+// loads, 4 no weight loads, 8 no MFMA.
+template <int C, int EPI, bool BOARDS, int ABL = 0>
+__global__ __launch_bounds__(256) void stem_mfma(const float* __restrict__ x, const int8_t* __restrict__ boards,
+                                                 const int8_t* __restrict__ players, const float* __restrict__ ws,
+                                                 const float* __restrict__ scale, const float* __restrict__ shift,
+                                                 float* __restrict__ out, int M)
+{
+    constexpr int CW = C < STEM_CW ? C : STEM_CW;
+    constexpr int NJ = CW / 32;
+    constexpr int KS = 14;                       // MFMA steps (K = 27 padded to 28)
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int r32 = lane & 31, h = lane >> 5;
+    const int m0 = (blockIdx.x * 4 + wid) * 32;
+    if (m0 >= M) return;                         // wave-uniform; the kernel has no barrier
+    const int c0 = blockIdx.y * CW;
+
+    float bw[NJ][KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        const int k = 2 * s + h;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+            bw[j][s] = (ABL & 4) ? (float)(k + j) : (k < 27 ? ws[k * C + c0 + 32 * j + r32] : 0.f);
+    }
+
+    const int m = min(m0 + r32, M - 1);
+    const int b = m / PIX, p = m - b * PIX;
+    const int y = p / BOARD, xq = p - y * BOARD;
+    // the 9 neighbourhood values of each input plane (0 outside the board)
+    float nb[3][9];
+    if (BOARDS) {
+        const int8_t* bb = boards + (size_t)b * PIX;
+        const int me = (int)players[b];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int yy = y + t / 3 - 1, xx = xq + t % 3 - 1;
+            const bool in = yy >= 0 && yy < BOARD && xx >= 0 && xx < BOARD;
+            const int c = in ? (int)bb[yy * BOARD + xx] : -1;
+            nb[0][t] = c == me ? 1.f : 0.f;
+            nb[1][t] = c == 3 - me ? 1.f : 0.f;
+            nb[2][t] = in ? 1.f : 0.f;
+        }
+    } else {
+        const float* xb = x + (size_t)b * 3 * PIX;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int yy = y + t / 3 - 1, xx = xq + t % 3 - 1;
+            const bool in = yy >= 0 && yy < BOARD && xx >= 0 && xx < BOARD;
+#pragma unroll
+            for (int ci = 0; ci < 3; ++ci)
+                nb[ci][t] = (ABL & 2) ? (float)(yy + xx + ci) : (in ? xb[ci * PIX + yy * BOARD + xx] : 0.f);
+        }
+    }
+    float av[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        const int k0 = 2 * s, k1 = 2 * s + 1;
+        const float v0 = nb[k0 / 9][k0 % 9];
+        const float v1 = k1 < 27 ? nb[k1 / 9][k1 % 9] : 0.f;
+        av[s] = h ? v1 : v0;
+    }
+
+    f32x16 acc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            if (ABL & 8) acc[j][s] = av[s] * bw[j][s];
+            else acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bw[j][s], acc[j], 0, 0, 0);
+        }
+
+    // epilogue through a wave-private LDS tile [32 px][32 ch] per accumulator: lane
+    // (p = lane/8 + 8*it, 16-B run lane%8) finishes 4 channels of one pixel and
+    // stores them as one 16 B (4x fewer store instructions than the 4-B C/D layout)
+    __shared__ __attribute__((aligned(16))) float es[4][32][32 + 4];
+    float (*E)[36] = es[wid];
+    const int ec = (lane & 7) * 4;
+    int orow[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        const int mm = m0 + (lane >> 3) + 8 * it;
+        orow[it] = mm < M ? pad_off(mm, C) : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) E[(r & 3) + 8 * (r >> 2) + 4 * h][r32] = acc[j][r];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int c = c0 + 32 * j + ec;
+        f32x4 s4 = {1.f, 1.f, 1.f, 1.f}, t4 = {0.f, 0.f, 0.f, 0.f};
+        if (EPI != EPI_RAW) {
+            s4 = *(const f32x4*)(scale + c);
+            t4 = *(const f32x4*)(shift + c);
+        }
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            f32x4 v = *(const f32x4*)(&E[(lane >> 3) + 8 * it][ec]);
+            if (orow[it] >= 0 && (!(ABL & 1) || v[0] == 1234.5f)) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (EPI == EPI_BN_RELU) v[e] = fmaxf(v[e] * s4[e] + t4[e], 0.f);
+                *(f32x4*)(out + orow[it] + c) = v;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
 // ---- host launchers ------------------------------------------------------
 
 template <int C, int BN, int WM, int TM, int NW, int EPI, int SB = 0>
@@ -567,10 +698,40 @@ int conv_tuned_shape(int C, int M)
     return it == tune_cache().end() ? -1 : it->second;
 }
 
+int g_stem_variant = 1;   // 1: fp32-MFMA stem (product); 0: VALU stem_conv (bitwise reference)
+int g_stem_ablation = 0;  // timing studies only (C = 128 float-plane stem)
+
 hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const float* scale,
                        const float* shift, float* out, int B, hipStream_t st, const int8_t* boards,
                        const int8_t* players)
 {
+    if (B <= 0) return hipSuccess;
+    if (epi != EPI_RAW && epi != EPI_BN_RELU) return hipErrorInvalidValue;
+    if (g_stem_variant == 1) {
+        const int M = B * PIX;
+        const int cw = C < STEM_CW ? C : STEM_CW;
+        const dim3 grid((M + 127) / 128, C / cw);
+        if (g_stem_ablation && C == 128 && !boards && epi == EPI_BN_RELU) {
+#define AZG_STEM_ABL(A) \
+    if (g_stem_ablation == A) hipLaunchKernelGGL((stem_mfma<128, EPI_BN_RELU, false, A>), grid, dim3(256), 0, st, x, boards, players, ws, scale, shift, out, M);
+            AZG_STEM_ABL(1) AZG_STEM_ABL(2) AZG_STEM_ABL(4) AZG_STEM_ABL(8) AZG_STEM_ABL(6) AZG_STEM_ABL(14) AZG_STEM_ABL(15)
+#undef AZG_STEM_ABL
+            return hipGetLastError();
+        }
+#define AZG_STEM_MFMA(CC)                                                                                       \
+    case CC:                                                                                                    \
+        if (boards) hipLaunchKernelGGL((stem_mfma<CC, EPI_BN_RELU, true>), grid, dim3(256), 0, st, x, boards, players, ws, scale, shift, out, M); \
+        else if (epi == EPI_RAW) hipLaunchKernelGGL((stem_mfma<CC, EPI_RAW, false>), grid, dim3(256), 0, st, x, boards, players, ws, scale, shift, out, M); \
+        else hipLaunchKernelGGL((stem_mfma<CC, EPI_BN_RELU, false>), grid, dim3(256), 0, st, x, boards, players, ws, scale, shift, out, M); \
+        return hipGetLastError();
+        switch (C) {
+            AZG_STEM_MFMA(64)
+            AZG_STEM_MFMA(128)
+            AZG_STEM_MFMA(256)
+            default: return hipErrorInvalidValue;
+        }
+#undef AZG_STEM_MFMA
+    }
 #define AZG_STEM_CASE(CC)                                                                              \
     case CC:                                                                                           \
         if (boards) hipLaunchKernelGGL((stem_conv<CC, EPI_BN_RELU, true>), dim3(B), dim3(256), 0, st, x, boards, players, ws, scale, shift, out); \
@@ -603,6 +764,16 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     if (key == 3) {   // ablation mask (timing studies only, C=128 EPI_BN_RELU launches)
         const int prev = azg::g_conv_ablation;
         azg::g_conv_ablation = value;
+        return prev;
+    }
+    if (key == 11) {  // stem ablation mask (timing studies only)
+        const int prev = azg::g_stem_ablation;
+        azg::g_stem_ablation = value;
+        return prev;
+    }
+    if (key == 9) {   // stem kernel: 1 fp32 MFMA (default), 0 VALU reference
+        const int prev = azg::g_stem_variant;
+        if (value == 0 || value == 1) azg::g_stem_variant = value;
         return prev;
     }
     if (key == 10) {  // persistent-tower tile body variant (A/B studies, bitwise identical)

@@ -21,7 +21,7 @@ __global__ __launch_bounds__(256) void heads_project(const float* __restrict__ a
                                                      const float* __restrict__ wvc,
                                                      const float* __restrict__ hscale,
                                                      const float* __restrict__ hshift, float* __restrict__ hout,
-                                                     int M)
+                                                     int M, int fs, int voff)
 {
     constexpr int Q = C / 4;        // channels per thread
     __shared__ float w[3][C];
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void heads_project(const float* __restrict__ a
     }
     if (m < M && q == 0) {
         const int b = m / PIX, p = m - b * PIX;
-        float* hb = hout + (size_t)b * 3 * PIX;
+        float* hb = hout + (size_t)b * fs;
         if (BN) {
             d0 = fmaxf(d0 * hscale[0] + hshift[0], 0.f);
             d1 = fmaxf(d1 * hscale[1] + hshift[1], 0.f);
@@ -59,11 +59,63 @@ __global__ __launch_bounds__(256) void heads_project(const float* __restrict__ a
         }
         hb[p] = d0;
         hb[PIX + p] = d1;
-        hb[2 * PIX + p] = d2;
+        hb[voff + p] = d2;
     }
 }
 
-constexpr int FC_OUT = ACTIONS + VHID;           // pre[b] = [policy logits (225) | value hidden (64)]
+// policy_fc + value_fc1 (network.py:104-106, 112-114) on fp32 MFMA: one workgroup
+// per 32 boards x 32 outputs (grid.y: 8 policy tiles then 2 value tiles, rows of
+// the packed wfc), K split over the 4 waves in blocks of 8: lane (r, h) loads one
+// float4 of its board's features and one float4 of its output's weights per block
+// (k = 8q + 4h + t, t = MFMA step), all loads of a wave issued before its first
+// MFMA; partial tiles summed in fixed wave order.  Each output row depends only on
+// its own board (batch independent).
+__global__ __launch_bounds__(256) void heads_fc(const float* __restrict__ feat, const float* __restrict__ wfc,
+                                                float* __restrict__ pre, int B)
+{
+    constexpr int QMAX = (FC_KP / 8 + 3) / 4;    // blocks per wave, at most
+    __shared__ float red[4][16][64];
+    const int tile = blockIdx.y;
+    const bool val = tile >= 8;
+    const int j0 = val ? ACTIONS + (tile - 8) * 32 : tile * 32;   // first output (= wfc row)
+    const int koff = val ? FC_KP : 0;
+    const int nblk = (val ? FC_KV : FC_KP) / 8;
+    const int i0 = blockIdx.x * 32;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int r32 = lane & 31, h = lane >> 5;
+    const float* a = feat + (size_t)min(i0 + r32, B - 1) * FC_FS + koff + 4 * h;
+    const float* w = wfc + (size_t)min(j0 + r32, FC_OUT - 1) * FC_KP + 4 * h;
+    const int q0 = wid * nblk / 4, nq = (wid + 1) * nblk / 4 - q0;
+    f32x4 av[QMAX], bv[QMAX];
+#pragma unroll
+    for (int u = 0; u < QMAX; ++u)
+        if (u < nq) {
+            av[u] = *(const f32x4*)(a + (q0 + u) * 8);
+            bv[u] = *(const f32x4*)(w + (q0 + u) * 8);
+        }
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int u = 0; u < QMAX; ++u)
+        if (u < nq) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u][t], bv[u][t], acc, 0, 0, 0);
+        }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wid][r][lane] = acc[r];
+    __syncthreads();
+    if (wid == 0) {
+        const int j = j0 + r32;
+        const bool jok = val || j < ACTIONS;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float v = ((red[0][r][lane] + red[1][r][lane]) + red[2][r][lane]) + red[3][r][lane];
+            const int i = i0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (i < B && jok) pre[(size_t)i * FC_OUT + j] = v;
+        }
+    }
+}
 
 // Per board (one wave): logits = pre + bias, softmax; value = tanh(relu(pre_v + b1) . w2 + b2).
 // priors (optional, with boards): probs * (board == 0), the reference's masked
@@ -112,13 +164,14 @@ __global__ __launch_bounds__(256) void heads_finalize(const float* __restrict__ 
 }
 
 hipError_t launch_heads_project(int C, bool bn, const float* act, const float* wpc, const float* wvc,
-                                const float* hscale, const float* hshift, float* hout, int M, hipStream_t st)
+                                const float* hscale, const float* hshift, float* hout, int M, hipStream_t st,
+                                int fs, int voff)
 {
     dim3 grid((M + PROJ_ROWS - 1) / PROJ_ROWS);
 #define AZG_PROJ_CASE(CC)                                                                                      \
     case CC:                                                                                                   \
-        if (bn) hipLaunchKernelGGL((heads_project<CC, true>), grid, dim3(256), 0, st, act, wpc, wvc, hscale, hshift, hout, M); \
-        else hipLaunchKernelGGL((heads_project<CC, false>), grid, dim3(256), 0, st, act, wpc, wvc, hscale, hshift, hout, M); \
+        if (bn) hipLaunchKernelGGL((heads_project<CC, true>), grid, dim3(256), 0, st, act, wpc, wvc, hscale, hshift, hout, M, fs, voff); \
+        else hipLaunchKernelGGL((heads_project<CC, false>), grid, dim3(256), 0, st, act, wpc, wvc, hscale, hshift, hout, M, fs, voff); \
         return hipGetLastError();
     switch (C) {
         AZG_PROJ_CASE(64)
@@ -130,18 +183,18 @@ hipError_t launch_heads_project(int C, bool bn, const float* act, const float* w
 }
 
 hipError_t launch_heads_fwd(int C, const float* act, const float* wpc, const float* wvc, const float* hscale,
-                            const float* hshift, const float* wpf, const float* bpf, const float* wv1,
+                            const float* hshift, const float* wfc, const float* bpf,
                             const float* bv1, const float* wv2, const float* bv2, float* hbuf, float* probs,
                             float* values, float* logits, int B, hipStream_t st, const int8_t* boards,
                             float* priors)
 {
-    hipError_t e = launch_heads_project(C, true, act, wpc, wvc, hscale, hshift, hbuf, B * PIX, st);
+    if (B <= 0) return hipSuccess;
+    // hbuf: [B][FC_FS] features (zero pads, set at allocation) then pre [B][FC_OUT]
+    hipError_t e = launch_heads_project(C, true, act, wpc, wvc, hscale, hshift, hbuf, B * PIX, st, FC_FS, FC_KP);
     if (e != hipSuccess) return e;
-    float* pre = hbuf + (size_t)B * 3 * PIX;
-    // policy_fc: pre[b][j] = sum_k feat[b][k] wpf[j][k] (k < 450); value_fc1 on feat[b][450..674]
-    GemmProb gp{hbuf, 3 * PIX, 1, wpf, 1, 2 * PIX, pre, FC_OUT, 1, nullptr, 0, 0, B, ACTIONS, 2 * PIX};
-    GemmProb gv{hbuf + 2 * PIX, 3 * PIX, 1, wv1, 1, PIX, pre + ACTIONS, FC_OUT, 1, nullptr, 0, 0, B, VHID, PIX};
-    e = launch_small_gemm(gp, &gv, st);
+    float* pre = hbuf + (size_t)B * FC_FS;
+    hipLaunchKernelGGL(heads_fc, dim3((B + 31) / 32, 10), dim3(256), 0, st, hbuf, wfc, pre, B);
+    e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(heads_finalize, dim3((B + 3) / 4), dim3(256), 0, st, pre, bpf, bv1, wv2, bv2, probs, values,
                        logits, B, boards, priors);

@@ -47,13 +47,15 @@ hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const fl
                        const float* shift, float* out, int B, hipStream_t st, const int8_t* boards = nullptr,
                        const int8_t* players = nullptr);
 hipError_t launch_heads_fwd(int C, const float* act, const float* wpc, const float* wvc,
-                            const float* hscale, const float* hshift, const float* wpf,
-                            const float* bpf, const float* wv1, const float* bv1,
+                            const float* hscale, const float* hshift, const float* wfc,
+                            const float* bpf, const float* bv1,
                             const float* wv2, const float* bv2, float* hbuf, float* probs,
                             float* values, float* logits, int B, hipStream_t st,
                             const int8_t* boards = nullptr, float* priors = nullptr);
 hipError_t launch_heads_project(int C, bool bn, const float* act, const float* wpc, const float* wvc,
-                                const float* hscale, const float* hshift, float* hout, int M, hipStream_t st);
+                                const float* hscale, const float* hshift, float* hout, int M, hipStream_t st,
+                                int fs = 3 * PIX, int voff = 2 * PIX);
+hipError_t launch_pack_fc(const float* wpf, const float* wv1, float* wfc, hipStream_t st);
 hipError_t launch_small_gemm(const GemmProb& p0, const GemmProb* p1, hipStream_t st);
 hipError_t launch_pack_convs(const float* params, const int64_t* offs, int nl, float* wp, float* wd, int C,
                              hipStream_t st);
@@ -92,6 +94,7 @@ struct azg_pv {
     float* wbase = nullptr;
     float* wpack = nullptr;   // 2*NB x [9*C/32][C][32]
     float* wstem = nullptr;   // [27][C]
+    float* wfc = nullptr;     // [FC_OUT][FC_KP] packed policy_fc + value_fc1 (pv_heads.hip heads_fc)
     float* scale = nullptr;   // folded BN (eval)
     float* shift = nullptr;
 

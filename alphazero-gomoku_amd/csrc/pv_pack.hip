@@ -85,6 +85,28 @@ hipError_t launch_pack_stem(const float* w, float* ws, int C, hipStream_t st)
     return hipGetLastError();
 }
 
+// head FC weights -> wfc[FC_OUT][FC_KP] (pv_common.h): policy_fc rows (K = 450) then
+// value_fc1 rows (K = 225), zero-padded to FC_KP
+__global__ void pack_fc_kernel(const float* __restrict__ wpf, const float* __restrict__ wv1, float* __restrict__ wfc)
+{
+    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < FC_OUT * FC_KP; idx += gridDim.x * blockDim.x) {
+        const int j = idx / FC_KP, k = idx - j * FC_KP;
+        float v = 0.f;
+        if (j < ACTIONS) {
+            if (k < 2 * PIX) v = wpf[j * 2 * PIX + k];
+        } else if (k < PIX) {
+            v = wv1[(j - ACTIONS) * PIX + k];
+        }
+        wfc[idx] = v;
+    }
+}
+
+hipError_t launch_pack_fc(const float* wpf, const float* wv1, float* wfc, hipStream_t st)
+{
+    hipLaunchKernelGGL(pack_fc_kernel, dim3(nblk(FC_OUT * FC_KP)), dim3(256), 0, st, wpf, wv1, wfc);
+    return hipGetLastError();
+}
+
 hipError_t launch_transpose(const float* src, float* dst, int R, int Cc, hipStream_t st)
 {
     hipLaunchKernelGGL(transpose_kernel, dim3(nblk(R * Cc)), dim3(256), 0, st, src, dst, R, Cc);

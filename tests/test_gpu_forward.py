@@ -261,3 +261,32 @@ def test_persistent_tower_under_concurrent_load():
         torch.cuda.synchronize()
         assert torch.equal(a, r1) and torch.equal(b, r2)
     lib.azg_pv_set_tuning(5, prev_mode)
+
+
+@pytest.mark.parametrize("blocks,ch,B", [(3, 64, 37), (6, 128, 300), (2, 256, 20)])
+def test_mfma_stem_bitwise_equals_valu_stem(blocks, ch, B):
+    """The fp32-MFMA stem (product) is bitwise the VALU stem_conv (tuning key 9 = 0):
+    same K order, and the MFMA is an exact fmaf chain.  Checked on the float-plane
+    forward, the int8-board forward (on-GPU encode) and a train step (EPI_RAW stem)."""
+    import _native
+    from oracle.boards import synth_targets
+    lib = _native.load_library()
+    boards, players = synth_positions(B, seed=41)
+    x = encode_batch(boards, players)
+    bi8, pl8 = np.asarray(boards, np.int8), np.asarray(players, np.int8)
+    pi, z = synth_targets(B, seed=42)
+    outs = []
+    prev = lib.azg_pv_set_tuning(9, 1)
+    try:
+        for variant in (0, 1):
+            lib.azg_pv_set_tuning(9, variant)
+            m = make_model(blocks, ch, seed=9)
+            p, v = m.predict(x)
+            pb, vb = m.predict_boards(bi8, pl8, masked=False)
+            m.train_batch(x, pi, z, epochs=1)
+            p2, v2 = m.predict(x)
+            outs.append((p, v, pb, vb, p2, v2))
+    finally:
+        lib.azg_pv_set_tuning(9, prev)
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b), float(np.abs(a - b).max())
