@@ -94,7 +94,7 @@ __device__ __forceinline__ int halo_vkey(int row)
 // scale/shift/residual, one 16-B store per run -- instead of 16 scalar stores (and
 // 16 pad_off divisions) per fragment.  Same per-element arithmetic.  The caller
 // guarantees every wave is past its last staging-buffer access (barrier).
-template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1, int ABL, int ELD>
+template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1, int ABL, int ELD, bool EARLY = false>
 __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<C, BN_, WM_, TM_, NW_>::TN],
                                               const float* __restrict__ scale, const float* __restrict__ shift,
                                               const float* __restrict__ resid, float* __restrict__ out,
@@ -107,6 +107,30 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
     const int wm = wid / WN, wn = wid % WN;
     const int r32 = lane & 31, h = lane >> 5;
     float* Es = smem;
+    constexpr int CPR = BN / 4;            // 16-B runs per pixel row
+    constexpr int RPI = T::NT / CPR;       // pixel rows per pass
+    constexpr int NPASS = BM / RPI;
+    static_assert(BM % RPI == 0, "epilogue passes");
+    const int ec = (tid % CPR) * 4;
+    const int er = tid / CPR;
+    const int col = n0 + ec;
+    const bool has_res = EPI == EPI_BN_RES_RELU || EPI == EPI_ADD || (EPI == EPI_BN_OPTRES_RELU && resid);
+    // EARLY: the residual / scale / shift loads are issued before the accumulator
+    // tile goes through LDS, so their latency overlaps the ds_write + barrier
+    f32x4 rve[EARLY ? NPASS : 1];
+    f32x4 s4 = {1.f, 1.f, 1.f, 1.f}, t4 = {0.f, 0.f, 0.f, 0.f};
+    if (EARLY) {
+        if (EPI == EPI_BN_RELU || EPI == EPI_BN_RES_RELU || EPI == EPI_BN_OPTRES_RELU) {
+            s4 = *(const f32x4*)(scale + col);
+            t4 = *(const f32x4*)(shift + col);
+        }
+#pragma unroll
+        for (int p = 0; p < (EARLY ? NPASS : 1); ++p) {
+            const int m = m0 + er + p * RPI;
+            rve[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (has_res && m < M) rve[p] = *(const f32x4*)(resid + pad_off(m, C) + col);
+        }
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -117,27 +141,20 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                 Es[row * ELD + wn * TN * 32 + j * 32 + r32] = acc[i][j][r];
             }
     __syncthreads();
-    constexpr int CPR = BN / 4;            // 16-B runs per pixel row
-    constexpr int RPI = T::NT / CPR;       // pixel rows per pass
-    static_assert(BM % RPI == 0, "epilogue passes");
-    const int ec = (tid % CPR) * 4;
-    const int er = tid / CPR;
-    const int col = n0 + ec;
-    f32x4 s4 = {1.f, 1.f, 1.f, 1.f}, t4 = {0.f, 0.f, 0.f, 0.f};
-    if (EPI == EPI_BN_RELU || EPI == EPI_BN_RES_RELU || EPI == EPI_BN_OPTRES_RELU) {
+    if (!EARLY && (EPI == EPI_BN_RELU || EPI == EPI_BN_RES_RELU || EPI == EPI_BN_OPTRES_RELU)) {
         s4 = *(const f32x4*)(scale + col);
         t4 = *(const f32x4*)(shift + col);
     }
 #pragma unroll
-    for (int p = 0; p < BM / RPI; ++p) {
+    for (int p = 0; p < NPASS; ++p) {
         const int row = er + p * RPI;
         const int m = m0 + row;
         f32x4 v = *(const f32x4*)(Es + row * ELD + ec);
         if (m < M && (!(ABL & 16) || v[0] == 1234.5f)) {
             const int o = pad_off(m, C) + col;
             f32x4 rv = {0.f, 0.f, 0.f, 0.f};
-            const bool has_res = EPI == EPI_BN_RES_RELU || EPI == EPI_ADD || (EPI == EPI_BN_OPTRES_RELU && resid);
-            if (has_res) rv = *(const f32x4*)(resid + o);
+            if (EARLY) rv = rve[EARLY ? p : 0];
+            else if (has_res) rv = *(const f32x4*)(resid + o);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 float x = v[e];
@@ -338,8 +355,8 @@ __device__ __forceinline__ void halo_tile(
     if constexpr ((VAR & 4) != 0) {   // LDS-DMA staging
         f32x16 acc[TM_][T::TN];
         halo_mainloop_glds<C, BN_, WM_, TM_, NW_, VAR>(in, wp, M, m0, n0, smem, acc);
-        halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, T::BN>(acc, scale, shift, resid, out, out_rs, M, m0, n0,
-                                                                   smem);
+        halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, T::BN, (VAR & 8) != 0>(acc, scale, shift, resid, out,
+                                                                                   out_rs, M, m0, n0, smem);
         return;
     }
     constexpr int RPP = T::RPP;
@@ -354,7 +371,7 @@ __device__ __forceinline__ void halo_tile(
     // VAR (A/B studies; the product uses 0, measured fastest): bit 1 = halo rows
     // swizzled on the padded board position (conflict-free fragment reads) and an
     // unpadded epilogue tile; bit 2 = weights staged two chunks ahead; bit 4 = LDS-DMA
-    // staging (halo_mainloop_glds).  Every VAR computes bitwise-identical results.
+    // staging (halo_mainloop_glds); bit 8 = epilogue loads issued before the LDS pass.  Every VAR computes bitwise-identical results.
     constexpr bool VSWZ = (VAR & 1) != 0;
     constexpr bool BPF2 = (VAR & 2) != 0;
     constexpr int NCHK = 9 * CG;
@@ -533,8 +550,8 @@ __device__ __forceinline__ void halo_tile(
     }
 
     // the last chunk ended with a barrier: the staging buffers are free
-    halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, (VSWZ ? BN : BN + 8)>(acc, scale, shift, resid, out, out_rs, M,
-                                                                             m0, n0, smem);
+    halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, (VSWZ ? BN : BN + 8), (VAR & 8) != 0>(
+        acc, scale, shift, resid, out, out_rs, M, m0, n0, smem);
 }
 
 }  // namespace azg
