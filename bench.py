@@ -153,6 +153,48 @@ def selfplay_leg(model, args, rank, dist, dev, local):
             "mean_batch": round(sp.boards / max(sp.forwards, 1), 1)}
 
 
+def big_net_leg(args, rank, dist, dev, local):
+    """BASELINE configs[4] network (10-block/256-filter ResNet, 15x15 Pente boards use
+    the same 3-plane input) at batch 512 per GPU: forward boards/s and the persistent
+    tower's MFMA fraction (device time of its launches, hipEvents)."""
+    from network import PyTorchModel
+    from synth import synth_encoded
+    nb, ch, B = 10, 256, 512
+    torch.manual_seed(1)
+    m = PyTorchModel(board_size=15, device=str(dev), n_res_blocks=nb, channels=ch)
+    eng = m.engine
+    x = torch.from_numpy(synth_encoded(B, seed=77 + rank)).to(dev)
+    probs = torch.empty((B, 225), device=dev)
+    values = torch.empty((B, 1), device=dev)
+    for _ in range(3):
+        eng.forward_into(x, probs, values)
+    barrier_sync(dist, local)
+    eng.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.big_steps):
+        eng.forward_into(x, probs, values)
+    barrier_sync(dist, local)
+    dt = time.perf_counter() - t0
+    prof = eng.profile_read()
+    eng.profile_enable(False)
+    v = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    dt = float(v.item())
+    world = dist.get_world_size() if dist is not None else 1
+    flop_conv = 2 * 225 * ch * 9 * ch * B * 2 * nb
+    tower_ms, tower_n = prof.get("tower", (0.0, 0))
+    if not tower_n:
+        tower_ms, tower_n = prof.get("conv3x3", (0.0, 0))
+        tower_n = max(tower_n // (2 * nb), 1)
+    conv_s = tower_ms / 1e3 / max(tower_n, 1)
+    return {"config": f"configs[4] network: {nb}x{ch} ResNet, batch {B}/GPU forward (eval BN)",
+            "boards_per_s": round(B * args.big_steps * world / dt, 1),
+            "ms_per_step": round(dt / args.big_steps * 1e3, 3),
+            "residual_convs_ms": round(conv_s * 1e3, 3),
+            "residual_convs_mfma_frac": round(flop_conv / conv_s / PEAK_F32_MFMA, 4) if conv_s > 0 else None}
+
+
 def train_leg(model, args, rank, world, dist, dev, local):
     """BASELINE configs[3] train half: PyTorchModel.train_batch_device on 128 samples
     per GPU (global 128 x N) with the flat-gradient all-reduce over RCCL between
@@ -196,6 +238,7 @@ def main():
     ap.add_argument("--sp-sims", type=int, default=400)
     ap.add_argument("--sp-moves", type=int, default=2, help="moves per game in the self-play leg (0: skip)")
     ap.add_argument("--train-steps", type=int, default=20, help="steps of the data-parallel train leg (0: skip)")
+    ap.add_argument("--big-steps", type=int, default=10, help="forward steps of the 10x256 net leg (0: skip)")
     args = ap.parse_args()
 
     rank, world, local, dist = dist_setup(args.gpus)
@@ -240,6 +283,10 @@ def main():
     train = None
     if args.train_steps > 0:
         train = train_leg(model, args, rank, world, dist, dev, local)
+
+    big = None
+    if args.big_steps > 0:
+        big = big_net_leg(args, rank, dist, dev, local)
 
     if rank != 0:
         dist.destroy_process_group()
@@ -287,6 +334,7 @@ def main():
         "kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in prof.items()},
         "selfplay": selfplay,
         "train": train,
+        "net_10x256": big,
     }
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
