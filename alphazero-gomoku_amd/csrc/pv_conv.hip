@@ -766,6 +766,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         azg::g_conv_ablation = value;
         return prev;
     }
+    if (key == 12) {  // train: conv weight grads on the caller's stream (1) or overlapped (0)
+        const int prev = azg::g_wgrad_serial;
+        azg::g_wgrad_serial = value ? 1 : 0;
+        return prev;
+    }
     if (key == 11) {  // stem ablation mask (timing studies only)
         const int prev = azg::g_stem_ablation;
         azg::g_stem_ablation = value;
@@ -798,7 +803,7 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     }
     if (key == 6) {   // persistent tower tile shape
         const int prev = azg::g_tower_shape;
-        if (value == 5 || value == 8) azg::g_tower_shape = value;
+        if (value == 5 || value == 8 || value == 9) azg::g_tower_shape = value;
         return prev;
     }
     if (key == 4) {   // conv kernel variant (1 halo-staged, 0 per-chunk staging; timing studies)

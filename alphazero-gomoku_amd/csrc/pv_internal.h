@@ -37,6 +37,7 @@ extern int g_tower_mode;
 extern int g_tower_shape;
 extern int g_tower_ablation;
 extern int g_tower_var;
+extern int g_wgrad_serial;
 constexpr int kTowerMaxBlocks = 32;
 int conv_batch_bucket(int M);
 size_t tower_sync_bytes(int nlayers, int M);

@@ -54,8 +54,13 @@ struct TowerArgs {
 
 constexpr unsigned kSpinLimit = 1u << 22;    // x s_sleep(2): seconds, far above any tile time
 
+// waves per SIMD the register budget is sized for: 4 (128 VGPRs) for the one-
+// accumulator tiles; 2 (256 VGPRs, one workgroup per CU) for 128-wide N tiles
+template <int BN_>
+constexpr int tower_min_waves() { return BN_ >= 128 ? 2 : 4; }
+
 template <int C, int BN_, int WM_, int TM_, int NW_, int VAR = 0>
-__global__ __launch_bounds__(64 * NW_, 4) void conv_tower(const TowerArgs a)
+__global__ __launch_bounds__(64 * NW_, tower_min_waves<BN_>()) void conv_tower(const TowerArgs a)
 {
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
     constexpr int NTN = C / T::BN;
@@ -182,6 +187,10 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     case CC:                                                                               \
         if (shape == 8) return launch_tower_t<CC, 64, 4, 1, 8>(a, st, nullptr);    \
         return launch_tower_t<CC, 64, 2, 1, 4>(a, st, nullptr);
+    if (C == 128 && shape == 9) {   // 128x128 tiles, 2 accumulators per wave, LDS-DMA staging (A/B study)
+        if (g_tower_var == 5) return launch_tower_t<128, 128, 4, 1, 8, 5>(a, st, nullptr);
+        return launch_tower_t<128, 128, 4, 1, 8, 4>(a, st, nullptr);
+    }
     if (C == 128 && shape == 8 && g_tower_var != 0) {   // A/B variants (bitwise identical)
         if (g_tower_var == 3) return launch_tower_t<128, 64, 4, 1, 8, 3>(a, st, nullptr);
         if (g_tower_var == 1) return launch_tower_t<128, 64, 4, 1, 8, 1>(a, st, nullptr);

@@ -865,6 +865,8 @@ static inline int grid_for(int64_t total) { int64_t b = (total + 255) / 256; ret
         if (_e != hipSuccess) return set_error(what, _e); \
     } while (0)
 
+int g_wgrad_serial = 0;   // 1: conv weight grads on the caller's stream (A/B timing)
+
 template <int C>
 static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, const float* zs, int B,
                                 float* losses, hipStream_t st)
@@ -927,6 +929,14 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     bool pending[2] = {false, false};
     float* dzbuf[2] = {w->DZ, w->DZ2};
     auto wgrad = [&](int slot, const float* xin, int tensor) -> int32_t {
+        if (g_wgrad_serial) {   // A/B: weight grads on the caller's stream, no overlap
+            int pr = prof_begin(h, AZG_PROF_TRAIN_WGRAD, st);
+            const int rps = wgrad_rows_per_split(C, M);
+            AZG_CK(launch_wgrad(C, dzbuf[slot], xin, w->slab, G + h->poff[tensor], M, (M + rps - 1) / rps, rps, st),
+                   "train: wgrad");
+            prof_end(h, pr, st);
+            return 0;
+        }
         AZG_CK(hipEventRecord(w->ev_ready[slot], st), "train: event record");
         AZG_CK(hipStreamWaitEvent(w->side, w->ev_ready[slot], 0), "train: stream wait");
         int pr = prof_begin(h, AZG_PROF_TRAIN_WGRAD, w->side);

@@ -140,7 +140,11 @@ int32_t azg_pv_profile_read(azg_pv* h, double* ms, int64_t* launches);
  *   keys 3, 7, 8: timing-only ablation switches (results invalid while set);
  *   key 10: tile-body variant of the C=128 128x64 persistent tower (0 = default;
  *          1..5 = swizzle / prefetch / LDS-DMA staging variants for A/B timing, all
- *          bitwise identical to 0).  Every call returns the previous value. */
+ *          bitwise identical to 0);
+ *   key 9: stem kernel (1 = fp32 MFMA, default; 0 = VALU reference, bitwise equal);
+ *   key 11: stem ablation mask (timing only, results invalid while set);
+ *   key 12: train step conv weight grads (0 = overlapped on a side stream, default;
+ *          1 = on the caller's stream).  Every call returns the previous value. */
 int32_t azg_pv_set_tuning(int32_t key, int32_t value);
 
 /* Persistent-tower health: 0, or nonzero if a tile of the last eval forward on
