@@ -783,7 +783,7 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     }
     if (key == 10) {  // persistent-tower tile body variant (A/B studies, bitwise identical)
         const int prev = azg::g_tower_var;
-        if ((value >= 0 && value <= 5) || value == 8 || value == 12) azg::g_tower_var = value;
+        if ((value >= 0 && value <= 8) || value == 12) azg::g_tower_var = value;
         return prev;
     }
     if (key == 8) {   // persistent-tower ablation mask (timing studies only)

@@ -68,7 +68,7 @@ constexpr int halo_lds_bytes()
 {
     using T = ConvTile<C, BN, WM, TM, NW>;
     const int hrg = (halo_span(T::BM) + 7) / 8 * 8;
-    const int staging = (VAR & 4) ? (2 * hrg + 2 * BN) * T::BK * 4
+    const int staging = (VAR & 4) ? (2 * hrg + ((VAR & 2) ? 3 : 2) * BN) * T::BK * 4
                                   : ((halo_span(T::BM) + T::RPP - 1) / T::RPP * T::RPP + 2 * BN) * T::BK * 4;
     const int epilogue = T::BM * (BN + 8) * 4;
     return staging > epilogue ? staging : epilogue;
@@ -206,6 +206,13 @@ __device__ __forceinline__ void halo_mainloop_glds(const float* __restrict__ in,
     constexpr int NBW = (NBP + NW - 1) / NW;
     constexpr int NCHK = 9 * CG;
     constexpr bool VSWZ = (VAR & 1) != 0;
+    // PF2 (VAR bit 2): three weight buffers, chunk j+2 issued at the top of chunk j and
+    // kept in flight across the chunk-end barrier (raw s_barrier + counted vmcnt
+    // instead of __syncthreads, whose fence drains every DMA)
+    constexpr bool PF2 = (VAR & 2) != 0;
+    constexpr int NWB = PF2 ? 3 : 2;
+    constexpr int NPF = NP / NW;              // taps at which EVERY wave issues a halo piece
+    static_assert(!PF2 || NBP % NW == 0, "counted waits need the same weight pieces per wave");
     static_assert(NPW <= 9, "halo pieces are spread over the 9 taps");
     static_assert(BN % 8 == 0, "weight pieces");
 
@@ -246,7 +253,7 @@ __device__ __forceinline__ void halo_mainloop_glds(const float* __restrict__ in,
 #pragma unroll
         for (int i = 0; i < NBW; ++i) {
             const int p = wid + NW * i;
-            if (p < NBP) glds(wk + woff[i], Bs + (j & 1) * BN * BK + p * 8 * BK);
+            if (p < NBP) glds(wk + woff[i], Bs + (j % NWB) * BN * BK + p * 8 * BK);
         }
     };
 
@@ -268,10 +275,33 @@ __device__ __forceinline__ void halo_mainloop_glds(const float* __restrict__ in,
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+    // vmcnt(n) with n an unrolled-loop constant
+    auto wait_vm = [](int n) {
+        if (n <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (n == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        else if (n == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    };
+    auto raw_barrier = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" ::: "memory");
+    };
+    // halo pieces every wave issued at chunk k (the smaller count where waves differ:
+    // a conservative wait, never a short one)
+    auto hcount = [&](int k) { return (k >= 0 && k / 9 + 1 < CG && k % 9 < NPF) ? 1 : 0; };
+
 #pragma unroll
     for (int i = 0; i < NPW; ++i) hpiece(0, i);
     bchunk(0);
-    __syncthreads();
+    if (PF2) {
+        bchunk(1);
+        wait_vm(NBW);            // halo of group 0 and weights of chunk 0 have landed
+        raw_barrier();
+    } else {
+        __syncthreads();
+    }
 
 #pragma unroll
     for (int cg = 0; cg < CG; ++cg) {
@@ -286,7 +316,11 @@ __device__ __forceinline__ void halo_mainloop_glds(const float* __restrict__ in,
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
             const int j = cg * 9 + tap;
-            if (j + 1 < NCHK) bchunk(j + 1);
+            if (PF2) {
+                if (j + 2 < NCHK) bchunk(j + 2);
+            } else {
+                if (j + 1 < NCHK) bchunk(j + 1);
+            }
             if (cg + 1 < CG && tap < NPW) hpiece(cg + 1, tap);
             __builtin_amdgcn_sched_barrier(0);
             const int d = (tap / 3 - 1) * PADW + (tap % 3 - 1);
@@ -298,7 +332,7 @@ __device__ __forceinline__ void halo_mainloop_glds(const float* __restrict__ in,
                 arow[i] = r * BK;
                 aswz[i] = VSWZ ? ((vpix[i] + vd) >> 1) & 7 : (r >> 1) & 7;
             }
-            const float* Bb = Bs + (j & 1) * BN * BK;
+            const float* Bb = Bs + (j % NWB) * BN * BK;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 f32x4 a[TM], b[TN];
@@ -315,7 +349,14 @@ __device__ __forceinline__ void halo_mainloop_glds(const float* __restrict__ in,
                         for (int jn = 0; jn < TN; ++jn)
                             at[i][jn] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[jn][s], at[i][jn], 0, 0, 0);
             }
-            __syncthreads();
+            if (PF2) {
+                // retire weights(j+1) (and, in order, everything issued before it: the
+                // next group's halo pieces); what was issued after it may stay in flight
+                wait_vm(hcount(j - 1) + (j + 2 < NCHK ? NBW : 0) + hcount(j));
+                raw_barrier();
+            } else {
+                __syncthreads();
+            }
         }
 #pragma unroll
         for (int i = 0; i < TM; ++i)

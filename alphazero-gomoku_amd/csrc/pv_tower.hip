@@ -140,7 +140,7 @@ static hipError_t launch_tower_t(const TowerArgs& a, hipStream_t st, int* grid_o
 }
 
 int g_tower_ablation = 0;
-int g_tower_var = 0;     // halo_tile VAR of the 128x64 C=128 tower (0 = product; 1..5, 8, 12 A/B studies)
+int g_tower_var = 0;     // halo_tile VAR of the 128x64 C=128 tower (0 = product; 1..8, 12 A/B studies)
 int g_tower_shape = 8;   // forced shape when g_tower_mode == 1: 5 = 64x64 (4 waves), 8 = 128x64 (8 waves)
 
 size_t tower_sync_bytes(int nlayers, int M)
@@ -198,6 +198,8 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
         if (g_tower_var == 4) return launch_tower_t<128, 64, 4, 1, 8, 4>(a, st, nullptr);
         if (g_tower_var == 5) return launch_tower_t<128, 64, 4, 1, 8, 5>(a, st, nullptr);
         if (g_tower_var == 8) return launch_tower_t<128, 64, 4, 1, 8, 8>(a, st, nullptr);
+        if (g_tower_var == 6) return launch_tower_t<128, 64, 4, 1, 8, 6>(a, st, nullptr);
+        if (g_tower_var == 7) return launch_tower_t<128, 64, 4, 1, 8, 7>(a, st, nullptr);
         if (g_tower_var == 12) return launch_tower_t<128, 64, 4, 1, 8, 12>(a, st, nullptr);
     }
     switch (C) {

@@ -227,7 +227,7 @@ def test_persistent_tower_bitwise_equals_per_layer_launches(blocks, ch, batches)
                     assert torch.equal(p0, p1) and torch.equal(v0, v1), (B, shape, rep)
             if ch == 128:   # tile-body variants of the 128x64 tower: same arithmetic
                 lib.azg_pv_set_tuning(6, 8)
-                for var in (0, 1, 2, 3, 4, 5, 8, 12):
+                for var in (0, 1, 2, 3, 4, 5, 6, 7, 8, 12):
                     prev_var = lib.azg_pv_set_tuning(10, var)
                     p1, v1, l1 = eng.forward(x, want_logits=True)
                     lib.azg_pv_set_tuning(10, prev_var)
