@@ -766,6 +766,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         azg::g_conv_ablation = value;
         return prev;
     }
+    if (key == 13) {  // train: wgrad K chunk (32 default, 16 A/B)
+        const int prev = azg::g_wgrad_bk;
+        if (value == 16 || value == 32) azg::g_wgrad_bk = value;
+        return prev;
+    }
     if (key == 12) {  // train: conv weight grads on the caller's stream (1) or overlapped (0)
         const int prev = azg::g_wgrad_serial;
         azg::g_wgrad_serial = value ? 1 : 0;

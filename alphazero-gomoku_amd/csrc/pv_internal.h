@@ -38,6 +38,7 @@ extern int g_tower_shape;
 extern int g_tower_ablation;
 extern int g_tower_var;
 extern int g_wgrad_serial;
+extern int g_wgrad_bk;
 constexpr int kTowerMaxBlocks = 32;
 int conv_batch_bucket(int M);
 size_t tower_sync_bytes(int nlayers, int M);

@@ -12,10 +12,10 @@
 
 namespace azg {
 
-template <int C>
+template <int C, int BK_ = 32>
 struct WgTile {
     static constexpr int BT = C < 128 ? C : 128;    // tile edge (co and ci)
-    static constexpr int BK = 32;                   // pixels per chunk
+    static constexpr int BK = BK_;                  // pixels per chunk
     static constexpr int LD = BT + 4;
     static constexpr int W = BT / 2;                // per-wave edge (2x2 waves)
     static constexpr int T = W / 32;                // 32x32 MFMA tiles per wave edge
@@ -24,14 +24,14 @@ struct WgTile {
     static constexpr int LDS_BYTES = 2 * 2 * BK * LD * 4;
 };
 
-template <int C>
+template <int C, int BK_ = 32>
 __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_mfma(
     const float* __restrict__ dz,   // padded NHWC [B][17][17][C]  (A^T: co)
     const float* __restrict__ x,    // padded NHWC                 (B: ci)
     float* __restrict__ slab,       // [S][9][C][C] partial dW[tap][co][ci]
     int M, int rows_per_split)
 {
-    using T = WgTile<C>;
+    using T = WgTile<C, BK_>;
     constexpr int BT = T::BT, BK = T::BK, LD = T::LD, W = T::W, TT = T::T, LDF4 = T::LDF4, NT = T::NT;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* As = smem;                 // [2][BK][LD]  dz rows
@@ -99,10 +99,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_mfma(
         // keep the next chunk's global loads at the top of the chunk: without this
         // fence hipcc sinks them to just before their vmcnt wait (latency exposed)
         __builtin_amdgcn_sched_barrier(0);
-        const float* Ab = As + cur * BK * LD + (h * 16) * LD + wm * W + r32;
-        const float* Bb = Bs + cur * BK * LD + (h * 16) * LD + wn * W + r32;
+        const float* Ab = As + cur * BK * LD + (h * (BK / 2)) * LD + wm * W + r32;
+        const float* Bb = Bs + cur * BK * LD + (h * (BK / 2)) * LD + wn * W + r32;
 #pragma unroll
-        for (int s = 0; s < 16; ++s) {
+        for (int s = 0; s < BK / 2; ++s) {
             float a[TT], b[TT];
 #pragma unroll
             for (int i = 0; i < TT; ++i) a[i] = Ab[s * LD + i * 32];
@@ -159,20 +159,20 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     }
 }
 
-template <int C>
+template <int C, int BK = 32>
 static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, float* dw, int M, int S, int rps,
                                  hipStream_t st)
 {
-    using T = WgTile<C>;
+    using T = WgTile<C, BK>;
     static bool attr_done = false;
     if (!attr_done) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_wgrad_mfma<C>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_wgrad_mfma<C, BK>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS_BYTES);
         if (e != hipSuccess) return e;
         attr_done = true;
     }
     dim3 grid(S, 9 * T::NT * T::NT);
-    hipLaunchKernelGGL(conv3x3_wgrad_mfma<C>, grid, dim3(256), T::LDS_BYTES, st, dz, x, slab, M, rps);
+    hipLaunchKernelGGL((conv3x3_wgrad_mfma<C, BK>), grid, dim3(256), T::LDS_BYTES, st, dz, x, slab, M, rps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int total = 9 * C * C;
@@ -184,11 +184,13 @@ static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, f
 // Rows per split (multiple of 32, >= 256): minimise rounds-of-workgroups x chunks
 // per workgroup + the slab reduction (S slabs of 9*C*C floats re-read once).  The
 // old fixed 512 gave 57 x 9 = 513 workgroups at B = 128 on 512 slots: one extra round.
+int g_wgrad_bk = 32;   // pixels per K chunk of the wgrad tile (32 default; 16 = A/B study)
+
 int wgrad_rows_per_split(int C, int M)
 {
     const int bt = C < 128 ? C : 128;
     const int tiles = 9 * (C / bt) * (C / bt);
-    const int lds = 2 * 2 * 32 * (bt + 4) * 4;
+    const int lds = 2 * 2 * g_wgrad_bk * (bt + 4) * 4;
     const int slots = 256 * (160 * 1024 / lds);
     const double chunk_us = 5.4 * (bt / 128.0) * (bt / 128.0) * (160.0 * 1024 / lds) / 2.0;
     const double red_us = 9.0 * C * C * 4 / 4.0e6;     // one slab at ~4 TB/s
@@ -210,7 +212,9 @@ hipError_t launch_wgrad(int C, const float* dz, const float* x, float* slab, flo
 {
     switch (C) {
         case 64: return launch_wgrad_t<64>(dz, x, slab, dw, M, S, rps, st);
-        case 128: return launch_wgrad_t<128>(dz, x, slab, dw, M, S, rps, st);
+        case 128:
+            if (g_wgrad_bk == 16) return launch_wgrad_t<128, 16>(dz, x, slab, dw, M, S, rps, st);
+            return launch_wgrad_t<128>(dz, x, slab, dw, M, S, rps, st);
         case 256: return launch_wgrad_t<256>(dz, x, slab, dw, M, S, rps, st);
         default: return hipErrorInvalidValue;
     }

@@ -144,7 +144,9 @@ int32_t azg_pv_profile_read(azg_pv* h, double* ms, int64_t* launches);
  *   key 9: stem kernel (1 = fp32 MFMA, default; 0 = VALU reference, bitwise equal);
  *   key 11: stem ablation mask (timing only, results invalid while set);
  *   key 12: train step conv weight grads (0 = overlapped on a side stream, default;
- *          1 = on the caller's stream).  Every call returns the previous value. */
+ *          1 = on the caller's stream);
+ *   key 13: train wgrad K chunk in pixels (32 default; 16 for A/B timing, C=128).
+ *   Every call returns the previous value. */
 int32_t azg_pv_set_tuning(int32_t key, int32_t value);
 
 /* Persistent-tower health: 0, or nonzero if a tile of the last eval forward on
