@@ -39,8 +39,11 @@ _SIGS = {
                                             _P, _P]),
     "azg_pv_profile_enable": (ctypes.c_int32, [_P, ctypes.c_int32]),
     "azg_pv_profile_read": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
+    "azg_pv_profile_boards": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_int64)]),
     "azg_pv_set_tuning": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32]),
     "azg_pv_tower_status": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_void_p]),
+    "azg_pv_status": (ctypes.c_int32, [_P]),
+    "azg_pv_clear_status": (ctypes.c_int32, [_P]),
     "azg_pv_debug_copy": (ctypes.c_int32, [_P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32, _P]),
 }
 EXPORTS = tuple(_SIGS)

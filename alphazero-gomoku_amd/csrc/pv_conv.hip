@@ -470,12 +470,17 @@ static hipError_t launch_conv_epi(int epi, const float* in, const float* wp, con
             default: return launch_halo_t<C, BN, WM, TM, NW, EPI_RAW>(in, wp, scale, shift, resid, out, M, st);
         }
     }
+#ifdef AZG_AB_STUDIES
+    // per-chunk A staging / single-buffer tiles: A/B timing studies only
     switch (epi) {
         case EPI_BN_RELU: return launch_conv_t<C, BN, WM, TM, NW, EPI_BN_RELU, SB>(in, wp, scale, shift, resid, out, M, st);
         case EPI_BN_RES_RELU: return launch_conv_t<C, BN, WM, TM, NW, EPI_BN_RES_RELU, SB>(in, wp, scale, shift, resid, out, M, st);
         case EPI_ADD: return launch_conv_t<C, BN, WM, TM, NW, EPI_ADD, SB>(in, wp, scale, shift, resid, out, M, st);
         default: return launch_conv_t<C, BN, WM, TM, NW, EPI_RAW, SB>(in, wp, scale, shift, resid, out, M, st);
     }
+#else
+    return hipErrorInvalidValue;   // built without AZG_AB_STUDIES (make study)
+#endif
 }
 
 // Tile shapes {BM, BN}: index into the switch below.
@@ -521,6 +526,14 @@ int pick_conv_tile(int C, int M)
 hipError_t launch_conv3x3_shape(int shape, int C, int epi, const float* in, const float* wp, const float* scale,
                                 const float* shift, const float* resid, float* out, int M, hipStream_t st)
 {
+#ifdef AZG_AB_STUDIES
+#define AZG_SB_SHAPES(CC)                                                                                       \
+        case 10: return launch_conv_epi<CC, 64, 2, 1, 4, 1>(epi, in, wp, scale, shift, resid, out, M, st);      \
+        case 11: return launch_conv_epi<CC, 64, 2, 2, 4, 1>(epi, in, wp, scale, shift, resid, out, M, st);      \
+        case 12: return launch_conv_epi<CC, 128, 2, 1, 4, 1>(epi, in, wp, scale, shift, resid, out, M, st);
+#else
+#define AZG_SB_SHAPES(CC)
+#endif
 #define AZG_SHAPES(CC)                                                                                          \
     switch (shape) {                                                                                            \
         case 0: return launch_conv_epi<CC, (CC < 128 ? CC : 128), 2, 2>(epi, in, wp, scale, shift, resid, out, M, st); \
@@ -533,9 +546,7 @@ hipError_t launch_conv3x3_shape(int shape, int C, int epi, const float* in, cons
         case 7: return launch_conv_epi<CC, 128, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);         \
         case 8: return launch_conv_epi<CC, 64, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);          \
         case 9: return launch_conv_epi<CC, 128, 2, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);         \
-        case 10: return launch_conv_epi<CC, 64, 2, 1, 4, 1>(epi, in, wp, scale, shift, resid, out, M, st);      \
-        case 11: return launch_conv_epi<CC, 64, 2, 2, 4, 1>(epi, in, wp, scale, shift, resid, out, M, st);      \
-        case 12: return launch_conv_epi<CC, 128, 2, 1, 4, 1>(epi, in, wp, scale, shift, resid, out, M, st);     \
+        AZG_SB_SHAPES(CC)                                                                                       \
         default: return hipErrorInvalidValue;                                                                   \
     }
     switch (C) {
@@ -545,8 +556,10 @@ hipError_t launch_conv3x3_shape(int shape, int C, int epi, const float* in, cons
                 case 5: return launch_conv_epi<64, 64, 2, 1>(epi, in, wp, scale, shift, resid, out, M, st);
                 case 4: return launch_conv_epi<64, 64, 2, 2>(epi, in, wp, scale, shift, resid, out, M, st);
                 case 8: return launch_conv_epi<64, 64, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);
+#ifdef AZG_AB_STUDIES
                 case 10: return launch_conv_epi<64, 64, 2, 1, 4, 1>(epi, in, wp, scale, shift, resid, out, M, st);
                 case 11: return launch_conv_epi<64, 64, 2, 2, 4, 1>(epi, in, wp, scale, shift, resid, out, M, st);
+#endif
                 default: return hipErrorInvalidValue;
             }
         case 128: AZG_SHAPES(128)
@@ -554,6 +567,7 @@ hipError_t launch_conv3x3_shape(int shape, int C, int epi, const float* in, cons
         default: return hipErrorInvalidValue;
     }
 #undef AZG_SHAPES
+#undef AZG_SB_SHAPES
 }
 
 int g_conv_shape_override = -1;
@@ -564,6 +578,7 @@ int g_conv_ablation = 0;
 // 128x64 8 waves per g_ablation_shape; C = 128, EPI_BN_RELU launches only)
 int g_ablation_shape = 5;
 
+#ifdef AZG_AB_STUDIES
 template <int ABL, int BN, int WM, int TM, int NW>
 static hipError_t launch_ablation_s(const float* in, const float* wp, const float* scale, const float* shift,
                                     const float* resid, float* out, int M, hipStream_t st)
@@ -596,6 +611,7 @@ static hipError_t launch_ablated(const float* in, const float* wp, const float* 
         default: return launch_ablation<0>(in, wp, scale, shift, resid, out, M, st);
     }
 }
+#endif
 
 // Autotune: the first launch for a (C, M) times every valid shape twice on the
 // real operands (each launch fully rewrites `out`, so this is idempotent) and
@@ -672,8 +688,10 @@ static int autotune_shape(int C, int epi, const float* in, const float* wp, cons
 hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, const float* scale,
                           const float* shift, const float* resid, float* out, int M, hipStream_t st)
 {
+#ifdef AZG_AB_STUDIES
     if (g_conv_ablation > 0 && C == 128 && epi == EPI_BN_RELU)
         return launch_ablated(in, wp, scale, shift, resid, out, M, st);
+#endif
     int shape = -1;
     if (g_conv_shape_override >= 0 && shape_ok(g_conv_shape_override, C)) {
         shape = g_conv_shape_override;
@@ -711,6 +729,7 @@ hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const fl
         const int M = B * PIX;
         const int cw = C < STEM_CW ? C : STEM_CW;
         const dim3 grid((M + 127) / 128, C / cw);
+#ifdef AZG_AB_STUDIES
         if (g_stem_ablation && C == 128 && !boards && epi == EPI_BN_RELU) {
 #define AZG_STEM_ABL(A) \
     if (g_stem_ablation == A) hipLaunchKernelGGL((stem_mfma<128, EPI_BN_RELU, false, A>), grid, dim3(256), 0, st, x, boards, players, ws, scale, shift, out, M);
@@ -718,6 +737,7 @@ hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const fl
 #undef AZG_STEM_ABL
             return hipGetLastError();
         }
+#endif
 #define AZG_STEM_MFMA(CC)                                                                                       \
     case CC:                                                                                                    \
         if (boards) hipLaunchKernelGGL((stem_mfma<CC, EPI_BN_RELU, true>), grid, dim3(256), 0, st, x, boards, players, ws, scale, shift, out, M); \
@@ -766,6 +786,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         azg::g_conv_ablation = value;
         return prev;
     }
+    if (key == 14) {  // tests: persistent-tower dependency spin bound (-1 restores the default)
+        const int prev = (int)azg::g_tower_spin_limit;
+        azg::g_tower_spin_limit = value < 0 ? (1u << 22) : (unsigned)value;
+        return prev;
+    }
     if (key == 13) {  // train: wgrad K chunk (32 default, 16 A/B)
         const int prev = azg::g_wgrad_bk;
         if (value == 16 || value == 32) azg::g_wgrad_bk = value;
@@ -788,7 +813,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     }
     if (key == 10) {  // persistent-tower tile body variant (A/B studies, bitwise identical)
         const int prev = azg::g_tower_var;
+#ifdef AZG_AB_STUDIES
         if ((value >= 0 && value <= 8) || value == 12) azg::g_tower_var = value;
+#else
+        if (value == 0) azg::g_tower_var = value;
+#endif
         return prev;
     }
     if (key == 8) {   // persistent-tower ablation mask (timing studies only)
@@ -808,13 +837,23 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     }
     if (key == 6) {   // persistent tower tile shape
         const int prev = azg::g_tower_shape;
-        if (value == 5 || value == 8 || value == 9) azg::g_tower_shape = value;
+        if (value == 5 || value == 8) azg::g_tower_shape = value;
+#ifdef AZG_AB_STUDIES
+        if (value == 9) azg::g_tower_shape = value;
+#endif
         return prev;
     }
     if (key == 4) {   // conv kernel variant (1 halo-staged, 0 per-chunk staging; timing studies)
         const int prev = azg::g_conv_variant;
         azg::g_conv_variant = value;
         return prev;
+    }
+    if (key == 15) {  // query: 1 if built with the A/B study variants (make study)
+#ifdef AZG_AB_STUDIES
+        return 1;
+#else
+        return 0;
+#endif
     }
     if (key == 2) {   // query: tuned shape for (C, M) packed as value = M*1024 + C
         return azg::conv_tuned_shape(value & 1023, value >> 10);

@@ -43,8 +43,9 @@ constexpr int kTowerMaxBlocks = 32;
 int conv_batch_bucket(int M);
 size_t tower_sync_bytes(int nlayers, int M);
 hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const float* wpack, const float* scale,
-                        const float* shift, const int* out_off, int M, unsigned* sync, hipStream_t st,
-                        float** result);
+                        const float* shift, const int* out_off, int M, unsigned* sync, unsigned* status,
+                        hipStream_t st, float** result);
+extern unsigned g_tower_spin_limit;
 hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const float* scale,
                        const float* shift, float* out, int B, hipStream_t st, const int8_t* boards = nullptr,
                        const int8_t* players = nullptr);
@@ -104,6 +105,8 @@ struct azg_pv {
     float* act[3] = {nullptr, nullptr, nullptr};
     float* hbuf = nullptr;
     unsigned* tower_sync = nullptr;   // persistent tower: work counter, error word, tile counters
+    unsigned* status_host = nullptr;  // sticky status word, pinned + mapped (kernels write it, azg_pv_status reads)
+    unsigned* status_dev = nullptr;   // device alias of status_host
     int act_cap = 0;
 
     // train workspace (pv_train.hip)
@@ -116,6 +119,7 @@ struct azg_pv {
     int prof_used = 0;
     double prof_ms[AZG_PROF_NCLASS] = {};
     int64_t prof_n[AZG_PROF_NCLASS] = {};
+    int64_t prof_work[AZG_PROF_NCLASS] = {};   // boards (or samples) processed per class
 };
 
 namespace azg {
@@ -125,7 +129,8 @@ void free_workspace(azg_pv* h);
 void free_train_workspace(azg_pv* h);
 int32_t ensure_eval_workspace(azg_pv* h, int batch, hipStream_t st);
 int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst = nullptr);   // dgrad_dst: also pack dgrad weights
-int prof_begin(azg_pv* h, int cls, hipStream_t st);   // returns pair index or -1
+int prof_begin(azg_pv* h, int cls, hipStream_t st, int64_t boards = 0);   // returns pair index or -1
+hipError_t prof_harvest(azg_pv* h);
 void prof_end(azg_pv* h, int pair, hipStream_t st);
 int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* values, float* logits,
                      hipStream_t st, const int8_t* boards, const int8_t* players, float* priors);

@@ -48,11 +48,14 @@ struct TowerArgs {
     int M;
     int act_bytes;       // bytes of one activation buffer (buffer descriptor range)
     unsigned* sync;      // [0] work counter, [1] error word, [4..] per-(layer, M tile) counters
+    unsigned* status;    // sticky host-mapped status word of the handle (azg_pv_status); may be null
+    unsigned spin_limit; // polls before a dependency wait is declared timed out
     int abl;             // timing studies only (0 in the product; results not valid otherwise):
                          // bit 1 skips the dependency wait + acquire, bit 2 the publish drain
 };
 
 constexpr unsigned kSpinLimit = 1u << 22;    // x s_sleep(2): seconds, far above any tile time
+unsigned g_tower_spin_limit = kSpinLimit;    // tuning key 14 (tests: 0 forces the timeout path)
 
 // waves per SIMD the register budget is sized for: 4 (128 VGPRs) for the one-
 // accumulator tiles; 2 (256 VGPRs, one workgroup per CU) for 128-wide N tiles
@@ -91,9 +94,15 @@ __global__ __launch_bounds__(64 * NW_, tower_min_waves<BN_>()) void conv_tower(c
                 const int j0 = max(mt - 1, 0), j1 = min(mt + 1, mtiles - 1);
                 for (int j = j0; j <= j1; ++j) {
                     unsigned spins = 0;
-                    while (__hip_atomic_load(c + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)NTN) {
-                        if (++spins > kSpinLimit) {
+                    // spin_limit 0 (tuning key 14, tests only) forces the timeout path
+                    while (a.spin_limit == 0 ||
+                           __hip_atomic_load(c + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)NTN) {
+                        if (++spins > a.spin_limit) {
+                            // the tile computes on stale inputs: flag the launch and the
+                            // handle (sticky, host-visible: the product raises on it)
                             __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (a.status)
+                                __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                             break;
                         }
                         __builtin_amdgcn_s_sleep(2);
@@ -154,8 +163,8 @@ size_t tower_sync_bytes(int nlayers, int M)
 // (act[0] holds the stem output; the result ends in act[0] or act[2], returned in
 // *result).  `sync` must hold tower_sync_bytes(2*NB, M) bytes.
 hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const float* wpack, const float* scale,
-                        const float* shift, const int* out_off, int M, unsigned* sync, hipStream_t st,
-                        float** result)
+                        const float* shift, const int* out_off, int M, unsigned* sync, unsigned* status,
+                        hipStream_t st, float** result)
 {
     if (2 * NB > kTowerMaxLayers) return hipErrorInvalidValue;
     const size_t act_bytes = (size_t)(M / PIX) * PADPIX * C * sizeof(float);
@@ -165,6 +174,8 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     a.M = M;
     a.act_bytes = (int)act_bytes;
     a.sync = sync;
+    a.status = status;
+    a.spin_limit = g_tower_spin_limit;
     a.abl = g_tower_ablation;
     float* X = act[0];
     float* H = act[1];
@@ -187,6 +198,7 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     case CC:                                                                               \
         if (shape == 8) return launch_tower_t<CC, 64, 4, 1, 8>(a, st, nullptr);    \
         return launch_tower_t<CC, 64, 2, 1, 4>(a, st, nullptr);
+#ifdef AZG_AB_STUDIES   // A/B tile-body variants and the 128x128 shape (make study)
     if (C == 128 && shape == 9) {   // 128x128 tiles, 2 accumulators per wave, LDS-DMA staging (A/B study)
         if (g_tower_var == 5) return launch_tower_t<128, 128, 4, 1, 8, 5>(a, st, nullptr);
         return launch_tower_t<128, 128, 4, 1, 8, 4>(a, st, nullptr);
@@ -202,6 +214,7 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
         if (g_tower_var == 7) return launch_tower_t<128, 64, 4, 1, 8, 7>(a, st, nullptr);
         if (g_tower_var == 12) return launch_tower_t<128, 64, 4, 1, 8, 12>(a, st, nullptr);
     }
+#endif
     switch (C) {
         AZG_TOWER_C(64)
         AZG_TOWER_C(128)

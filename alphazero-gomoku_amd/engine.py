@@ -96,6 +96,18 @@ class PolicyValueEngine:
     def mark_dirty(self):
         check(self.lib.azg_pv_mark_dirty(self.h), self.lib)
 
+    def check_status(self):
+        """Raise if any forward on this handle computed on stale inputs (sticky
+        device status, include/azg_pv.h azg_pv_status).  A plain host load: call it
+        after synchronising with the forwards it should cover."""
+        s = int(self.lib.azg_pv_status(self.h))
+        if s:
+            raise RuntimeError(f"libazg_pv: persistent residual tower timed out waiting for its inputs "
+                               f"(status {s}); the outputs of the affected forward are invalid")
+
+    def clear_status(self):
+        check(self.lib.azg_pv_clear_status(self.h), self.lib)
+
     def reattach_grads(self):
         for p, g in zip(self.params, self.grad_views):
             if p.grad is None or p.grad.data_ptr() != g.data_ptr():
@@ -175,3 +187,10 @@ class PolicyValueEngine:
         n = (ctypes.c_int64 * 8)()
         check(self.lib.azg_pv_profile_read(self.h, ms, n), self.lib)
         return {PROF_CLASSES[i]: (ms[i], int(n[i])) for i in range(8) if n[i]}
+
+    def profile_boards(self) -> dict:
+        """{class: boards processed} since the last profile_enable."""
+        from _native import PROF_CLASSES
+        b = (ctypes.c_int64 * 8)()
+        check(self.lib.azg_pv_profile_boards(self.h, b), self.lib)
+        return {PROF_CLASSES[i]: int(b[i]) for i in range(8) if b[i]}

@@ -161,13 +161,17 @@ class NativeSelfPlay:
                 self.evals.append(_BoardsAdapter(evaluator_factory((hi - lo) * batch_size), f))
         self.forest = self.forests[0]
         self.boards = self.forwards = self.max_batch = 0
+        self.moves = self.rounds = 0
+        self.game_lengths: List[int] = []
         self.nn_seconds = self.search_seconds = 0.0
 
     def play(self, temp_fn: Callable[[int], float], max_moves: int = 225, use_symmetries: bool = True,
-             seeds: Optional[Sequence[int]] = None, games: Optional[list] = None):
+             seeds: Optional[Sequence[int]] = None, games: Optional[list] = None,
+             progress: Optional[Callable[[int], None]] = None):
         """Play one game per slot to the end; returns [(examples, winner)] in slot
         order.  ``seeds`` seed each game's RandomState (default: drawn from numpy's
-        global RNG); ``games`` optionally gives the starting positions."""
+        global RNG); ``games`` optionally gives the starting positions; ``progress``
+        (optional) is called with the number of live games once per round."""
         from selfplay import sample_action_from_pi
         G = self.n_games
         if seeds is None:
@@ -191,6 +195,8 @@ class NativeSelfPlay:
             live[k] = hi - lo
         pending = [False] * len(self.forests)
         while any(live) or any(pending):
+            if progress is not None:
+                progress(sum(live))
             for k, (lo, hi) in enumerate(self.slices):
                 f, ev = self.forests[k], self.evals[k]
                 t0 = time.perf_counter()
@@ -222,8 +228,10 @@ class NativeSelfPlay:
                     hist[g].append((state_enc, pi.copy(), int(game.current_player)))
                     game.do_move(divmod(action, game.size))
                     moves[g] += 1
+                    self.moves += 1
                     if game.is_game_over() or moves[g] >= max_moves:
                         results[g] = self._finish(hist[g], game.get_winner(), use_symmetries)
+                        self.game_lengths.append(moves[g])
                         live[k] -= 1
                     else:
                         f.set_root(i, game, len(game.move_history))
@@ -236,6 +244,7 @@ class NativeSelfPlay:
                     self.boards += n
                     self.forwards += 1
                     self.max_batch = max(self.max_batch, n)
+        self.rounds = max(self.rounds, max(moves) if moves else 0)
         return results
 
     @staticmethod

@@ -219,6 +219,7 @@ class BoardEvaluator:
         """-> (priors [n,225], values [n,1]) numpy views of the pinned buffers."""
         if self.n:
             self.event.synchronize()
+            self.model.engine.check_status()
         return self.h_priors.numpy()[:self.n], self.h_values.numpy()[:self.n]
 
 
@@ -259,10 +260,14 @@ class PyTorchModel:
         running stats; the module's train/eval flag is left as it was."""
         x = torch.from_numpy(np.ascontiguousarray(encoded_states, dtype=np.float32))
         probs, values = self.predict_device(x)
-        return probs.cpu().numpy(), values.cpu().numpy()
+        out = probs.cpu().numpy(), values.cpu().numpy()
+        self.engine.check_status()
+        return out
 
     def predict_device(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Device-resident predict: x [B,3,15,15] -> (probs, values) on the GPU."""
+        """Device-resident predict: x [B,3,15,15] -> (probs, values) on the GPU.
+        Asynchronous: the sticky tower status (engine.check_status) is checked by
+        the next host-synchronising call (predict, predict_boards, evaluator wait)."""
         probs, values, _ = self.engine.forward(x)
         return probs, values
 
@@ -280,7 +285,9 @@ class PyTorchModel:
         values = torch.empty((B, 1), dtype=torch.float32, device=eng.device)
         priors = torch.empty_like(probs) if masked else None
         eng.forward_boards_into(b, pl, probs, values, priors)
-        return (priors if masked else probs).cpu().numpy(), values.cpu().numpy()
+        out = (priors if masked else probs).cpu().numpy(), values.cpu().numpy()
+        eng.check_status()
+        return out
 
     def board_evaluator(self, capacity: int) -> "BoardEvaluator":
         return BoardEvaluator(self, capacity)

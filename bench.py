@@ -1,27 +1,40 @@
-"""Benchmark: BASELINE.json configs[1] -- batch-512 policy/value forward of the
-6-block/128-filter ResNet on synthetic legal 15x15 positions, one MI355X per rank.
+"""Benchmark: BASELINE.json's metric -- self-play boards/s on 15x15 Gomoku with the
+6-block/128-filter ResNet at 400 sims/move (configs[2]: 256 concurrent games per
+GPU), every game played to its end, one MI355X per rank.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
 N>1 is launched by the driver as torchrun (one process per GPU, RCCL).  Self-play
-leaf evaluation shards by game, so every rank runs its own independent batches
-(weak scaling, no collective in the timed region).  A step = one forward of 512
-boards already resident in HBM.  Prints ONE JSON line on rank 0 with a live
-`roofline` for the dominant kernel (the fused 3x3 conv, timed by hipEvents on its
-own stream over the timed region) and a bounded `cpu_baseline` (the CPU oracle,
-i.e. the reference's PyTorch-CPU algorithm, timed on this host).
+shards by game: every rank plays its own 256 games (weak scaling, no collective
+inside the timed region); value = leaf boards summed over ranks / max wall time.
 
-After the timed forward loop, a `selfplay` object reports BASELINE configs[2] end to
-end on every rank: 256 concurrent games x 400 simulations/move through the native
-C++ search (int8 leaves, on-GPU encoding, search of one half of the games overlapped
-with the forward of the other), for --sp-moves moves per game; leaf boards summed over
-ranks / max wall time over ranks (weak scaling, no collective inside).
+Headline (`value`): one self-play generation as train.py plays it
+(train.py:360-412 per game, __main__ settings train.py:847-889: cpuct 1.0,
+Dirichlet alpha 0.05 / eps 0.15 on the first 10 moves, temperature max(0, 1 - n/10),
+8-fold symmetry augmentation, max_moves 225), through the native C++ search and
+the batched HIP forward.  Every game runs until is_game_over(); the run ends when
+the last game does, so the shrinking batches of the tail are inside the timed
+region.  A "step" is one move round (every live game makes one move, 400
+simulations); `steps` is the number of rounds the generation took (its longest
+game), NOT --steps: the workload is fixed by the config, --steps K / --warmup W
+size the configs[1] forward sub-leg.  `roofline` is the persistent residual tower
+(`conv_tower`, the dominant kernel) over its launches INSIDE the self-play run:
+algorithmic FLOPs of the boards each launch evaluated / hipEvent device time of
+those launches on the stream they ran on.
+
+Sub-legs (extra keys): `forward_b512` (configs[1]: K forwards of 512 boards in HBM,
+own roofline), `train` (configs[3] train step, 6x128, B=128/GPU, RCCL all-reduce
+at N>1), `pente_10x256` (configs[4]: Pente self-play with the 10x256 net at 800
+sims for a stated move window, its 10x256 forward at B=512 and train step at
+B=128), and `cpu_baseline` (rank 0 at N=1: the reference CPU path, i.e. the oracle
+restatement of network.py + the reference-semantics Python MCTS, on this host).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -35,9 +48,33 @@ import torch
 
 METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
 BLOCKS, CHANNELS, BATCH = 6, 128, 512
-FLOP_CONV = 2 * 225 * CHANNELS * 9 * CHANNELS            # per board per 3x3 res conv = 66,355,200
-FLOP_BOARD = 798_221_828                                 # whole forward, SURVEY §8(d)
 PEAK_F32_MFMA = 157.3e12                                 # MI355X_MICROARCH.md: FP32 matrix peak
+
+
+def conv_flop(ch: int) -> int:
+    """One 3x3 C->C conv on one 15x15 board: 2 * 225 * C * 9C."""
+    return 2 * 225 * ch * 9 * ch
+
+
+def fwd_flop(blocks: int, ch: int) -> int:
+    """Whole eval forward per board (6x128 = 798,221,828)."""
+    stem = 2 * 225 * ch * 27
+    heads = 2 * 225 * ch * 3 + 2 * 450 * 225 + 2 * 225 * 64 + 2 * 64
+    return stem + 2 * blocks * conv_flop(ch) + heads
+
+
+def train_flop(blocks: int, ch: int) -> int:
+    """Train step per sample: forward + data grads + weight grads = 3x forward minus
+    the stem's data grad (not needed): 6x128 = 2,393 MFLOP."""
+    return 3 * fwd_flop(blocks, ch) - 2 * 225 * ch * 27
+
+
+# selfplay settings of the reference's __main__ (train.py:847-889)
+SP_CPUCT, SP_ALPHA, SP_EPS, SP_NOISE_MOVES, SP_TEMP_THRESHOLD = 1.0, 0.05, 0.15, 10, 10
+
+
+def sp_temp(n: int) -> float:
+    return max(0.0, 1.0 - n / SP_TEMP_THRESHOLD)      # train.py:647-648
 
 
 def dist_setup(n_gpus: int):
@@ -58,6 +95,19 @@ def barrier_sync(dist, local):
     torch.cuda.synchronize()
 
 
+def reduce_(dist, dev, vals, op="sum"):
+    """Sum (or max) a list of floats over ranks."""
+    v = torch.tensor(vals, dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(v, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
+    return [float(a) for a in v.tolist()]
+
+
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+# --------------------------------------------------------------------- CPU host
 def _cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -65,143 +115,311 @@ def _cpu_model() -> str:
                 return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return "unknown"
+    return platform.processor() or "unknown"
 
 
-def cpu_baseline(seconds: float = 12.0) -> dict:
-    """Oracle (PyTorch-CPU restatement of reference network.py) timed on this host:
-    batches of 64 boards, ~2/3 of `seconds` at up to 16 threads (the reported value)
-    and ~1/3 single-threaded (1 thread and all cores)."""
-    from oracle.boards import encode_batch, synth_positions
+def host_cores() -> dict:
+    """CPUs this process may run on: affinity mask, cgroup CPU quota, physical cores."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    phys = set()
+    try:
+        cur = {}
+        for line in open("/proc/cpuinfo"):
+            if ":" in line:
+                k, v = (t.strip() for t in line.split(":", 1))
+                cur[k] = v
+            elif cur:
+                if "physical id" in cur and "core id" in cur:
+                    phys.add((cur["physical id"], cur["core id"]))
+                cur = {}
+    except OSError:
+        pass
+    usable = min(aff, quota) if quota else aff
+    if phys:
+        usable = min(usable, len(phys))      # physical cores, not SMT siblings
+    return {"affinity_cpus": aff, "cgroup_quota_cpus": quota, "physical_cores": len(phys) or None,
+            "threads_used": usable, "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count()}
+
+
+def cpu_baseline(game_seconds: float) -> dict:
+    """The reference CPU path on this host (BASELINE.md:50-59), rank 0 at N=1:
+      * configs[0]: 1 self-play game, 100 sims/move, 6x128, the oracle's predict
+        (oracle/ref_net.py = reference network.py:168-183 restated, PyTorch CPU) driven
+        by the reference-semantics Python MCTS (mcts/new_mcts_alpha.py, bit-exact vs
+        the reference goldens) at its batch of <= 32 leaves, __main__ settings; played
+        to game end or until `game_seconds` of wall time (stated in `sample`);
+      * the B=512 forward (configs[1]) and a B=128 train_batch (configs[3] train half);
+    each at 1 thread and at all usable physical cores."""
+    from games.gomoku import Gomoku
+    from mcts.new_mcts_alpha import MCTS
+    from oracle.boards import encode_batch, synth_positions, synth_targets
     from oracle.ref_net import RefModel
+    from selfplay import sample_action_from_pi
 
-    def timed(threads, budget):
-        torch.set_num_threads(threads)
-        n = 0
-        ref.predict(x)                   # warm-up at this thread count
-        t0 = time.perf_counter()
-        while time.perf_counter() - t0 < budget:
-            ref.predict(x)
-            n += 64
-        return n, time.perf_counter() - t0
-
-    threads = max(1, min(16, os.cpu_count() or 1))
+    cores = host_cores()
+    nthr = cores["threads_used"]
     torch.manual_seed(0)
     ref = RefModel(BLOCKS, CHANNELS)
-    b, p = synth_positions(64, seed=99)
-    x = encode_batch(b, p)
-    n, dt = timed(threads, seconds * 2 / 3)
-    n1, dt1 = timed(1, seconds / 3)
-    return {"value": round(n / dt, 2), "unit": "boards/s", "cores": threads, "kind": "port",
-            "sample": f"{n} boards as {n // 64} predict() batches of 64, 6x128, torch-CPU oracle "
-                      f"(oracle/ref_net.py = reference network.py:168-183 restated), {dt:.1f}s, "
-                      f"{threads} threads",
-            "value_1_thread": round(n1 / dt1, 2), "cpu_model": _cpu_model(),
-            "host_cpus_visible": os.cpu_count()}
+
+    class Counting:
+        boards = 0
+
+        def predict(self, x):
+            Counting.boards += len(x)
+            return ref.predict(x)
+
+    def game(threads):
+        torch.set_num_threads(threads)
+        np.random.seed(0)
+        Counting.boards = 0
+        mcts = MCTS(Gomoku, 100, Counting(), cpuct=SP_CPUCT, dirichlet_alpha=SP_ALPHA, epsilon=SP_EPS,
+                    apply_dirichlet_n_first_moves=SP_NOISE_MOVES, add_dirichlet_noise=True)
+        g = Gomoku(size=15)
+        g.current_player = 1
+        moves, t0 = 0, time.perf_counter()
+        while True:                                 # train.py:369-393
+            pi = mcts.run(g, len(g.move_history))
+            a = sample_action_from_pi(pi, sp_temp(moves))
+            if g.get_valid_moves()[a] != 1.0:
+                a = int(np.argmax(pi))
+            g.do_move(divmod(a, 15))
+            moves += 1
+            if g.is_game_over() or moves >= 225:
+                ended = True
+                break
+            if time.perf_counter() - t0 > game_seconds:
+                ended = False
+                break
+        dt = time.perf_counter() - t0
+        return {"boards_per_s": round(Counting.boards / dt, 1), "moves_per_s": round(moves / dt, 3),
+                "moves": moves, "boards": Counting.boards, "seconds": round(dt, 2), "game_over": ended}
+
+    def forward(threads, reps):
+        torch.set_num_threads(threads)
+        b, p = synth_positions(BATCH, seed=99)
+        x = encode_batch(b, p)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ref.predict(x)
+        return round(BATCH * reps / (time.perf_counter() - t0), 1)
+
+    def train(threads, reps):
+        torch.set_num_threads(threads)
+        b, p = synth_positions(128, seed=98)
+        x = encode_batch(b, p)
+        pi, z = synth_targets(128, seed=97)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ref.train_batch(x, pi, z)
+        return round(128 * reps / (time.perf_counter() - t0), 1)
+
+    out = {}
+    g_all = game(nthr)
+    g_one = game(1)
+    forward(nthr, 1)                                # warm the allocator / weights in cache
+    fwd_all, fwd_one = forward(nthr, 3), forward(1, 1)
+    trn_all, trn_one = train(nthr, 3), train(1, 1)
+    torch.set_num_threads(nthr)
+    out.update({
+        "value": g_all["boards_per_s"], "unit": "boards/s", "cores": nthr, "kind": "port",
+        "sample": (f"configs[0]: 1 self-play game, 100 sims/move, 6x128, torch-CPU oracle predict (reference "
+                   f"network.py:168-183 restated) under the reference-semantics Python MCTS (batch <= 32), "
+                   f"{g_all['moves']} moves / {g_all['boards']} leaf boards in {g_all['seconds']} s at {nthr} "
+                   f"threads ({'to game end' if g_all['game_over'] else 'stopped at the time bound'})"),
+        "configs0_game": {"threads_all": g_all, "threads_1": g_one},
+        "forward_b512_boards_per_s": {"threads_all": fwd_all, "threads_1": fwd_one},
+        "train_b128_samples_per_s": {"threads_all": trn_all, "threads_1": trn_one},
+        "value_1_thread": g_one["boards_per_s"],
+        "host": cores,
+    })
+    return out
 
 
-def load_traffic(kernel):
-    """HBM bytes per launch of `kernel` ("tower" or "conv3x3") from the committed PMC
-    pass (profiles/conv_traffic.json, scripts/summarize_profile.py), or None."""
-    path = os.path.join(REPO, "profiles", "conv_traffic.json")
-    if not os.path.exists(path):
+# --------------------------------------------------------------------- GPU legs
+def roofline_from_profile(prof, boards, blocks, ch, kname_tower, kname_layer):
+    """Residual-conv roofline from hipEvent-timed launches: the persistent tower
+    when it ran (dominant kernel), else the per-layer conv3x3 launches."""
+    cf = conv_flop(ch)
+    tower_ms, tower_n = prof.get("tower", (0.0, 0))
+    layer_ms, layer_n = prof.get("conv3x3", (0.0, 0))
+    tower_flop = cf * 2 * blocks * boards.get("tower", 0)
+    layer_flop = cf * boards.get("conv3x3", 0)
+    if tower_n:
+        achieved = tower_flop / (tower_ms / 1e3)
+        roof = {"kernel": kname_tower, "launches": tower_n, "avg_launch_us": round(tower_ms / tower_n * 1e3, 2),
+                "flop_per_launch": round(tower_flop / tower_n), "boards": boards.get("tower", 0)}
+    elif layer_n:
+        achieved = layer_flop / (layer_ms / 1e3)
+        roof = {"kernel": kname_layer, "launches": layer_n, "avg_launch_us": round(layer_ms / layer_n * 1e3, 2),
+                "flop_per_launch": round(layer_flop / layer_n)}
+    else:
         return None
+    out = {"bound": "mfma", "achieved": round(achieved / 1e12, 3), "peak": PEAK_F32_MFMA / 1e12,
+           "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA, 4), "traffic": None}
+    out.update(roof)
+    if tower_n and layer_n:
+        out["all_residual_convs_frac"] = round((tower_flop + layer_flop) / ((tower_ms + layer_ms) / 1e3)
+                                               / PEAK_F32_MFMA, 4)
+        out["per_layer_launches"] = layer_n
+    return out
+
+
+def load_traffic(kernel, config):
+    """HBM bytes per launch of `kernel` from the committed PMC pass
+    (profiles/conv_traffic.json, scripts/summarize_profile.py), or None."""
+    path = os.path.join(REPO, "profiles", "conv_traffic.json")
     try:
         d = json.load(open(path))
-        if d.get("config") == f"{BLOCKS}x{CHANNELS}_B{BATCH}" and d.get("kernel", "conv3x3") == kernel:
+        if d.get("config") == config and d.get("kernel", "conv3x3") == kernel:
             return d.get("hbm_bytes_per_launch")
     except Exception:
         pass
     return None
 
 
-def selfplay_leg(model, args, rank, dist, dev, local):
-    """BASELINE configs[2]: G games x S sims/move on this rank (native search +
-    pipelined board evaluator); returns aggregate leaf boards/s over ranks."""
-    from games.gomoku import Gomoku
-    from mcts.native_mcts import NativeSelfPlay
-    G, S = args.sp_games, args.sp_sims
-    sp = NativeSelfPlay(None, Gomoku, G, S, cpuct=1.0, dirichlet_alpha=0.03, epsilon=0.25,
-                        apply_dirichlet_n_first_moves=10, evaluator_factory=model.board_evaluator, groups=2)
-    warm = NativeSelfPlay(None, Gomoku, 8, 64, evaluator_factory=model.board_evaluator, groups=2)
-    warm.play(lambda n: 1.0, max_moves=1, use_symmetries=False, seeds=list(range(8)))
-    # conv tile autotuning is cached per batch bucket: visit the buckets the timed
-    # run's leaf batches (up to G/2 x 32 boards per group) fall in
-    top = (G + 1) // 2 * 32
+def visit_buckets(model, top):
+    """Conv/tower variant autotuning is cached per batch bucket: visit the buckets a
+    self-play run's leaf batches fall in, so no tuning happens in the timed region."""
     z8 = np.zeros((top, 225), np.int8)
-    for b in sorted({max(1, top * k // 16) for k in range(4, 17)}):
-        model.predict_boards(z8[:b], np.ones(b, np.int8))
-    barrier_sync(dist, local)
+    sizes = sorted({max(1, top * k // 32) for k in range(1, 33)} | {1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256})
+    for b in sizes:
+        if b <= top:
+            model.predict_boards(z8[:b], np.ones(b, np.int8))
+
+
+def selfplay_run(model, game_class, G, S, max_moves, seeds, profile=True):
+    """One self-play generation of G concurrent games (native search, pipelined
+    int8-board evaluator, 2 groups) -> (driver, seconds, profile, boards per class)."""
+    from mcts.native_mcts import NativeSelfPlay
+    sp = NativeSelfPlay(None, game_class, G, S, cpuct=SP_CPUCT, dirichlet_alpha=SP_ALPHA, epsilon=SP_EPS,
+                        apply_dirichlet_n_first_moves=SP_NOISE_MOVES, evaluator_factory=model.board_evaluator,
+                        groups=2 if G > 1 else 1)
+    eng = model.engine
+    eng.clear_status()
+    if profile:
+        eng.profile_enable(True)
     t0 = time.perf_counter()
-    sp.play(lambda n: 1.0, max_moves=args.sp_moves, use_symmetries=False,
-            seeds=[1000 * rank + i for i in range(G)])
-    barrier_sync(dist, local)
+    last = [t0]
+
+    def progress(live):
+        now = time.perf_counter()
+        if now - last[0] > 20.0:
+            last[0] = now
+            log(f"  {live} games live, {sp.moves} moves, {sp.boards} leaf boards, {now - t0:.0f} s")
+    results = sp.play(sp_temp, max_moves=max_moves, use_symmetries=True, seeds=seeds, progress=progress)
+    torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    v = torch.tensor([float(sp.boards), dt], dtype=torch.float64, device=dev)
-    if dist is not None:
-        b = v[:1].clone()
-        dist.all_reduce(b)
-        m = v[1:].clone()
-        dist.all_reduce(m, op=dist.ReduceOp.MAX)
-        v = torch.cat([b, m])
-    boards, dt = float(v[0]), float(v[1])
-    return {"config": f"configs[2]: {G} concurrent games/GPU x {S} sims/move, {args.sp_moves} moves/game, "
-                      f"native C++ search + batched HIP forward (6x128)",
-            "boards_per_s": round(boards / dt, 1), "leaf_boards": int(boards), "seconds": round(dt, 3),
-            "moves_per_s": round(G * args.sp_moves * (dist.get_world_size() if dist else 1) / dt, 1),
-            "nn_share_rank0": round(sp.nn_seconds / dt, 3), "search_share_rank0": round(sp.search_seconds / dt, 3),
-            "mean_batch": round(sp.boards / max(sp.forwards, 1), 1)}
+    prof = eng.profile_read() if profile else {}
+    boards = eng.profile_boards() if profile else {}
+    if profile:
+        eng.profile_enable(False)
+    eng.check_status()
+    return sp, dt, prof, boards, results
 
 
-def big_net_leg(args, rank, dist, dev, local):
-    """BASELINE configs[4] network (10-block/256-filter ResNet, 15x15 Pente boards use
-    the same 3-plane input) at batch 512 per GPU: forward boards/s and the persistent
-    tower's MFMA fraction (device time of its launches, hipEvents)."""
-    from network import PyTorchModel
+def selfplay_leg(model, args, rank, world, dist, dev, local):
+    """configs[2] headline: G games x S sims/move per rank, every game to its end."""
+    from games.gomoku import Gomoku
+    G, S = args.sp_games, args.sp_sims
+    model.net.eval()
+    warm_seeds = [10_000 + i for i in range(8)]
+    selfplay_run(model, Gomoku, 8, 64, 2, warm_seeds, profile=False)       # code objects, pinned pools
+    visit_buckets(model, (G + 1) // 2 * 32)
+    barrier_sync(dist, local)
+    log(f"self-play: {G} games x {S} sims/move to game end")
+    sp, dt, prof, boards, results = selfplay_run(model, Gomoku, G, S, args.sp_max_moves,
+                                                 [1000 * rank + i for i in range(G)])
+    barrier_sync(dist, local)
+    n_boards, n_moves, n_games, n_ex = reduce_(dist, dev, [float(sp.boards), float(sp.moves), float(G),
+                                                           float(sum(len(ex) for ex, _ in results))])
+    dt_max, rounds_max = reduce_(dist, dev, [dt, float(sp.rounds)], op="max")
+    winners = {w: sum(1 for _, x in results if x == w) for w in (0, 1, 2)}
+    lengths = np.asarray(sp.game_lengths)
+    roof = roofline_from_profile(prof, boards, BLOCKS, CHANNELS,
+                                 "azg::conv_tower<128,64,4,1,8> (persistent residual tower: 12 fused 3x3 conv + "
+                                 "BN + residual + ReLU layers per launch; launches inside the self-play run)",
+                                 "azg::conv3x3_halo<128,*> (fused 3x3 conv + BN + residual + ReLU)")
+    nn_ms = sum(v[0] for v in prof.values())
+    return {
+        "boards": n_boards, "seconds": dt_max, "rounds": int(rounds_max),
+        "boards_per_s": n_boards / dt_max, "moves_per_s": n_moves / dt_max, "games": int(n_games),
+        "examples": int(n_ex),
+        "detail": {
+            "moves_per_game": "to game end (is_game_over(), max_moves 225)",
+            "game_length_rank0": {"mean": round(float(lengths.mean()), 1), "min": int(lengths.min()),
+                                  "max": int(lengths.max())},
+            "winners_rank0": winners,
+            "leaf_boards_rank0": sp.boards, "forwards_rank0": sp.forwards,
+            "mean_batch_rank0": round(sp.boards / max(sp.forwards, 1), 1), "max_batch_rank0": sp.max_batch,
+            "gpu_busy_share_rank0": round(nn_ms / 1e3 / dt, 3),
+            "host_wait_share_rank0": round(sp.nn_seconds / dt, 3),
+            "host_search_share_rank0": round(sp.search_seconds / dt, 3),
+            "kernel_ms_rank0": {k: round(v[0], 1) for k, v in prof.items()},
+            "kernel_launches_rank0": {k: v[1] for k, v in prof.items()},
+            "settings": f"cpuct {SP_CPUCT}, Dirichlet alpha {SP_ALPHA} eps {SP_EPS} on the first {SP_NOISE_MOVES} "
+                        f"moves, temperature max(0, 1 - n/{SP_TEMP_THRESHOLD}), 8 symmetries, leaf batch 32 "
+                        f"per game (train.py:847-889, mcts/new_mcts_alpha.py:12)",
+        },
+        "roofline": roof,
+    }
+
+
+def forward_leg(model, args, rank, world, dist, dev, local, blocks=BLOCKS, ch=CHANNELS, B=BATCH, steps=None,
+                warmup=None):
+    """configs[1] (and the configs[4] network): `steps` forwards of B synthetic boards
+    resident in HBM; roofline of the residual tower from hipEvents."""
     from synth import synth_encoded
-    nb, ch, B = 10, 256, 512
-    torch.manual_seed(1)
-    m = PyTorchModel(board_size=15, device=str(dev), n_res_blocks=nb, channels=ch)
-    eng = m.engine
-    x = torch.from_numpy(synth_encoded(B, seed=77 + rank)).to(dev)
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
+    eng = model.engine
+    x = torch.from_numpy(synth_encoded(B, seed=1234 + rank)).to(dev)
     probs = torch.empty((B, 225), device=dev)
     values = torch.empty((B, 1), device=dev)
-    for _ in range(3):
+    for _ in range(max(warmup, 1)):
         eng.forward_into(x, probs, values)
     barrier_sync(dist, local)
     eng.profile_enable(True)
+    barrier_sync(dist, local)
     t0 = time.perf_counter()
-    for _ in range(args.big_steps):
+    for _ in range(steps):
         eng.forward_into(x, probs, values)
     barrier_sync(dist, local)
-    dt = time.perf_counter() - t0
+    elapsed = time.perf_counter() - t0
     prof = eng.profile_read()
+    boards = eng.profile_boards()
     eng.profile_enable(False)
-    v = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if dist is not None:
-        dist.all_reduce(v, op=dist.ReduceOp.MAX)
-    dt = float(v.item())
-    world = dist.get_world_size() if dist is not None else 1
-    flop_conv = 2 * 225 * ch * 9 * ch * B * 2 * nb
-    tower_ms, tower_n = prof.get("tower", (0.0, 0))
-    if not tower_n:
-        tower_ms, tower_n = prof.get("conv3x3", (0.0, 0))
-        tower_n = max(tower_n // (2 * nb), 1)
-    conv_s = tower_ms / 1e3 / max(tower_n, 1)
-    return {"config": f"configs[4] network: {nb}x{ch} ResNet, batch {B}/GPU forward (eval BN)",
-            "boards_per_s": round(B * args.big_steps * world / dt, 1),
-            "ms_per_step": round(dt / args.big_steps * 1e3, 3),
-            "residual_convs_ms": round(conv_s * 1e3, 3),
-            "residual_convs_mfma_frac": round(flop_conv / conv_s / PEAK_F32_MFMA, 4) if conv_s > 0 else None}
+    eng.check_status()
+    assert torch.isfinite(probs).all() and torch.isfinite(values).all()
+    (elapsed,) = reduce_(dist, dev, [elapsed], op="max")
+    roof = roofline_from_profile(prof, boards, blocks, ch,
+                                 f"azg::conv_tower<{ch},*> (persistent residual tower, {2 * blocks} convs per launch)",
+                                 f"azg::conv3x3_halo<{ch},*>")
+    if roof is not None and blocks == BLOCKS and ch == CHANNELS and B == BATCH:
+        roof["traffic"] = load_traffic("tower" if prof.get("tower") else "conv3x3", f"{blocks}x{ch}_B{B}")
+    return {"config": f"{blocks}x{ch} ResNet, batch {B}/GPU eval forward (BN running stats, softmax + tanh), "
+                      f"inputs resident in HBM",
+            "boards_per_s": round(B * steps * world / elapsed, 1), "ms_per_step": round(elapsed / steps * 1e3, 4),
+            "steps": steps, "warmup": warmup,
+            "whole_forward_mfma_frac": round(B * steps / elapsed * fwd_flop(blocks, ch) / PEAK_F32_MFMA, 4),
+            "kernel_ms_per_step": {k: round(v[0] / steps, 4) for k, v in prof.items()},
+            "roofline": roof}
 
 
-def train_leg(model, args, rank, world, dist, dev, local):
-    """BASELINE configs[3] train half: PyTorchModel.train_batch_device on 128 samples
-    per GPU (global 128 x N) with the flat-gradient all-reduce over RCCL between
-    backward and clip+Adam (distributed.grad_hook); max step time over ranks."""
+def train_leg(model, args, rank, world, dist, dev, local, blocks=BLOCKS, ch=CHANNELS, steps=None):
+    """configs[3] train half: PyTorchModel.train_batch_device on 128 samples per GPU
+    (global 128 x N) with the flat-gradient all-reduce over RCCL between backward
+    and clip+Adam (distributed.grad_hook); max step time over ranks."""
     import distributed as D
     from synth import synth_encoded
-    B, K = 128, args.train_steps
+    B = 128
+    K = args.train_steps if steps is None else steps
     rng = np.random.default_rng(77 + rank)
     x = torch.from_numpy(synth_encoded(B, seed=77 + rank)).to(dev)
     pi = rng.random((B, 225)).astype(np.float32)
@@ -216,29 +434,67 @@ def train_leg(model, args, rank, world, dist, dev, local):
     for _ in range(K):
         losses = model.train_batch_device(x, pi, z, return_tensor=True)
     barrier_sync(dist, local)
-    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    if dist is not None:
-        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-    dt = float(dt.item())
+    (dt,) = reduce_(dist, dev, [time.perf_counter() - t0], op="max")
     assert torch.isfinite(losses).all()
-    return {"config": f"configs[3] train step: 6x128, {B} samples/GPU (global {B * world}), "
-                      f"{'RCCL all-reduce of the flat fp32 gradient (7.57 MB) + ' if world > 1 else ''}clip 3.0 + Adam",
-            "samples_per_s": round(B * K * world / dt, 1), "ms_per_step": round(dt / K * 1e3, 3), "steps": K}
+    model.grad_hook = None
+    flop = train_flop(blocks, ch) * B
+    nparam = model.engine.nparam
+    return {"config": f"{blocks}x{ch}, {B} samples/GPU (global {B * world}), "
+                      f"{f'RCCL all-reduce of the flat fp32 gradient ({nparam * 4 / 1e6:.2f} MB) + ' if world > 1 else ''}"
+                      f"clip 3.0 + Adam",
+            "samples_per_s": round(B * K * world / dt, 1), "ms_per_step": round(dt / K * 1e3, 3), "steps": K,
+            "flop_per_step": flop, "mfma_frac": round(flop / (dt / K) / PEAK_F32_MFMA, 4)}
+
+
+def pente_leg(args, rank, world, dist, dev, local):
+    """configs[4] on one GPU: the 10x256 net -- Pente self-play at 800 sims/move for
+    a stated window of moves, the B=512 forward and the B=128 train step."""
+    from games.pente import Pente
+    from network import PyTorchModel
+    nb, ch = 10, 256
+    torch.manual_seed(1)
+    m = PyTorchModel(board_size=15, device=str(dev), n_res_blocks=nb, channels=ch)
+    out = {"net": f"{nb}x{ch}"}
+    out["forward_b512"] = forward_leg(m, args, rank, world, dist, dev, local, nb, ch, BATCH, args.big_steps, 2)
+    out["train_b128"] = train_leg(m, args, rank, world, dist, dev, local, nb, ch, steps=args.big_train_steps)
+    if args.pente_moves > 0:
+        G, S = args.pente_games, 800
+        m.net.eval()
+        selfplay_run(m, Pente, 4, 32, 1, [20_000 + i for i in range(4)], profile=False)
+        visit_buckets(m, (G + 1) // 2 * 32)
+        barrier_sync(dist, local)
+        sp, dt, prof, boards, _ = selfplay_run(m, Pente, G, S, args.pente_moves, [2000 * rank + i for i in range(G)])
+        barrier_sync(dist, local)
+        (nbd,) = reduce_(dist, dev, [float(sp.boards)])
+        (dtm,) = reduce_(dist, dev, [dt], op="max")
+        out["selfplay"] = {
+            "config": f"Pente (capture rules), {G} concurrent games/GPU x {S} sims/move, first {args.pente_moves} "
+                      f"moves of every game (window; max_moves), native C++ search + batched HIP forward ({nb}x{ch})",
+            "boards_per_s": round(nbd / dtm, 1), "leaf_boards": int(nbd), "seconds": round(dtm, 2),
+            "mean_batch_rank0": round(sp.boards / max(sp.forwards, 1), 1),
+            "roofline": roofline_from_profile(prof, boards, nb, ch, f"azg::conv_tower<{ch},*>",
+                                              f"azg::conv3x3_halo<{ch},*>")}
+    del m
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=BATCH)
+    ap.add_argument("--steps", type=int, default=50, help="forwards of the configs[1] sub-leg")
+    ap.add_argument("--warmup", type=int, default=10, help="untimed forwards before the configs[1] sub-leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-game-seconds", type=float, default=12.0,
+                    help="wall-time bound per configs[0] CPU game (1 thread and all cores)")
     ap.add_argument("--sp-games", type=int, default=256)
     ap.add_argument("--sp-sims", type=int, default=400)
-    ap.add_argument("--sp-moves", type=int, default=2, help="moves per game in the self-play leg (0: skip)")
-    ap.add_argument("--train-steps", type=int, default=20, help="steps of the data-parallel train leg (0: skip)")
-    ap.add_argument("--big-steps", type=int, default=10, help="forward steps of the 10x256 net leg (0: skip)")
+    ap.add_argument("--sp-max-moves", type=int, default=225, help="train.py's max_moves (board size squared)")
+    ap.add_argument("--train-steps", type=int, default=20, help="steps of the configs[3] train leg (0: skip)")
+    ap.add_argument("--big-steps", type=int, default=10, help="10x256 forwards (configs[4] net; 0: skip the leg)")
+    ap.add_argument("--big-train-steps", type=int, default=5)
+    ap.add_argument("--pente-games", type=int, default=64)
+    ap.add_argument("--pente-moves", type=int, default=3, help="move window of the configs[4] Pente self-play")
     args = ap.parse_args()
 
     rank, world, local, dist = dist_setup(args.gpus)
@@ -246,100 +502,64 @@ def main():
     torch.cuda.set_device(dev)
 
     from network import PyTorchModel
-    from synth import synth_encoded
 
     torch.manual_seed(0)
     model = PyTorchModel(board_size=15, device=str(dev), n_res_blocks=BLOCKS, channels=CHANNELS)
-    eng = model.engine
-    B = args.batch
-    x = torch.from_numpy(synth_encoded(B, seed=1234 + rank)).to(dev)
-    probs = torch.empty((B, 225), device=dev)
-    values = torch.empty((B, 1), device=dev)
 
-    for _ in range(args.warmup):
-        eng.forward_into(x, probs, values)
-    barrier_sync(dist, local)
-
-    eng.profile_enable(True)
-    barrier_sync(dist, local)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.forward_into(x, probs, values)
-    barrier_sync(dist, local)
-    elapsed = time.perf_counter() - t0
-    prof = eng.profile_read()
-    eng.profile_enable(False)
-
-    assert torch.isfinite(probs).all() and torch.isfinite(values).all()
-
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if dist is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-
-    selfplay = None
-    if args.sp_moves > 0:
-        selfplay = selfplay_leg(model, args, rank, dist, dev, local)
+    log("configs[1] forward leg")
+    fwd = forward_leg(model, args, rank, world, dist, dev, local)
+    sp = selfplay_leg(model, args, rank, world, dist, dev, local)
+    log(f"self-play done: {sp['boards_per_s']:.0f} boards/s over {sp['seconds']:.1f} s")
     train = None
     if args.train_steps > 0:
+        log("configs[3] train leg")
         train = train_leg(model, args, rank, world, dist, dev, local)
-
     big = None
     if args.big_steps > 0:
-        big = big_net_leg(args, rank, dist, dev, local)
+        log("configs[4] 10x256 legs")
+        del model
+        torch.cuda.empty_cache()
+        big = pente_leg(args, rank, world, dist, dev, local)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline (reference CPU path on the host)")
+        cpu = cpu_baseline(args.cpu_game_seconds)
 
     if rank != 0:
         dist.destroy_process_group()
         return
 
-    boards = B * args.steps * world
-    value = boards / elapsed
-    tower = bool(prof.get("tower", (0.0, 0))[1])
-    if tower:
-        # persistent residual tower: one launch runs all 2*BLOCKS convs
-        conv_ms, conv_n = prof["tower"]
-        flop_launch = FLOP_CONV * B * 2 * BLOCKS
-        kname = ("azg::conv_tower<128,*> (persistent residual tower: all 12 fused 3x3 conv + BN + "
-                 "residual + ReLU layers in one launch, halo-staged tiles)")
-    else:
-        conv_ms, conv_n = prof.get("conv3x3", (0.0, 0))
-        flop_launch = FLOP_CONV * B
-        kname = "azg::conv3x3_halo<128,*> (fused 3x3 conv + BN + residual + ReLU, halo-staged)"
-    conv_avg_s = conv_ms / 1e3 / max(conv_n, 1)
-    achieved = flop_launch / conv_avg_s
-    roof = {"bound": "mfma", "achieved": round(achieved / 1e12, 3), "peak": PEAK_F32_MFMA / 1e12,
-            "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA, 4),
-            "traffic": load_traffic("tower" if tower else "conv3x3"),
-            "kernel": kname, "avg_launch_us": round(conv_avg_s * 1e6, 2), "launches": conv_n,
-            "flop_per_launch": flop_launch}
     out = {
         "metric": METRIC,
-        "value": round(value, 2),
+        "value": round(sp["boards_per_s"], 1),
         "unit": "boards/s",
         "n_gpus": world,
-        "steps": args.steps,
+        "steps": sp["rounds"],
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "ms_per_step": round(sp["seconds"] / max(sp["rounds"], 1) * 1e3, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (seeded legal 15x15 positions; seeded Kaiming init weights, no checkpoint)",
-        "config": {"workload": "configs[1]: batch-512 policy/value forward (eval BN, softmax + tanh), "
-                               "6-block/128-filter ResNet, inputs resident in HBM",
-                   "global_batch": B * world, "per_gpu_batch": B, "net": f"{BLOCKS}x{CHANNELS}",
-                   "parallelism": f"replicas{world} (games shard by GPU; no collective in timed region)"},
-        "roofline": roof,
-        "whole_forward_mfma_frac": round(value / world * FLOP_BOARD / PEAK_F32_MFMA, 4),
-        "kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in prof.items()},
-        "selfplay": selfplay,
+        "data": "synthetic (self-play from the empty board; seeded Kaiming-init 6x128 weights, no checkpoint)",
+        "config": {"workload": f"configs[2]: {args.sp_games} concurrent self-play games/GPU x {args.sp_sims} "
+                               f"sims/move, 15x15 Gomoku, 6-block/128-filter ResNet, every game played to its end "
+                               f"(train.py:360-412); value = NN-evaluated leaf boards / wall time of the whole "
+                               f"generation incl. its tail",
+                   "step": "one move round (every live game makes one move); steps = rounds of the generation",
+                   "moves_per_game": "to game end",
+                   "games_per_gpu": args.sp_games, "sims_per_move": args.sp_sims, "net": f"{BLOCKS}x{CHANNELS}",
+                   "global_batch": "leaf batch varies: up to 32 x games per forward",
+                   "parallelism": f"replicas{world} (games shard by GPU; no collective in the timed region)"},
+        "roofline": sp["roofline"],
+        "selfplay": {k: v for k, v in sp.items() if k != "roofline"},
+        "forward_b512": fwd,
         "train": train,
-        "net_10x256": big,
+        "pente_10x256": big,
+        "cpu_baseline": cpu,
+        "steps_requested": args.steps,
     }
-    if not args.no_cpu_baseline and world == 1:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-    else:
-        out["cpu_baseline"] = None
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

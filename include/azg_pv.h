@@ -124,6 +124,11 @@ enum {
 };
 int32_t azg_pv_profile_enable(azg_pv* h, int32_t enable);
 int32_t azg_pv_profile_read(azg_pv* h, double* ms, int64_t* launches);
+/* Boards (eval) / samples (train) processed per class since the last enable, so a
+ * caller can price launches of varying batch (self-play) in algorithmic FLOPs.
+ * A residual-conv launch (CONV3X3) counts its batch once per conv; a TOWER launch
+ * counts its batch once for all 2*blocks convs. */
+int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
 
 /* Process-wide tuning knobs (benchmarks / A-B tests).  Returns the previous value.
  *   key 0: force the 3x3-conv tile shape index (-1 = automatic);
@@ -145,13 +150,28 @@ int32_t azg_pv_profile_read(azg_pv* h, double* ms, int64_t* launches);
  *   key 11: stem ablation mask (timing only, results invalid while set);
  *   key 12: train step conv weight grads (0 = overlapped on a side stream, default;
  *          1 = on the caller's stream);
- *   key 13: train wgrad K chunk in pixels (32 default; 16 for A/B timing, C=128).
+ *   key 13: train wgrad K chunk in pixels (32 default; 16 for A/B timing, C=128);
+ *   key 14: persistent-tower dependency spin bound (tests only: 0 makes every
+ *          dependency wait time out at once, exercising the error path; -1
+ *          restores the default).
  *   Every call returns the previous value. */
 int32_t azg_pv_set_tuning(int32_t key, int32_t value);
 
 /* Persistent-tower health: 0, or nonzero if a tile of the last eval forward on
  * this handle timed out waiting for its inputs (synchronises `stream`). */
 int32_t azg_pv_tower_status(azg_pv* h, void* stream);
+
+/* Sticky device-side status of the handle: 0 = every forward so far was computed
+ * on complete inputs; nonzero = a persistent-tower tile timed out waiting for its
+ * inputs and computed on stale data (outputs of that forward are invalid).  Kernels
+ * write it straight into pinned, mapped host memory, so reading it is a plain load
+ * with no device call: it is complete for every forward the caller has already
+ * synchronised with (event / stream sync / D2H copy).  The Python layer checks it
+ * after every host-synchronising forward and raises RuntimeError (the reference
+ * contract: errors are an int status + exception).  It stays set
+ * until azg_pv_clear_status. */
+int32_t azg_pv_status(const azg_pv* h);
+int32_t azg_pv_clear_status(azg_pv* h);
 
 /* Debug/test access to train-workspace activations of the last train step:
  * copies the interior [batch][15][15][C] (NHWC) of buffer `which` (block `index`

@@ -8,6 +8,11 @@ shape produces bitwise-identical outputs (the K order does not depend on tiling)
 --variants: conv kernel variants (1 halo-staged product kernel, 0 per-chunk A staging);
 outputs are compared bitwise within a variant (the K order differs between variants).
 """
+import os as _os
+
+# A/B study variants live only in the study build (make -C alphazero-gomoku_amd/csrc study)
+_os.environ.setdefault("AZG_PV_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))),
+                                                   "alphazero-gomoku_amd", "libazg_pv_study.so"))
 import argparse
 import json
 import os

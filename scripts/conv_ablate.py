@@ -3,6 +3,11 @@ tile shape 5 = 64x64 / 8 = 128x64 [default 5]), per-layer launches:
 mask bit 1 = no weight loads, 2 = no halo loads, 4 = no per-chunk barrier,
 8 = no LDS fragment reads, 16 = no epilogue stores.
 Only conv1 launches (EPI_BN_RELU) are ablated; we time those."""
+import os as _os
+
+# A/B study variants live only in the study build (make -C alphazero-gomoku_amd/csrc study)
+_os.environ.setdefault("AZG_PV_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))),
+                                                   "alphazero-gomoku_amd", "libazg_pv_study.so"))
 import os, sys, json, statistics
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "alphazero-gomoku_amd")]

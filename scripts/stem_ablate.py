@@ -1,6 +1,11 @@
 """Stem kernel timing ablation (timing-only switches compiled into stem_mfma, C=128
 float-plane path): device time of the stem per forward for each mask.
     python scripts/stem_ablate.py [--batch 512]"""
+import os as _os
+
+# A/B study variants live only in the study build (make -C alphazero-gomoku_amd/csrc study)
+_os.environ.setdefault("AZG_PV_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))),
+                                                   "alphazero-gomoku_amd", "libazg_pv_study.so"))
 import argparse
 import json
 import os

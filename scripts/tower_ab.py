@@ -4,6 +4,11 @@ wall time, per batch size and tower tile shape.
 
     python scripts/tower_ab.py [--batches 128,512,4096] [--steps 10]
 """
+import os as _os
+
+# A/B study variants live only in the study build (make -C alphazero-gomoku_amd/csrc study)
+_os.environ.setdefault("AZG_PV_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))),
+                                                   "alphazero-gomoku_amd", "libazg_pv_study.so"))
 import argparse
 import json
 import os

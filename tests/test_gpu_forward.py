@@ -225,7 +225,7 @@ def test_persistent_tower_bitwise_equals_per_layer_launches(blocks, ch, batches)
                     assert lib.azg_pv_tower_status(eng.h, stream) == 0
                     assert torch.equal(l0, l1), (B, shape, rep, float((l0 - l1).abs().max()))
                     assert torch.equal(p0, p1) and torch.equal(v0, v1), (B, shape, rep)
-            if ch == 128:   # tile-body variants of the 128x64 tower: same arithmetic
+            if ch == 128 and lib.azg_pv_set_tuning(15, 0) == 1:   # study build: tile-body variants, same arithmetic
                 lib.azg_pv_set_tuning(6, 8)
                 for var in (0, 1, 2, 3, 4, 5, 6, 7, 8, 12):
                     prev_var = lib.azg_pv_set_tuning(10, var)
@@ -261,6 +261,47 @@ def test_persistent_tower_under_concurrent_load():
         torch.cuda.synchronize()
         assert torch.equal(a, r1) and torch.equal(b, r2)
     lib.azg_pv_set_tuning(5, prev_mode)
+
+
+def test_tower_timeout_is_a_hard_error():
+    """A persistent-tower tile whose dependency wait times out computes on stale
+    inputs; the sticky status word must turn that into a RuntimeError on every
+    host-synchronising product path (predict, predict_boards, BoardEvaluator.wait).
+    Tuning key 14 = 0 makes every unsatisfied dependency poll time out."""
+    import _native
+    lib = _native.load_library()
+    m = make_model(6, 128, seed=6)
+    boards, players = synth_positions(512, seed=61)
+    x = encode_batch(boards, players)
+    bi8, pl8 = np.asarray(boards, np.int8).reshape(512, 225), np.asarray(players, np.int8)
+    prev_mode = lib.azg_pv_set_tuning(5, 1)
+    prev_shape = lib.azg_pv_set_tuning(6, 8)
+    try:
+        p_ok, v_ok = m.predict(x)                    # healthy: no error
+        assert lib.azg_pv_status(m.engine.h) == 0
+        lib.azg_pv_set_tuning(14, 0)
+        with pytest.raises(RuntimeError, match="timed out"):
+            m.predict(x)
+        lib.azg_pv_set_tuning(14, -1)
+        # sticky: stays raised until cleared, even for a healthy forward
+        with pytest.raises(RuntimeError, match="timed out"):
+            m.predict_boards(bi8, pl8)
+        ev = m.board_evaluator(512)
+        ev.boards[:] = bi8
+        ev.players[:] = pl8
+        ev.submit(512)
+        with pytest.raises(RuntimeError, match="timed out"):
+            ev.wait()
+        m.engine.clear_status()
+        p, v = m.predict(x)
+        assert np.array_equal(p, p_ok) and np.array_equal(v, v_ok)
+        ev.submit(512)
+        ev.wait()
+    finally:
+        lib.azg_pv_set_tuning(14, -1)
+        lib.azg_pv_set_tuning(6, prev_shape)
+        lib.azg_pv_set_tuning(5, prev_mode)
+        m.engine.clear_status()
 
 
 @pytest.mark.parametrize("blocks,ch,B", [(3, 64, 37), (6, 128, 300), (2, 256, 20)])
