@@ -31,6 +31,8 @@ _SIGS = {
     "azg_pv_param_layout": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "azg_pv_bind": (ctypes.c_int32, [_P, _P, _P, _P]),
     "azg_pv_mark_dirty": (ctypes.c_int32, [_P]),
+    "azg_pv_bind_counters": (ctypes.c_int32, [_P, _P]),
+    "azg_pv_num_bn_layers": (ctypes.c_int32, [_P]),
     "azg_pv_forward": (ctypes.c_int32, [_P, _P, ctypes.c_int32, _P, _P, _P, _P]),
     "azg_pv_forward_boards": (ctypes.c_int32, [_P, _P, _P, ctypes.c_int32, _P, _P, _P, _P]),
     "azg_pv_train_backward": (ctypes.c_int32, [_P, _P, _P, _P, ctypes.c_int32, _P, _P]),

@@ -135,6 +135,15 @@ int32_t azg_pv_bind(azg_pv* h, float* params, float* grads, float* bn_stats)
     return 0;
 }
 
+int32_t azg_pv_bind_counters(azg_pv* h, int64_t* num_batches_tracked)
+{
+    if (!h) return fail("azg_pv_bind_counters: null handle");
+    h->nbt = num_batches_tracked;
+    return 0;
+}
+
+int32_t azg_pv_num_bn_layers(const azg_pv* h) { return h ? (int32_t)h->bn_desc.size() : -1; }
+
 int32_t azg_pv_mark_dirty(azg_pv* h)
 {
     if (!h) return fail("azg_pv_mark_dirty: null handle");

@@ -218,6 +218,26 @@ __global__ __launch_bounds__(64 * NW_, 2) void conv3x3_halo(
                                           __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0, 0x00020000), M,
                                           (t / NTN) * T::BM, (t % NTN) * T::BN, smem);
 }
+// Train-step conv (forward z = conv(a), dgrad = conv(dZ, flipped W) [+ resid]) with
+// the BatchNorm partial sums fused into the epilogue (pv_halo.h XE_STATS / XE_BNBWD):
+// one fixed tile shape (128 x 64, 8 waves; the shape autotuning picked at B = 128)
+// so the partials are per 128-row M tile.  Same XCD-aware tile order as above.
+template <int C, int EPI, int XE>
+__global__ __launch_bounds__(512, 2) void conv3x3_train(
+    const float* __restrict__ in, const float* __restrict__ wp, const float* __restrict__ resid,
+    float* __restrict__ out, int M, EpiX ex)
+{
+    using T = ConvTile<C, 64, 4, 1, 8>;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int NTN = C / T::BN;
+    const int L = blockIdx.x, nt = gridDim.x;
+    const int xcd = L & 7, q8 = nt >> 3, r8 = nt & 7;
+    const int t = xcd * q8 + min(xcd, r8) + (L >> 3);
+    halo_tile<C, 64, 4, 1, 8, EPI, false, 0, 0, XE>(in, wp, nullptr, nullptr, resid, out,
+                                                 __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0, 0x00020000), M,
+                                                 (t / NTN) * T::BM, (t % NTN) * T::BN, smem, ex);
+}
+
 // Stem conv 3->C (K = 27) on the VALU: 0.2 % of the forward FLOPs.  One
 // workgroup per board; the board's 3 input planes are staged into LDS with a
 // zero halo; each thread owns one output channel (27 weights in registers) and a
@@ -710,6 +730,44 @@ hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, cons
     return launch_conv3x3_shape(shape, C, epi, in, wp, scale, shift, resid, out, M, st);
 }
 
+template <int C, int EPI, int XE>
+static hipError_t launch_train_t(const float* in, const float* wp, const float* resid, float* out, int M,
+                                 const EpiX& ex, hipStream_t st)
+{
+    using T = ConvTile<C, 64, 4, 1, 8>;
+    constexpr int lds = halo_lds_bytes<C, 64, 4, 1, 8>();
+    static bool attr_done = false;
+    if (!attr_done) {
+        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return e;
+        attr_done = true;
+    }
+    dim3 grid(((M + T::BM - 1) / T::BM) * (C / T::BN));
+    hipLaunchKernelGGL((conv3x3_train<C, EPI, XE>), grid, dim3(T::NT), lds, st, in, wp, resid, out, M, ex);
+    return hipGetLastError();
+}
+
+// Train conv with fused BN partials: (EPI_RAW, XE_STATS) forward; (EPI_RAW |
+// EPI_ADD, XE_BNBWD) dgrad.  Partials are per TRAIN_BM-row M tile.
+hipError_t launch_conv3x3_train(int C, int epi, int xe, const float* in, const float* wp, const float* resid,
+                                float* out, int M, const EpiX& ex, hipStream_t st)
+{
+#define AZG_TRAIN_C(CC)                                                                            \
+    case CC:                                                                                       \
+        if (epi == EPI_RAW && xe == XE_STATS) return launch_train_t<CC, EPI_RAW, XE_STATS>(in, wp, resid, out, M, ex, st); \
+        if (epi == EPI_RAW && xe == XE_BNBWD) return launch_train_t<CC, EPI_RAW, XE_BNBWD>(in, wp, resid, out, M, ex, st); \
+        if (epi == EPI_ADD && xe == XE_BNBWD) return launch_train_t<CC, EPI_ADD, XE_BNBWD>(in, wp, resid, out, M, ex, st); \
+        return hipErrorInvalidValue;
+    switch (C) {
+        AZG_TRAIN_C(64)
+        AZG_TRAIN_C(128)
+        AZG_TRAIN_C(256)
+        default: return hipErrorInvalidValue;
+    }
+#undef AZG_TRAIN_C
+}
+
 int conv_tuned_shape(int C, int M)
 {
     auto it = tune_cache().find(std::make_pair(C, conv_batch_bucket(M)));
@@ -789,6 +847,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     if (key == 14) {  // tests: persistent-tower dependency spin bound (-1 restores the default)
         const int prev = (int)azg::g_tower_spin_limit;
         azg::g_tower_spin_limit = value < 0 ? (1u << 22) : (unsigned)value;
+        return prev;
+    }
+    if (key == 16) {  // train: wgrad kernel (1 K-contiguous staging, default; 0 row staging, A/B)
+        const int prev = azg::g_wgrad_kernel;
+        azg::g_wgrad_kernel = value ? 1 : 0;
         return prev;
     }
     if (key == 13) {  // train: wgrad K chunk (32 default, 16 A/B)

@@ -78,6 +78,26 @@ constexpr int halo_lds_bytes()
 // (EPI_BN_RELU / EPI_BN_RES_RELU chosen at run time, same arithmetic).
 constexpr int EPI_BN_OPTRES_RELU = 4;
 
+// Train-step epilogue extras (template XE of halo_tile / halo_epilogue), computed
+// from the tile while it is on chip so no separate pass re-reads the conv output:
+//  XE_STATS  (train forward, EPI_RAW): per M tile and output channel the mean and
+//            M2 = S (z - mean)^2 of the tile's valid rows (two-pass, fp32) ->
+//            pa / pb [mtile][C]; the batch statistics combine the tiles exactly in
+//            fp64 (bn_finalize_tiles_kernel, Chan's formula).
+//  XE_BNBWD  (dgrad, EPI_RAW / EPI_ADD): the output g is the gradient of a BN+ReLU
+//            output; per M tile and channel S dy and S (z - mean) dy with
+//            dy = g * (act > 0) -> pa / pb [mtile][C] (BatchNorm backward sums).
+constexpr int XE_NONE = 0;
+constexpr int XE_STATS = 1;
+constexpr int XE_BNBWD = 2;
+struct EpiX {
+    const float* act;    // XE_BNBWD: post-ReLU activation (mask)
+    const float* z;      // XE_BNBWD: BN input
+    const float* mean;   // XE_BNBWD: batch mean of z per channel
+    float* pa;           // [mtiles][C]
+    float* pb;           // [mtiles][C]
+};
+
 // key of the 16-B slot swizzle of halo row `row` (padded-pixel index): the padded
 // board position v = yy*15 + xx (see halo_tile)
 __device__ __forceinline__ int halo_vkey(int row)
@@ -94,11 +114,13 @@ __device__ __forceinline__ int halo_vkey(int row)
 // scale/shift/residual, one 16-B store per run -- instead of 16 scalar stores (and
 // 16 pad_off divisions) per fragment.  Same per-element arithmetic.  The caller
 // guarantees every wave is past its last staging-buffer access (barrier).
-template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1, int ABL, int ELD, bool EARLY = false>
+template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1, int ABL, int ELD, bool EARLY = false,
+          int XE = XE_NONE>
 __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<C, BN_, WM_, TM_, NW_>::TN],
                                               const float* __restrict__ scale, const float* __restrict__ shift,
                                               const float* __restrict__ resid, float* __restrict__ out,
-                                              __amdgpu_buffer_rsrc_t out_rs, int M, int m0, int n0, float* smem)
+                                              __amdgpu_buffer_rsrc_t out_rs, int M, int m0, int n0, float* smem,
+                                              const EpiX& ex = EpiX{})
 {
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
     constexpr int BM = T::BM, BN = T::BN, WN = T::WN, TM = T::TM, TN = T::TN;
@@ -145,13 +167,23 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
         s4 = *(const f32x4*)(scale + col);
         t4 = *(const f32x4*)(shift + col);
     }
+    // XE partials of this thread's 4 channels over its rows
+    f32x4 xa = {0.f, 0.f, 0.f, 0.f}, xb = {0.f, 0.f, 0.f, 0.f}, xmu = {0.f, 0.f, 0.f, 0.f};
+    f32x4 vk[XE == XE_STATS ? NPASS : 1];
+    if (XE == XE_BNBWD) xmu = *(const f32x4*)(ex.mean + col);
 #pragma unroll
     for (int p = 0; p < NPASS; ++p) {
         const int row = er + p * RPI;
         const int m = m0 + row;
         f32x4 v = *(const f32x4*)(Es + row * ELD + ec);
+        if (XE == XE_STATS) vk[p] = v;
         if (m < M && (!(ABL & 16) || v[0] == 1234.5f)) {
             const int o = pad_off(m, C) + col;
+            f32x4 xact, xz;
+            if (XE == XE_BNBWD) {
+                xact = *(const f32x4*)(ex.act + o);
+                xz = *(const f32x4*)(ex.z + o);
+            }
             f32x4 rv = {0.f, 0.f, 0.f, 0.f};
             if (EARLY) rv = rve[EARLY ? p : 0];
             else if (has_res) rv = *(const f32x4*)(resid + o);
@@ -169,11 +201,67 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                 }
                 v[e] = x;
             }
+            if (XE == XE_STATS) xa += v;
+            if (XE == XE_BNBWD) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float dy = xact[e] > 0.f ? v[e] : 0.f;
+                    xa[e] += dy;
+                    xb[e] = fmaf(xz[e] - xmu[e], dy, xb[e]);
+                }
+            }
             if constexpr (SC1) {
                 __builtin_amdgcn_raw_buffer_store_b128(
                     __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), out_rs, o * 4, 0, 16);
             } else {
                 *(f32x4*)(out + o) = v;
+            }
+        }
+    }
+    if constexpr (XE != XE_NONE) {
+        // fixed-order LDS reduction over the RPI row groups (bitwise reproducible)
+        static_assert(2 * RPI * BN + BN <= BM * ELD, "XE reduction scratch");
+        float* R = smem;                       // [RPI][BN] partial a, then [RPI][BN] partial b
+        float* Mu = smem + 2 * RPI * BN;       // [BN] tile mean (XE_STATS)
+        const int mt = m0 / BM;
+        const int rows = min(BM, M - m0);
+        __syncthreads();                       // every thread is past its Es reads
+        *(f32x4*)(R + er * BN + ec) = xa;
+        if (XE == XE_BNBWD) *(f32x4*)(R + RPI * BN + er * BN + ec) = xb;
+        __syncthreads();
+        if (tid < BN) {
+            float sa = 0.f, sb = 0.f;
+            for (int r = 0; r < RPI; ++r) sa += R[r * BN + tid];
+            if (XE == XE_BNBWD) {
+                for (int r = 0; r < RPI; ++r) sb += R[RPI * BN + r * BN + tid];
+                ex.pa[(size_t)mt * C + n0 + tid] = sa;
+                ex.pb[(size_t)mt * C + n0 + tid] = sb;
+            } else {
+                const float mu = sa / (float)rows;
+                Mu[tid] = mu;
+                ex.pa[(size_t)mt * C + n0 + tid] = mu;
+            }
+        }
+        if constexpr (XE == XE_STATS) {
+            __syncthreads();
+            const f32x4 mu4 = *(const f32x4*)(Mu + ec);
+            f32x4 q = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int p = 0; p < NPASS; ++p) {
+                if (er + p * RPI < rows) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float d = vk[p][e] - mu4[e];
+                        q[e] = fmaf(d, d, q[e]);
+                    }
+                }
+            }
+            *(f32x4*)(R + RPI * BN + er * BN + ec) = q;
+            __syncthreads();
+            if (tid < BN) {
+                float sb = 0.f;
+                for (int r = 0; r < RPI; ++r) sb += R[RPI * BN + r * BN + tid];
+                ex.pb[(size_t)mt * C + n0 + tid] = sb;
             }
         }
     }
@@ -385,12 +473,13 @@ __device__ __forceinline__ void halo_mainloop_glds(const float* __restrict__ in,
 // set): bit 1 skips the weight loads, bit 2 the halo loads, bit 4 the per-chunk
 // barriers, bit 8 replaces LDS fragment reads by register values, bit 16 skips the
 // epilogue stores (kept live by a never-true compare).
-template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1 = false, int ABL = 0, int VAR = 0>
+template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1 = false, int ABL = 0, int VAR = 0,
+          int XE = XE_NONE>
 __device__ __forceinline__ void halo_tile(
     const float* __restrict__ in, const float* __restrict__ wp,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ resid, float* __restrict__ out, __amdgpu_buffer_rsrc_t out_rs,
-    int M, int m0, int n0, float* smem)
+    int M, int m0, int n0, float* smem, const EpiX& ex = EpiX{})
 {
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
     if constexpr ((VAR & 4) != 0) {   // LDS-DMA staging
@@ -591,8 +680,8 @@ __device__ __forceinline__ void halo_tile(
     }
 
     // the last chunk ended with a barrier: the staging buffers are free
-    halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, (VSWZ ? BN : BN + 8), (VAR & 8) != 0>(
-        acc, scale, shift, resid, out, out_rs, M, m0, n0, smem);
+    halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, (VSWZ ? BN : BN + 8), (VAR & 8) != 0, XE>(
+        acc, scale, shift, resid, out, out_rs, M, m0, n0, smem, ex);
 }
 
 }  // namespace azg

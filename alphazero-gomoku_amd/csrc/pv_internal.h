@@ -33,12 +33,17 @@ struct BlockBn { int first, second; };
 // kernel launchers (pv_conv.hip, pv_heads.hip, pv_pack.hip, pv_train.hip)
 hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, const float* scale,
                           const float* shift, const float* resid, float* out, int M, hipStream_t st);
+struct EpiX;
+constexpr int TRAIN_BM = 128;   // rows per M tile of conv3x3_train (BN partials granularity)
+hipError_t launch_conv3x3_train(int C, int epi, int xe, const float* in, const float* wp, const float* resid,
+                                float* out, int M, const EpiX& ex, hipStream_t st);
 extern int g_tower_mode;
 extern int g_tower_shape;
 extern int g_tower_ablation;
 extern int g_tower_var;
 extern int g_wgrad_serial;
 extern int g_wgrad_bk;
+extern int g_wgrad_kernel;
 constexpr int kTowerMaxBlocks = 32;
 int conv_batch_bucket(int M);
 size_t tower_sync_bytes(int nlayers, int M);
@@ -91,6 +96,7 @@ struct azg_pv {
     float* params = nullptr;
     float* grads = nullptr;
     float* bn = nullptr;
+    int64_t* nbt = nullptr;   // optional: num_batches_tracked per BN layer (azg_pv_bind_counters)
     bool dirty = true;
 
     // packed / derived weights (one allocation)

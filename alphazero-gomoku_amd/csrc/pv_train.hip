@@ -15,6 +15,7 @@
 //  * clip_grad_norm_: total = ||grads||_2, coef = min(max_norm/(total+1e-6), 1),
 //    grads *= coef (always).
 #include "pv_internal.h"
+#include "pv_halo.h"
 
 #include <cmath>
 #include <cstdlib>
@@ -25,6 +26,8 @@ namespace azg {
 hipError_t launch_wgrad(int C, const float* dz, const float* x, float* slab, float* dw, int M, int S, int rps,
                         hipStream_t st);
 int wgrad_rows_per_split(int C, int M);
+int wgrad_splits(int C, int M);
+constexpr int kMaxWgradSplits = 64;   // wgrad_splits <= slots / tiles <= 56, rounded to 8
 
 constexpr int TROWS = 64;    // rows per statistics tile (BN stats / BN backward partials)
 constexpr int HROWS = 128;   // rows per tile of the head-projection backward partials
@@ -149,47 +152,6 @@ __global__ __launch_bounds__(256) void col_stats_kernel(const float* __restrict_
     }
 }
 
-// combine tile partials -> batch stats, apply coefficients, running-stat update.
-// One workgroup per channel of BN layer `d`.
-__global__ __launch_bounds__(256) void bn_finalize_kernel(
-    const float* __restrict__ pmean, const float* __restrict__ pm2, int ntile, int M, int C, const BnDesc* desc,
-    int layer, const float* __restrict__ params, float* __restrict__ stats, float* __restrict__ bmean,
-    float* __restrict__ binv, float* __restrict__ bscale, float* __restrict__ bshift)
-{
-    __shared__ double red[8];
-    const BnDesc d = desc[layer];
-    const int c = blockIdx.x;
-    double s = 0.0;
-    for (int t = threadIdx.x; t < ntile; t += blockDim.x) {
-        const int cnt = min(TROWS, M - t * TROWS);
-        s += (double)cnt * (double)pmean[t * C + c];
-    }
-    s = block_sum_d(s, red);
-    const double mean = s / (double)M;
-    double q = 0.0;
-    for (int t = threadIdx.x; t < ntile; t += blockDim.x) {
-        const int cnt = min(TROWS, M - t * TROWS);
-        const double dm = (double)pmean[t * C + c] - mean;
-        q += (double)pm2[t * C + c] + (double)cnt * dm * dm;
-    }
-    q = block_sum_d(q, red);
-    if (threadIdx.x == 0) {
-        const double var = q / (double)M;
-        const float mean_f = (float)mean;
-        const float inv_f = (float)(1.0 / sqrt(var + (double)BN_EPS));
-        const float alpha = inv_f * params[d.gamma_off + c];
-        bmean[d.out_off + c] = mean_f;
-        binv[d.out_off + c] = inv_f;
-        bscale[d.out_off + c] = alpha;
-        bshift[d.out_off + c] = params[d.beta_off + c] - mean_f * alpha;
-        const double unb = M > 1 ? q / (double)(M - 1) : var;
-        float* rm = stats + d.stat_off;
-        float* rv = stats + d.stat_off + d.c;
-        rm[c] = (float)((double)BN_MOMENTUM * mean + (1.0 - (double)BN_MOMENTUM) * (double)rm[c]);
-        rv[c] = (float)((double)BN_MOMENTUM * unb + (1.0 - (double)BN_MOMENTUM) * (double)rv[c]);
-    }
-}
-
 // a = relu(z*scale + shift [+ res]) over the interior of padded NHWC tensors
 template <int C, bool RES>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ z, const float* __restrict__ res,
@@ -263,27 +225,91 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
     }
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
+// fixed-order fp64 block sum of NV values per thread (256 threads, 4 waves):
+// wave shuffles, then the 4 wave sums in wave order
+template <int NV>
+__device__ __forceinline__ void block_sum4_d(double (&v)[NV], double (*red)[4])
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) red[k][wid] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = ((red[k][0] + red[k][1]) + red[k][2]) + red[k][3];
+}
+
+// Batch statistics of one BN layer from per-tile (mean, M2) partials (tile t holds
+// min(prow, M - t*prow) rows), one workgroup per channel, every tile's partial
+// loaded by its own thread (all loads in flight at once: latency-bound, not a
+// loop), ONE fp64 block reduction: mean = S n_t m_t / N,
+// var = (S (M2_t + n_t m_t^2) - N mean^2) / N  (fp64: 53 bits, no cancellation at
+// fp32 precision).  Then the coefficients and the running-stat update as ATen's
+// CPU batch_norm (invstd in fp64 stored fp32, unbiased running var, momentum 0.1).
+__global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(
+    const float* __restrict__ pmean, const float* __restrict__ pm2, int ntile, int prow, int M, int C,
+    const BnDesc* desc, int layer, const float* __restrict__ params, float* __restrict__ stats,
+    float* __restrict__ bmean, float* __restrict__ binv, float* __restrict__ bscale, float* __restrict__ bshift)
+{
+    __shared__ double red[2][4];
+    const BnDesc d = desc[layer];
+    const int c = blockIdx.x;
+    double v[2] = {0.0, 0.0};
+    for (int t = threadIdx.x; t < ntile; t += 256) {
+        const double n = (double)min(prow, M - t * prow);
+        const double mt = (double)pmean[(size_t)t * C + c];
+        v[0] += n * mt;
+        v[1] += (double)pm2[(size_t)t * C + c] + n * mt * mt;
+    }
+    block_sum4_d<2>(v, red);
+    if (threadIdx.x == 0) {
+        const double mean = v[0] / (double)M;
+        double q = v[1] - (double)M * mean * mean;     // S (z - mean)^2
+        q = q > 0.0 ? q : 0.0;
+        const double var = q / (double)M;
+        const float mean_f = (float)mean;
+        const float inv_f = (float)(1.0 / sqrt(var + (double)BN_EPS));
+        const float alpha = inv_f * params[d.gamma_off + c];
+        bmean[d.out_off + c] = mean_f;
+        binv[d.out_off + c] = inv_f;
+        bscale[d.out_off + c] = alpha;
+        bshift[d.out_off + c] = params[d.beta_off + c] - mean_f * alpha;
+        const double unb = M > 1 ? q / (double)(M - 1) : var;
+        float* rm = stats + d.stat_off;
+        float* rv = stats + d.stat_off + d.c;
+        rm[c] = (float)((double)BN_MOMENTUM * mean + (1.0 - (double)BN_MOMENTUM) * (double)rm[c]);
+        rv[c] = (float)((double)BN_MOMENTUM * unb + (1.0 - (double)BN_MOMENTUM) * (double)rv[c]);
+    }
+}
+
+// BN-backward sums from per-tile partials (S dy, S (z-mean) dy), one workgroup per
+// channel, fp64 fixed-order block sum; dgamma = S(z-mean)dy * invstd, dbeta = S dy,
+// and for bn_bwd_apply gm = S dy / N, k = S(z-mean)dy invstd^2 / N, iw = invstd*gamma.
+__global__ __launch_bounds__(256) void bn_bwd_finalize_tiles_kernel(
     const float* __restrict__ pa, const float* __restrict__ pb, int ntile, int M, int C, const BnDesc* desc,
     int layer, const float* __restrict__ params, float* __restrict__ grads, const float* __restrict__ binv,
     float* __restrict__ bgm, float* __restrict__ bk, float* __restrict__ biw)
 {
-    __shared__ double red[8];
+    __shared__ double red[2][4];
     const BnDesc d = desc[layer];
     const int c = blockIdx.x;
-    double s = 0.0, q = 0.0;
-    for (int t = threadIdx.x; t < ntile; t += blockDim.x) {
-        s += (double)pa[t * C + c];
-        q += (double)pb[t * C + c];
+    double v[2] = {0.0, 0.0};
+    for (int t = threadIdx.x; t < ntile; t += 256) {
+        v[0] += (double)pa[(size_t)t * C + c];
+        v[1] += (double)pb[(size_t)t * C + c];
     }
-    s = block_sum_d(s, red);
-    q = block_sum_d(q, red);
+    block_sum4_d<2>(v, red);
     if (threadIdx.x == 0) {
         const double inv = (double)binv[d.out_off + c];
-        grads[d.gamma_off + c] = (float)(q * inv);
-        grads[d.beta_off + c] = (float)s;
-        bgm[d.out_off + c] = (float)(s / (double)M);
-        bk[d.out_off + c] = (float)(q * inv * inv / (double)M);
+        grads[d.gamma_off + c] = (float)(v[1] * inv);
+        grads[d.beta_off + c] = (float)v[0];
+        bgm[d.out_off + c] = (float)(v[0] / (double)M);
+        bk[d.out_off + c] = (float)(v[1] * inv * inv / (double)M);
         biw[d.out_off + c] = (float)inv * params[d.gamma_off + c];
     }
 }
@@ -353,12 +379,16 @@ __global__ __launch_bounds__(256) void head_stats_partial_kernel(const float* __
 }
 
 // batch stats of the 3 head BN channels -> folded coefficients + running stats
+// Also advances every BN layer's num_batches_tracked (int64, bound with
+// azg_pv_bind_counters) by one: the train-mode forward's counter update.
 __global__ void head_stats_finalize_kernel(const double* __restrict__ part, int B, const BnDesc* desc, int pol_layer,
                                            int val_layer, const float* __restrict__ params,
                                            float* __restrict__ stats, float* __restrict__ bmean,
                                            float* __restrict__ binv, float* __restrict__ bscale,
-                                           float* __restrict__ bshift)
+                                           float* __restrict__ bshift, int64_t* __restrict__ nbt, int nbn)
 {
+    if (nbt)
+        for (int i = threadIdx.x; i < nbn; i += blockDim.x) nbt[i] += 1;
     const int ch = threadIdx.x;
     if (ch >= 3) return;
     const BnDesc d = desc[ch < 2 ? pol_layer : val_layer];
@@ -806,7 +836,12 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     A(w->GR, act, true);
     A(w->DZ2, act, true);
     {
-        hipError_t e = hipStreamCreateWithFlags(&w->side, hipStreamNonBlocking);
+        // the weight grads are off the critical path: their stream gets the LOWEST
+        // priority so the dependent chain on the caller's stream (BN kernels, dgrad)
+        // is dispatched first whenever workgroup slots free up
+        int least = 0, greatest = 0;
+        hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&w->side, hipStreamNonBlocking, least);
         for (int i = 0; i < 2 && e == hipSuccess; ++i) {
             e = hipEventCreateWithFlags(&w->ev_ready[i], hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&w->ev_done[i], hipEventDisableTiming);
@@ -822,8 +857,7 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     A(w->hpart, (size_t)((M + HROWS - 1) / HROWS) * 3 * C, false);
     A(w->spart, (size_t)cap * 27 * C, false);
     // split-K for wgrad: ~512 rows per split
-    w->rps = 256;                         // smallest split wgrad_rows_per_split picks
-    w->S = (M + w->rps - 1) / w->rps;
+    w->S = kMaxWgradSplits;
     A(w->slab, (size_t)w->S * 9 * C * C, false);
     A(w->zh, (size_t)cap * 3 * PIX, false);
     A(w->fp, (size_t)cap * 2 * PIX, false);
@@ -881,13 +915,19 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     const BnDesc* bdd = (const BnDesc*)h->bn_desc_dev;
     const int gM = grid_for((int64_t)M * C / 4);
 
+    const int ntt = (M + TRAIN_BM - 1) / TRAIN_BM;   // M tiles of conv3x3_train (partials per tile)
+    auto fin_fwd = [&](int layer, int prow, int nt) -> int32_t {
+        hipLaunchKernelGGL(bn_finalize_tiles_kernel, dim3(bd[layer].c), dim3(256), 0, st, w->part_a,
+                           w->part_b, nt, prow, M, C, bdd, layer, P, h->bn, w->bmean, w->binv, w->bscale, w->bshift);
+        AZG_CK(hipGetLastError(), "train: bn_finalize_tiles");
+        return 0;
+    };
+    // stem: separate column statistics (64-row tiles)
     auto stats = [&](const float* z, int layer) -> int32_t {
         int pr = prof_begin(h, AZG_PROF_TRAIN_OTHER, st);
         hipLaunchKernelGGL((col_stats_kernel<C>), dim3(ntile), dim3(256), 0, st, z, w->part_a, w->part_b, M);
         AZG_CK(hipGetLastError(), "train: col_stats");
-        hipLaunchKernelGGL(bn_finalize_kernel, dim3(bd[layer].c), dim3(256), 0, st, w->part_a, w->part_b, ntile, M,
-                           C, bdd, layer, P, h->bn, w->bmean, w->binv, w->bscale, w->bshift);
-        AZG_CK(hipGetLastError(), "train: bn_finalize");
+        if (int32_t r = fin_fwd(layer, TROWS, ntile)) return r;
         prof_end(h, pr, st);
         return 0;
     };
@@ -902,20 +942,31 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         AZG_CK(hipGetLastError(), "train: bn_apply");
         return 0;
     };
-    auto conv = [&](int epi, const float* in, const float* wp, const float* res, float* out) -> int32_t {
-        int pr = prof_begin(h, AZG_PROF_TRAIN_CONV, st);
-        AZG_CK(launch_conv3x3(C, epi, in, wp, nullptr, nullptr, res, out, M, st), "train: conv3x3");
+    // train-mode conv: forward (z + BN tile statistics) or dgrad (+ BN-backward tile
+    // sums of the layer below: act / z / layer `xl`); partials land in part_a / part_b
+    auto conv = [&](int epi, int xe, const float* in, const float* wp, const float* res, float* out,
+                    const float* xact, const float* xz, int xl) -> int32_t {
+        int pr = prof_begin(h, AZG_PROF_TRAIN_CONV, st, B);
+        const EpiX ex{xact, xz, xl >= 0 ? w->bmean + bd[xl].out_off : nullptr, w->part_a, w->part_b};
+        AZG_CK(launch_conv3x3_train(C, epi, xe, in, wp, res, out, M, ex, st), "train: conv3x3");
         prof_end(h, pr, st);
         return 0;
     };
-    auto bwd_bn = [&](const float* g, const float* act, const float* z, int layer, float* dz, float* gres) -> int32_t {
-        const int o = bd[layer].out_off;
-        hipLaunchKernelGGL((bn_bwd_reduce_kernel<C>), dim3(ntile), dim3(256), 0, st, g, act, z, w->bmean + o,
-                           w->part_a, w->part_b, M);
+    auto bwd_reduce = [&](const float* g, const float* act, const float* z, int layer) -> int32_t {
+        hipLaunchKernelGGL((bn_bwd_reduce_kernel<C>), dim3(ntile), dim3(256), 0, st, g, act, z,
+                           w->bmean + bd[layer].out_off, w->part_a, w->part_b, M);
         AZG_CK(hipGetLastError(), "train: bn_bwd_reduce");
-        hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bd[layer].c), dim3(256), 0, st, w->part_a, w->part_b, ntile,
-                           M, C, bdd, layer, P, G, w->binv, w->bgm, w->bk, w->biw);
-        AZG_CK(hipGetLastError(), "train: bn_bwd_finalize");
+        return 0;
+    };
+    auto bwd_fin = [&](int layer, int nt) -> int32_t {
+        hipLaunchKernelGGL(bn_bwd_finalize_tiles_kernel, dim3(bd[layer].c), dim3(256), 0, st,
+                           w->part_a, w->part_b, nt, M, C, bdd, layer, P, G, w->binv, w->bgm, w->bk, w->biw);
+        AZG_CK(hipGetLastError(), "train: bn_bwd_finalize_tiles");
+        return 0;
+    };
+    auto bwd_apply = [&](const float* g, const float* act, const float* z, int layer, float* dz,
+                         float* gres) -> int32_t {
+        const int o = bd[layer].out_off;
         if (gres)
             hipLaunchKernelGGL((bn_bwd_apply_kernel<C, true>), dim3(gM), dim3(256), 0, st, g, act, z, w->bmean + o,
                                w->bgm + o, w->bk + o, w->biw + o, dz, gres, M);
@@ -931,8 +982,9 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     auto wgrad = [&](int slot, const float* xin, int tensor) -> int32_t {
         if (g_wgrad_serial) {   // A/B: weight grads on the caller's stream, no overlap
             int pr = prof_begin(h, AZG_PROF_TRAIN_WGRAD, st);
-            const int rps = wgrad_rows_per_split(C, M);
-            AZG_CK(launch_wgrad(C, dzbuf[slot], xin, w->slab, G + h->poff[tensor], M, (M + rps - 1) / rps, rps, st),
+            const int rps = wgrad_rows_per_split(C, M), S = wgrad_splits(C, M);
+            if (S > w->S) return set_error("train: wgrad splits exceed the slab workspace", hipErrorInvalidValue);
+            AZG_CK(launch_wgrad(C, dzbuf[slot], xin, w->slab, G + h->poff[tensor], M, S, rps, st),
                    "train: wgrad");
             prof_end(h, pr, st);
             return 0;
@@ -940,8 +992,9 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         AZG_CK(hipEventRecord(w->ev_ready[slot], st), "train: event record");
         AZG_CK(hipStreamWaitEvent(w->side, w->ev_ready[slot], 0), "train: stream wait");
         int pr = prof_begin(h, AZG_PROF_TRAIN_WGRAD, w->side);
-        const int rps = wgrad_rows_per_split(C, M);
-        AZG_CK(launch_wgrad(C, dzbuf[slot], xin, w->slab, G + h->poff[tensor], M, (M + rps - 1) / rps, rps, w->side),
+        const int rps = wgrad_rows_per_split(C, M), S = wgrad_splits(C, M);
+        if (S > w->S) return set_error("train: wgrad splits exceed the slab workspace", hipErrorInvalidValue);
+        AZG_CK(launch_wgrad(C, dzbuf[slot], xin, w->slab, G + h->poff[tensor], M, S, rps, w->side),
                "train: wgrad");
         prof_end(h, pr, w->side);
         AZG_CK(hipEventRecord(w->ev_done[slot], w->side), "train: event record");
@@ -965,11 +1018,12 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     R(apply(w->z0, nullptr, h->bn_stem, w->a0));
     const float* X = w->a0;
     for (int i = 0; i < NB; ++i) {
-        R(conv(EPI_RAW, X, h->wpack + (size_t)(2 * i) * 9 * C * C, nullptr, w->z1[i]));
-        R(stats(w->z1[i], h->bn_blk[i].first));
+        R(conv(EPI_RAW, XE_STATS, X, h->wpack + (size_t)(2 * i) * 9 * C * C, nullptr, w->z1[i], nullptr, nullptr, -1));
+        R(fin_fwd(h->bn_blk[i].first, TRAIN_BM, ntt));
         R(apply(w->z1[i], nullptr, h->bn_blk[i].first, w->hh[i]));
-        R(conv(EPI_RAW, w->hh[i], h->wpack + (size_t)(2 * i + 1) * 9 * C * C, nullptr, w->z2[i]));
-        R(stats(w->z2[i], h->bn_blk[i].second));
+        R(conv(EPI_RAW, XE_STATS, w->hh[i], h->wpack + (size_t)(2 * i + 1) * 9 * C * C, nullptr, w->z2[i], nullptr,
+               nullptr, -1));
+        R(fin_fwd(h->bn_blk[i].second, TRAIN_BM, ntt));
         R(apply(w->z2[i], X, h->bn_blk[i].second, w->xo[i]));
         X = w->xo[i];
     }
@@ -982,7 +1036,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         hipLaunchKernelGGL(head_stats_partial_kernel, dim3(3, HSC), dim3(256), 0, st, w->zh, B, w->hspart);
         AZG_CK(hipGetLastError(), "train: head_stats_partial");
         hipLaunchKernelGGL(head_stats_finalize_kernel, dim3(1), dim3(64), 0, st, w->hspart, B, bdd, h->bn_pol,
-                           h->bn_val, P, h->bn, w->bmean, w->binv, w->bscale, w->bshift);
+                           h->bn_val, P, h->bn, w->bmean, w->binv, w->bscale, w->bshift, h->nbt,
+                           (int)h->bn_desc.size());
         AZG_CK(hipGetLastError(), "train: head_stats_finalize");
         const int ho = bd[h->bn_pol].out_off;   // policy ch0, ch1, value: contiguous
         const int gH = grid_for((int64_t)B * 3 * PIX);
@@ -1043,22 +1098,41 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     };
     R(snap(0));
     // ---- tower backward ----
+    // The BN-backward sums of every layer but the last block's bn2 come out of the
+    // epilogue of the dgrad conv that produces its gradient (XE_BNBWD, per 128-row
+    // tile); the last block's gradient comes from the heads (separate reduction).
+    int bwd_nt = ntt;
+    if (NB > 0) {
+        R(bwd_reduce(w->gX, w->xo[NB - 1], w->z2[NB - 1], h->bn_blk[NB - 1].second));
+        bwd_nt = ntile;
+    }
     for (int i = NB - 1; i >= 0; --i) {
         const float* Xin = i == 0 ? w->a0 : w->xo[i - 1];
+        const float* zin = i == 0 ? w->z0 : w->z2[i - 1];
+        const int lin = i == 0 ? h->bn_stem : h->bn_blk[i - 1].second;
+        R(bwd_fin(h->bn_blk[i].second, bwd_nt));
         R(reuse(0));
-        R(bwd_bn(w->gX, w->xo[i], w->z2[i], h->bn_blk[i].second, dzbuf[0], w->GR));
+        R(bwd_apply(w->gX, w->xo[i], w->z2[i], h->bn_blk[i].second, dzbuf[0], w->GR));
         R(wgrad(0, w->hh[i], h->t_blk[i].w2));
-        R(conv(EPI_RAW, dzbuf[0], w->wdpack + (size_t)(2 * i + 1) * 9 * C * C, nullptr, w->DH));
+        R(conv(EPI_RAW, XE_BNBWD, dzbuf[0], w->wdpack + (size_t)(2 * i + 1) * 9 * C * C, nullptr, w->DH, w->hh[i],
+               w->z1[i], h->bn_blk[i].first));
+        R(bwd_fin(h->bn_blk[i].first, ntt));
         R(reuse(1));
-        R(bwd_bn(w->DH, w->hh[i], w->z1[i], h->bn_blk[i].first, dzbuf[1], nullptr));
+        R(bwd_apply(w->DH, w->hh[i], w->z1[i], h->bn_blk[i].first, dzbuf[1], nullptr));
         R(wgrad(1, Xin, h->t_blk[i].w1));
-        R(conv(EPI_ADD, dzbuf[1], w->wdpack + (size_t)(2 * i) * 9 * C * C, w->GR, w->gX));
+        R(conv(EPI_ADD, XE_BNBWD, dzbuf[1], w->wdpack + (size_t)(2 * i) * 9 * C * C, w->GR, w->gX, Xin, zin, lin));
+        bwd_nt = ntt;
         R(snap(NB - i));
     }
     // ---- stem backward ----
     R(reuse(0));
     R(reuse(1));                 // joins the side stream: every conv weight grad is done
-    R(bwd_bn(w->gX, w->a0, w->z0, h->bn_stem, w->DZ, nullptr));
+    if (NB == 0) {
+        R(bwd_reduce(w->gX, w->a0, w->z0, h->bn_stem));
+        bwd_nt = ntile;
+    }
+    R(bwd_fin(h->bn_stem, bwd_nt));
+    R(bwd_apply(w->gX, w->a0, w->z0, h->bn_stem, w->DZ, nullptr));
     hipLaunchKernelGGL((stem_wgrad_kernel<C>), dim3(B), dim3(256), 0, st, x, w->DZ, w->spart);
     AZG_CK(hipGetLastError(), "train: stem_wgrad");
     hipLaunchKernelGGL(reduce_partials_kernel, dim3((27 * C + 63) / 64), dim3(256), 0, st, w->spart, B, 27 * C,

@@ -39,8 +39,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_mfma(
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
-    const int split = blockIdx.x;
-    int t = blockIdx.y;
+    // XCD-aware order (cdna_hip_programming.md T1; speed only): blocks b and b+8
+    // share an XCD, so every tile of one pixel split is given to the same block
+    // label b % 8 -- the split's dz rows and (tap-shifted) x rows are fetched into
+    // that XCD's L2 once and served to all 9*NT*NT of its tiles.  gridDim.x =
+    // S * tiles with S % 8 == 0.
+    constexpr int TILES = 9 * NT * NT;
+    const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
+    const int split = (k / TILES) * 8 + xcd;
+    int t = k % TILES;
     const int tap = t / (NT * NT);
     t -= tap * NT * NT;
     const int co0 = (t / NT) * BT, ci0 = (t % NT) * BT;
@@ -132,6 +139,122 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_mfma(
             }
 }
 
+// Same GEMM with K-CONTIGUOUS operand staging: each thread loads a 4-pixel x
+// 4-channel block of dz and of the tap-shifted x (four 16-B loads), transposes it
+// in registers and writes four 16-B channel rows [c][pix] to LDS, so the MFMA
+// fragments (lane = one co / ci, 4 consecutive pixels of its K half) are 16-B
+// ds_read_b128 instead of one ds_read_b32 per MFMA: per 32-pixel chunk a wave
+// issues 16 fragment reads for its 64 MFMAs (was 64).  K order per output: chunks
+// in order, within a chunk pixel pairs (s, 16+s), s = 0..15.
+template <int C>
+__global__ __launch_bounds__(256, 2) void conv3x3_wgrad_t(
+    const float* __restrict__ dz, const float* __restrict__ x, float* __restrict__ slab, int M, int rows_per_split)
+{
+    using T = WgTile<C, 32>;
+    constexpr int BT = T::BT, BK = 32, W = T::W, TT = T::T, NT = T::NT;
+    constexpr int LDT = BK + 4;                       // 36: conflict-free b128 reads, 16-B aligned rows
+    constexpr int NBLK = (BT / 4) * (BK / 4);         // 4x4 staging blocks per operand per chunk
+    static_assert(NBLK <= 256, "one staging block per thread");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* As = smem;                                 // [2][BT][LDT] dz^T
+    float* Bs = smem + 2 * BT * LDT;                  // [2][BT][LDT] x^T (tap-shifted)
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    constexpr int TILES = 9 * NT * NT;
+    const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;   // XCD-aware order, see conv3x3_wgrad_mfma
+    const int split = (k / TILES) * 8 + xcd;
+    int t = k % TILES;
+    const int tap = t / (NT * NT);
+    t -= tap * NT * NT;
+    const int co0 = (t / NT) * BT, ci0 = (t % NT) * BT;
+    const int ky = tap / 3, kx = tap - ky * 3;
+    const int toff = ((ky - 1) * PADW + (kx - 1)) * C;
+    const int mbeg = split * rows_per_split;
+    const int mend = min(M, mbeg + rows_per_split);
+    const int nch = (mend - mbeg + BK - 1) / BK;
+
+    const bool stager = tid < NBLK;
+    const int pb = tid % (BK / 4), cb = tid / (BK / 4);     // pixel block, channel block
+    f32x4 ra[4], rb[4];
+    auto gload = [&](int kc) {
+        if (!stager) return;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = mbeg + kc * BK + 4 * pb + i;
+            if (m < mend) {
+                const int po = pad_off(m, C);
+                ra[i] = *(const f32x4*)(dz + po + co0 + 4 * cb);
+                rb[i] = *(const f32x4*)(x + po + toff + ci0 + 4 * cb);
+            } else {
+                ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    };
+    auto lstore = [&](int buf) {
+        if (!stager) return;
+        float* a = As + buf * BT * LDT + (4 * cb) * LDT + 4 * pb;
+        float* b = Bs + buf * BT * LDT + (4 * cb) * LDT + 4 * pb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            *(f32x4*)(a + j * LDT) = f32x4{ra[0][j], ra[1][j], ra[2][j], ra[3][j]};
+            *(f32x4*)(b + j * LDT) = f32x4{rb[0][j], rb[1][j], rb[2][j], rb[3][j]};
+        }
+    };
+
+    f32x16 acc[TT][TT];
+#pragma unroll
+    for (int i = 0; i < TT; ++i)
+#pragma unroll
+        for (int j = 0; j < TT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int r32 = lane & 31, h = lane >> 5;
+    if (nch > 0) {
+        gload(0);
+        lstore(0);
+    }
+    __syncthreads();
+    for (int kc = 0; kc < nch; ++kc) {
+        const int cur = kc & 1;
+        if (kc + 1 < nch) gload(kc + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        const float* Ab = As + cur * BT * LDT + (wm * W + r32) * LDT + h * (BK / 2);
+        const float* Bb = Bs + cur * BT * LDT + (wn * W + r32) * LDT + h * (BK / 2);
+#pragma unroll
+        for (int q = 0; q < BK / 8; ++q) {
+            f32x4 a[TT], b[TT];
+#pragma unroll
+            for (int i = 0; i < TT; ++i) a[i] = *(const f32x4*)(Ab + i * 32 * LDT + 4 * q);
+#pragma unroll
+            for (int j = 0; j < TT; ++j) b[j] = *(const f32x4*)(Bb + j * 32 * LDT + 4 * q);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+                for (int i = 0; i < TT; ++i)
+#pragma unroll
+                    for (int j = 0; j < TT; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s4], b[j][s4], acc[i][j], 0, 0, 0);
+        }
+        if (kc + 1 < nch) lstore(cur ^ 1);
+        __syncthreads();
+    }
+
+    float* out = slab + ((size_t)split * 9 + tap) * C * C;
+#pragma unroll
+    for (int i = 0; i < TT; ++i)
+#pragma unroll
+        for (int j = 0; j < TT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int co = co0 + wm * W + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int ci = ci0 + wn * W + j * 32 + r32;
+                out[co * C + ci] = acc[i][j][r];
+            }
+}
+
 // dW (torch layout [co][ci][3][3]) = sum over slabs, fixed order: four interleaved
 // partial sums (slabs k = 0,1,2,3 mod 4: independent loads in flight) combined as
 // ((p0 + p1) + (p2 + p3)).
@@ -159,20 +282,35 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     }
 }
 
+int g_wgrad_kernel = 1;   // 1: K-contiguous staging (conv3x3_wgrad_t, default); 0: row staging (A/B)
+
 template <int C, int BK = 32>
 static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, float* dw, int M, int S, int rps,
                                  hipStream_t st)
 {
     using T = WgTile<C, BK>;
-    static bool attr_done = false;
-    if (!attr_done) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_wgrad_mfma<C, BK>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS_BYTES);
-        if (e != hipSuccess) return e;
-        attr_done = true;
+    if (S % 8) return hipErrorInvalidValue;           // wgrad_splits guarantees S % 8 == 0
+    dim3 grid(S * 9 * T::NT * T::NT);
+    if (g_wgrad_kernel == 1 && BK == 32) {
+        constexpr int lds = 2 * 2 * T::BT * (32 + 4) * 4;
+        static bool attr_t = false;
+        if (!attr_t) {
+            hipError_t e = hipFuncSetAttribute((const void*)conv3x3_wgrad_t<C>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            if (e != hipSuccess) return e;
+            attr_t = true;
+        }
+        hipLaunchKernelGGL((conv3x3_wgrad_t<C>), grid, dim3(256), lds, st, dz, x, slab, M, rps);
+    } else {
+        static bool attr_done = false;
+        if (!attr_done) {
+            hipError_t e = hipFuncSetAttribute((const void*)conv3x3_wgrad_mfma<C, BK>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS_BYTES);
+            if (e != hipSuccess) return e;
+            attr_done = true;
+        }
+        hipLaunchKernelGGL((conv3x3_wgrad_mfma<C, BK>), grid, dim3(256), T::LDS_BYTES, st, dz, x, slab, M, rps);
     }
-    dim3 grid(S, 9 * T::NT * T::NT);
-    hipLaunchKernelGGL((conv3x3_wgrad_mfma<C, BK>), grid, dim3(256), T::LDS_BYTES, st, dz, x, slab, M, rps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int total = 9 * C * C;
@@ -181,29 +319,30 @@ static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, f
     return hipGetLastError();
 }
 
-// Rows per split (multiple of 32, >= 256): minimise rounds-of-workgroups x chunks
-// per workgroup + the slab reduction (S slabs of 9*C*C floats re-read once).  The
-// old fixed 512 gave 57 x 9 = 513 workgroups at B = 128 on 512 slots: one extra round.
+// Pixel splits: S is a multiple of 8 (the XCD-aware order keeps each split on one
+// XCD); the smallest S whose S * tiles workgroups fill the resident slots in ONE
+// round (fewest chunks per workgroup), falling back to whole rounds for tiny M.
+// Returns rows per split; S = ceil(M / rps).
 int g_wgrad_bk = 32;   // pixels per K chunk of the wgrad tile (32 default; 16 = A/B study)
 
 int wgrad_rows_per_split(int C, int M)
 {
     const int bt = C < 128 ? C : 128;
     const int tiles = 9 * (C / bt) * (C / bt);
-    const int lds = 2 * 2 * g_wgrad_bk * (bt + 4) * 4;
-    const int slots = 256 * (160 * 1024 / lds);
-    const double chunk_us = 5.4 * (bt / 128.0) * (bt / 128.0) * (160.0 * 1024 / lds) / 2.0;
-    const double red_us = 9.0 * C * C * 4 / 4.0e6;     // one slab at ~4 TB/s
-    int best = 512;
-    double best_cost = 1e30;
-    for (int rps = 256; rps <= 4096; rps += 32) {
-        const int S = (M + rps - 1) / rps;
-        const int rounds = (S * tiles + slots - 1) / slots;
-        const double cost = rounds * (rps / 32) * chunk_us + S * red_us;
-        if (cost < best_cost - 1e-9) { best_cost = cost; best = rps; }
-        if (S == 1) break;
-    }
-    return best;
+    const int lds = 2 * 2 * bt * (g_wgrad_bk + 4) * 4;   // K-contiguous staging (LDS rows of BK + 4)
+    const int per_cu = 160 * 1024 / lds < 2 ? 160 * 1024 / lds : 2;
+    const int slots = 256 * per_cu;
+    int S = (slots / tiles) / 8 * 8;
+    if (S < 8) S = 8;
+    while (S > 8 && (M + S - 1) / S < 64) S -= 8;   // keep >= 2 chunks per split
+    return (M + S - 1) / S;
+}
+
+int wgrad_splits(int C, int M)
+{
+    const int rps = wgrad_rows_per_split(C, M);
+    const int S = (M + rps - 1) / rps;
+    return (S + 7) / 8 * 8;
 }
 
 // slab must hold S*9*C*C floats, S = ceil(M / rps).

@@ -44,6 +44,18 @@ def init_from_env(backend: Optional[str] = None) -> tuple:
     return r, ws, lr, device
 
 
+def _on_host(t: torch.Tensor, fn) -> torch.Tensor:
+    """Run collective `fn` on `t`; a device tensor under gloo is staged through host
+    memory (gloo is the CPU test backend: world-size-2 DP tests of the HIP engine)."""
+    if t.is_cuda and dist.get_backend() != "nccl":
+        h = t.detach().to("cpu")
+        fn(h)
+        t.copy_(h)
+    else:
+        fn(t)
+    return t
+
+
 def allreduce_mean_(t: torch.Tensor) -> torch.Tensor:
     """In-place average across ranks: RCCL's AVG (one pass over xGMI, no extra
     kernel) on GPU tensors, SUM then scale on gloo (no AVG there)."""
@@ -52,14 +64,22 @@ def allreduce_mean_(t: torch.Tensor) -> torch.Tensor:
         if t.is_cuda and dist.get_backend() == "nccl":
             dist.all_reduce(t, op=dist.ReduceOp.AVG)
         else:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
-            t.div_(n)
+            def f(x):
+                dist.all_reduce(x, op=dist.ReduceOp.SUM)
+                x.div_(n)
+            _on_host(t, f)
     return t
 
 
 def allreduce_sum_(t: torch.Tensor) -> torch.Tensor:
     if world() > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        _on_host(t, lambda x: dist.all_reduce(x, op=dist.ReduceOp.SUM))
+    return t
+
+
+def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    if world() > 1:
+        _on_host(t, lambda x: dist.broadcast(x, src))
     return t
 
 
@@ -77,15 +97,21 @@ def grad_hook():
 
 
 def broadcast_model(model, src: int = 0) -> None:
-    """Make every replica identical to `src`: params, BN stats and counters, Adam moments."""
+    """Make every replica identical to `src`: params, BN stats and counters, Adam
+    moments and the Adam step counter (bias correction)."""
     if world() == 1:
         return
     eng = model.engine
     for t in (eng.flat_params, eng.flat_bn, eng.flat_nbt):
-        dist.broadcast(t, src)
+        broadcast_(t, src)
     opt = model.optimizer
-    dist.broadcast(opt.flat_exp_avg, src)
-    dist.broadcast(opt.flat_exp_avg_sq, src)
+    broadcast_(opt.flat_exp_avg, src)
+    broadcast_(opt.flat_exp_avg_sq, src)
+    opt._ensure_state()
+    step = torch.tensor([float(opt.state[eng.params[0]]["step"])], dtype=torch.float64)
+    broadcast_(step, src)
+    for p in eng.params:
+        opt.state[p]["step"].fill_(float(step.item()))
     eng.mark_dirty()
 
 

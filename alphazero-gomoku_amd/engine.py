@@ -76,6 +76,10 @@ class PolicyValueEngine:
                 o += 2 * c
         self.params = params
         check(self.lib.azg_pv_bind(h, ptr(self.flat_params), ptr(self.flat_grads), ptr(self.flat_bn)), self.lib)
+        if self.lib.azg_pv_num_bn_layers(h) != len(bns):
+            raise RuntimeError("BatchNorm layer count does not match the engine layout")
+        # num_batches_tracked advances inside the train kernels (no extra launch)
+        check(self.lib.azg_pv_bind_counters(h, ptr(self.flat_nbt)), self.lib)
         self._seen = self._versions()
         self._out_cache = {}
 

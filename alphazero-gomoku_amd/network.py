@@ -152,10 +152,11 @@ class HipAdam(torch.optim.Adam):
                 ea.copy_(st["exp_avg"])
                 es.copy_(st["exp_avg_sq"])
                 st["exp_avg"], st["exp_avg_sq"] = ea, es
-                if not torch.is_tensor(st["step"]):
-                    st["step"] = torch.tensor(float(st["step"]), dtype=torch.float32)
-                else:
-                    st["step"] = st["step"].detach().to("cpu", torch.float32)
+                # a private step counter: torch's load_state_dict hands back the SOURCE
+                # step tensor, and hip_step's fill_ would otherwise advance the other
+                # optimizer's step too (the moments above are private copies as well --
+                # clean copy semantics; the reference aliases both, train.py:817,827)
+                st["step"] = torch.tensor(float(st["step"]), dtype=torch.float32)
 
     def hip_step(self, max_norm: float = float("inf"), total_norm: Optional[torch.Tensor] = None):
         """One optimiser step on the bound flat grads: clip to max_norm, then Adam."""
@@ -321,7 +322,6 @@ class PyTorchModel:
             if self.grad_hook is not None:
                 self.grad_hook(eng.flat_grads)
             self.optimizer.hip_step(self.max_grad_norm)
-            eng.flat_nbt.add_(1)
             if epochs > 1:
                 acc = losses.double() if acc is None else acc + losses
         mean = losses if epochs == 1 else (acc / float(epochs)).float()

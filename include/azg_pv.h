@@ -71,6 +71,13 @@ int32_t azg_pv_param_layout(const azg_pv* h, int64_t* offsets, int64_t* numels);
  * bn_stats: azg_pv_bn_count floats.  grads may be NULL for inference-only use. */
 int32_t azg_pv_bind(azg_pv* h, float* params, float* grads, float* bn_stats);
 
+/* Optional: bind the int64 num_batches_tracked counters, one per BatchNorm layer
+ * in module order (azg_pv_num_bn_layers of them, device).  Each
+ * azg_pv_train_backward then advances all of them by one inside its own kernels
+ * (the train-mode forward's update, network.py:213 via nn.BatchNorm2d). */
+int32_t azg_pv_bind_counters(azg_pv* h, int64_t* num_batches_tracked);
+int32_t azg_pv_num_bn_layers(const azg_pv* h);
+
 /* Parameters or BN stats changed outside the library (load_state_dict, copy_):
  * re-derive packed weights / folded BN before the next forward. */
 int32_t azg_pv_mark_dirty(azg_pv* h);
@@ -151,6 +158,8 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *   key 12: train step conv weight grads (0 = overlapped on a side stream, default;
  *          1 = on the caller's stream);
  *   key 13: train wgrad K chunk in pixels (32 default; 16 for A/B timing, C=128);
+ *   key 16: train conv weight-grad kernel (1 = K-contiguous staging with 16-B
+ *          fragment reads, default; 0 = row staging with 4-B reads, A/B timing);
  *   key 14: persistent-tower dependency spin bound (tests only: 0 makes every
  *          dependency wait time out at once, exercising the error path; -1
  *          restores the default).

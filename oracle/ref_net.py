@@ -157,31 +157,56 @@ def param_count(blocks: int, channels: int, board: int = 15) -> int:
     return stem + tower + pol + val
 
 
-def masked_grads_fp64(state: dict, blocks: int, channels: int, x, pi, z, masks: dict):
+def masked_forward_fp64(net: nn.Module, x, masks: dict):
+    """Train-mode forward in float64 where every ReLU is replaced by the caller's
+    0/1 mask (e.g. the GPU's own forward).  Returns (logits, value, pre) where
+    pre[name] is the fp64 PRE-activation of the masked ReLU `name` (a0, h{i}, xo{i},
+    fp, fv, hv) given the masks upstream of it -- what a flipped mask is judged by."""
+    t = lambda a: torch.as_tensor(np.asarray(a), dtype=torch.float64)
+    mk = {k: t(v) for k, v in masks.items()}
+    pre = {}
+    z = net.bn(net.conv(t(x)))
+    pre["a0"] = z
+    h = z * mk["a0"]
+    for i, blk in enumerate(net.res_blocks):
+        z = blk.bn1(blk.conv1(h))
+        pre[f"h{i}"] = z
+        hh = z * mk[f"h{i}"]
+        z = blk.bn2(blk.conv2(hh)) + h
+        pre[f"xo{i}"] = z
+        h = z * mk[f"xo{i}"]
+    B = h.shape[0]
+    z = net.policy_bn(net.policy_conv(h)).reshape(B, -1)
+    pre["fp"] = z
+    logits = net.policy_fc(z * mk["fp"])
+    z = net.value_bn(net.value_conv(h)).reshape(B, -1)
+    pre["fv"] = z
+    z = net.value_fc1(z * mk["fv"])
+    pre["hv"] = z
+    value = torch.tanh(net.value_fc2(z * mk["hv"]))
+    return logits, value, pre
+
+
+def masked_grads_fp64(state: dict, blocks: int, channels: int, x, pi, z, masks: dict, return_pre: bool = False):
     """Autograd gradients of the train-step loss (network.py:213-222) in float64,
     with every ReLU's 0/1 derivative mask SUPPLIED by the caller (e.g. the GPU's
     own forward) instead of recomputed.  A pre-activation within fp32 rounding of
     zero flips a mask between two correct fp32 implementations and the gradient
     jumps there; fixing the masks makes the comparison well-conditioned.
     masks: a0 [B,C,15,15], h{i}, xo{i} (NCHW), fp [B,450], fv [B,225], hv [B,64];
-    1.0 where the GPU's ReLU output was > 0.  Returns (grads dict, (pl, vl))."""
+    1.0 where the GPU's ReLU output was > 0.  Returns (grads dict, (pl, vl)), and
+    the fp64 pre-activations (numpy) as a third element when return_pre."""
     net = RefNet(blocks, channels).double()
     load_numpy_state(net, {k: (np.asarray(v, dtype=np.float64) if np.asarray(v).dtype.kind == "f" else v)
                            for k, v in state.items()})
     net.train()
     t = lambda a: torch.as_tensor(np.asarray(a), dtype=torch.float64)
-    mk = {k: t(v) for k, v in masks.items()}
-    h = net.bn(net.conv(t(x))) * mk["a0"]
-    for i, blk in enumerate(net.res_blocks):
-        hh = blk.bn1(blk.conv1(h)) * mk[f"h{i}"]
-        h = (blk.bn2(blk.conv2(hh)) + h) * mk[f"xo{i}"]
-    B = h.shape[0]
-    p = net.policy_bn(net.policy_conv(h)).reshape(B, -1) * mk["fp"]
-    logits = net.policy_fc(p)
-    v = net.value_bn(net.value_conv(h)).reshape(B, -1) * mk["fv"]
-    v = net.value_fc1(v) * mk["hv"]
-    value = torch.tanh(net.value_fc2(v))
+    logits, value, pre = masked_forward_fp64(net, x, masks)
     pl = F.kl_div(F.log_softmax(logits, dim=1), t(pi), reduction="batchmean")
     vl = F.mse_loss(value, t(z))
     (pl + vl).backward()
-    return {n: q.grad.numpy() for n, q in net.named_parameters()}, (float(pl), float(vl))
+    grads = {n: q.grad.numpy() for n, q in net.named_parameters()}
+    losses = (float(pl.detach()), float(vl.detach()))
+    if return_pre:
+        return grads, losses, {k: v.detach().numpy() for k, v in pre.items()}
+    return grads, losses

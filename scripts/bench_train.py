@@ -26,7 +26,16 @@ def main():
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--channels", type=int, default=128)
     ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--serial", action="store_true", help="conv weight grads on the caller's stream (key 12)")
+    ap.add_argument("--tune", action="append", default=[], help="KEY=VALUE tuning key (include/azg_pv.h)")
     args = ap.parse_args()
+    import _native
+    lib = _native.load_library()
+    if args.serial:
+        lib.azg_pv_set_tuning(12, 1)
+    for kv in args.tune:
+        k, v = (int(t) for t in kv.split("="))
+        lib.azg_pv_set_tuning(k, v)
     from network import PyTorchModel
     from synth import synth_encoded
 
@@ -50,6 +59,13 @@ def main():
     torch.cuda.synchronize()
     dt_sync = time.perf_counter() - t0
     # pipelined: losses stay on the device
+    # pipelined, no instrumentation: host enqueue time vs device time
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m.train_batch_device(x, pi, z, return_tensor=True)
+    t_enq = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    dt_pipe = time.perf_counter() - t0
     eng.profile_enable(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -59,9 +75,12 @@ def main():
     prof = eng.profile_read()
     eng.profile_enable(False)
     fwd_flop = 2 * 225 * args.channels * 9 * args.channels * (2 * args.blocks)   # tower convs per sample
-    out = {"net": f"{args.blocks}x{args.channels}", "batch": B, "steps": args.steps,
-           "ms_per_step": round(dt / args.steps * 1e3, 3), "samples_per_s": round(B * args.steps / dt, 1),
+    out = {"net": f"{args.blocks}x{args.channels}", "batch": B, "steps": args.steps, "tune": args.tune,
+           "serial": args.serial,
+           "ms_per_step_profiled": round(dt / args.steps * 1e3, 3), "samples_per_s": round(B * args.steps / dt, 1),
            "ms_per_step_sync": round(dt_sync / args.steps * 1e3, 3),
+           "ms_per_step_pipelined": round(dt_pipe / args.steps * 1e3, 3),
+           "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
            "tower_tflops_fwd_bwd": round(3 * fwd_flop * B * args.steps / dt / 1e12, 2),
            "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in prof.items()},
            "launches_per_step": {k: v[1] // args.steps for k, v in prof.items()}}

@@ -1,0 +1,115 @@
+"""Data parallelism THROUGH THE PRODUCT: world size 2, gloo, both
+ranks on the HIP engine (cuda:0 here -- one GPU box; the collectives stage through
+host memory under gloo, RCCL's path differs only in transport).  Each rank builds
+PyTorchModel from a DIFFERENT seed, `distributed.broadcast_model` makes rank 1 a
+copy of rank 0 (params, BN stats and counters, Adam moments and step), then K
+`train_batch` steps on rank-local batches with `distributed.grad_hook()` between
+azg_pv_train_backward and azg_pv_train_apply, and `sync_bn_stats` at the end.
+
+Checked: params, Adam moments and step, BN running stats and counters bitwise
+identical across ranks, and equal (<= 2e-6) to a single-process run that evaluates
+both ranks' batches with azg_pv_train_backward, averages the two flat gradients,
+and applies clip + Adam once per step (BN running stats evolved per rank, then
+averaged -- what sync_bn_stats does)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import PKG, REPO, has_gpu
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")]
+
+K, B, BLOCKS, CH = 3, 32, 2, 64
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _batch(rank, step):
+    from oracle.boards import encode_batch, synth_positions, synth_targets
+    b, p = synth_positions(B, seed=1000 + 10 * step + rank)
+    pi, z = synth_targets(B, seed=2000 + 10 * step + rank)
+    return encode_batch(b, p), pi, z
+
+
+def _state(m):
+    eng, opt = m.engine, m.optimizer
+    torch.cuda.synchronize()
+    return {"params": eng.flat_params.cpu().numpy().copy(), "bn": eng.flat_bn.cpu().numpy().copy(),
+            "nbt": eng.flat_nbt.cpu().numpy().copy(), "m": opt.flat_exp_avg.cpu().numpy().copy(),
+            "v": opt.flat_exp_avg_sq.cpu().numpy().copy(),
+            "step": np.array([float(opt.state[eng.params[0]]["step"])])}
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+    sys.path[:0] = [REPO, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    torch.set_num_threads(1)
+    torch.distributed.init_process_group("gloo")
+    import distributed as D
+    from network import PyTorchModel
+    torch.manual_seed(rank)                              # replicas start DIFFERENT
+    m = PyTorchModel(board_size=15, device="cuda:0", n_res_blocks=BLOCKS, channels=CH)
+    if rank == 1:                                        # and a different Adam history
+        x, pi, z = _batch(7, 7)
+        m.train_batch(x, pi, z)
+    D.broadcast_model(m, 0)
+    m.grad_hook = D.grad_hook()
+    for s in range(K):
+        x, pi, z = _batch(rank, s)
+        m.train_batch(x, pi, z)
+    D.sync_bn_stats(m)
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **_state(m))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_dp_train_through_hip_engine_world2(tmp_path):
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = (dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(2))
+    for k in r0:
+        assert np.array_equal(r0[k], r1[k]), k          # replicas bitwise identical
+
+    # single process: both ranks' batches through azg_pv_train_backward, averaged
+    # flat gradient, one clip + Adam per step; per-rank BN running stats, averaged
+    from network import PyTorchModel
+    torch.manual_seed(0)
+    m = PyTorchModel(board_size=15, device="cuda:0", n_res_blocks=BLOCKS, channels=CH)
+    eng = m.engine
+    bn = [eng.flat_bn.clone(), eng.flat_bn.clone()]
+    nbt0 = eng.flat_nbt.clone()
+    losses = torch.empty(3, device=eng.device)
+    m.net.train()
+    for s in range(K):
+        gs = []
+        for r in range(2):
+            x, pi, z = (torch.from_numpy(np.asarray(a, np.float32)).to(eng.device) for a in _batch(r, s))
+            with torch.no_grad():
+                eng.flat_bn.copy_(bn[r])
+            eng.flat_nbt.copy_(nbt0)
+            eng.train_backward(x, pi, z.reshape(-1, 1), losses)
+            gs.append(eng.flat_grads.clone())
+            bn[r] = eng.flat_bn.clone()
+        with torch.no_grad():
+            eng.flat_grads.copy_((gs[0] + gs[1]) / 2)
+        m.optimizer.hip_step(m.max_grad_norm)
+        nbt0 += 1
+    with torch.no_grad():
+        eng.flat_bn.copy_((bn[0] + bn[1]) / 2)
+        eng.flat_nbt.copy_(nbt0)
+    want = _state(m)
+    for k in ("params", "m", "v", "bn"):
+        d = float(np.abs(r0[k] - want[k]).max())
+        print(f"{k}: max |dp - single| = {d:.2e}")
+        assert d <= 2e-6, (k, d)
+    assert np.array_equal(r0["nbt"], want["nbt"]) and r0["step"][0] == want["step"][0] == K

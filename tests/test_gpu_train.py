@@ -3,12 +3,18 @@ PyTorchModel.train_batch) against the CPU oracle (autograd) and the reference
 goldens.
 
 Tolerances (fp32; stated per check):
-  * gradients: |g_gpu - g_ref| <= 1e-4 * max|g_ref| (per tensor) + 1e-7 -- fp32
-    backward through 7-13 BN layers with different summation orders;
+  * gradients: |g_gpu - g_64| <= 2e-5 * max|g_64| (per tensor) + 1e-8 against fp64
+    autograd that uses the GPU's own ReLU masks; every mask flip (GPU vs the exact
+    fp64 pre-activation) must sit at |pre-activation| <= max(1e-6 x the layer's max,
+    2 x the GPU's own max error on that layer), and flips vs the fp32 oracle's own
+    masks are counted and printed;
   * losses: 1e-5 relative;
-  * params after Adam: the reference itself is not reproducible across thread
-    counts here (sign of near-zero gradients decides +-lr): same gate as
-    tests/test_oracle_golden.py::check_train_state.
+  * params after 2 steps (clip + Adam): <= 1 % of elements beyond 2e-5 -- against
+    the fp64 trajectory with the GPU's masks (all params), and against the
+    reference goldens for every param not below a mask flip (a flip at block k
+    perturbs the gradients of blocks <= k and the stem at ~1e-3 relative, and Adam
+    turns that into +-lr; those blocks are reported, and covered by the fp64
+    trajectory test).
 """
 import numpy as np
 import pytest
@@ -18,7 +24,6 @@ import torch.nn.functional as F
 from conftest import golden_state, has_gpu, load_golden
 from oracle.boards import encode_batch, synth_positions, synth_targets
 from oracle.ref_net import RefModel, load_numpy_state, state_to_numpy
-from test_oracle_golden import check_train_state
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")]
 
@@ -42,6 +47,46 @@ def oracle_grads(ref, x, pi, z):
     (pl + vl).backward()
     return ({n: p.grad.detach().numpy().copy() for n, p in ref.net.named_parameters()},
             (float(pl), float(vl), float(pl + vl)))
+
+
+def mask_flips(mk: dict, pre: dict, gpu_err: dict = None):
+    """Per masked ReLU: positions where the GPU's mask disagrees with the exact
+    (fp64) pre-activation's sign, and the largest |pre| there relative to the
+    layer's max|pre|."""
+    out = {}
+    for k, m in mk.items():
+        p = pre[k]
+        flip = (m > 0) != (p > 0)
+        n = int(flip.sum())
+        mx = float(np.abs(p).max()) + 1e-30
+        worst = float(np.abs(p[flip]).max()) if n else 0.0
+        out[k] = (n, worst, mx)
+    return out
+
+
+def flipped_block(flips: dict, blocks: int) -> int:
+    """Highest residual block whose gradients a flip perturbs (-1: none, blocks:
+    a head mask flipped, so every block is below it)."""
+    hi = -1
+    for k, (n, _, _) in flips.items():
+        if not n:
+            continue
+        if k == "a0":
+            hi = max(hi, 0)
+        elif k[0] in "hx":
+            hi = max(hi, int(k.lstrip("hxo")))
+        else:
+            hi = blocks
+    return hi
+
+
+def block_of(name: str, blocks: int) -> int:
+    """Residual block index of a parameter (stem: 0, heads: blocks)."""
+    if name.startswith("res_blocks."):
+        return int(name.split(".")[1])
+    if name.startswith("conv.") or name.startswith("bn."):
+        return 0
+    return blocks
 
 
 def gpu_masks(eng, blocks, B):
@@ -79,8 +124,27 @@ def test_gradients_match_oracle(tag, blocks, ch, B):
     losses = torch.empty(3, device=dev)
     eng.train_backward(torch.from_numpy(x).to(dev), torch.from_numpy(pi).to(dev), torch.from_numpy(z).to(dev),
                        losses)
-    want, (pl, vl) = masked_grads_fp64(st, blocks, ch, x, pi, z, gpu_masks(eng, blocks, B))
+    mk = gpu_masks(eng, blocks, B)
+    want, (pl, vl), pre = masked_grads_fp64(st, blocks, ch, x, pi, z, mk, return_pre=True)
     np.testing.assert_allclose(losses.cpu().numpy(), [pl, vl, pl + vl], rtol=1e-5, atol=1e-7)
+    # mask flips: GPU vs exact, and GPU vs the fp32 oracle's own masks
+    flips = mask_flips(mk, pre)
+    ref_masks = fp32_masks(st, blocks, ch, x)
+    nchw = lambda t: t.permute(0, 3, 1, 2).double().cpu().numpy()
+    gpu_pre = {"a0": nchw(eng.debug_tensor("a0", B))}
+    for i in range(blocks):
+        gpu_pre[f"h{i}"] = nchw(eng.debug_tensor("h", B, i))
+        gpu_pre[f"xo{i}"] = nchw(eng.debug_tensor("xo", B, i))
+    for n_ in ("fp", "fv", "hv"):
+        gpu_pre[n_] = eng.debug_tensor(n_, B).double().cpu().numpy()
+    for k, (n, worst, mx) in flips.items():
+        n32 = int(((mk[k] > 0) != (ref_masks[k] > 0)).sum())
+        # GPU's own error on this layer (post-ReLU values, where both are positive)
+        err = float(np.abs(gpu_pre[k] - np.maximum(pre[k], 0)).max()) if k in gpu_pre else 0.0
+        if n or n32:
+            print(f"mask flips {k}: gpu-vs-fp64 {n} (worst |pre| {worst:.2e} = {worst / mx:.1e} x max), "
+                  f"gpu-vs-fp32-oracle {n32}, gpu max err {err:.2e}")
+        assert worst <= max(1e-6 * mx, 2 * err), (k, n, worst, mx, err)
     ref = RefModel(blocks, ch)
     load_numpy_state(ref.net, st)
     want32, _ = oracle_grads(ref, x, pi, z)
@@ -97,24 +161,69 @@ def test_gradients_match_oracle(tag, blocks, ch, B):
     assert not bad, bad
 
 
+def fp32_masks(st, blocks, ch, x):
+    """The fp32 CPU oracle's own ReLU masks (train-mode forward), NCHW / [B, n]."""
+    net = RefModel(blocks, ch).net
+    load_numpy_state(net, st)
+    net.train()
+    out = {}
+    with torch.no_grad():
+        h = F.relu(net.bn(net.conv(torch.from_numpy(x))))
+        out["a0"] = h
+        for i, blk in enumerate(net.res_blocks):
+            hh = F.relu(blk.bn1(blk.conv1(h)))
+            out[f"h{i}"] = hh
+            h = F.relu(blk.bn2(blk.conv2(hh)) + h)
+            out[f"xo{i}"] = h
+        B = h.shape[0]
+        p = F.relu(net.policy_bn(net.policy_conv(h))).reshape(B, -1)
+        v = F.relu(net.value_bn(net.value_conv(h))).reshape(B, -1)
+        out["fp"], out["fv"], out["hv"] = p, v, F.relu(net.value_fc1(v))
+    return {k: (t > 0).double().numpy() for k, t in out.items()}
+
+
+def _golden_steps(g):
+    for s in range(2):
+        yield encode_batch(g[f"train/boards{s}"], g[f"train/players{s}"]), g[f"train/pi{s}"], g[f"train/z{s}"]
+
+
 @pytest.mark.parametrize("tag,blocks,ch", [("3x64", 3, 64), ("6x128", 6, 128)])
 def test_train_batch_matches_reference_goldens(tag, blocks, ch):
+    """Two train_batch steps vs the reference's own two steps.  Losses to 1e-5; the
+    optimizer state in torch format; params <= 1 % beyond 2e-5 for every block above
+    the highest GPU mask flip (flips: GPU masks vs the exact fp64 pre-activations of
+    the GPU's own params, see the module docstring); the flipped-below blocks are
+    reported here and gated by test_two_steps_match_fp64_trajectory."""
+    from oracle.ref_net import masked_grads_fp64
     g = load_golden(tag)
     m = make_model(blocks, ch, golden_state(g))
-    losses = []
-    for s in range(2):
-        x = encode_batch(g[f"train/boards{s}"], g[f"train/players{s}"])
-        li = m.train_batch(x, g[f"train/pi{s}"], g[f"train/z{s}"])
+    losses, hi = [], -1
+    for x, pi, z in _golden_steps(g):
+        st = state_to_numpy(m.net)
+        li = m.train_batch(x, pi, z)
         losses.append([li["policy_loss"], li["value_loss"], li["total_loss"]])
+        mk = gpu_masks(m.engine, blocks, len(x))
+        _, _, pre = masked_grads_fp64(st, blocks, ch, x, pi, z, mk, return_pre=True)
+        fl = mask_flips(mk, pre)
+        print({k: v[0] for k, v in fl.items() if v[0]})
+        hi = max(hi, flipped_block(fl, blocks))
     np.testing.assert_allclose(np.array(losses), g["train/losses"], rtol=1e-5, atol=1e-6)
-    # GPU vs reference: ReLU-mask flips add gradient noise on top of the thread-count
-    # effect (6x128: 1.3 % of params beyond 2e-5 after 2 steps, measured); the
-    # gradients themselves are gated at 2e-5 vs fp64 in test_gradients_match_oracle
-    # and clip+Adam at 2e-6 vs torch in test_clip_and_adam_match_torch.
-    check_train_state(m, g, max_bad_frac=0.03)
+    bad = tot = 0
+    for n, p in m.net.named_parameters():
+        idx = g[f"train/idx/{n}"]
+        d = np.abs(p.detach().reshape(-1).cpu().numpy()[idx] - g[f"train/param/{n}"])
+        assert d.max() <= 2 * 2 * 1e-3 * 1.01, (n, d.max())      # two Adam steps, any sign
+        nb = int((d > 2e-5).sum())
+        if block_of(n, blocks) > hi:
+            bad += nb
+            tot += d.size
+        elif nb:
+            print(f"{n}: {nb}/{d.size} beyond 2e-5 (below a mask flip at block {hi})")
+    print(f"highest flipped block {hi}: {bad}/{tot} compared elements beyond 2e-5")
+    assert bad <= 0.01 * tot, (bad, tot)
     sd = m.net.state_dict()
     for k in sd:
-        if "running" in k or "num_batches" in k:
+        if ("running" in k or "num_batches" in k) and block_of(k, blocks) > hi:
             # step-2 stats come from step-1 params that already differ (see above)
             np.testing.assert_allclose(sd[k].cpu().numpy(), g[f"train/buf/{k}"], atol=5e-4, rtol=1e-3, err_msg=k)
     assert int(sd["bn.num_batches_tracked"]) == int(g["train/buf/bn.num_batches_tracked"])
@@ -122,6 +231,44 @@ def test_train_batch_matches_reference_goldens(tag, blocks, ch):
     osd = m.optimizer.state_dict()
     assert len(osd["state"]) == len(list(m.net.parameters()))
     assert float(osd["state"][0]["step"]) == 2.0
+
+
+@pytest.mark.parametrize("tag,blocks,ch", [("3x64", 3, 64), ("6x128", 6, 128)])
+def test_two_steps_match_fp64_trajectory(tag, blocks, ch):
+    """Two GPU train_batch steps vs the exact trajectory: fp64 autograd with the
+    GPU's ReLU masks of each step + torch clip_grad_norm_(3.0) + Adam(1e-3, wd 1e-4)
+    in fp64.  Every param: <= 1 % of elements beyond 2e-5 (Adam's first steps move
+    every element by ~lr * sign(g), so only gradients within fp32 rounding of zero
+    may disagree)."""
+    from oracle.ref_net import RefNet, masked_grads_fp64
+    g = load_golden(tag)
+    st0 = golden_state(g)
+    m = make_model(blocks, ch, st0)
+    net64 = RefNet(blocks, ch).double()
+    load_numpy_state(net64, {k: (np.asarray(v, np.float64) if np.asarray(v).dtype.kind == "f" else v)
+                             for k, v in st0.items()})
+    opt = torch.optim.Adam(net64.parameters(), lr=1e-3, weight_decay=1e-4)
+    for x, pi, z in _golden_steps(g):
+        m.train_batch(x, pi, z)
+        mk = gpu_masks(m.engine, blocks, len(x))
+        st = {k: v.detach().numpy() for k, v in net64.state_dict().items()}
+        grads, _ = masked_grads_fp64(st, blocks, ch, x, pi, z, mk)
+        for n, p in net64.named_parameters():
+            p.grad = torch.from_numpy(grads[n])
+        torch.nn.utils.clip_grad_norm_(net64.parameters(), 3.0)
+        opt.step()
+    bad = tot = 0
+    want = dict(net64.named_parameters())
+    for n, p in m.net.named_parameters():
+        d = np.abs(p.detach().double().cpu().numpy() - want[n].detach().numpy())
+        nb = int((d > 2e-5).sum())
+        if nb:
+            print(f"{n}: {nb}/{d.size} beyond 2e-5, max {d.max():.2e}")
+        assert d.max() <= 2 * 2 * 1e-3 * 1.01, (n, d.max())
+        bad += nb
+        tot += d.size
+    print(f"{tag}: {bad}/{tot} params beyond 2e-5 of the fp64 trajectory")
+    assert bad <= 0.01 * tot, (bad, tot)
 
 
 def test_clip_and_adam_match_torch():
