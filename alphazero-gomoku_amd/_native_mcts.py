@@ -36,6 +36,7 @@ _SIGS = {
     "azg_mcts_get_pi": (_I32, [_P, _I32, _P]),
     "azg_mcts_clear": (_I32, [_P, _I32]),
     "azg_mcts_tree_size": (ctypes.c_int64, [_P, _I32]),
+    "azg_mcts_replay": (_I32, [_I32, _I32, _P, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _P]),
 }
 EXPORTS = tuple(_SIGS)
 
@@ -154,3 +155,20 @@ class SearchForest:
 
     def tree_size(self, g: int) -> int:
         return int(self.lib.azg_mcts_tree_size(self.h, g))
+
+
+def replay(rules: int, actions, start=None, player: int = 1, caps=(0, 0), board: int = 15):
+    """Play `actions` with the native rule engine (azg_mcts_replay): per move the
+    board [n, board*board] int8, captured pairs [n, 2], winner [n], game over [n]."""
+    lib = load_library()
+    acts = np.ascontiguousarray(np.asarray(actions, dtype=np.int32).reshape(-1))
+    n = int(acts.size)
+    A = board * board
+    st = None if start is None else np.ascontiguousarray(np.asarray(start, dtype=np.int8).reshape(-1))
+    boards = np.zeros((n, A), np.int8)
+    cap = np.zeros((n, 2), np.int32)
+    win = np.zeros(n, np.int32)
+    over = np.zeros(n, np.int32)
+    _check(lib.azg_mcts_replay(int(rules), int(board), None if st is None else _addr(st), int(player), int(caps[0]),
+                               int(caps[1]), _addr(acts), n, _addr(boards), _addr(cap), _addr(win), _addr(over)))
+    return boards, cap, win, over.astype(bool)

@@ -65,9 +65,12 @@ struct KeyHash {
     size_t operator()(const Key& k) const
     {
         uint64_t h = 1469598103934665603ull;
-        const uint64_t* w = reinterpret_cast<const uint64_t*>(k.b.data());
+        // 8-byte words through memcpy: the key bytes have no 8-byte alignment (a
+        // reinterpret_cast load was undefined behaviour -- found by the UBSan driver)
         for (size_t i = 0; i < (MAXN + 1) / 8; ++i) {
-            h ^= w[i];
+            uint64_t wi;
+            std::memcpy(&wi, k.b.data() + 8 * i, sizeof(wi));
+            h ^= wi;
             h *= 1099511628211ull;
             h ^= h >> 29;
         }
@@ -581,6 +584,35 @@ int64_t azg_mcts_tree_size(const azg_mcts* h, int32_t g)
 {
     if (!h || g < 0 || g >= (int)h->games.size()) return -1;
     return (int64_t)h->games[g].nodes.size();
+}
+
+int32_t azg_mcts_replay(int32_t rules, int32_t board, const int8_t* start, int32_t player, int32_t cap1,
+                        int32_t cap2, const int32_t* actions, int32_t n, int8_t* boards_out, int32_t* caps_out,
+                        int32_t* winner_out, int32_t* over_out)
+{
+    if ((rules != 0 && rules != 1) || board < 5 || board * board > MAXN || !actions || n < 0)
+        return fail("azg_mcts_replay: bad arguments");
+    State s;
+    s.n = board;
+    s.rules = rules;
+    const int A = board * board;
+    for (int i = 0; i < A; ++i) s.board[i] = start ? start[i] : 0;
+    s.player = player;
+    s.cap[1] = cap1;
+    s.cap[2] = cap2;
+    for (int k = 0; k < n; ++k) {
+        const int a = actions[k];
+        if (a < 0 || a >= A || s.board[a] != 0) return fail("azg_mcts_replay: illegal move");
+        s.do_move(a);
+        if (boards_out) std::memcpy(boards_out + (size_t)k * A, s.board.data(), A);
+        if (caps_out) {
+            caps_out[2 * k] = s.cap[1];
+            caps_out[2 * k + 1] = s.cap[2];
+        }
+        if (winner_out) winner_out[k] = s.winner();
+        if (over_out) over_out[k] = s.game_over() ? 1 : 0;
+    }
+    return 0;
 }
 
 }  // extern "C"

@@ -264,12 +264,24 @@ class NativeEval:
     """Evaluation games between two networks (reference train.py:418-487 game body,
     = train.eval_game_gen): every game keeps one native tree per network; the side to
     move searches its own tree and plays argmax(pi).  Each round the pending leaves
-    of all games are evaluated with ONE forward per network."""
+    of all games are evaluated with ONE forward per network.
 
-    def __init__(self, evaluators: dict, game_class, n_games: int, n_simulations: int, cpuct: float = 1.0,
-                 batch_size: int = 32, n_threads: int = 0):
-        self.tags = list(evaluators)
+    ``evaluators`` {tag: evaluate(X float planes) -> (probs, values)} (synchronous), or
+    ``evaluator_factories`` {tag: factory(capacity)} giving pinned int8-board
+    evaluators (PyTorchModel.board_evaluator): the leaves leave the search as int8
+    boards, are encoded on the GPU, both networks' batches are submitted before
+    either is waited on, and the masked priors come back (same results: the
+    search's own masking of an already-masked prior is the identity)."""
+
+    def __init__(self, evaluators: Optional[dict], game_class, n_games: int, n_simulations: int,
+                 cpuct: float = 1.0, batch_size: int = 32, n_threads: int = 0,
+                 evaluator_factories: Optional[dict] = None):
+        if (evaluators is None) == (evaluator_factories is None):
+            raise ValueError("give exactly one of evaluators / evaluator_factories")
+        self.tags = list(evaluators if evaluators is not None else evaluator_factories)
         self.evaluators = evaluators
+        self.boards_ev = None if evaluator_factories is None else \
+            {t: f(n_games * batch_size) for t, f in evaluator_factories.items()}
         self.n_games = n_games
         g0 = game_class()
         self.forests = {t: SearchForest(n_games, n_simulations, rules=_rules_of(game_class), board=g0.size,
@@ -304,7 +316,11 @@ class NativeEval:
                 start(g)
         while to_move:
             t0 = time.perf_counter()
-            ns = {t: f.advance() for t, f in self.forests.items()}
+            if self.boards_ev is None:
+                ns = {t: f.advance() for t, f in self.forests.items()}
+            else:
+                ns = {t: f.advance_boards(self.boards_ev[t].boards, self.boards_ev[t].players)
+                      for t, f in self.forests.items()}
             self.search_seconds += time.perf_counter() - t0
             for g in sorted(to_move):
                 f = self.forests[to_move[g]]
@@ -319,15 +335,22 @@ class NativeEval:
                     del to_move[g]
                 else:
                     start(g)
+            t0 = time.perf_counter()
+            if self.boards_ev is not None:     # both networks' batches in flight, then wait
+                for t, n in ns.items():
+                    if n:
+                        self.boards_ev[t].submit(n)
             for t, n in ns.items():
                 if not n:
                     continue
                 f = self.forests[t]
-                t0 = time.perf_counter()
-                probs, values = self.evaluators[t](f.leaves[:n])
-                self.nn_seconds += time.perf_counter() - t0
+                if self.boards_ev is None:
+                    probs, values = self.evaluators[t](f.leaves[:n])
+                else:
+                    probs, values = self.boards_ev[t].wait()
                 self.boards += n
                 self.forwards += 1
                 self.max_batch = max(self.max_batch, n)
                 f.feed(probs, values)
+            self.nn_seconds += time.perf_counter() - t0
         return winners

@@ -60,11 +60,12 @@ def eval_game_gen(mcts_new, mcts_best, game, new_starts: bool):
 
 def evaluate_models(model_new: PyTorchModel, model_best: PyTorchModel, game_name: str = "gomoku",
                     n_games: int = 20, n_simulations: int = 100, cpuct: float = 1.0,
-                    native: bool = True) -> Tuple[int, float, int]:
+                    native: bool = True, record: Optional[list] = None) -> Tuple[int, float, int]:
     """(new_wins, win_rate, draws) over n_games (sharded across ranks), each opened
     by one random move in the centre 9x9 (train.py:440-445), new model first on
     even game indices.  native=True: both searches in C++ (mcts/native_mcts.NativeEval);
-    native=False: Python searches under BatchedSelfPlay."""
+    native=False: Python searches under BatchedSelfPlay.  ``record`` (optional list)
+    receives this rank's finished games."""
     size = model_new.board_size
     center, radius = size // 2, 4
     games, starts = [], []
@@ -77,8 +78,14 @@ def evaluate_models(model_new: PyTorchModel, model_best: PyTorchModel, game_name
         winners = []
     elif native:
         from mcts.native_mcts import NativeEval
-        arena = NativeEval({"new": model_new.predict, "best": model_best.predict}, GameClass, len(games),
-                           n_simulations, cpuct=cpuct)
+        if hasattr(model_new, "board_evaluator") and hasattr(model_best, "board_evaluator"):
+            # HIP models: int8 leaves, on-GPU encoding, both networks' batches in flight
+            arena = NativeEval(None, GameClass, len(games), n_simulations, cpuct=cpuct,
+                               evaluator_factories={"new": model_new.board_evaluator,
+                                                    "best": model_best.board_evaluator})
+        else:
+            arena = NativeEval({"new": model_new.predict, "best": model_best.predict}, GameClass, len(games),
+                               n_simulations, cpuct=cpuct)
         winners = arena.play(games, ["new" if s else "best" for s in starts])
     else:
         gens = []
@@ -87,9 +94,12 @@ def evaluate_models(model_new: PyTorchModel, model_best: PyTorchModel, game_name
             mb = MCTS(GameClass, n_simulations, model_best, cpuct=cpuct, add_dirichlet_noise=False)
             gens.append(eval_game_gen(mn, mb, game, new_starts))
         winners = BatchedSelfPlay({"new": model_new, "best": model_best}).run(gens)
+    if record is not None:
+        record.extend(games)
     new_wins = sum(1 for w, s in zip(winners, starts) if (w == 1 and s) or (w == 2 and not s))
     draws = sum(1 for w in winners if w == 0)
-    dev = model_new.engine.device
+    eng = getattr(model_new, "engine", None)
+    dev = eng.device if eng is not None else "cpu"
     tot = torch.tensor([new_wins, draws], dtype=torch.int64, device=dev)
     D.allreduce_sum_(tot)
     new_wins, draws = (int(v) for v in tot.tolist())

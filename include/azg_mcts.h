@@ -93,6 +93,16 @@ int32_t azg_mcts_get_pi(azg_mcts* h, int32_t g, float* pi);
 int32_t azg_mcts_clear(azg_mcts* h, int32_t g);
 int64_t azg_mcts_tree_size(const azg_mcts* h, int32_t g);
 
+/* Rule-engine known-answer hook (the search's own State): from `start` (board*board
+ * int8, NULL = empty), side to move `player` and captured pairs (cap1, cap2), play
+ * `actions[0..n)` with the Gomoku (rules 0, games/gomoku.py:60-193) or Pente (rules
+ * 1, games/pente.py:57-230) rules; after each move k write the board
+ * (boards_out[k], may be NULL), the captured-pair counts (caps_out[2k..2k+1]), the
+ * winner and the game-over flag.  Fails on an illegal move. */
+int32_t azg_mcts_replay(int32_t rules, int32_t board, const int8_t* start, int32_t player, int32_t cap1,
+                        int32_t cap2, const int32_t* actions, int32_t n, int8_t* boards_out, int32_t* caps_out,
+                        int32_t* winner_out, int32_t* over_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -178,6 +178,13 @@ def test_native_eval_equals_python_eval():
     arena = NativeEval({"new": mn_model.predict, "best": mb_model.predict}, Gomoku, len(openings), 30, cpuct=1.3)
     games_n = fresh()
     w_native = arena.play(games_n, ["new" if s else "best" for s in starts])
+    # the pinned int8-board evaluator path (both networks' batches in flight)
+    arena_b = NativeEval(None, Gomoku, len(openings), 30, cpuct=1.3,
+                         evaluator_factories={"new": lambda c: FakeBoardEvaluator(mn_model, c),
+                                              "best": lambda c: FakeBoardEvaluator(mb_model, c)})
+    games_b = fresh()
+    assert arena_b.play(games_b, ["new" if s else "best" for s in starts]) == w_native
+    assert [g.move_history for g in games_b] == [g.move_history for g in games_n]
     gens = []
     games_p = fresh()
     for game, s in zip(games_p, starts):
