@@ -393,12 +393,12 @@ int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst)
 {
     const int C = h->C;
     const float* P = h->params;
-    AZG_TRY(launch_pack_stem(P + h->poff[h->t_stem_w], h->wstem, C, st), "repack: stem");
-    AZG_TRY(launch_pack_fc(P + h->poff[h->t_pfc_w], P + h->poff[h->t_vfc1_w], h->wfc, st), "repack: head fc");
-    if (h->NB > 0)   // every residual conv in one launch (and its dgrad packing when training)
-        AZG_TRY(launch_pack_convs(P, h->conv_off_dev, 2 * h->NB, h->wpack, dgrad_dst, C, st), "repack: convs");
-    AZG_TRY(launch_fold_bn(P, h->bn, h->bn_desc_dev, (int)h->bn_desc.size(), h->scale, h->shift, st),
-            "repack: fold_bn");
+    // stem, head FCs, every residual conv (+ its dgrad packing when training) and
+    // the eval BN fold: one launch
+    AZG_TRY(launch_repack_all(P, h->conv_off_dev, 2 * h->NB, h->wpack, dgrad_dst, C, P + h->poff[h->t_stem_w],
+                              h->wstem, P + h->poff[h->t_pfc_w], P + h->poff[h->t_vfc1_w], h->wfc, h->bn,
+                              h->bn_desc_dev, (int)h->bn_desc.size(), h->scale, h->shift, st),
+            "repack");
     return 0;
 }
 

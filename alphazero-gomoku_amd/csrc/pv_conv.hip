@@ -849,9 +849,14 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         azg::g_tower_spin_limit = value < 0 ? (1u << 22) : (unsigned)value;
         return prev;
     }
+    if (key == 17) {  // persistent tower claim granularity (0 one tile, 1 one M tile x all N tiles)
+        const int prev = azg::g_tower_group;
+        azg::g_tower_group = value ? 1 : 0;
+        return prev;
+    }
     if (key == 16) {  // train: wgrad kernel (1 K-contiguous staging, default; 0 row staging, A/B)
         const int prev = azg::g_wgrad_kernel;
-        azg::g_wgrad_kernel = value ? 1 : 0;
+        if (value >= 0 && value <= 2) azg::g_wgrad_kernel = value;
         return prev;
     }
     if (key == 13) {  // train: wgrad K chunk (32 default, 16 A/B)

@@ -51,6 +51,7 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
                         const float* shift, const int* out_off, int M, unsigned* sync, unsigned* status,
                         hipStream_t st, float** result);
 extern unsigned g_tower_spin_limit;
+extern int g_tower_group;
 hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const float* scale,
                        const float* shift, float* out, int B, hipStream_t st, const int8_t* boards = nullptr,
                        const int8_t* players = nullptr);
@@ -69,6 +70,10 @@ hipError_t launch_pack_convs(const float* params, const int64_t* offs, int nl, f
                              hipStream_t st);
 hipError_t launch_pack_stem(const float* w, float* ws, int C, hipStream_t st);
 hipError_t launch_transpose(const float* src, float* dst, int R, int Cc, hipStream_t st);
+hipError_t launch_repack_all(const float* params, const int64_t* conv_offs, int nl, float* wp, float* wd, int C,
+                             const float* stem_w, float* ws, const float* wpf, const float* wv1, float* wfc,
+                             const float* stats, const void* desc, int nbn, float* scale, float* shift,
+                             hipStream_t st);
 hipError_t launch_fold_bn(const float* params, const float* stats, const void* desc, int nlayers,
                           float* scale, float* shift, hipStream_t st);
 

@@ -68,6 +68,83 @@ __global__ void fold_bn_kernel(const float* __restrict__ params, const float* __
     }
 }
 
+// Every re-pack of repack() in ONE launch (it runs at the start of every train step,
+// on the critical path): blockIdx.y < nl packs residual conv l (as pack_convs_kernel),
+// y == nl the stem, y == nl + 1 the head FCs, y == nl + 2 folds the eval BN (one
+// layer per blockIdx.x).  Same per-element arithmetic as the separate kernels.
+struct RepackArgs {
+    const float* params;
+    const int64_t* conv_offs;
+    float* wp;
+    float* wd;
+    int C, nl;
+    const float* stem_w;
+    float* ws;
+    const float* wpf;
+    const float* wv1;
+    float* wfc;
+    const float* stats;
+    const BnDesc* desc;
+    int nbn;
+    float* scale;
+    float* shift;
+};
+
+__global__ __launch_bounds__(256) void repack_all_kernel(const RepackArgs a)
+{
+    const int y = blockIdx.y;
+    const int C = a.C;
+    const int stride = gridDim.x * blockDim.x;
+    const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (y < a.nl) {
+        const int total = 9 * C * C, cg_n = C / 32;
+        const float* w = a.params + a.conv_offs[y];
+        float* wpl = a.wp + (size_t)y * total;
+        float* wdl = a.wd ? a.wd + (size_t)y * total : nullptr;
+        for (int idx = i0; idx < total; idx += stride) {
+            const int k = idx & 31, n = (idx >> 5) % C, kc = idx / (32 * C);
+            const int tap = kc / cg_n, c2 = (kc - tap * cg_n) * 32 + k;
+            wpl[idx] = w[(n * C + c2) * 9 + tap];
+            if (wdl) wdl[idx] = w[(c2 * C + n) * 9 + (8 - tap)];
+        }
+    } else if (y == a.nl) {
+        for (int idx = i0; idx < 27 * C; idx += stride) a.ws[idx] = a.stem_w[(idx % C) * 27 + idx / C];
+    } else if (y == a.nl + 1) {
+        for (int idx = i0; idx < FC_OUT * FC_KP; idx += stride) {
+            const int j = idx / FC_KP, k = idx - j * FC_KP;
+            float v = 0.f;
+            if (j < ACTIONS) {
+                if (k < 2 * PIX) v = a.wpf[j * 2 * PIX + k];
+            } else if (k < PIX) {
+                v = a.wv1[(j - ACTIONS) * PIX + k];
+            }
+            a.wfc[idx] = v;
+        }
+    } else if (blockIdx.x < (unsigned)a.nbn) {
+        const BnDesc d = a.desc[blockIdx.x];
+        for (int c = threadIdx.x; c < d.c; c += blockDim.x) {
+            const float invstd = 1.0f / sqrtf(a.stats[d.stat_off + d.c + c] + BN_EPS);
+            const float alpha = invstd * a.params[d.gamma_off + c];
+            a.scale[d.out_off + c] = alpha;
+            a.shift[d.out_off + c] = a.params[d.beta_off + c] - a.stats[d.stat_off + c] * alpha;
+        }
+    }
+}
+
+hipError_t launch_repack_all(const float* params, const int64_t* conv_offs, int nl, float* wp, float* wd, int C,
+                             const float* stem_w, float* ws, const float* wpf, const float* wv1, float* wfc,
+                             const float* stats, const void* desc, int nbn, float* scale, float* shift,
+                             hipStream_t st)
+{
+    RepackArgs a{params, conv_offs, wp, wd, C, nl, stem_w, ws, wpf, wv1, wfc, stats, (const BnDesc*)desc, nbn,
+                 scale, shift};
+    int nb = (9 * C * C + 255) / 256;
+    nb = nb > 256 ? 256 : nb;
+    nb = nb < nbn ? nbn : nb;
+    hipLaunchKernelGGL(repack_all_kernel, dim3(nb, nl + 3), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 static inline int nblk(int total) { int b = (total + 255) / 256; return b > 4096 ? 4096 : b; }
 
 hipError_t launch_pack_convs(const float* params, const int64_t* offs, int nl, float* wp, float* wd, int C,

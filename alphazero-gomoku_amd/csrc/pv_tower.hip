@@ -50,12 +50,16 @@ struct TowerArgs {
     unsigned* sync;      // [0] work counter, [1] error word, [4..] per-(layer, M tile) counters
     unsigned* status;    // sticky host-mapped status word of the handle (azg_pv_status); may be null
     unsigned spin_limit; // polls before a dependency wait is declared timed out
+    int group;           // 1: a claim is one (M, N) tile; NTN: one M tile with all its N
+                         // tiles, run back to back by the claiming workgroup (the second
+                         // N tile's halo rows are hits in that XCD's L2)
     int abl;             // timing studies only (0 in the product; results not valid otherwise):
                          // bit 1 skips the dependency wait + acquire, bit 2 the publish drain
 };
 
 constexpr unsigned kSpinLimit = 1u << 22;    // x s_sleep(2): seconds, far above any tile time
 unsigned g_tower_spin_limit = kSpinLimit;    // tuning key 14 (tests: 0 forces the timeout path)
+int g_tower_group = 1;                       // tuning key 17: 1 (default) = claim an M tile with all its N tiles
 
 // waves per SIMD the register budget is sized for: 4 (128 VGPRs) for the one-
 // accumulator tiles; 2 (256 VGPRs, one workgroup per CU) for 128-wide N tiles
@@ -73,7 +77,8 @@ __global__ __launch_bounds__(64 * NW_, tower_min_waves<BN_>()) void conv_tower(c
 
     const int tid = threadIdx.x;
     const int mtiles = (a.M + T::BM - 1) / T::BM;
-    const int tpl = mtiles * NTN;
+    const int grp = a.group;                     // N tiles per claim (1 or NTN)
+    const int tpl = mtiles * (NTN / grp);        // claims per layer
     const int total = tpl * a.nlayers;
     unsigned* work = a.sync;
     unsigned* err = a.sync + 1;
@@ -84,7 +89,7 @@ __global__ __launch_bounds__(64 * NW_, tower_min_waves<BN_>()) void conv_tower(c
     int w = s_claim[0];
     while (w < total) {
         const int l = w / tpl, t = w - l * tpl;
-        const int mt = t / NTN, nt = t - mt * NTN;
+        const int mt = t / (NTN / grp), nt0 = (t - mt * (NTN / grp)) * grp;
         __syncthreads();                          // every wave has read s_claim
         if (tid == 0) {
             // next claim now: its latency overlaps this tile (read after the tile)
@@ -115,13 +120,17 @@ __global__ __launch_bounds__(64 * NW_, tower_min_waves<BN_>()) void conv_tower(c
         __syncthreads();
         const TowerLayer& Ly = a.L[l];
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Ly.out, (short)0, a.act_bytes, 0x00020000);
-        halo_tile<C, BN_, WM_, TM_, NW_, EPI_BN_OPTRES_RELU, true, 0, VAR>(Ly.in, Ly.wp, Ly.scale, Ly.shift, Ly.resid, Ly.out,
-                                                                  rs, a.M, mt * T::BM, nt * T::BN, smem);
+        for (int nt = nt0; nt < nt0 + grp; ++nt) {
+            if (nt > nt0) __syncthreads();        // the previous tile's epilogue is done with LDS
+            halo_tile<C, BN_, WM_, TM_, NW_, EPI_BN_OPTRES_RELU, true, 0, VAR>(Ly.in, Ly.wp, Ly.scale, Ly.shift, Ly.resid,
+                                                                      Ly.out, rs, a.M, mt * T::BM, nt * T::BN, smem);
+        }
         if (!(a.abl & 2)) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
             __syncthreads();
         }
-        if (tid == 0) __hip_atomic_fetch_add(cnt + (size_t)l * mtiles + mt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) __hip_atomic_fetch_add(cnt + (size_t)l * mtiles + mt, (unsigned)grp, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
         w = s_claim[0];
     }
 }
@@ -176,6 +185,7 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     a.sync = sync;
     a.status = status;
     a.spin_limit = g_tower_spin_limit;
+    a.group = g_tower_group ? C / (shape == 8 || shape == 5 ? 64 : 128) : 1;
     a.abl = g_tower_ablation;
     float* X = act[0];
     float* H = act[1];

@@ -1125,19 +1125,21 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         R(snap(NB - i));
     }
     // ---- stem backward ----
-    R(reuse(0));
-    R(reuse(1));                 // joins the side stream: every conv weight grad is done
+    // overlaps the last conv weight grads still on the side stream: its dz goes to
+    // DH (no pending weight grad reads DH), the join comes after it
     if (NB == 0) {
         R(bwd_reduce(w->gX, w->a0, w->z0, h->bn_stem));
         bwd_nt = ntile;
     }
     R(bwd_fin(h->bn_stem, bwd_nt));
-    R(bwd_apply(w->gX, w->a0, w->z0, h->bn_stem, w->DZ, nullptr));
-    hipLaunchKernelGGL((stem_wgrad_kernel<C>), dim3(B), dim3(256), 0, st, x, w->DZ, w->spart);
+    R(bwd_apply(w->gX, w->a0, w->z0, h->bn_stem, w->DH, nullptr));
+    hipLaunchKernelGGL((stem_wgrad_kernel<C>), dim3(B), dim3(256), 0, st, x, w->DH, w->spart);
     AZG_CK(hipGetLastError(), "train: stem_wgrad");
     hipLaunchKernelGGL(reduce_partials_kernel, dim3((27 * C + 63) / 64), dim3(256), 0, st, w->spart, B, 27 * C,
                        G + h->poff[h->t_stem_w], nullptr, 27 * C, 1, C);
     AZG_CK(hipGetLastError(), "train: stem_wgrad_reduce");
+    R(reuse(0));
+    R(reuse(1));                 // joins the side stream: every conv weight grad is done
 #undef R
     return 0;
 }

@@ -146,7 +146,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_mfma(
 // ds_read_b128 instead of one ds_read_b32 per MFMA: per 32-pixel chunk a wave
 // issues 16 fragment reads for its 64 MFMAs (was 64).  K order per output: chunks
 // in order, within a chunk pixel pairs (s, 16+s), s = 0..15.
-template <int C>
+// PF2: global loads issued two chunks ahead (two register sets, the loop unrolled
+// by two so the sets are static): a load has a whole chunk of MFMAs more to land.
+template <int C, bool PF2 = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_t(
     const float* __restrict__ dz, const float* __restrict__ x, float* __restrict__ slab, int M, int rows_per_split)
 {
@@ -176,7 +178,32 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_t(
 
     const bool stager = tid < NBLK;
     const int pb = tid % (BK / 4), cb = tid / (BK / 4);     // pixel block, channel block
-    f32x4 ra[4], rb[4];
+    f32x4 ra[4], rb[4], ra2[4], rb2[4];
+    auto gload_to = [&](int kc, f32x4 (&xa)[4], f32x4 (&xb)[4]) {
+        if (!stager) return;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = mbeg + kc * BK + 4 * pb + i;
+            if (m < mend) {
+                const int po = pad_off(m, C);
+                xa[i] = *(const f32x4*)(dz + po + co0 + 4 * cb);
+                xb[i] = *(const f32x4*)(x + po + toff + ci0 + 4 * cb);
+            } else {
+                xa[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                xb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    };
+    auto lstore_from = [&](int buf, const f32x4 (&xa)[4], const f32x4 (&xb)[4]) {
+        if (!stager) return;
+        float* a = As + buf * BT * LDT + (4 * cb) * LDT + 4 * pb;
+        float* b = Bs + buf * BT * LDT + (4 * cb) * LDT + 4 * pb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            *(f32x4*)(a + j * LDT) = f32x4{xa[0][j], xa[1][j], xa[2][j], xa[3][j]};
+            *(f32x4*)(b + j * LDT) = f32x4{xb[0][j], xb[1][j], xb[2][j], xb[3][j]};
+        }
+    };
     auto gload = [&](int kc) {
         if (!stager) return;
 #pragma unroll
@@ -212,15 +239,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_t(
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     const int r32 = lane & 31, h = lane >> 5;
-    if (nch > 0) {
-        gload(0);
-        lstore(0);
-    }
-    __syncthreads();
-    for (int kc = 0; kc < nch; ++kc) {
-        const int cur = kc & 1;
-        if (kc + 1 < nch) gload(kc + 1);
-        __builtin_amdgcn_sched_barrier(0);
+    auto compute = [&](int cur) {
         const float* Ab = As + cur * BT * LDT + (wm * W + r32) * LDT + h * (BK / 2);
         const float* Bb = Bs + cur * BT * LDT + (wn * W + r32) * LDT + h * (BK / 2);
 #pragma unroll
@@ -238,8 +257,41 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_t(
                     for (int j = 0; j < TT; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s4], b[j][s4], acc[i][j], 0, 0, 0);
         }
-        if (kc + 1 < nch) lstore(cur ^ 1);
+    };
+    if constexpr (PF2) {
+        // chunk j lives in register set j & 1 from its load (two chunks ahead) to its
+        // LDS store (end of chunk j - 1)
+        if (nch > 0) {
+            gload_to(0, ra, rb);
+            lstore_from(0, ra, rb);
+        }
+        if (nch > 1) gload_to(1, ra2, rb2);
         __syncthreads();
+        auto iter = [&](int kc, f32x4 (&la)[4], f32x4 (&lb)[4], f32x4 (&sa)[4], f32x4 (&sb)[4]) {
+            if (kc + 2 < nch) gload_to(kc + 2, la, lb);
+            __builtin_amdgcn_sched_barrier(0);
+            compute(kc & 1);
+            if (kc + 1 < nch) lstore_from((kc + 1) & 1, sa, sb);
+            __syncthreads();
+        };
+        for (int kc = 0; kc < nch; kc += 2) {
+            iter(kc, ra, rb, ra2, rb2);
+            if (kc + 1 < nch) iter(kc + 1, ra2, rb2, ra, rb);
+        }
+    } else {
+        if (nch > 0) {
+            gload(0);
+            lstore(0);
+        }
+        __syncthreads();
+        for (int kc = 0; kc < nch; ++kc) {
+            const int cur = kc & 1;
+            if (kc + 1 < nch) gload(kc + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            compute(cur);
+            if (kc + 1 < nch) lstore(cur ^ 1);
+            __syncthreads();
+        }
     }
 
     float* out = slab + ((size_t)split * 9 + tap) * C * C;
@@ -291,16 +343,22 @@ static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, f
     using T = WgTile<C, BK>;
     if (S % 8) return hipErrorInvalidValue;           // wgrad_splits guarantees S % 8 == 0
     dim3 grid(S * 9 * T::NT * T::NT);
-    if (g_wgrad_kernel == 1 && BK == 32) {
+    if (g_wgrad_kernel >= 1 && BK == 32) {
         constexpr int lds = 2 * 2 * T::BT * (32 + 4) * 4;
         static bool attr_t = false;
         if (!attr_t) {
             hipError_t e = hipFuncSetAttribute((const void*)conv3x3_wgrad_t<C>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)conv3x3_wgrad_t<C, true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
             if (e != hipSuccess) return e;
             attr_t = true;
         }
-        hipLaunchKernelGGL((conv3x3_wgrad_t<C>), grid, dim3(256), lds, st, dz, x, slab, M, rps);
+        if (g_wgrad_kernel == 2)
+            hipLaunchKernelGGL((conv3x3_wgrad_t<C, true>), grid, dim3(256), lds, st, dz, x, slab, M, rps);
+        else
+            hipLaunchKernelGGL((conv3x3_wgrad_t<C>), grid, dim3(256), lds, st, dz, x, slab, M, rps);
     } else {
         static bool attr_done = false;
         if (!attr_done) {

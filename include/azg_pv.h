@@ -160,6 +160,10 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *   key 13: train wgrad K chunk in pixels (32 default; 16 for A/B timing, C=128);
  *   key 16: train conv weight-grad kernel (1 = K-contiguous staging with 16-B
  *          fragment reads, default; 0 = row staging with 4-B reads, A/B timing);
+ *   key 17: persistent-tower claim granularity (1 = one M tile with all its N
+ *          tiles, run back to back by the claiming workgroup, default: the second
+ *          tile's halo rows hit the XCD's L2, +2 % at B = 512 and 4096, measured;
+ *          0 = one 128x64 tile per claim); bitwise identical results;
  *   key 14: persistent-tower dependency spin bound (tests only: 0 makes every
  *          dependency wait time out at once, exercising the error path; -1
  *          restores the default).

@@ -46,7 +46,8 @@ def main():
         values = torch.empty((B, 1), device="cuda")
         flop = 2 * 225 * C * 9 * C * B * 2 * args.blocks
         row = {"batch": B}
-        variants = [("layers", 0, 5, 0, 0), ("tower64", 1, 5, 0, 0), ("tower128", 1, 8, 0, 0)]
+        variants = [("layers", 0, 5, 0, 0), ("tower64", 1, 5, 0, 0), ("tower128", 1, 8, 0, 0),
+                    ("tower128_group", 1, 8, 0, 0)]
         variants += [(f"tower128_abl{a}", 1, 8, int(a), 0) for a in args.ablations.split(",") if a]
         variants += [(f"tower_s{t}", 1, int(t), 0, 0) for t in args.shapes.split(",") if t]
         variants += [(f"tower128_v{v}", 1, 8, 0, int(v)) for v in args.vars.split(",") if v]
@@ -55,6 +56,7 @@ def main():
             lib.azg_pv_set_tuning(6, shape)
             lib.azg_pv_set_tuning(8, abl)
             lib.azg_pv_set_tuning(10, var)
+            lib.azg_pv_set_tuning(17, 1 if name.endswith("_group") else 0)   # claim an M tile x all N tiles
             for _ in range(2):
                 eng.forward_into(x, probs, values)
             best_dev, best_wall = None, None
