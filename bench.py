@@ -271,6 +271,15 @@ def roofline_from_profile(prof, boards, blocks, ch, kname_tower, kname_layer):
     return out
 
 
+def load_traffic_record():
+    try:
+        d = json.load(open(os.path.join(REPO, "profiles", "conv_traffic.json")))
+        d.setdefault("boards_per_launch", BATCH)
+        return d
+    except Exception:
+        return None
+
+
 def load_traffic(kernel, config):
     """HBM bytes per launch of `kernel` from the committed PMC pass
     (profiles/conv_traffic.json, scripts/summarize_profile.py), or None."""
@@ -495,7 +504,15 @@ def main():
     ap.add_argument("--big-train-steps", type=int, default=5)
     ap.add_argument("--pente-games", type=int, default=64)
     ap.add_argument("--pente-moves", type=int, default=3, help="move window of the configs[4] Pente self-play")
+    ap.add_argument("--skip-forward", action="store_true", help="profiling runs: no configs[1] sub-leg")
+    ap.add_argument("--tune", action="append", default=[], help="KEY=VALUE tuning key (A/B and profiling runs)")
     args = ap.parse_args()
+    if args.tune:
+        import _native
+        lib = _native.load_library()
+        for kv in args.tune:
+            k, v = (int(t) for t in kv.split("="))
+            lib.azg_pv_set_tuning(k, v)
 
     rank, world, local, dist = dist_setup(args.gpus)
     dev = torch.device("cuda", local)
@@ -506,10 +523,13 @@ def main():
     torch.manual_seed(0)
     model = PyTorchModel(board_size=15, device=str(dev), n_res_blocks=BLOCKS, channels=CHANNELS)
 
-    log("configs[1] forward leg")
-    fwd = forward_leg(model, args, rank, world, dist, dev, local)
-    sp = selfplay_leg(model, args, rank, world, dist, dev, local)
-    log(f"self-play done: {sp['boards_per_s']:.0f} boards/s over {sp['seconds']:.1f} s")
+    fwd = sp = None
+    if not args.skip_forward:
+        log("configs[1] forward leg")
+        fwd = forward_leg(model, args, rank, world, dist, dev, local)
+    if args.sp_games > 0:
+        sp = selfplay_leg(model, args, rank, world, dist, dev, local)
+        log(f"self-play done: {sp['boards_per_s']:.0f} boards/s over {sp['seconds']:.1f} s")
     train = None
     if args.train_steps > 0:
         log("configs[3] train leg")
@@ -529,6 +549,22 @@ def main():
     if rank != 0:
         dist.destroy_process_group()
         return
+    if sp is None:      # profiling runs only (--sp-games 0): not the headline metric
+        print(json.dumps({"profiling_run": True, "forward_b512": fwd, "train": train, "pente_10x256": big}),
+              flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    if sp["roofline"] is not None:
+        # HBM bytes of the tower, from the PMC pass at B=512 (profiles/conv_traffic.json),
+        # scaled per board to the average tower launch of this run
+        t = load_traffic_record()
+        if t and t.get("kernel") == "tower" and sp["roofline"].get("boards"):
+            per_board = t["hbm_bytes_per_launch"] / t["boards_per_launch"]
+            sp["roofline"]["traffic"] = round(per_board * sp["roofline"]["boards"] / sp["roofline"]["launches"])
+            sp["roofline"]["traffic_basis"] = (f"PMC FETCH_SIZE x2 + WRITE_SIZE of the tower at B=512 "
+                                               f"({t['tag']}), {per_board / 1e6:.3f} MB per board, x boards per "
+                                               f"launch of this run")
 
     out = {
         "metric": METRIC,
