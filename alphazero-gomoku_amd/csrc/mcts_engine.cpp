@@ -176,6 +176,26 @@ struct Node {
     float V = 0.f;
 };
 
+// Node storage in fixed chunks: growing never moves a node.  (A std::vector<Node>
+// doubled by reallocation: at 16 k nodes of 2.9 KB that is a 47 MB copy per tree,
+// and the trees of one forest cross the doubling sizes in the same round -- the
+// self-play timeline showed 140-340 ms stalls of one advance call at those rounds.)
+class NodeStore {
+    static constexpr int kShift = 8, kChunk = 1 << kShift;   // 256 nodes (~750 KB) per chunk
+    std::vector<std::unique_ptr<Node[]>> chunks_;
+    size_t n_ = 0;
+
+public:
+    size_t size() const { return n_; }
+    Node& operator[](size_t i) { return chunks_[i >> kShift][i & (kChunk - 1)]; }
+    const Node& operator[](size_t i) const { return chunks_[i >> kShift][i & (kChunk - 1)]; }
+    void emplace_back()
+    {
+        if ((n_ >> kShift) == chunks_.size()) chunks_.emplace_back(new Node[kChunk]());
+        ++n_;
+    }
+};
+
 struct Pending {
     Key key;
     State st;
@@ -183,7 +203,7 @@ struct Pending {
 
 struct GameSearch {
     std::unordered_map<Key, int32_t, KeyHash> index;
-    std::vector<Node> nodes;
+    NodeStore nodes;
     // current move
     bool active = false;
     State root;

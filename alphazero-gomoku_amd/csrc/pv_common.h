@@ -51,6 +51,33 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// Write-through (sc1) 16-B / 4-B stores through a raw buffer resource: a kernel whose
+// outputs are stored this way leaves no dirty L2 lines behind, so the dependent launch
+// does not wait for their write-back at the kernel boundary (MI355X_MICROARCH.md
+// "boundary": + B / 6 TB/s for B dirty bytes; a train conv leaves 14.7 MB at B=128).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base, size_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+template <bool WT>
+__device__ __forceinline__ void store4(float* base, __amdgpu_buffer_rsrc_t rs, int off, f32x4 v) {
+    if constexpr (WT)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                               rs, off * 4, 0, 16);
+    else
+        *(f32x4*)(base + off) = v;
+}
+template <bool WT>
+__device__ __forceinline__ void store1(float* base, __amdgpu_buffer_rsrc_t rs, int off, float v) {
+    if constexpr (WT)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rs, off * 4, 0, 16);
+    else
+        base[off] = v;
+}
+// bytes of a padded NHWC tensor holding the M interior pixels (whole boards)
+__device__ __forceinline__ size_t padded_bytes(int M, int C) {
+    return (size_t)((M + PIX - 1) / PIX) * PADPIX * C * sizeof(float);
+}
+
 enum Epi : int {
     EPI_BN_RELU = 0,      // relu(acc*scale + shift)
     EPI_BN_RES_RELU = 1,  // relu(acc*scale + shift + resid)

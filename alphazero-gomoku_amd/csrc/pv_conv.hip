@@ -222,7 +222,8 @@ __global__ __launch_bounds__(64 * NW_, 2) void conv3x3_halo(
 // the BatchNorm partial sums fused into the epilogue (pv_halo.h XE_STATS / XE_BNBWD):
 // one fixed tile shape (128 x 64, 8 waves; the shape autotuning picked at B = 128)
 // so the partials are per 128-row M tile.  Same XCD-aware tile order as above.
-template <int C, int EPI, int XE>
+// WT: outputs stored write-through (no dirty L2 lines at the kernel boundary).
+template <int C, int EPI, int XE, bool WT>
 __global__ __launch_bounds__(512, 2) void conv3x3_train(
     const float* __restrict__ in, const float* __restrict__ wp, const float* __restrict__ resid,
     float* __restrict__ out, int M, EpiX ex)
@@ -233,9 +234,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_train(
     const int L = blockIdx.x, nt = gridDim.x;
     const int xcd = L & 7, q8 = nt >> 3, r8 = nt & 7;
     const int t = xcd * q8 + min(xcd, r8) + (L >> 3);
-    halo_tile<C, 64, 4, 1, 8, EPI, false, 0, 0, XE>(in, wp, nullptr, nullptr, resid, out,
-                                                 __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0, 0x00020000), M,
-                                                 (t / NTN) * T::BM, (t % NTN) * T::BN, smem, ex);
+    halo_tile<C, 64, 4, 1, 8, EPI, WT, 0, 0, XE>(in, wp, nullptr, nullptr, resid, out, wt_rsrc(out, padded_bytes(M, C)),
+                                              M, (t / NTN) * T::BM, (t % NTN) * T::BN, smem, ex);
 }
 
 // Stem conv 3->C (K = 27) on the VALU: 0.2 % of the forward FLOPs.  One
@@ -730,6 +730,8 @@ hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, cons
     return launch_conv3x3_shape(shape, C, epi, in, wp, scale, shift, resid, out, M, st);
 }
 
+int g_train_wt = 7;   // key 18 bits: 1 train conv outputs, 2 BN apply outputs, 4 wgrad slabs write-through
+
 template <int C, int EPI, int XE>
 static hipError_t launch_train_t(const float* in, const float* wp, const float* resid, float* out, int M,
                                  const EpiX& ex, hipStream_t st)
@@ -738,13 +740,19 @@ static hipError_t launch_train_t(const float* in, const float* wp, const float* 
     constexpr int lds = halo_lds_bytes<C, 64, 4, 1, 8>();
     static bool attr_done = false;
     if (!attr_done) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, false>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
         attr_done = true;
     }
     dim3 grid(((M + T::BM - 1) / T::BM) * (C / T::BN));
-    hipLaunchKernelGGL((conv3x3_train<C, EPI, XE>), grid, dim3(T::NT), lds, st, in, wp, resid, out, M, ex);
+    if (g_train_wt & 1)
+        hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, true>), grid, dim3(T::NT), lds, st, in, wp, resid, out, M, ex);
+    else
+        hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, false>), grid, dim3(T::NT), lds, st, in, wp, resid, out, M, ex);
     return hipGetLastError();
 }
 
@@ -852,6 +860,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     if (key == 17) {  // persistent tower claim granularity (0 one tile, 1 one M tile x all N tiles)
         const int prev = azg::g_tower_group;
         azg::g_tower_group = value ? 1 : 0;
+        return prev;
+    }
+    if (key == 18) {  // train: write-through outputs (bits: 1 convs, 2 BN apply, 4 wgrad slabs)
+        const int prev = azg::g_train_wt;
+        if (value >= 0 && value <= 7) azg::g_train_wt = value;
         return prev;
     }
     if (key == 16) {  // train: wgrad kernel (1 K-contiguous staging, default; 0 row staging, A/B)

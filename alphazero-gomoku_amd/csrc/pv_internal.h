@@ -44,6 +44,7 @@ extern int g_tower_var;
 extern int g_wgrad_serial;
 extern int g_wgrad_bk;
 extern int g_wgrad_kernel;
+extern int g_train_wt;
 constexpr int kTowerMaxBlocks = 32;
 int conv_batch_bucket(int M);
 size_t tower_sync_bytes(int nlayers, int M);

@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void col_stats_kernel(const float* __restrict_
 }
 
 // a = relu(z*scale + shift [+ res]) over the interior of padded NHWC tensors
-template <int C, bool RES>
+template <int C, bool RES, bool WT = false>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ z, const float* __restrict__ res,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, float* __restrict__ out,
@@ -161,6 +161,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
 {
     constexpr int F4 = C / 4;
     const int total = M * F4;
+    const __amdgpu_buffer_rsrc_t rs = wt_rsrc(out, padded_bytes(M, C));
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
         const int m = i / F4, c = (i - m * F4) * 4;
         const int o = pad_off(m, C) + c;
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
             if (RES) y += r[k];
             v[k] = fmaxf(y, 0.f);
         }
-        *(f32x4*)(out + o) = v;
+        store4<WT>(out, rs, o, v);
     }
 }
 
@@ -315,7 +316,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_tiles_kernel(
 }
 
 // dz = ((dy - gm) - (z - mean)*k) * invstd*gamma ; optional gres = dy
-template <int C, bool GRES>
+template <int C, bool GRES, bool WT = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* __restrict__ g, const float* __restrict__ act, const float* __restrict__ z,
     const float* __restrict__ mean, const float* __restrict__ gm, const float* __restrict__ kk,
@@ -323,6 +324,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
 {
     constexpr int F4 = C / 4;
     const int total = M * F4;
+    const __amdgpu_buffer_rsrc_t rz = wt_rsrc(dz, padded_bytes(M, C));
+    const __amdgpu_buffer_rsrc_t rg = wt_rsrc(GRES ? gres : dz, padded_bytes(M, C));
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
         const int m = i / F4, c = (i - m * F4) * 4;
         const int o = pad_off(m, C) + c;
@@ -340,8 +343,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
             dyv[q] = dy;
             out[q] = ((dy - g_[q]) - (zv[q] - mu[q]) * k_[q]) * w_[q];
         }
-        *(f32x4*)(dz + o) = out;
-        if (GRES) *(f32x4*)(gres + o) = dyv;
+        store4<WT>(dz, rz, o, out);
+        if (GRES) store4<WT>(gres, rg, o, dyv);
     }
 }
 
@@ -933,8 +936,15 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     };
     auto apply = [&](const float* z, const float* res, int layer, float* out) -> int32_t {
         const int o = bd[layer].out_off;
-        if (res)
+        const bool wt = (g_train_wt & 2) != 0;
+        if (res && wt)
+            hipLaunchKernelGGL((bn_apply_kernel<C, true, true>), dim3(gM), dim3(256), 0, st, z, res, w->bscale + o,
+                               w->bshift + o, out, M);
+        else if (res)
             hipLaunchKernelGGL((bn_apply_kernel<C, true>), dim3(gM), dim3(256), 0, st, z, res, w->bscale + o,
+                               w->bshift + o, out, M);
+        else if (wt)
+            hipLaunchKernelGGL((bn_apply_kernel<C, false, true>), dim3(gM), dim3(256), 0, st, z, res, w->bscale + o,
                                w->bshift + o, out, M);
         else
             hipLaunchKernelGGL((bn_apply_kernel<C, false>), dim3(gM), dim3(256), 0, st, z, res, w->bscale + o,
@@ -967,12 +977,15 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     auto bwd_apply = [&](const float* g, const float* act, const float* z, int layer, float* dz,
                          float* gres) -> int32_t {
         const int o = bd[layer].out_off;
-        if (gres)
-            hipLaunchKernelGGL((bn_bwd_apply_kernel<C, true>), dim3(gM), dim3(256), 0, st, g, act, z, w->bmean + o,
-                               w->bgm + o, w->bk + o, w->biw + o, dz, gres, M);
-        else
-            hipLaunchKernelGGL((bn_bwd_apply_kernel<C, false>), dim3(gM), dim3(256), 0, st, g, act, z, w->bmean + o,
-                               w->bgm + o, w->bk + o, w->biw + o, dz, gres, M);
+        const bool wt = (g_train_wt & 2) != 0;
+#define AZG_BWD_APPLY(GR, W)                                                                                  \
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<C, GR, W>), dim3(gM), dim3(256), 0, st, g, act, z, w->bmean + o, \
+                           w->bgm + o, w->bk + o, w->biw + o, dz, gres, M)
+        if (gres && wt) AZG_BWD_APPLY(true, true);
+        else if (gres) AZG_BWD_APPLY(true, false);
+        else if (wt) AZG_BWD_APPLY(false, true);
+        else AZG_BWD_APPLY(false, false);
+#undef AZG_BWD_APPLY
         AZG_CK(hipGetLastError(), "train: bn_bwd_apply");
         return 0;
     };

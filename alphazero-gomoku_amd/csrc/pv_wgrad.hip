@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_mfma(
 // in order, within a chunk pixel pairs (s, 16+s), s = 0..15.
 // PF2: global loads issued two chunks ahead (two register sets, the loop unrolled
 // by two so the sets are static): a load has a whole chunk of MFMAs more to land.
-template <int C, bool PF2 = false>
+template <int C, bool PF2 = false, bool WT = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_t(
     const float* __restrict__ dz, const float* __restrict__ x, float* __restrict__ slab, int M, int rows_per_split)
 {
@@ -295,6 +295,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_t(
     }
 
     float* out = slab + ((size_t)split * 9 + tap) * C * C;
+    const __amdgpu_buffer_rsrc_t rs = wt_rsrc(out, (size_t)C * C * sizeof(float));
 #pragma unroll
     for (int i = 0; i < TT; ++i)
 #pragma unroll
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_t(
             for (int r = 0; r < 16; ++r) {
                 const int co = co0 + wm * W + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 const int ci = ci0 + wn * W + j * 32 + r32;
-                out[co * C + ci] = acc[i][j][r];
+                store1<WT>(out, rs, co * C + ci, acc[i][j][r]);
             }
 }
 
@@ -352,11 +353,16 @@ static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, f
             if (e == hipSuccess)
                 e = hipFuncSetAttribute((const void*)conv3x3_wgrad_t<C, true>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)conv3x3_wgrad_t<C, false, true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
             if (e != hipSuccess) return e;
             attr_t = true;
         }
         if (g_wgrad_kernel == 2)
             hipLaunchKernelGGL((conv3x3_wgrad_t<C, true>), grid, dim3(256), lds, st, dz, x, slab, M, rps);
+        else if (g_train_wt & 4)
+            hipLaunchKernelGGL((conv3x3_wgrad_t<C, false, true>), grid, dim3(256), lds, st, dz, x, slab, M, rps);
         else
             hipLaunchKernelGGL((conv3x3_wgrad_t<C>), grid, dim3(256), lds, st, dz, x, slab, M, rps);
     } else {

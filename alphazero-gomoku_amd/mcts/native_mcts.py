@@ -215,8 +215,22 @@ class NativeSelfPlay:
                     self.search_seconds += time.perf_counter() - t0
                     continue
                 n = ev.advance()
+                done = np.nonzero(f.status == DONE)[0]
+                if n:
+                    # the leaves are staged: the GPU starts on them while the host plays
+                    # the finished games' moves (their trees hold no pending leaves, so
+                    # this order changes no result)
+                    t1 = time.perf_counter()
+                    ev.submit(n)
+                    dt = time.perf_counter() - t1
+                    self.nn_seconds += dt
+                    t0 += dt            # search_seconds excludes the submit
+                    pending[k] = True
+                    self.boards += n
+                    self.forwards += 1
+                    self.max_batch = max(self.max_batch, n)
                 # games whose move search finished: sample (per-game RNG), play, restart
-                for i in np.nonzero(f.status == DONE)[0]:
+                for i in done:
                     i = int(i)
                     g = lo + i
                     game = games[g]
@@ -236,14 +250,6 @@ class NativeSelfPlay:
                     else:
                         f.set_root(i, game, len(game.move_history))
                 self.search_seconds += time.perf_counter() - t0
-                if n:
-                    t0 = time.perf_counter()
-                    ev.submit(n)
-                    self.nn_seconds += time.perf_counter() - t0
-                    pending[k] = True
-                    self.boards += n
-                    self.forwards += 1
-                    self.max_batch = max(self.max_batch, n)
         self.rounds = max(self.rounds, max(moves) if moves else 0)
         return results
 
@@ -322,6 +328,12 @@ class NativeEval:
                 ns = {t: f.advance_boards(self.boards_ev[t].boards, self.boards_ev[t].players)
                       for t, f in self.forests.items()}
             self.search_seconds += time.perf_counter() - t0
+            t0 = time.perf_counter()
+            if self.boards_ev is not None:     # both networks' batches in flight, then the moves
+                for t, n in ns.items():        # (finished trees hold no pending leaves)
+                    if n:
+                        self.boards_ev[t].submit(n)
+            self.nn_seconds += time.perf_counter() - t0
             for g in sorted(to_move):
                 f = self.forests[to_move[g]]
                 if f.status[g] != DONE:
@@ -336,10 +348,6 @@ class NativeEval:
                 else:
                     start(g)
             t0 = time.perf_counter()
-            if self.boards_ev is not None:     # both networks' batches in flight, then wait
-                for t, n in ns.items():
-                    if n:
-                        self.boards_ev[t].submit(n)
             for t, n in ns.items():
                 if not n:
                     continue

@@ -68,12 +68,31 @@ def evaluate_models(model_new: PyTorchModel, model_best: PyTorchModel, game_name
     receives this rank's finished games."""
     size = model_new.board_size
     center, radius = size // 2, 4
-    games, starts = [], []
+    games, starts, winners, failure = [], [], [], None
     for i in D.shard(n_games):
         game = GameClass(size=size)
         game.do_move((random.randint(center - radius, center + radius), random.randint(center - radius, center + radius)))
         games.append(game)
         starts.append(i % 2 == 0)
+    try:
+        winners = _play_eval_games(model_new, model_best, games, starts, n_simulations, cpuct, native)
+    except Exception as e:   # every rank must still reach the collective below
+        failure, winners = e, []
+    if record is not None:
+        record.extend(games)
+    new_wins = sum(1 for w, s in zip(winners, starts) if (w == 1 and s) or (w == 2 and not s))
+    draws = sum(1 for w in winners if w == 0)
+    eng = getattr(model_new, "engine", None)
+    dev = eng.device if eng is not None else "cpu"
+    tot = torch.tensor([new_wins, draws, int(failure is not None)], dtype=torch.int64, device=dev)
+    D.allreduce_sum_(tot)
+    new_wins, draws, failed = (int(v) for v in tot.tolist())
+    if failed:   # all ranks agree; the caller counts it as a loss (reference train.py:803-805)
+        raise RuntimeError(f"evaluation failed on {failed} rank(s)" + (f": {failure}" if failure else ""))
+    return new_wins, new_wins / float(n_games), draws
+
+
+def _play_eval_games(model_new, model_best, games, starts, n_simulations, cpuct, native):
     if not games:
         winners = []
     elif native:
@@ -94,16 +113,7 @@ def evaluate_models(model_new: PyTorchModel, model_best: PyTorchModel, game_name
             mb = MCTS(GameClass, n_simulations, model_best, cpuct=cpuct, add_dirichlet_noise=False)
             gens.append(eval_game_gen(mn, mb, game, new_starts))
         winners = BatchedSelfPlay({"new": model_new, "best": model_best}).run(gens)
-    if record is not None:
-        record.extend(games)
-    new_wins = sum(1 for w, s in zip(winners, starts) if (w == 1 and s) or (w == 2 and not s))
-    draws = sum(1 for w in winners if w == 0)
-    eng = getattr(model_new, "engine", None)
-    dev = eng.device if eng is not None else "cpu"
-    tot = torch.tensor([new_wins, draws], dtype=torch.int64, device=dev)
-    D.allreduce_sum_(tot)
-    new_wins, draws = (int(v) for v in tot.tolist())
-    return new_wins, new_wins / float(n_games), draws
+    return winners
 
 
 def evaluate_models_mp(model_new, model_best, board_size, action_size, n_games, n_simulations, cpuct, **_ignored):

@@ -63,6 +63,22 @@ def _worker(rank, world, port, out_dir):
     torch.nn.utils.clip_grad_norm_(params, 3.0)           # clip sees the GLOBAL grad
     ref.optimizer.step()
     np.save(os.path.join(out_dir, f"params{rank}.npy"), torch.cat([q.detach().reshape(-1) for q in params]).numpy())
+
+    # evaluation that fails on ONE rank: both ranks reach the collective and raise
+    import train
+    real = train._play_eval_games
+
+    def flaky(*a, **k):
+        if rank == 1:
+            raise ValueError("rank-1 failure")
+        return real(*a, **k)
+
+    train._play_eval_games = flaky
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    from fake_model import FakeModel
+    with pytest.raises(RuntimeError, match="1 rank"):
+        train.evaluate_models(FakeModel(seed=3), FakeModel(seed=4), "gomoku", n_games=2, n_simulations=8)
+    train._play_eval_games = real
     torch.distributed.destroy_process_group()
 
 
