@@ -849,7 +849,9 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     }
     if (key == 3) {   // ablation mask (timing studies only, C=128 EPI_BN_RELU launches)
         const int prev = azg::g_conv_ablation;
+#ifdef AZG_AB_STUDIES   // timing studies only: the product library ignores it
         azg::g_conv_ablation = value;
+#endif
         return prev;
     }
     if (key == 14) {  // tests: persistent-tower dependency spin bound (-1 restores the default)
@@ -884,7 +886,9 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     }
     if (key == 11) {  // stem ablation mask (timing studies only)
         const int prev = azg::g_stem_ablation;
+#ifdef AZG_AB_STUDIES   // timing studies only: the product library ignores it
         azg::g_stem_ablation = value;
+#endif
         return prev;
     }
     if (key == 9) {   // stem kernel: 1 fp32 MFMA (default), 0 VALU reference
@@ -903,12 +907,16 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     }
     if (key == 8) {   // persistent-tower ablation mask (timing studies only)
         const int prev = azg::g_tower_ablation;
+#ifdef AZG_AB_STUDIES   // timing studies only: the product library ignores it
         azg::g_tower_ablation = value;
+#endif
         return prev;
     }
     if (key == 7) {   // ablation tile shape (5 or 8)
         const int prev = azg::g_ablation_shape;
+#ifdef AZG_AB_STUDIES   // timing studies only: the product library ignores it
         azg::g_ablation_shape = value;
+#endif
         return prev;
     }
     if (key == 5) {   // persistent residual tower on/off
@@ -926,7 +934,9 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     }
     if (key == 4) {   // conv kernel variant (1 halo-staged, 0 per-chunk staging; timing studies)
         const int prev = azg::g_conv_variant;
+#ifdef AZG_AB_STUDIES   // timing studies only: the product library ignores it
         azg::g_conv_variant = value;
+#endif
         return prev;
     }
     if (key == 15) {  // query: 1 if built with the A/B study variants (make study)

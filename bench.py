@@ -243,54 +243,58 @@ def cpu_baseline(game_seconds: float) -> dict:
 
 
 # --------------------------------------------------------------------- GPU legs
-def roofline_from_profile(prof, boards, blocks, ch, kname_tower, kname_layer):
-    """Residual-conv roofline from hipEvent-timed launches: the persistent tower
-    when it ran (dominant kernel), else the per-layer conv3x3 launches."""
-    cf = conv_flop(ch)
-    tower_ms, tower_n = prof.get("tower", (0.0, 0))
-    layer_ms, layer_n = prof.get("conv3x3", (0.0, 0))
-    tower_flop = cf * 2 * blocks * boards.get("tower", 0)
-    layer_flop = cf * boards.get("conv3x3", 0)
-    if tower_n:
-        achieved = tower_flop / (tower_ms / 1e3)
-        roof = {"kernel": kname_tower, "launches": tower_n, "avg_launch_us": round(tower_ms / tower_n * 1e3, 2),
-                "flop_per_launch": round(tower_flop / tower_n), "boards": boards.get("tower", 0)}
-    elif layer_n:
-        achieved = layer_flop / (layer_ms / 1e3)
-        roof = {"kernel": kname_layer, "launches": layer_n, "avg_launch_us": round(layer_ms / layer_n * 1e3, 2),
-                "flop_per_launch": round(layer_flop / layer_n)}
-    else:
-        return None
-    out = {"bound": "mfma", "achieved": round(achieved / 1e12, 3), "peak": PEAK_F32_MFMA / 1e12,
-           "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA, 4), "traffic": None}
-    out.update(roof)
-    if tower_n and layer_n:
-        out["all_residual_convs_frac"] = round((tower_flop + layer_flop) / ((tower_ms + layer_ms) / 1e3)
-                                               / PEAK_F32_MFMA, 4)
-        out["per_layer_launches"] = layer_n
-    return out
-
-
-def load_traffic_record():
+def traffic_records():
+    """HBM-traffic records of the residual-conv kernels from the committed PMC passes
+    (profiles/conv_traffic.json: scripts/summarize_profile.py, summarize_conv_pmc.py)."""
     try:
         d = json.load(open(os.path.join(REPO, "profiles", "conv_traffic.json")))
-        d.setdefault("boards_per_launch", BATCH)
-        return d
+        return d.get("records", [d])
     except Exception:
+        return []
+
+
+def roofline_from_profile(prof, boards, blocks, ch, kname_tower, kname_layer, traffic=True):
+    """Residual-conv roofline from hipEvent-timed launches.  The kernel is the
+    DOMINANT class by device time: the persistent tower (`tower`) or the per-layer
+    conv3x3 launches (`conv3x3`); the other class is reported beside it.  traffic:
+    HBM bytes per launch from the committed PMC record of that kernel, scaled per
+    board to this run's average launch (6x128 only)."""
+    cf = conv_flop(ch)
+    cls = {}
+    for k, convs, name in (("tower", 2 * blocks, kname_tower), ("conv3x3", 1, kname_layer)):
+        ms, n = prof.get(k, (0.0, 0))
+        if n:
+            flop = cf * convs * boards.get(k, 0)
+            cls[k] = {"kernel": name, "launches": n, "device_ms": round(ms, 1), "avg_launch_us": round(ms / n * 1e3, 2),
+                      "flop_per_launch": round(flop / n), "boards_per_launch": round(boards.get(k, 0) / n, 1),
+                      "frac": round(flop / (ms / 1e3) / PEAK_F32_MFMA, 4), "_flop": flop, "_ms": ms}
+    if not cls:
         return None
-
-
-def load_traffic(kernel, config):
-    """HBM bytes per launch of `kernel` from the committed PMC pass
-    (profiles/conv_traffic.json, scripts/summarize_profile.py), or None."""
-    path = os.path.join(REPO, "profiles", "conv_traffic.json")
-    try:
-        d = json.load(open(path))
-        if d.get("config") == config and d.get("kernel", "conv3x3") == kernel:
-            return d.get("hbm_bytes_per_launch")
-    except Exception:
-        pass
-    return None
+    dom = max(cls, key=lambda k: cls[k]["_ms"])
+    d = cls[dom]
+    achieved = d["_flop"] / (d["_ms"] / 1e3)
+    out = {"bound": "mfma", "achieved": round(achieved / 1e12, 3), "peak": PEAK_F32_MFMA / 1e12,
+           "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA, 4), "traffic": None}
+    out.update({k: v for k, v in d.items() if not k.startswith("_") and k != "frac"})
+    if traffic and (blocks, ch) == (BLOCKS, CHANNELS):
+        recs = [r for r in traffic_records() if r.get("kernel") == dom]
+        if recs:
+            # per board over the record's launches (both epilogues of the per-layer
+            # conv alternate: mean of the two records)
+            per_board = sum(r["hbm_bytes_per_launch"] / r["boards_per_launch"] for r in recs) / len(recs)
+            out["traffic"] = round(per_board * d["boards_per_launch"])
+            out["traffic_basis"] = "; ".join(
+                f"PMC FETCH_SIZE x2 + WRITE_SIZE of {r['kernel']} ({r.get('epilogue', 'all convs')}) at "
+                f"{r['config']} ({r['tag']}): {r['hbm_bytes_per_launch'] / 1e6:.1f} MB per launch, "
+                f"{r.get('traffic_over_algorithmic', 0)}x algorithmic" for r in recs) + \
+                "; scaled per board to this run's average launch"
+    others = [k for k in cls if k != dom]
+    if others:
+        tot_f = sum(c["_flop"] for c in cls.values())
+        tot_ms = sum(c["_ms"] for c in cls.values())
+        out["all_residual_convs_frac"] = round(tot_f / (tot_ms / 1e3) / PEAK_F32_MFMA, 4)
+        out["other_classes"] = {k: {kk: vv for kk, vv in cls[k].items() if not kk.startswith("_")} for k in others}
+    return out
 
 
 def visit_buckets(model, top):
@@ -410,8 +414,6 @@ def forward_leg(model, args, rank, world, dist, dev, local, blocks=BLOCKS, ch=CH
     roof = roofline_from_profile(prof, boards, blocks, ch,
                                  f"azg::conv_tower<{ch},*> (persistent residual tower, {2 * blocks} convs per launch)",
                                  f"azg::conv3x3_halo<{ch},*>")
-    if roof is not None and blocks == BLOCKS and ch == CHANNELS and B == BATCH:
-        roof["traffic"] = load_traffic("tower" if prof.get("tower") else "conv3x3", f"{blocks}x{ch}_B{B}")
     return {"config": f"{blocks}x{ch} ResNet, batch {B}/GPU eval forward (BN running stats, softmax + tanh), "
                       f"inputs resident in HBM",
             "boards_per_s": round(B * steps * world / elapsed, 1), "ms_per_step": round(elapsed / steps * 1e3, 4),
@@ -555,17 +557,6 @@ def main():
         if dist is not None:
             dist.destroy_process_group()
         return
-    if sp["roofline"] is not None:
-        # HBM bytes of the tower, from the PMC pass at B=512 (profiles/conv_traffic.json),
-        # scaled per board to the average tower launch of this run
-        t = load_traffic_record()
-        if t and t.get("kernel") == "tower" and sp["roofline"].get("boards"):
-            per_board = t["hbm_bytes_per_launch"] / t["boards_per_launch"]
-            sp["roofline"]["traffic"] = round(per_board * sp["roofline"]["boards"] / sp["roofline"]["launches"])
-            sp["roofline"]["traffic_basis"] = (f"PMC FETCH_SIZE x2 + WRITE_SIZE of the tower at B=512 "
-                                               f"({t['tag']}), {per_board / 1e6:.3f} MB per board, x boards per "
-                                               f"launch of this run")
-
     out = {
         "metric": METRIC,
         "value": round(sp["boards_per_s"], 1),

@@ -1,0 +1,58 @@
+"""HBM bytes per launch of the per-layer conv3x3_halo<128,64,4,1,8,EPI> at B=4096
+(scripts/gpu_conv_pmc.sh: scripts/conv_probe.py under FETCH_SIZE / WRITE_SIZE /
+MFMA-busy passes) -> a "conv3x3" record in profiles/conv_traffic.json (the tower
+record of scripts/summarize_profile.py is kept).  gfx950 corrections per the
+MI355X guide: FETCH_SIZE x2, KiB -> bytes.  The probe's first forward autotunes
+(every candidate shape runs once); only the 128x64/8-wave shape is summarised.
+
+    python scripts/summarize_conv_pmc.py gpurun_out/pmc_conv r2
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+B, C = 4096, 128
+
+
+def means(path, counter):
+    acc = collections.defaultdict(list)
+    for r in csv.DictReader(open(path, newline="")):
+        if r["Counter_Name"] == counter and "conv3x3_halo<128, 64, 4, 1, 8," in r["Kernel_Name"]:
+            epi = r["Kernel_Name"].split("conv3x3_halo<128, 64, 4, 1, 8, ")[1][0]
+            acc[int(epi)].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    root, tag = sys.argv[1], sys.argv[2]
+    fetch = means(os.path.join(root, "pmc_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = means(os.path.join(root, "pmc_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE")
+    d = os.path.join(root, "pmc_SQ_VALU_MFMA_BUSY_CYCLES_GRBM_GUI_ACTIVE", "run_counter_collection.csv")
+    mf, gr = means(d, "SQ_VALU_MFMA_BUSY_CYCLES"), means(d, "GRBM_GUI_ACTIVE")
+    act = B * 225 * C * 4                       # one interior activation tensor
+    path = os.path.join(REPO, "profiles", "conv_traffic.json")
+    cur = json.load(open(path))
+    recs = cur["records"] if "records" in cur else [cur]
+    recs = [r for r in recs if r.get("kernel") != "conv3x3"]
+    for epi, name, reads in ((0, "bn_relu", 1), (1, "bn_res_relu", 2)):
+        if epi not in fetch:
+            continue
+        f = fetch[epi] * 2 * 1024
+        w = write.get(epi, write.get(0)) * 1024
+        alg = (reads + 1) * act + 9 * C * C * 4
+        rec = {"kernel": "conv3x3", "shape": "128x64, 8 waves (conv3x3_halo<128,64,4,1,8>)", "epilogue": name,
+               "config": f"6x128_B{B}", "tag": tag, "boards_per_launch": B, "convs_per_launch": 1,
+               "hbm_bytes_per_launch": round(f + w), "fetch_bytes": round(f), "write_bytes": round(w),
+               "algorithmic_bytes": alg, "traffic_over_algorithmic": round((f + w) / alg, 3)}
+        if epi in mf and epi in gr:
+            rec["mfma_busy"] = round(mf[epi] * 8 / (4 * 256 * gr[epi]), 4)
+        recs.append(rec)
+        print(json.dumps(rec))
+    json.dump({"records": recs}, open(path, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

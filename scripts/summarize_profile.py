@@ -191,12 +191,16 @@ def main():
             f"clock ~ {clk:.2f} GHz",
             "",
         ]
-        with open(os.path.join(PROF, "conv_traffic.json"), "w") as f:
-            json.dump({"config": f"{BLOCKS}x{CHANNELS}_B{BATCH}", "tag": args.tag,
-                       "kernel": "tower" if towers else "conv3x3", "convs_per_launch": convs_per_launch,
-                       "hbm_bytes_per_launch": round(traffic), "fetch_bytes": round(fetch_b),
-                       "write_bytes": round(write_b), "algorithmic_bytes": round(alg),
-                       "avg_launch_us": round(avg_ns / 1e3, 2)}, f, indent=1)
+        rec = {"config": f"{BLOCKS}x{CHANNELS}_B{BATCH}", "tag": args.tag, "boards_per_launch": BATCH,
+               "kernel": "tower" if towers else "conv3x3", "convs_per_launch": convs_per_launch,
+               "hbm_bytes_per_launch": round(traffic), "fetch_bytes": round(fetch_b),
+               "write_bytes": round(write_b), "algorithmic_bytes": round(alg),
+               "traffic_over_algorithmic": round(traffic / alg, 3), "avg_launch_us": round(avg_ns / 1e3, 2)}
+        path = os.path.join(PROF, "conv_traffic.json")
+        old = json.load(open(path)) if os.path.exists(path) else {"records": []}
+        recs = [r for r in old.get("records", [old]) if (r.get("kernel"), r.get("config")) != (rec["kernel"], rec["config"])]
+        with open(path, "w") as f:
+            json.dump({"records": recs + [rec]}, f, indent=1)
     lines += ["## HBM-bound kernels of the forward (B=512)", ""] + bw_table(stats, hbm_models(BATCH))
     if args.train:
         tpath = os.path.join(args.train, "trace", "run_kernel_stats.csv")
