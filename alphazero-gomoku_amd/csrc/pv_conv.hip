@@ -864,6 +864,13 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         azg::g_tower_group = value ? 1 : 0;
         return prev;
     }
+    if (key == 19) {  // study build only: skip BN kernels of the train step (bits 1 apply, 2 finalize, 4 bwd apply, 8 bwd finalize; results invalid)
+        const int prev = azg::g_train_skip;
+#ifdef AZG_AB_STUDIES
+        azg::g_train_skip = value;
+#endif
+        return prev;
+    }
     if (key == 18) {  // train: write-through outputs (bits: 1 convs, 2 BN apply, 4 wgrad slabs)
         const int prev = azg::g_train_wt;
         if (value >= 0 && value <= 7) azg::g_train_wt = value;

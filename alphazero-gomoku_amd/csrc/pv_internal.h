@@ -42,6 +42,7 @@ extern int g_tower_shape;
 extern int g_tower_ablation;
 extern int g_tower_var;
 extern int g_wgrad_serial;
+extern int g_train_skip;
 extern int g_wgrad_bk;
 extern int g_wgrad_kernel;
 extern int g_train_wt;

@@ -903,6 +903,7 @@ static inline int grid_for(int64_t total) { int64_t b = (total + 255) / 256; ret
     } while (0)
 
 int g_wgrad_serial = 0;   // 1: conv weight grads on the caller's stream (A/B timing)
+int g_train_skip = 0;     // study build only (key 19): skip BN kernels to time them in situ (results invalid)
 
 template <int C>
 static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, const float* zs, int B,
@@ -920,6 +921,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
 
     const int ntt = (M + TRAIN_BM - 1) / TRAIN_BM;   // M tiles of conv3x3_train (partials per tile)
     auto fin_fwd = [&](int layer, int prow, int nt) -> int32_t {
+        if (g_train_skip & 2) return 0;
         hipLaunchKernelGGL(bn_finalize_tiles_kernel, dim3(bd[layer].c), dim3(256), 0, st, w->part_a,
                            w->part_b, nt, prow, M, C, bdd, layer, P, h->bn, w->bmean, w->binv, w->bscale, w->bshift);
         AZG_CK(hipGetLastError(), "train: bn_finalize_tiles");
@@ -935,6 +937,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         return 0;
     };
     auto apply = [&](const float* z, const float* res, int layer, float* out) -> int32_t {
+        if (g_train_skip & 1) return 0;
         const int o = bd[layer].out_off;
         const bool wt = (g_train_wt & 2) != 0;
         if (res && wt)
@@ -969,6 +972,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         return 0;
     };
     auto bwd_fin = [&](int layer, int nt) -> int32_t {
+        if (g_train_skip & 8) return 0;
         hipLaunchKernelGGL(bn_bwd_finalize_tiles_kernel, dim3(bd[layer].c), dim3(256), 0, st,
                            w->part_a, w->part_b, nt, M, C, bdd, layer, P, G, w->binv, w->bgm, w->bk, w->biw);
         AZG_CK(hipGetLastError(), "train: bn_bwd_finalize_tiles");
@@ -976,6 +980,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     };
     auto bwd_apply = [&](const float* g, const float* act, const float* z, int layer, float* dz,
                          float* gres) -> int32_t {
+        if (g_train_skip & 4) return 0;
         const int o = bd[layer].out_off;
         const bool wt = (g_train_wt & 2) != 0;
 #define AZG_BWD_APPLY(GR, W)                                                                                  \

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--channels", type=int, default=128)
+    ap.add_argument("--no-bitwise", action="store_true", help="timing-only variants (study keys): skip the check")
     args = ap.parse_args()
     import _native
     lib = _native.load_library()
@@ -59,7 +60,7 @@ def main():
 
     # bitwise: two steps from the same state under every variant
     ref = None
-    for v in variants:
+    for v in ([] if args.no_bitwise else variants):
         select(v)
         model.net.load_state_dict(state)
         model.optimizer.load_state_dict(opt)
