@@ -83,15 +83,25 @@ def dist_setup(n_gpus: int):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("AZG_BENCH_SHARE_GPU"):
+            # rehearsal of the N>1 path on a 1-GPU box (never a measurement): ranks share
+            # the visible GPUs and talk over gloo (RCCL refuses two ranks on one GPU)
+            local = local % torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         return rank, world, local, dist
     return 0, 1, 0, None
 
 
 def barrier_sync(dist, local):
     if dist is not None:
-        dist.barrier(device_ids=[local])
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[local])
+        else:
+            dist.barrier()
     torch.cuda.synchronize()
 
 
@@ -99,6 +109,8 @@ def reduce_(dist, dev, vals, op="sum"):
     """Sum (or max) a list of floats over ranks."""
     v = torch.tensor(vals, dtype=torch.float64, device=dev)
     if dist is not None:
+        if dist.get_backend() != "nccl":
+            v = v.cpu()
         dist.all_reduce(v, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
     return [float(a) for a in v.tolist()]
 
