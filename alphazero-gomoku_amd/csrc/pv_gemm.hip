@@ -17,7 +17,6 @@
 namespace azg {
 
 constexpr int GK = 512;                       // K chunk (one chunk for every head GEMM up to B = 512)
-constexpr int GU = 32;                        // loads in flight per thread while staging
 constexpr int GLDK_MAX = GK + 2;
 constexpr int G_LDS = 2 * 32 * GLDK_MAX * 4;  // 131,584 B
 
@@ -46,44 +45,37 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(GemmPair gp)
         const int kc = min(GK, P.K - k0);
         const int ldk = gemm_ldk(kc);
         float* Bs = smem + 32 * ldk;
-        // stage A tile [32][ldk] and B^T tile [32][ldk], zero outside the problem.
-        // Batches of GU independent loads per thread are issued before their LDS
-        // stores (the loads would otherwise serialise on L2 latency).
-        const int tot = 32 * ldk;
-        const float inv_ldk = 1.f / (float)ldk;
-        auto split = [&](int e, int& r, int& k) {   // e = r*ldk + k, exact for e < 2^20
-            r = (int)((float)e * inv_ldk);
-            k = e - r * ldk;
-            if (k < 0) { --r; k += ldk; }
-            else if (k >= ldk) { ++r; k -= ldk; }
-        };
-        for (int e0 = 0; e0 < tot; e0 += 256 * GU) {
-            float va[GU], vb[GU];
+        // stage A tile [32][ldk] and B^T tile [32][ldk], zero outside the problem (the
+        // pad column k = kc of an odd chunk included).  Each thread owns one tile row
+        // and a k stride of 8 (k-contiguous operands: 8 threads per row read 32-B runs)
+        // or one k phase and a row (row-contiguous operands: 32 threads read a 128-B
+        // row of the other dimension); no per-element index division, UNR loads in
+        // flight per thread before their LDS stores.
+        constexpr int UNR = 8;
+        auto stage = [&](const float* X, int sx_row, int sx_k, int rlim, int rbase, float* dst) {
+            const bool kcontig = sx_k == 1;
+            const int r = kcontig ? (tid >> 3) : (tid & 31);
+            const int kq = kcontig ? (tid & 7) : (tid >> 5);
+            const bool rok = rbase + r < rlim;
+            const float* src = X + (size_t)(rbase + r) * sx_row + (size_t)k0 * sx_k;
+            float* d = dst + r * ldk;
+            const int kend = kc + (kc & 1);
+            for (int kb = kq; kb < kend; kb += 8 * UNR) {
+                float v[UNR];
 #pragma unroll
-            for (int u = 0; u < GU; ++u) {
-                const int e = e0 + u * 256 + tid;
-                int r, k;
-                if (P.sak == 1) split(e, r, k); else { k = e >> 5; r = e & 31; }
-                const int i = i0 + r;
-                va[u] = (e < tot && k < kc && i < P.M) ? P.A[(size_t)i * P.sai + (size_t)(k0 + k) * P.sak] : 0.f;
-                int c, kb;
-                if (P.sbk == 1) split(e, c, kb); else { kb = e >> 5; c = e & 31; }
-                const int j = j0 + c;
-                vb[u] = (e < tot && kb < kc && j < P.N) ? P.B[(size_t)(k0 + kb) * P.sbk + (size_t)j * P.sbj] : 0.f;
-            }
+                for (int u = 0; u < UNR; ++u) {
+                    const int k = kb + 8 * u;
+                    v[u] = (rok && k < kc) ? src[(size_t)k * sx_k] : 0.f;
+                }
 #pragma unroll
-            for (int u = 0; u < GU; ++u) {
-                const int e = e0 + u * 256 + tid;
-                if (e < tot) {
-                    int r, k;
-                    if (P.sak == 1) split(e, r, k); else { k = e >> 5; r = e & 31; }
-                    As[r * ldk + k] = va[u];
-                    int c, kb;
-                    if (P.sbk == 1) split(e, c, kb); else { kb = e >> 5; c = e & 31; }
-                    Bs[c * ldk + kb] = vb[u];
+                for (int u = 0; u < UNR; ++u) {
+                    const int k = kb + 8 * u;
+                    if (k < kend) d[k] = v[u];
                 }
             }
-        }
+        };
+        stage(P.A, P.sai, P.sak, P.M, i0, As);
+        stage(P.B, P.sbj, P.sbk, P.N, j0, Bs);
         __syncthreads();
         const int steps = (kc + 1) >> 1;
         const int s0 = wid * steps / 4, s1 = (wid + 1) * steps / 4;

@@ -625,40 +625,58 @@ __global__ __launch_bounds__(256) void heads_bwd_proj_kernel(const float* __rest
                                                              float* __restrict__ gx, float* __restrict__ hpart,
                                                              int M)
 {
-    constexpr int TPC = 256 / C;
-    __shared__ float red[3][256];
-    const int c = threadIdx.x % C, rg = threadIdx.x / C;
+    // float4 over channels (C/4 threads per pixel row, 256*4/C rows per pass, 4 rows
+    // in flight per thread); the per-thread partial sums of the three 1x1-conv weight
+    // grads are added over the row groups in fixed order
+    constexpr int Q = C / 4, RG = 256 / Q, UNR = 4;
+    __shared__ f32x4 red[3][RG][Q];
+    const int q = threadIdx.x % Q, rg = threadIdx.x / Q;
+    const int c = 4 * q;
     const int m0 = blockIdx.x * HROWS;
     const int rows = min(HROWS, M - m0);
-    const float w0 = wpc[c], w1 = wpc[C + c], w2 = wvc[c];
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-    for (int r = rg; r < rows; r += TPC) {
-        const int m = m0 + r;
-        const int b = m / PIX, p = m - b * PIX;
-        const float d0 = dzh[(b * 3 + 0) * PIX + p];
-        const float d1 = dzh[(b * 3 + 1) * PIX + p];
-        const float d2 = dzh[(b * 3 + 2) * PIX + p];
-        const int o = pad_off(m, C) + c;
-        const float xv = act[o];
-        s0 = fmaf(d0, xv, s0);
-        s1 = fmaf(d1, xv, s1);
-        s2 = fmaf(d2, xv, s2);
-        gx[o] = d0 * w0 + d1 * w1 + d2 * w2;
+    const f32x4 w0 = *(const f32x4*)(wpc + c), w1 = *(const f32x4*)(wpc + C + c), w2 = *(const f32x4*)(wvc + c);
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0;
+    for (int r0 = rg; r0 < rows; r0 += RG * UNR) {
+        f32x4 xv[UNR];
+        float d0[UNR], d1[UNR], d2[UNR];
+        int o[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const int r = r0 + RG * u;
+            const int m = m0 + min(r, rows - 1);
+            const int b = m / PIX, p = m - b * PIX;
+            d0[u] = dzh[(b * 3 + 0) * PIX + p];
+            d1[u] = dzh[(b * 3 + 1) * PIX + p];
+            d2[u] = dzh[(b * 3 + 2) * PIX + p];
+            o[u] = pad_off(m, C) + c;
+            xv[u] = *(const f32x4*)(act + o[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            if (r0 + RG * u < rows) {
+                f32x4 g;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    s0[e] = fmaf(d0[u], xv[u][e], s0[e]);
+                    s1[e] = fmaf(d1[u], xv[u][e], s1[e]);
+                    s2[e] = fmaf(d2[u], xv[u][e], s2[e]);
+                    g[e] = d0[u] * w0[e] + d1[u] * w1[e] + d2[u] * w2[e];
+                }
+                *(f32x4*)(gx + o[u]) = g;
+            }
+        }
     }
-    red[0][threadIdx.x] = s0;
-    red[1][threadIdx.x] = s1;
-    red[2][threadIdx.x] = s2;
+    red[0][rg][q] = s0;
+    red[1][rg][q] = s1;
+    red[2][rg][q] = s2;
     __syncthreads();
     if (rg == 0) {
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-        for (int k = 0; k < TPC; ++k) {
-            a0 += red[0][k * C + c];
-            a1 += red[1][k * C + c];
-            a2 += red[2][k * C + c];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            f32x4 a = red[k][0][q];
+            for (int g = 1; g < RG; ++g) a += red[k][g][q];
+            *(f32x4*)(hpart + ((size_t)blockIdx.x * 3 + k) * C + c) = a;
         }
-        hpart[(blockIdx.x * 3 + 0) * C + c] = a0;
-        hpart[(blockIdx.x * 3 + 1) * C + c] = a1;
-        hpart[(blockIdx.x * 3 + 2) * C + c] = a2;
     }
 }
 
@@ -669,16 +687,31 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __res
                                                               float* __restrict__ out0, float* __restrict__ out1,
                                                               int split, int mode, int C)
 {
-    __shared__ float red[4][64];
-    const int jl = threadIdx.x & 63, g = threadIdx.x >> 6;
-    const int j = blockIdx.x * 64 + jl;
+    // 16 outputs x 16 t-phases per workgroup: every thread sums ~T/16 partials with
+    // 8 loads in flight, then the 16 phases are added in fixed order
+    constexpr int NJ = 16, NG = 16, UNR = 8;
+    __shared__ float red[NG][NJ];
+    const int jl = threadIdx.x % NJ, g = threadIdx.x / NJ;
+    const int j = blockIdx.x * NJ + jl;
     float s = 0.f;
-    if (j < n)
-        for (int t = g; t < T; t += 4) s += part[(size_t)t * n + j];
+    if (j < n) {
+        for (int t0 = g; t0 < T; t0 += NG * UNR) {
+            float v[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const int t = t0 + NG * u;
+                v[u] = t < T ? part[(size_t)t * n + j] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) s += v[u];
+        }
+    }
     red[g][jl] = s;
     __syncthreads();
     if (g == 0 && j < n) {
-        const float v = ((red[0][jl] + red[1][jl]) + red[2][jl]) + red[3][jl];
+        float v = red[0][jl];
+#pragma unroll
+        for (int k = 1; k < NG; ++k) v += red[k][jl];
         if (mode == 0) {
             if (j < split) out0[j] = v;
             else out1[j - split] = v;
@@ -690,12 +723,18 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __res
 }
 
 // stem weight gradient partials per board: part[b][k][c] = S_p dz[p][c] * xpatch[p][k]
+constexpr int STEM_WG_CHUNKS = 3;   // pixel chunks per board (75 pixels each) of the stem weight grad
+
+// Stem weight grad partials: one workgroup per (board, 75-pixel chunk); thread =
+// channel x pixel phase, 4 pixels' dz loads in flight; the board's padded input
+// planes in LDS.  spart[(b * STEM_WG_CHUNKS + chunk) * 27 + k][C].
 template <int C>
 __global__ __launch_bounds__(256) void stem_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dz,
                                                          float* __restrict__ spart)
 {
     __shared__ float xs[3 * PADPIX];
-    const int b = blockIdx.x, tid = threadIdx.x;
+    constexpr int PCH = PIX / STEM_WG_CHUNKS;
+    const int b = blockIdx.x / STEM_WG_CHUNKS, chunk = blockIdx.x % STEM_WG_CHUNKS, tid = threadIdx.x;
     const float* xb = x + (size_t)b * 3 * PIX;
     for (int i = tid; i < 3 * PADPIX; i += 256) {
         const int ci = i / PADPIX, rem = i - ci * PADPIX;
@@ -706,23 +745,34 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const float* __restrict
     }
     __syncthreads();
     constexpr int TPC = C < 256 ? 256 / C : 1;
+    constexpr int UNR = 4;
     __shared__ float red[27][256];
     const int c = tid % C, rg = tid / C;
     if (C <= 256) {
         float acc[27];
 #pragma unroll
         for (int k = 0; k < 27; ++k) acc[k] = 0.f;
-        for (int p = rg; p < PIX; p += TPC) {
-            const int y = p / BOARD, xq = p - y * BOARD;
-            const float d = dz[(size_t)(b * PADPIX + (y + 1) * PADW + (xq + 1)) * C + c];
+        for (int i0 = rg; i0 < PCH; i0 += TPC * UNR) {
+            float d[UNR];
+            int yx[UNR];
 #pragma unroll
-            for (int ci = 0; ci < 3; ++ci)
+            for (int u = 0; u < UNR; ++u) {
+                const int i = min(i0 + TPC * u, PCH - 1);
+                const int p = chunk * PCH + i;
+                const int y = p / BOARD, xq = p - y * BOARD;
+                yx[u] = y * PADW + xq;
+                d[u] = i0 + TPC * u < PCH ? dz[(size_t)(b * PADPIX + (y + 1) * PADW + (xq + 1)) * C + c] : 0.f;
+            }
 #pragma unroll
-                for (int ky = 0; ky < 3; ++ky)
+            for (int u = 0; u < UNR; ++u)
 #pragma unroll
-                    for (int kx = 0; kx < 3; ++kx)
-                        acc[ci * 9 + ky * 3 + kx] =
-                            fmaf(d, xs[ci * PADPIX + (y + ky) * PADW + (xq + kx)], acc[ci * 9 + ky * 3 + kx]);
+                for (int ci = 0; ci < 3; ++ci)
+#pragma unroll
+                    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                        for (int kx = 0; kx < 3; ++kx)
+                            acc[ci * 9 + ky * 3 + kx] =
+                                fmaf(d[u], xs[ci * PADPIX + yx[u] + ky * PADW + kx], acc[ci * 9 + ky * 3 + kx]);
         }
 #pragma unroll
         for (int k = 0; k < 27; ++k) red[k][tid] = acc[k];
@@ -731,7 +781,7 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const float* __restrict
             for (int k = 0; k < 27; ++k) {
                 float s = 0.f;
                 for (int g = 0; g < TPC; ++g) s += red[k][g * C + c];
-                spart[((size_t)b * 27 + k) * C + c] = s;
+                spart[((size_t)blockIdx.x * 27 + k) * C + c] = s;
             }
         }
     }
@@ -858,7 +908,7 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     A(w->part_a, (size_t)ntile * C, false);
     A(w->part_b, (size_t)ntile * C, false);
     A(w->hpart, (size_t)((M + HROWS - 1) / HROWS) * 3 * C, false);
-    A(w->spart, (size_t)cap * 27 * C, false);
+    A(w->spart, (size_t)cap * STEM_WG_CHUNKS * 27 * C, false);
     // split-K for wgrad: ~512 rows per split
     w->S = kMaxWgradSplits;
     A(w->slab, (size_t)w->S * 9 * C * C, false);
@@ -1103,7 +1153,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
                            P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], w->gX, w->hpart, M);
         AZG_CK(hipGetLastError(), "train: heads_bwd_proj");
         // policy_conv.weight [2][C] then value_conv.weight [C]: partial layout [t][3][C]
-        hipLaunchKernelGGL(reduce_partials_kernel, dim3((3 * C + 63) / 64), dim3(256), 0, st, w->hpart, hntile, 3 * C,
+        hipLaunchKernelGGL(reduce_partials_kernel, dim3((3 * C + 15) / 16), dim3(256), 0, st, w->hpart, hntile, 3 * C,
                            G + h->poff[h->t_pc_w], G + h->poff[h->t_vc_w], 2 * C, 0, C);
         AZG_CK(hipGetLastError(), "train: heads proj wgrad");
         prof_end(h, pr, st);
@@ -1151,9 +1201,9 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     }
     R(bwd_fin(h->bn_stem, bwd_nt));
     R(bwd_apply(w->gX, w->a0, w->z0, h->bn_stem, w->DH, nullptr));
-    hipLaunchKernelGGL((stem_wgrad_kernel<C>), dim3(B), dim3(256), 0, st, x, w->DH, w->spart);
+    hipLaunchKernelGGL((stem_wgrad_kernel<C>), dim3(B * STEM_WG_CHUNKS), dim3(256), 0, st, x, w->DH, w->spart);
     AZG_CK(hipGetLastError(), "train: stem_wgrad");
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3((27 * C + 63) / 64), dim3(256), 0, st, w->spart, B, 27 * C,
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3((27 * C + 15) / 16), dim3(256), 0, st, w->spart, B * STEM_WG_CHUNKS, 27 * C,
                        G + h->poff[h->t_stem_w], nullptr, 27 * C, 1, C);
     AZG_CK(hipGetLastError(), "train: stem_wgrad_reduce");
     R(reuse(0));

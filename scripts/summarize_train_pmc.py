@@ -1,0 +1,91 @@
+"""Train-step PMC evidence (scripts/gpu_pmc_train.sh: rocprofv3 --pmc passes over
+scripts/bench_train.py --serial, 6x128, B=128) + the serial kernel trace
+(scripts/gpu_train_wt.sh) -> profiles/<tag>_train_pmc.md: per kernel the serial
+duration, MFMA fraction of the fp32 peak (algorithmic FLOP / duration), SQ MFMA
+busy, HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections) and GB/s, wait
+and LDS profile.
+
+    python scripts/summarize_train_pmc.py gpurun_out/pmc_train2 gpurun_out/wt/serial/run_results.db r2
+"""
+import collections
+import csv
+import glob
+import os
+import sqlite3
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+B, C = 128, 128
+M = B * 225
+CONV_FLOP = 2 * M * 9 * C * C                      # one 3x3 conv, fwd / dgrad / wgrad
+ACT = M * C * 4
+
+
+def main():
+    pmc_dir, db, tag = sys.argv[1], sys.argv[2], sys.argv[3]
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(pmc_dir, "p*", "run_counter_collection.csv")):
+        for r in csv.DictReader(open(f, newline="")):
+            acc[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    con = sqlite3.connect(db)
+    dur = collections.defaultdict(list)
+    trace = sorted(con.execute("select name, start, end from kernels"), key=lambda r: r[1])
+    for name, s, e in trace:
+        dur[name.split("(")[0]].append((e - s) / 1e3)
+    # kernels of one train step (between two stem launches): setup kernels excluded
+    starts = [i for i, r in enumerate(trace) if "stem_mfma" in r[0]]
+    in_step = collections.Counter(r[0].split("(")[0] for r in trace[starts[-3]:starts[-2]])
+    flops = {"conv3x3_wgrad_t": CONV_FLOP, "conv3x3_train": CONV_FLOP}
+    algo = {"conv3x3_train<128, 2, 1": 2 * ACT, "conv3x3_train<128, 2, 2": 4 * ACT, "conv3x3_train<128, 3, 2": 5 * ACT,
+            "conv3x3_wgrad_t": 2 * ACT, "bn_apply_kernel<128, false": 2 * ACT, "bn_apply_kernel<128, true": 3 * ACT,
+            "bn_bwd_apply_kernel<128, false": 4 * ACT, "bn_bwd_apply_kernel<128, true": 5 * ACT}
+    rows = []
+    for k, d in acc.items():
+        m = {c: sum(v) / len(v) for c, v in d.items()}
+        if k not in dur or k not in in_step:
+            continue
+        ds = sorted(dur[k])
+        us = ds[len(ds) // 2]
+        hbm = m.get("FETCH_SIZE", 0) * 2 * 1024 + m.get("WRITE_SIZE", 0) * 1024
+        row = {"kernel": k.replace("void ", "").replace("azg::", ""), "us": us, "n": in_step[k], "hbm_mb": hbm / 1e6,
+               "gbs": hbm / (us * 1e-6) / 1e9}
+        for key, f in flops.items():
+            if key in k:
+                row["frac"] = f / (us * 1e-6) / 157.3e12
+        for key, a in algo.items():
+            if key in k:
+                row["alg_mb"] = a / 1e6
+        if "GRBM_GUI_ACTIVE" in m and m["GRBM_GUI_ACTIVE"]:
+            row["busy"] = m.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) * 8 / (1024 * m["GRBM_GUI_ACTIVE"])
+        wc = m.get("SQ_WAVE_CYCLES", 0)
+        if wc:
+            row["wait"] = m.get("SQ_WAIT_ANY", 0) / wc
+            row["lds_wait"] = m.get("SQ_WAIT_INST_LDS", 0) / wc
+        row["conf"] = m.get("SQ_LDS_BANK_CONFLICT", 0)
+        row["valu_per_mfma"] = m.get("SQ_INSTS_VALU", 0) / m["SQ_INSTS_MFMA"] if m.get("SQ_INSTS_MFMA") else None
+        rows.append(row)
+    rows.sort(key=lambda r: -r["us"])
+    L = [f"# Train step PMC ({tag}): 6x128, B = 128, serial schedule (key 12 = 1)", "",
+         "Durations: median of the serial rocprofv3 kernel trace (`scripts/gpu_train_wt.sh`); counters: "
+         "`scripts/gpu_pmc_train.sh` (separate --pmc passes, averaged over the launches of each kernel). "
+         "MFMA fraction = algorithmic FLOP (2·M·9·C², M = 28,800 pixels) / duration / 157.3 TFLOP/s; "
+         "SQ busy = SQ_VALU_MFMA_BUSY_CYCLES / (4 SIMD x 256 CU x GRBM_GUI_ACTIVE / 8); "
+         "HBM = FETCH_SIZE x2 + WRITE_SIZE (KiB -> bytes, gfx950 correction).", "",
+         "| kernel | per step | us | MFMA frac | SQ MFMA busy | HBM MB (alg.) | GB/s | wait_any | LDS wait | LDS conflict cyc | VALU/MFMA |",
+         "|---|---|---|---|---|---|---|---|---|---|---|"]
+    for r in rows:
+        f = lambda key, fmt: (fmt.format(r[key]) if r.get(key) is not None else "")
+        L.append(f"| `{r['kernel'][:48]}` | {r['n']} | {r['us']:.1f} | {f('frac', '{:.1%}')} | {f('busy', '{:.1%}')} | "
+                 f"{r['hbm_mb']:.1f}{' (' + format(r['alg_mb'], '.1f') + ')' if r.get('alg_mb') else ''} | "
+                 f"{r['gbs']:.0f} | {f('wait', '{:.1%}')} | {f('lds_wait', '{:.1%}')} | {r['conf']:.0f} | "
+                 f"{f('valu_per_mfma', '{:.2f}')} |")
+    L += ["", "Reading: the convs are MFMA-bound at 64-68 % SQ busy inside an 88 % tile-quantization ceiling "
+              "(450 tiles of 128x64 on 256 CUs); the BN kernels are HBM passes at 3-6 TB/s; wgrad_reduce reads "
+              "the split-K slabs (33 MB) the weight-grad kernel wrote.", ""]
+    out = os.path.join(REPO, "profiles", f"{tag}_train_pmc.md")
+    open(out, "w").write("\n".join(L) + "\n")
+    print("\n".join(L))
+
+
+if __name__ == "__main__":
+    main()
