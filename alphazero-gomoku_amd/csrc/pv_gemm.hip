@@ -51,37 +51,49 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(GemmPair gp)
         // or one k phase and a row (row-contiguous operands: 32 threads read a 128-B
         // row of the other dimension); no per-element index division, UNR loads in
         // flight per thread before their LDS stores.
-        constexpr int UNR = 8;
-        auto stage = [&](const float* X, int sx_row, int sx_k, int rlim, int rbase, float* dst) {
+        constexpr int UNR = 16;
+        struct Op { const float* src; float* d; bool rok; int sx_k; int kq; };
+        auto op = [&](const float* X, int sx_row, int sx_k, int rlim, int rbase, float* dst) {
             const bool kcontig = sx_k == 1;
             const int r = kcontig ? (tid >> 3) : (tid & 31);
             const int kq = kcontig ? (tid & 7) : (tid >> 5);
-            const bool rok = rbase + r < rlim;
-            const float* src = X + (size_t)(rbase + r) * sx_row + (size_t)k0 * sx_k;
-            float* d = dst + r * ldk;
-            const int kend = kc + (kc & 1);
-            for (int kb = kq; kb < kend; kb += 8 * UNR) {
-                float v[UNR];
-#pragma unroll
-                for (int u = 0; u < UNR; ++u) {
-                    const int k = kb + 8 * u;
-                    v[u] = (rok && k < kc) ? src[(size_t)k * sx_k] : 0.f;
-                }
-#pragma unroll
-                for (int u = 0; u < UNR; ++u) {
-                    const int k = kb + 8 * u;
-                    if (k < kend) d[k] = v[u];
-                }
-            }
+            return Op{X + (size_t)(rbase + r) * sx_row + (size_t)k0 * sx_k, dst + r * ldk, rbase + r < rlim, sx_k, kq};
         };
-        stage(P.A, P.sai, P.sak, P.M, i0, As);
-        stage(P.B, P.sbj, P.sbk, P.N, j0, Bs);
+        const Op oa = op(P.A, P.sai, P.sak, P.M, i0, As), ob = op(P.B, P.sbj, P.sbk, P.N, j0, Bs);
+        const int kend = kc + (kc & 1);
+        // both operands' loads of a step in flight together (UNR each), then their stores
+        for (int kb = 0; kb < kend; kb += 8 * UNR) {
+            float va[UNR], vb[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const int ka = kb + oa.kq + 8 * u, kbb = kb + ob.kq + 8 * u;
+                va[u] = (oa.rok && ka < kc) ? oa.src[(size_t)ka * oa.sx_k] : 0.f;
+                vb[u] = (ob.rok && kbb < kc) ? ob.src[(size_t)kbb * ob.sx_k] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const int ka = kb + oa.kq + 8 * u, kbb = kb + ob.kq + 8 * u;
+                if (ka < kend) oa.d[ka] = va[u];
+                if (kbb < kend) ob.d[kbb] = vb[u];
+            }
+        }
         __syncthreads();
         const int steps = (kc + 1) >> 1;
         const int s0 = wid * steps / 4, s1 = (wid + 1) * steps / 4;
         const float* ar = As + r32 * ldk + h;
         const float* br = Bs + r32 * ldk + h;
-        for (int s = s0; s < s1; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[2 * s], br[2 * s], acc, 0, 0, 0);
+        int s = s0;
+        for (; s + 4 <= s1; s += 4) {   // 4 steps' fragments read ahead of their MFMAs
+            float a4[4], b4[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                a4[u] = ar[2 * (s + u)];
+                b4[u] = br[2 * (s + u)];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[u], b4[u], acc, 0, 0, 0);
+        }
+        for (; s < s1; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[2 * s], br[2 * s], acc, 0, 0, 0);
         __syncthreads();
     }
     float* red = smem;   // [4][16][64]
