@@ -543,6 +543,34 @@ int pick_conv_tile(int C, int M)
     return best;
 }
 
+// Tail split of the 128x64 / 8-wave launch (shape 8): its tiles run in rounds of 512
+// resident workgroups (2 per CU), and a last round holding a few tiles costs a whole
+// round (B = 2048: 7,200 tiles = 14 rounds + 32 tiles).  The boards of the last,
+// partial round go to a second launch of 64x64 / 4-wave tiles, which spreads them
+// over the chip at up to 4 per CU.  Every tile shape computes the same per-element K
+// order, so the split is bitwise neutral.  Key 21 (default 1) switches it.
+int g_conv_tail_split = 1;
+
+template <int CC>
+static hipError_t launch_shape8_split(int epi, const float* in, const float* wp, const float* scale,
+                                      const float* shift, const float* resid, float* out, int M, hipStream_t st)
+{
+    constexpr int BM = 128, NTN = CC / 64, SLOTS = 512;
+    const int B = M / PIX;
+    const int ntiles = ((M + BM - 1) / BM) * NTN;
+    const int rounds = ntiles / SLOTS, rem = ntiles - rounds * SLOTS;
+    if (!g_conv_tail_split || M % PIX != 0 || rounds < 2 || rem == 0 || rem > SLOTS / 2)
+        return launch_conv_epi<CC, 64, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);
+    int B1 = (int)((long)rounds * SLOTS / NTN * BM / PIX);    // boards of whole rounds
+    while (B1 > 0 && ((B1 * PIX + BM - 1) / BM) * NTN > rounds * SLOTS) --B1;
+    if (B1 <= 0 || B1 >= B) return launch_conv_epi<CC, 64, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);
+    hipError_t e = launch_conv_epi<CC, 64, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, B1 * PIX, st);
+    if (e != hipSuccess) return e;
+    const size_t off = (size_t)B1 * PADPIX * CC;
+    return launch_conv_epi<CC, 64, 2, 1>(epi, in + off, wp, scale, shift, resid ? resid + off : nullptr, out + off,
+                                         (B - B1) * PIX, st);
+}
+
 hipError_t launch_conv3x3_shape(int shape, int C, int epi, const float* in, const float* wp, const float* scale,
                                 const float* shift, const float* resid, float* out, int M, hipStream_t st)
 {
@@ -564,7 +592,7 @@ hipError_t launch_conv3x3_shape(int shape, int C, int epi, const float* in, cons
         case 5: return launch_conv_epi<CC, 64, 2, 1>(epi, in, wp, scale, shift, resid, out, M, st);             \
         case 6: return launch_conv_epi<CC, 128, 2, 2, 8>(epi, in, wp, scale, shift, resid, out, M, st);         \
         case 7: return launch_conv_epi<CC, 128, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);         \
-        case 8: return launch_conv_epi<CC, 64, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);          \
+        case 8: return launch_shape8_split<CC>(epi, in, wp, scale, shift, resid, out, M, st);                   \
         case 9: return launch_conv_epi<CC, 128, 2, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);         \
         AZG_SB_SHAPES(CC)                                                                                       \
         default: return hipErrorInvalidValue;                                                                   \
@@ -869,6 +897,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
 #ifdef AZG_AB_STUDIES
         azg::g_train_skip = value;
 #endif
+        return prev;
+    }
+    if (key == 21) {  // per-layer conv: last partial round of the 128x64 launch as 64x64 tiles (1) or not (0)
+        const int prev = azg::g_conv_tail_split;
+        azg::g_conv_tail_split = value ? 1 : 0;
         return prev;
     }
     if (key == 18) {  // train: write-through outputs (bits: 1 convs, 2 BN apply, 4 wgrad slabs)

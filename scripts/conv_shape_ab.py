@@ -35,7 +35,16 @@ def main():
     m = PyTorchModel(board_size=15, device=str(dev), n_res_blocks=args.blocks, channels=args.channels)
     m.net.eval()
     eng = m.engine
-    shapes = [int(s) for s in args.shapes.split(",")]
+    # a variant is "SHAPE" or "SHAPE/KEY=VAL" (e.g. 8/21=0: shape 8 without the tail split)
+    shapes = args.shapes.split(",")
+
+    def select(v):
+        lib.azg_pv_set_tuning(21, 1)
+        sh, *kv = v.split("/")
+        lib.azg_pv_set_tuning(0, int(sh))
+        for item in kv:
+            k, val = (int(a) for a in item.split("="))
+            lib.azg_pv_set_tuning(k, val)
     C = args.channels
     for B in (int(b) for b in args.batches.split(",")):
         x = torch.from_numpy(synth_encoded(B, seed=B)).to(dev)
@@ -44,7 +53,7 @@ def main():
         ref = None
         res = {s: [] for s in shapes}
         for s in shapes:   # bitwise check + warm-up
-            lib.azg_pv_set_tuning(0, s)
+            select(s)
             eng.forward_into(x, probs, values)
             torch.cuda.synchronize()
             out = torch.cat([probs.reshape(-1), values.reshape(-1)]).cpu()
@@ -55,7 +64,7 @@ def main():
                 sys.exit(3)
         for _ in range(args.rounds):
             for s in shapes:
-                lib.azg_pv_set_tuning(0, s)
+                select(s)
                 eng.forward_into(x, probs, values)
                 eng.profile_enable(True)
                 for _ in range(args.steps):

@@ -315,3 +315,33 @@ def test_train_then_predict_uses_new_weights():
     assert not np.allclose(p0, p1)
     np.testing.assert_allclose(p1, rp, atol=1e-5)
     np.testing.assert_allclose(v1, rv, atol=1e-5)
+
+
+@pytest.mark.parametrize("key,values", [(18, (0, 1, 2, 4, 7)), (12, (0, 1)), (16, (0, 1, 2))])
+def test_train_schedule_keys_bitwise(key, values):
+    """Train-step tuning keys change cache policy (18: write-through stores), stream
+    schedule (12: weight grads overlapped or serial) or the weight-grad staging (16):
+    two steps from one state must give bitwise-identical params, grads, BN buffers
+    and Adam moments under every value."""
+    import _native
+    lib = _native.load_library()
+    b, p = synth_positions(128, seed=91)
+    x = encode_batch(b, p)
+    pi, z = synth_targets(128, seed=92)
+    prev = lib.azg_pv_set_tuning(key, values[0])
+    ref = None
+    try:
+        for v in values:
+            lib.azg_pv_set_tuning(key, v)
+            m = make_model(2, 128, seed=3)
+            for _ in range(2):
+                m.train_batch(x, pi, z)
+            got = [t.detach().cpu().clone() for t in m.net.state_dict().values()]
+            got += [m.engine.flat_grads.cpu().clone(), m.optimizer.flat_exp_avg.cpu().clone(),
+                    m.optimizer.flat_exp_avg_sq.cpu().clone()]
+            if ref is None:
+                ref = got
+            else:
+                assert all(torch.equal(a, c) for a, c in zip(ref, got)), (key, v)
+    finally:
+        lib.azg_pv_set_tuning(key, prev)
