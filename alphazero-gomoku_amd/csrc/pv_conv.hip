@@ -202,7 +202,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ / 2) void conv3x3_mfma(
 // workgroup L is dispatched to XCD L % 8, so each XCD gets a contiguous run of
 // logical tiles (the N-tiles of one M tile adjacent, then neighbouring M tiles) and
 // the halo rows they share are L2 hits on that XCD.
-template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, int ABL = 0>
+template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, int ABL = 0, int VAR = 0>
 __global__ __launch_bounds__(64 * NW_, 2) void conv3x3_halo(
     const float* __restrict__ in, const float* __restrict__ wp,
     const float* __restrict__ scale, const float* __restrict__ shift,
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(64 * NW_, 2) void conv3x3_halo(
     const int L = blockIdx.x, nt = gridDim.x;
     const int xcd = L & 7, q8 = nt >> 3, r8 = nt & 7;
     const int t = xcd * q8 + min(xcd, r8) + (L >> 3);
-    halo_tile<C, BN_, WM_, TM_, NW_, EPI, false, ABL>(in, wp, scale, shift, resid, out,
+    halo_tile<C, BN_, WM_, TM_, NW_, EPI, false, ABL, VAR>(in, wp, scale, shift, resid, out,
                                           __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0, 0x00020000), M,
                                           (t / NTN) * T::BM, (t % NTN) * T::BN, smem);
 }
@@ -456,22 +456,22 @@ static hipError_t launch_conv_t(const float* in, const float* wp, const float* s
     return hipGetLastError();
 }
 
-template <int C, int BN, int WM, int TM, int NW, int EPI>
+template <int C, int BN, int WM, int TM, int NW, int EPI, int VAR = 0>
 static hipError_t launch_halo_t(const float* in, const float* wp, const float* scale, const float* shift,
                                 const float* resid, float* out, int M, hipStream_t st)
 {
     using T = ConvTile<C, BN, WM, TM, NW>;
-    constexpr int lds = halo_lds_bytes<C, BN, WM, TM, NW>();
+    constexpr int lds = halo_lds_bytes<C, BN, WM, TM, NW, VAR>();
     static bool attr_done = false;
     if (!attr_done) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_halo<C, BN, WM, TM, NW, EPI>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_halo<C, BN, WM, TM, NW, EPI, 0, VAR>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
         attr_done = true;
     }
     dim3 grid(((M + T::BM - 1) / T::BM) * (C / T::BN));
-    hipLaunchKernelGGL((conv3x3_halo<C, BN, WM, TM, NW, EPI>), grid, dim3(T::NT), lds, st, in, wp, scale, shift,
-                       resid, out, M);
+    hipLaunchKernelGGL((conv3x3_halo<C, BN, WM, TM, NW, EPI, 0, VAR>), grid, dim3(T::NT), lds, st, in, wp, scale,
+                       shift, resid, out, M);
     return hipGetLastError();
 }
 
@@ -551,6 +551,23 @@ int pick_conv_tile(int C, int M)
 // order, so the split is bitwise neutral.  Key 21 (default 1) switches it.
 int g_conv_tail_split = 1;
 
+int g_conv_var = 1;   // key 22: tile-body variant of the per-layer 128x64 launch (1 default: halo rows keyed on
+                      // the board position, conflict-free fragment reads, +0.5 % in-process A/B; 0, 4, 5; bitwise identical)
+
+template <int CC>
+static hipError_t launch_s8(int epi, const float* in, const float* wp, const float* scale, const float* shift,
+                            const float* resid, float* out, int M, hipStream_t st)
+{
+#define AZG_S8_VAR(V)                                                                                                  \
+    if (g_conv_var == V) {                                                                                             \
+        if (epi == EPI_BN_RELU) return launch_halo_t<CC, 64, 4, 1, 8, EPI_BN_RELU, V>(in, wp, scale, shift, resid, out, M, st); \
+        if (epi == EPI_BN_RES_RELU) return launch_halo_t<CC, 64, 4, 1, 8, EPI_BN_RES_RELU, V>(in, wp, scale, shift, resid, out, M, st); \
+    }
+    AZG_S8_VAR(1) AZG_S8_VAR(4) AZG_S8_VAR(5)
+#undef AZG_S8_VAR
+    return launch_conv_epi<CC, 64, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);
+}
+
 template <int CC>
 static hipError_t launch_shape8_split(int epi, const float* in, const float* wp, const float* scale,
                                       const float* shift, const float* resid, float* out, int M, hipStream_t st)
@@ -560,11 +577,11 @@ static hipError_t launch_shape8_split(int epi, const float* in, const float* wp,
     const int ntiles = ((M + BM - 1) / BM) * NTN;
     const int rounds = ntiles / SLOTS, rem = ntiles - rounds * SLOTS;
     if (!g_conv_tail_split || M % PIX != 0 || rounds < 2 || rem == 0 || rem > SLOTS / 2)
-        return launch_conv_epi<CC, 64, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);
+        return launch_s8<CC>(epi, in, wp, scale, shift, resid, out, M, st);
     int B1 = (int)((long)rounds * SLOTS / NTN * BM / PIX);    // boards of whole rounds
     while (B1 > 0 && ((B1 * PIX + BM - 1) / BM) * NTN > rounds * SLOTS) --B1;
-    if (B1 <= 0 || B1 >= B) return launch_conv_epi<CC, 64, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, M, st);
-    hipError_t e = launch_conv_epi<CC, 64, 4, 1, 8>(epi, in, wp, scale, shift, resid, out, B1 * PIX, st);
+    if (B1 <= 0 || B1 >= B) return launch_s8<CC>(epi, in, wp, scale, shift, resid, out, M, st);
+    hipError_t e = launch_s8<CC>(epi, in, wp, scale, shift, resid, out, B1 * PIX, st);
     if (e != hipSuccess) return e;
     const size_t off = (size_t)B1 * PADPIX * CC;
     return launch_conv_epi<CC, 64, 2, 1>(epi, in + off, wp, scale, shift, resid ? resid + off : nullptr, out + off,
@@ -897,6 +914,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
 #ifdef AZG_AB_STUDIES
         azg::g_train_skip = value;
 #endif
+        return prev;
+    }
+    if (key == 22) {  // per-layer 128x64 conv tile-body variant (1 default; 0, 4, 5 A/B, bitwise identical)
+        const int prev = azg::g_conv_var;
+        if (value == 0 || value == 1 || value == 4 || value == 5) azg::g_conv_var = value;
         return prev;
     }
     if (key == 21) {  // per-layer conv: last partial round of the 128x64 launch as 64x64 tiles (1) or not (0)

@@ -212,6 +212,7 @@ def test_persistent_tower_bitwise_equals_per_layer_launches(blocks, ch, batches)
     eng = m.engine
     stream = torch.cuda.current_stream().cuda_stream
     prev_mode = lib.azg_pv_set_tuning(5, 1)
+    prev_shape = lib.azg_pv_set_tuning(6, 8)
     try:
         for B in batches:
             x = torch.from_numpy(synth_encoded(B, seed=B)).cuda()
@@ -237,8 +238,37 @@ def test_persistent_tower_bitwise_equals_per_layer_launches(blocks, ch, batches)
                     assert lib.azg_pv_tower_status(eng.h, stream) == 0
                     assert torch.equal(l0, l1), ("var", var, B, float((l0 - l1).abs().max()))
     finally:
-        lib.azg_pv_set_tuning(6, 5)
+        lib.azg_pv_set_tuning(6, prev_shape)
         lib.azg_pv_set_tuning(5, prev_mode)
+
+
+@pytest.mark.parametrize("B", [300, 2048, 2600])
+def test_per_layer_variants_bitwise(B):
+    """Per-layer launches (key 5 = 0): forced tile shapes 5 (64x64) and 8 (128x64),
+    the 128x64 tile-body variants (key 22: 0, 1 default, 4, 5) and its tail split
+    (key 21: the last partial round as 64x64 tiles) compute the same per-element K
+    order: outputs bitwise equal."""
+    import _native
+    from synth import synth_encoded
+    lib = _native.load_library()
+    m = make_model(6, 128, seed=4)
+    eng = m.engine
+    x = torch.from_numpy(synth_encoded(B, seed=B + 1)).cuda()
+    prev = {k: lib.azg_pv_set_tuning(k, v) for k, v in ((5, 0), (0, 5))}
+    prev[22] = lib.azg_pv_set_tuning(22, 1)
+    prev[21] = lib.azg_pv_set_tuning(21, 1)
+    try:
+        _, _, l0 = eng.forward(x, want_logits=True)
+        lib.azg_pv_set_tuning(0, 8)
+        for var in (0, 1, 4, 5):
+            for split in (0, 1):
+                lib.azg_pv_set_tuning(22, var)
+                lib.azg_pv_set_tuning(21, split)
+                _, _, l1 = eng.forward(x, want_logits=True)
+                assert torch.equal(l0, l1), (B, var, split, float((l0 - l1).abs().max()))
+    finally:
+        for k, v in prev.items():
+            lib.azg_pv_set_tuning(k, v)
 
 
 def test_persistent_tower_under_concurrent_load():
