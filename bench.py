@@ -309,14 +309,27 @@ def roofline_from_profile(prof, boards, blocks, ch, kname_tower, kname_layer, tr
     return out
 
 
+def batch_buckets(top):
+    """Every batch bucket of the engine's autotuning caches up to `top` boards (the
+    C++ conv_batch_bucket, pv_conv.hip: multiples of 16 up to 256 boards, then
+    1/8-octave steps), each as the largest batch that falls in it."""
+    out = set(range(16, min(top, 256) + 1, 16))
+    p = 256
+    while p < top:
+        q = p // 8
+        out.update(range(p + q, min(2 * p, top) + 1, q))
+        p *= 2
+    out.add(top)
+    return sorted(b for b in out if b <= top)
+
+
 def visit_buckets(model, top):
-    """Conv/tower variant autotuning is cached per batch bucket: visit the buckets a
-    self-play run's leaf batches fall in, so no tuning happens in the timed region."""
+    """Conv/tower variant autotuning is cached per batch bucket: visit EVERY bucket a
+    self-play run's leaf batches can fall in, so no tuning happens in the timed region
+    (a missed bucket tunes mid-run: ~10 shapes x 4 timed launches + a stream sync)."""
     z8 = np.zeros((top, 225), np.int8)
-    sizes = sorted({max(1, top * k // 32) for k in range(1, 33)} | {1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256})
-    for b in sizes:
-        if b <= top:
-            model.predict_boards(z8[:b], np.ones(b, np.int8))
+    for b in sorted(set(batch_buckets(top)) | {1, 2, 4, 8}):
+        model.predict_boards(z8[:b], np.ones(b, np.int8))
 
 
 def selfplay_run(model, game_class, G, S, max_moves, seeds, profile=True):

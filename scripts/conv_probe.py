@@ -22,10 +22,12 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--tower", type=int, default=0)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--shape", type=int, default=-1, help="force the per-layer tile shape (key 0)")
     args = ap.parse_args()
     import _native
     lib = _native.load_library()
     lib.azg_pv_set_tuning(5, args.tower)
+    lib.azg_pv_set_tuning(0, args.shape)
     from network import PyTorchModel
     from synth import synth_encoded
     dev = torch.device("cuda", 0)

@@ -32,7 +32,6 @@ def main():
     write = means(os.path.join(root, "pmc_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE")
     d = os.path.join(root, "pmc_SQ_VALU_MFMA_BUSY_CYCLES_GRBM_GUI_ACTIVE", "run_counter_collection.csv")
     mf, gr = means(d, "SQ_VALU_MFMA_BUSY_CYCLES"), means(d, "GRBM_GUI_ACTIVE")
-    act = B * 225 * C * 4                       # one interior activation tensor
     path = os.path.join(REPO, "profiles", "conv_traffic.json")
     cur = json.load(open(path))
     recs = cur["records"] if "records" in cur else [cur]
@@ -42,9 +41,12 @@ def main():
             continue
         f = fetch[epi] * 2 * 1024
         w = write.get(epi, write.get(0)) * 1024
-        alg = (reads + 1) * act + 9 * C * C * 4
+        # the 128x64 launch covers the boards of whole rounds (the tail split sends the
+        # rest to 64x64 tiles): its boards follow from the bytes it wrote
+        nb = round(w / (225 * C * 4))
+        alg = (reads + 1) * nb * 225 * C * 4 + 9 * C * C * 4
         rec = {"kernel": "conv3x3", "shape": "128x64, 8 waves (conv3x3_halo<128,64,4,1,8>)", "epilogue": name,
-               "config": f"6x128_B{B}", "tag": tag, "boards_per_launch": B, "convs_per_launch": 1,
+               "config": f"6x128_B{B}", "tag": tag, "boards_per_launch": nb, "convs_per_launch": 1,
                "hbm_bytes_per_launch": round(f + w), "fetch_bytes": round(f), "write_bytes": round(w),
                "algorithmic_bytes": alg, "traffic_over_algorithmic": round((f + w) / alg, 3)}
         if epi in mf and epi in gr:
