@@ -242,8 +242,8 @@ def test_persistent_tower_bitwise_equals_per_layer_launches(blocks, ch, batches)
         lib.azg_pv_set_tuning(5, prev_mode)
 
 
-@pytest.mark.parametrize("B", [300, 2048, 2600])
-def test_per_layer_variants_bitwise(B):
+@pytest.mark.parametrize("blocks,ch,B", [(6, 128, 300), (6, 128, 2048), (6, 128, 2600), (2, 256, 600), (2, 64, 2100)])
+def test_per_layer_variants_bitwise(blocks, ch, B):
     """Per-layer launches (key 5 = 0): forced tile shapes 5 (64x64) and 8 (128x64),
     the 128x64 tile-body variants (key 22: 0, 1 default, 4, 5) and its tail split
     (key 21: the last partial round as 64x64 tiles) compute the same per-element K
@@ -251,7 +251,7 @@ def test_per_layer_variants_bitwise(B):
     import _native
     from synth import synth_encoded
     lib = _native.load_library()
-    m = make_model(6, 128, seed=4)
+    m = make_model(blocks, ch, seed=4)
     eng = m.engine
     x = torch.from_numpy(synth_encoded(B, seed=B + 1)).cuda()
     prev = {k: lib.azg_pv_set_tuning(k, v) for k, v in ((5, 0), (0, 5))}
@@ -265,7 +265,7 @@ def test_per_layer_variants_bitwise(B):
                 lib.azg_pv_set_tuning(22, var)
                 lib.azg_pv_set_tuning(21, split)
                 _, _, l1 = eng.forward(x, want_logits=True)
-                assert torch.equal(l0, l1), (B, var, split, float((l0 - l1).abs().max()))
+                assert torch.equal(l0, l1), (blocks, ch, B, var, split, float((l0 - l1).abs().max()))
     finally:
         for k, v in prev.items():
             lib.azg_pv_set_tuning(k, v)
