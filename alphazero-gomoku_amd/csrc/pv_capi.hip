@@ -455,7 +455,7 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
 // Tower variant per (C, blocks, batch bucket): g_tower_mode 0 = per-layer launches,
 // 1 = persistent tower with shape g_tower_shape, 2 = timed on first use of the
 // bucket (stem + tower, every variant, best of 2 after a warm pass; the persistent
-// tower wins from ~128 boards, per-layer launches below and at the largest
+// tower wins from ~128 to ~1024 boards, per-layer launches below and at the largest
 // batches).  While the stream is being captured the untuned default is used.
 static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, const int8_t* boards,
                          const int8_t* players)
@@ -494,11 +494,13 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
                 int b = 0;
                 for (int c = 1; c < 3; ++c)
                     if (best_ms[c] < best_ms[b]) b = c;
-                // the 128x64 persistent tower is kept unless another variant is > 2 %
-                // faster: single-round timings flip between near-equal variants (the
-                // self-play run then mixes both), and one kernel per forward keeps
-                // the roofline attribution and the rocprof summary unambiguous
-                if (best_ms[2] <= 1.02f * best_ms[b]) b = 2;
+                // a preferred variant is kept unless another is > 2 % faster (single-
+                // round timings flip between near-equal variants): the 128x64
+                // persistent tower below 1536 boards, per-layer launches above (their
+                // 128x64 tiles measured ~1-2 % ahead of the tower at 2048-4096 boards,
+                // scripts/conv_shape_ab.py / conv_probe.py)
+                const int pref = batch >= 1536 ? 0 : 2;
+                if (best_ms[pref] <= 1.02f * best_ms[b]) b = pref;
                 choice = cand[b];
             }
             (void)hipEventDestroy(e1);
