@@ -164,6 +164,15 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          tiles, run back to back by the claiming workgroup, default: the second
  *          tile's halo rows hit the XCD's L2, +2 % at B = 512 and 4096, measured;
  *          0 = one 128x64 tile per claim); bitwise identical results;
+ *   key 18: train write-through stores (bits: 1 conv outputs, 2 BN-apply outputs,
+ *          4 weight-grad slabs; default 7): no dirty L2 lines at the kernel
+ *          boundaries; bitwise identical;
+ *   key 19: study build only: skip train BN kernels (timing, results invalid);
+ *   key 21: per-layer 128x64 conv: the last partial round of workgroups runs as a
+ *          second launch of 64x64 tiles (1, default) or not (0); bitwise identical;
+ *   key 22: per-layer 128x64 conv tile body (1 = halo rows keyed on the board
+ *          position, conflict-free fragment reads, default; 0 = row-keyed; 4 / 5 =
+ *          LDS-DMA staging); bitwise identical;
  *   key 14: persistent-tower dependency spin bound (tests only: 0 makes every
  *          dependency wait time out at once, exercising the error path; -1
  *          restores the default).
