@@ -935,9 +935,9 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         if (value >= 0 && value <= 7) azg::g_train_wt = value;
         return prev;
     }
-    if (key == 16) {  // train: wgrad kernel (1 K-contiguous staging, default; 0 row staging, A/B)
+    if (key == 16) {  // train: wgrad kernel (3 LDS-DMA natural rows, default; 1 K-contiguous, 2 same 2 ahead, 0 row staging; bitwise identical)
         const int prev = azg::g_wgrad_kernel;
-        if (value >= 0 && value <= 2) azg::g_wgrad_kernel = value;
+        if (value >= 0 && value <= 3) azg::g_wgrad_kernel = value;
         return prev;
     }
     if (key == 13) {  // train: wgrad K chunk (32 default, 16 A/B)

@@ -23,9 +23,8 @@
 
 namespace azg {
 
-hipError_t launch_wgrad(int C, const float* dz, const float* x, float* slab, float* dw, int M, int S, int rps,
+hipError_t launch_wgrad(int C, const float* dz, const float* x, float* slab, float* dw, int M, int S,
                         hipStream_t st);
-int wgrad_rows_per_split(int C, int M);
 int wgrad_splits(int C, int M);
 constexpr int kMaxWgradSplits = 64;   // wgrad_splits <= slots / tiles <= 56, rounded to 8
 
@@ -1050,9 +1049,9 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     auto wgrad = [&](int slot, const float* xin, int tensor) -> int32_t {
         if (g_wgrad_serial) {   // A/B: weight grads on the caller's stream, no overlap
             int pr = prof_begin(h, AZG_PROF_TRAIN_WGRAD, st);
-            const int rps = wgrad_rows_per_split(C, M), S = wgrad_splits(C, M);
+            const int S = wgrad_splits(C, M);
             if (S > w->S) return set_error("train: wgrad splits exceed the slab workspace", hipErrorInvalidValue);
-            AZG_CK(launch_wgrad(C, dzbuf[slot], xin, w->slab, G + h->poff[tensor], M, S, rps, st),
+            AZG_CK(launch_wgrad(C, dzbuf[slot], xin, w->slab, G + h->poff[tensor], M, S, st),
                    "train: wgrad");
             prof_end(h, pr, st);
             return 0;
@@ -1060,9 +1059,9 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         AZG_CK(hipEventRecord(w->ev_ready[slot], st), "train: event record");
         AZG_CK(hipStreamWaitEvent(w->side, w->ev_ready[slot], 0), "train: stream wait");
         int pr = prof_begin(h, AZG_PROF_TRAIN_WGRAD, w->side);
-        const int rps = wgrad_rows_per_split(C, M), S = wgrad_splits(C, M);
+        const int S = wgrad_splits(C, M);
         if (S > w->S) return set_error("train: wgrad splits exceed the slab workspace", hipErrorInvalidValue);
-        AZG_CK(launch_wgrad(C, dzbuf[slot], xin, w->slab, G + h->poff[tensor], M, S, rps, w->side),
+        AZG_CK(launch_wgrad(C, dzbuf[slot], xin, w->slab, G + h->poff[tensor], M, S, w->side),
                "train: wgrad");
         prof_end(h, pr, w->side);
         AZG_CK(hipEventRecord(w->ev_done[slot], w->side), "train: event record");

@@ -5,12 +5,19 @@
 // writes its 128x128 (64x64 at C=64) partial tile to a slab; wgrad_reduce sums
 // the slabs in a fixed order (bitwise reproducible) into torch's [Cout][Cin][3][3].
 //
-// Operand staging keeps the natural NHWC rows ([32 pixels][channels]) in LDS;
-// MFMA fragments are read with ds_read_b32 (lanes 0-31 read 32 consecutive
-// channels of one pixel: conflict-free).  Rows past M load zeros.
+// Split s covers the whole 32-pixel chunks [s*NCH/S, (s+1)*NCH/S) of the batch
+// (NCH = ceil(M/32)): every split has 16 or 17 chunks at B = 128 instead of a fixed
+// row count whose last chunk is mostly padding.  Rows past M load zeros.
 #include "pv_internal.h"
 
 namespace azg {
+
+__device__ __forceinline__ void wgrad_split_rows(int split, int S, int M, int& mbeg, int& mend)
+{
+    const int nch = (M + 31) / 32;
+    mbeg = (int)((int64_t)split * nch / S) * 32;
+    mend = min(M, (int)((int64_t)(split + 1) * nch / S) * 32);
+}
 
 template <int C, int BK_ = 32>
 struct WgTile {
@@ -29,7 +36,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_mfma(
     const float* __restrict__ dz,   // padded NHWC [B][17][17][C]  (A^T: co)
     const float* __restrict__ x,    // padded NHWC                 (B: ci)
     float* __restrict__ slab,       // [S][9][C][C] partial dW[tap][co][ci]
-    int M, int rows_per_split)
+    int M, int S)
 {
     using T = WgTile<C, BK_>;
     constexpr int BT = T::BT, BK = T::BK, LD = T::LD, W = T::W, TT = T::T, LDF4 = T::LDF4, NT = T::NT;
@@ -53,8 +60,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_mfma(
     const int co0 = (t / NT) * BT, ci0 = (t % NT) * BT;
     const int ky = tap / 3, kx = tap - ky * 3;
     const int toff = ((ky - 1) * PADW + (kx - 1)) * C;
-    const int mbeg = split * rows_per_split;
-    const int mend = min(M, mbeg + rows_per_split);
+    int mbeg, mend;
+    wgrad_split_rows(split, S, M, mbeg, mend);
     const int nch = (mend - mbeg + BK - 1) / BK;
 
     // staging: LDF4 float4 per thread per operand; thread -> (row, col4)
@@ -150,7 +157,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_mfma(
 // by two so the sets are static): a load has a whole chunk of MFMAs more to land.
 template <int C, bool PF2 = false, bool WT = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_t(
-    const float* __restrict__ dz, const float* __restrict__ x, float* __restrict__ slab, int M, int rows_per_split)
+    const float* __restrict__ dz, const float* __restrict__ x, float* __restrict__ slab, int M, int S)
 {
     using T = WgTile<C, 32>;
     constexpr int BT = T::BT, BK = 32, W = T::W, TT = T::T, NT = T::NT;
@@ -172,8 +179,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_t(
     const int co0 = (t / NT) * BT, ci0 = (t % NT) * BT;
     const int ky = tap / 3, kx = tap - ky * 3;
     const int toff = ((ky - 1) * PADW + (kx - 1)) * C;
-    const int mbeg = split * rows_per_split;
-    const int mend = min(M, mbeg + rows_per_split);
+    int mbeg, mend;
+    wgrad_split_rows(split, S, M, mbeg, mend);
     const int nch = (mend - mbeg + BK - 1) / BK;
 
     const bool stager = tid < NBLK;
@@ -308,6 +315,124 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_t(
             }
 }
 
+
+// Same GEMM with NATURAL operand rows in LDS filled by LDS-DMA (default, key 16 = 3):
+// each wave-instruction global_load_lds_dwordx4 moves 1 KiB = 256/BT pixel rows of
+// BT channels straight into LDS (no staging VGPRs, no register transposition, no
+// ds_write), issued one chunk ahead.  MFMA step s reads, per operand, one
+// ds_read_b32 per lane: lanes 0-31 pixel s, lanes 32-63 pixel s + 16, 32
+// consecutive channels (co for dz, ci for x) -- the same K order as
+// conv3x3_wgrad_t, so all three kernels are bitwise identical.  16-B chunk j of LDS
+// row p holds global chunk j ^ 8*((p >> 4) & 1) (swizzle applied to each lane's
+// source address, cdna_hip_programming.md §5.4): the two half-waves of a fragment
+// read land on disjoint bank halves.  Rows past the split read padded pixel 0 (the
+// zero halo).  Measured at 6x128, B = 128 (scripts/wgrad_lab.hip): 74.0 vs 89.2 us
+// (hipEvent incl. launch) for the K-contiguous kernel.
+template <int C, bool WT = true>
+__global__ __launch_bounds__(256, 2) void conv3x3_wgrad_nat(
+    const float* __restrict__ dz, const float* __restrict__ x, float* __restrict__ slab, int M, int S)
+{
+    constexpr int BT = C < 128 ? C : 128, BK = 32, NT = C / BT, W = BT / 2, TT = BT / 64;
+    constexpr int RPI = 256 / BT;      // pixel rows per wave-instruction (1 KiB)
+    constexpr int CPR = BT / 4;        // 16-B chunks per row
+    constexpr int IPW = BK / RPI / 4;  // instructions per wave per operand per chunk
+    static_assert(IPW >= 1 && CPR >= 16, "tile");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* As = smem;                  // [2][BK][BT]  dz rows (co)
+    float* Bs = smem + 2 * BK * BT;    // [2][BK][BT]  x rows (ci, tap-shifted)
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 1, wn = wid & 1;
+    constexpr int TILES = 9 * NT * NT;
+    const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;   // XCD-aware order, see conv3x3_wgrad_mfma
+    const int split = (k / TILES) * 8 + xcd;
+    int t = k % TILES;
+    const int tap = t / (NT * NT);
+    t -= tap * NT * NT;
+    const int co0 = (t / NT) * BT, ci0 = (t % NT) * BT;
+    const int ky = tap / 3, kx = tap - ky * 3;
+    const int toff = ((ky - 1) * PADW + (kx - 1)) * C;
+    int mbeg, mend;
+    wgrad_split_rows(split, S, M, mbeg, mend);
+    const int nch = (mend - mbeg + BK - 1) / BK;
+
+    auto glds = [](const float* src, float* dst) {
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    };
+    const int ri = lane / CPR, jl = lane % CPR;
+    auto issue = [&](int kc, int buf) {
+#pragma unroll
+        for (int i = 0; i < IPW; ++i) {
+            const int r0 = (wid * IPW + i) * RPI;       // first LDS row of this instruction
+            const int p = r0 + ri;
+            const int m = mbeg + kc * BK + p;
+            const int j = jl ^ (((p >> 4) & 1) << 3);
+            const int po = m < mend ? pad_off(m, C) : 0;
+            const int px = m < mend ? po + toff : 0;
+            glds(dz + po + co0 + 4 * j, As + buf * BK * BT + r0 * BT);
+            glds(x + px + ci0 + 4 * j, Bs + buf * BK * BT + r0 * BT);
+        }
+    };
+    const int r32 = lane & 31, h = lane >> 5;
+    int aoff[TT], boff[TT];
+#pragma unroll
+    for (int i = 0; i < TT; ++i) {
+        const int ca = wm * W + i * 32 + r32, cb = wn * W + i * 32 + r32;
+        aoff[i] = 16 * h * BT + (((ca >> 2) ^ (h << 3)) << 2) + (ca & 3);
+        boff[i] = 16 * h * BT + (((cb >> 2) ^ (h << 3)) << 2) + (cb & 3);
+    }
+
+    f32x16 acc[TT][TT];
+#pragma unroll
+    for (int i = 0; i < TT; ++i)
+#pragma unroll
+        for (int j = 0; j < TT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    if (nch > 0) issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kc = 0; kc < nch; ++kc) {
+        const int cur = kc & 1;
+        // the other buffer's last reads ended at the previous chunk's barrier
+        if (kc + 1 < nch) issue(kc + 1, cur ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+        const float* Ab = As + cur * BK * BT;
+        const float* Bb = Bs + cur * BK * BT;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            float a[TT], b[TT];
+#pragma unroll
+            for (int i = 0; i < TT; ++i) a[i] = Ab[s * BT + aoff[i]];
+#pragma unroll
+            for (int j = 0; j < TT; ++j) b[j] = Bb[s * BT + boff[j]];
+#pragma unroll
+            for (int i = 0; i < TT; ++i)
+#pragma unroll
+                for (int j = 0; j < TT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of chunk kc+1 retired
+        __syncthreads();
+    }
+
+    float* out = slab + ((size_t)split * 9 + tap) * C * C;
+    const __amdgpu_buffer_rsrc_t rs = wt_rsrc(out, (size_t)C * C * sizeof(float));
+#pragma unroll
+    for (int i = 0; i < TT; ++i)
+#pragma unroll
+        for (int j = 0; j < TT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int co = co0 + wm * W + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int ci = ci0 + wn * W + j * 32 + r32;
+                store1<WT>(out, rs, co * C + ci, acc[i][j][r]);
+            }
+}
+
 // dW (torch layout [co][ci][3][3]) = sum over slabs, fixed order: four interleaved
 // partial sums (slabs k = 0,1,2,3 mod 4: independent loads in flight) combined as
 // ((p0 + p1) + (p2 + p3)).
@@ -335,16 +460,34 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     }
 }
 
-int g_wgrad_kernel = 1;   // 1: K-contiguous staging (conv3x3_wgrad_t, default); 0: row staging (A/B)
+// 3: LDS-DMA natural rows (conv3x3_wgrad_nat, default); 1: K-contiguous register
+// staging; 2: the same two chunks ahead; 0: row staging (A/B; all bitwise identical)
+int g_wgrad_kernel = 3;
 
 template <int C, int BK = 32>
-static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, float* dw, int M, int S, int rps,
+static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, float* dw, int M, int S,
                                  hipStream_t st)
 {
     using T = WgTile<C, BK>;
     if (S % 8) return hipErrorInvalidValue;           // wgrad_splits guarantees S % 8 == 0
     dim3 grid(S * 9 * T::NT * T::NT);
-    if (g_wgrad_kernel >= 1 && BK == 32) {
+    if (g_wgrad_kernel == 3 && BK == 32) {
+        constexpr int lds = 2 * 2 * 32 * T::BT * 4;
+        static bool attr_n = false;
+        if (!attr_n) {
+            hipError_t e = hipFuncSetAttribute((const void*)conv3x3_wgrad_nat<C, true>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)conv3x3_wgrad_nat<C, false>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            if (e != hipSuccess) return e;
+            attr_n = true;
+        }
+        if (g_train_wt & 4)
+            hipLaunchKernelGGL((conv3x3_wgrad_nat<C, true>), grid, dim3(256), lds, st, dz, x, slab, M, S);
+        else
+            hipLaunchKernelGGL((conv3x3_wgrad_nat<C, false>), grid, dim3(256), lds, st, dz, x, slab, M, S);
+    } else if (g_wgrad_kernel >= 1 && BK == 32) {
         constexpr int lds = 2 * 2 * T::BT * (32 + 4) * 4;
         static bool attr_t = false;
         if (!attr_t) {
@@ -360,11 +503,11 @@ static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, f
             attr_t = true;
         }
         if (g_wgrad_kernel == 2)
-            hipLaunchKernelGGL((conv3x3_wgrad_t<C, true>), grid, dim3(256), lds, st, dz, x, slab, M, rps);
+            hipLaunchKernelGGL((conv3x3_wgrad_t<C, true>), grid, dim3(256), lds, st, dz, x, slab, M, S);
         else if (g_train_wt & 4)
-            hipLaunchKernelGGL((conv3x3_wgrad_t<C, false, true>), grid, dim3(256), lds, st, dz, x, slab, M, rps);
+            hipLaunchKernelGGL((conv3x3_wgrad_t<C, false, true>), grid, dim3(256), lds, st, dz, x, slab, M, S);
         else
-            hipLaunchKernelGGL((conv3x3_wgrad_t<C>), grid, dim3(256), lds, st, dz, x, slab, M, rps);
+            hipLaunchKernelGGL((conv3x3_wgrad_t<C>), grid, dim3(256), lds, st, dz, x, slab, M, S);
     } else {
         static bool attr_done = false;
         if (!attr_done) {
@@ -373,7 +516,7 @@ static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, f
             if (e != hipSuccess) return e;
             attr_done = true;
         }
-        hipLaunchKernelGGL((conv3x3_wgrad_mfma<C, BK>), grid, dim3(256), T::LDS_BYTES, st, dz, x, slab, M, rps);
+        hipLaunchKernelGGL((conv3x3_wgrad_mfma<C, BK>), grid, dim3(256), T::LDS_BYTES, st, dz, x, slab, M, S);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -385,40 +528,34 @@ static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, f
 
 // Pixel splits: S is a multiple of 8 (the XCD-aware order keeps each split on one
 // XCD); the smallest S whose S * tiles workgroups fill the resident slots in ONE
-// round (fewest chunks per workgroup), falling back to whole rounds for tiny M.
-// Returns rows per split; S = ceil(M / rps).
-int g_wgrad_bk = 32;   // pixels per K chunk of the wgrad tile (32 default; 16 = A/B study)
+// round (fewest chunks per workgroup), falling back to whole rounds for tiny M;
+// every split keeps >= 2 whole 32-pixel chunks.
+int g_wgrad_bk = 32;   // pixels per K chunk of the row-staging tile (32 default; 16 = A/B study)
 
-int wgrad_rows_per_split(int C, int M)
+int wgrad_splits(int C, int M)
 {
     const int bt = C < 128 ? C : 128;
     const int tiles = 9 * (C / bt) * (C / bt);
-    const int lds = 2 * 2 * bt * (g_wgrad_bk + 4) * 4;   // K-contiguous staging (LDS rows of BK + 4)
+    const int lds = 2 * 2 * bt * (g_wgrad_bk + 4) * 4;   // largest variant (K-contiguous staging)
     const int per_cu = 160 * 1024 / lds < 2 ? 160 * 1024 / lds : 2;
     const int slots = 256 * per_cu;
     int S = (slots / tiles) / 8 * 8;
     if (S < 8) S = 8;
-    while (S > 8 && (M + S - 1) / S < 64) S -= 8;   // keep >= 2 chunks per split
-    return (M + S - 1) / S;
+    const int nch = (M + 31) / 32;
+    while (S > 8 && nch < 2 * S) S -= 8;
+    return S;
 }
 
-int wgrad_splits(int C, int M)
-{
-    const int rps = wgrad_rows_per_split(C, M);
-    const int S = (M + rps - 1) / rps;
-    return (S + 7) / 8 * 8;
-}
-
-// slab must hold S*9*C*C floats, S = ceil(M / rps).
-hipError_t launch_wgrad(int C, const float* dz, const float* x, float* slab, float* dw, int M, int S, int rps,
+// slab must hold S*9*C*C floats, S = wgrad_splits(C, M).
+hipError_t launch_wgrad(int C, const float* dz, const float* x, float* slab, float* dw, int M, int S,
                         hipStream_t st)
 {
     switch (C) {
-        case 64: return launch_wgrad_t<64>(dz, x, slab, dw, M, S, rps, st);
+        case 64: return launch_wgrad_t<64>(dz, x, slab, dw, M, S, st);
         case 128:
-            if (g_wgrad_bk == 16) return launch_wgrad_t<128, 16>(dz, x, slab, dw, M, S, rps, st);
-            return launch_wgrad_t<128>(dz, x, slab, dw, M, S, rps, st);
-        case 256: return launch_wgrad_t<256>(dz, x, slab, dw, M, S, rps, st);
+            if (g_wgrad_bk == 16) return launch_wgrad_t<128, 16>(dz, x, slab, dw, M, S, st);
+            return launch_wgrad_t<128>(dz, x, slab, dw, M, S, st);
+        case 256: return launch_wgrad_t<256>(dz, x, slab, dw, M, S, st);
         default: return hipErrorInvalidValue;
     }
 }

@@ -158,8 +158,10 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *   key 12: train step conv weight grads (0 = overlapped on a side stream, default;
  *          1 = on the caller's stream);
  *   key 13: train wgrad K chunk in pixels (32 default; 16 for A/B timing, C=128);
- *   key 16: train conv weight-grad kernel (1 = K-contiguous staging with 16-B
- *          fragment reads, default; 0 = row staging with 4-B reads, A/B timing);
+ *   key 16: train conv weight-grad kernel (3 = natural pixel rows moved into LDS
+ *          by LDS-DMA, default; 1 = K-contiguous register staging with 16-B
+ *          fragment reads; 2 = the same two chunks ahead; 0 = row staging with 4-B
+ *          reads; A/B timing, all bitwise identical);
  *   key 17: persistent-tower claim granularity (1 = one M tile with all its N
  *          tiles, run back to back by the claiming workgroup, default: the second
  *          tile's halo rows hit the XCD's L2, +2 % at B = 512 and 4096, measured;
