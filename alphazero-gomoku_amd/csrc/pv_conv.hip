@@ -223,10 +223,12 @@ __global__ __launch_bounds__(64 * NW_, 2) void conv3x3_halo(
 // one fixed tile shape (128 x 64, 8 waves; the shape autotuning picked at B = 128)
 // so the partials are per 128-row M tile.  Same XCD-aware tile order as above.
 // WT: outputs stored write-through (no dirty L2 lines at the kernel boundary).
-template <int C, int EPI, int XE, bool WT>
-__global__ __launch_bounds__(512, 2) void conv3x3_train(
+// PRO (forward only): the input is the previous layer's raw output z and its BN +
+// ReLU (+ residual) is applied in the halo staging (pv_halo.h ProX).
+template <int C, int EPI, int XE, bool WT, int PRO = PRO_NONE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv3x3_train(
     const float* __restrict__ in, const float* __restrict__ wp, const float* __restrict__ resid,
-    float* __restrict__ out, int M, EpiX ex)
+    float* __restrict__ out, int M, EpiX ex, ProX px, FinX fx)
 {
     using T = ConvTile<C, 64, 4, 1, 8>;
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -234,8 +236,9 @@ __global__ __launch_bounds__(512, 2) void conv3x3_train(
     const int L = blockIdx.x, nt = gridDim.x;
     const int xcd = L & 7, q8 = nt >> 3, r8 = nt & 7;
     const int t = xcd * q8 + min(xcd, r8) + (L >> 3);
-    halo_tile<C, 64, 4, 1, 8, EPI, WT, 0, 0, XE>(in, wp, nullptr, nullptr, resid, out, wt_rsrc(out, padded_bytes(M, C)),
-                                              M, (t / NTN) * T::BM, (t % NTN) * T::BN, smem, ex);
+    halo_tile<C, 64, 4, 1, 8, EPI, WT, 0, 0, XE, PRO>(in, wp, nullptr, nullptr, resid, out,
+                                                   wt_rsrc(out, padded_bytes(M, C)), M, (t / NTN) * T::BM,
+                                                   (t % NTN) * T::BN, smem, ex, px, fx);
 }
 
 // Stem conv 3->C (K = 27) on the VALU: 0.2 % of the forward FLOPs.  One
@@ -781,40 +784,50 @@ hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, cons
 
 int g_train_wt = 7;   // key 18 bits: 1 train conv outputs, 2 BN apply outputs, 4 wgrad slabs write-through
 
-template <int C, int EPI, int XE>
+template <int C, int EPI, int XE, int PRO = PRO_NONE>
 static hipError_t launch_train_t(const float* in, const float* wp, const float* resid, float* out, int M,
-                                 const EpiX& ex, hipStream_t st)
+                                 const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st)
 {
     using T = ConvTile<C, 64, 4, 1, 8>;
-    constexpr int lds = halo_lds_bytes<C, 64, 4, 1, 8>();
+    constexpr int lds = halo_lds_bytes<C, 64, 4, 1, 8, 0, PRO>();
     static bool attr_done = false;
     if (!attr_done) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, false>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, false, PRO>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, true>,
+            e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, true, PRO>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
         attr_done = true;
     }
     dim3 grid(((M + T::BM - 1) / T::BM) * (C / T::BN));
     if (g_train_wt & 1)
-        hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, true>), grid, dim3(T::NT), lds, st, in, wp, resid, out, M, ex);
+        hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, true, PRO>), grid, dim3(T::NT), lds, st, in, wp, resid, out, M,
+                           ex, px, fx);
     else
-        hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, false>), grid, dim3(T::NT), lds, st, in, wp, resid, out, M, ex);
+        hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, false, PRO>), grid, dim3(T::NT), lds, st, in, wp, resid, out,
+                           M, ex, px, fx);
     return hipGetLastError();
 }
 
-// Train conv with fused BN partials: (EPI_RAW, XE_STATS) forward; (EPI_RAW |
-// EPI_ADD, XE_BNBWD) dgrad.  Partials are per TRAIN_BM-row M tile.
+// Train conv with fused BN partials: (EPI_RAW, XE_STATS) forward, optionally with
+// the input layer's BN applied in the staging (px: PRO_BN / PRO_BN_RES); (EPI_RAW |
+// EPI_ADD, XE_BNBWD) dgrad.  Partials are per TRAIN_BM-row M tile; with fx (cnt set)
+// the last workgroup of each N tile also runs the BN finalize (pv_halo.h FinX).
 hipError_t launch_conv3x3_train(int C, int epi, int xe, const float* in, const float* wp, const float* resid,
-                                float* out, int M, const EpiX& ex, hipStream_t st)
+                                float* out, int M, const EpiX& ex, hipStream_t st, const ProX* px, const FinX* fxp)
 {
+    const ProX p0{};
+    const FinX fx = fxp ? *fxp : FinX{};
 #define AZG_TRAIN_C(CC)                                                                            \
     case CC:                                                                                       \
-        if (epi == EPI_RAW && xe == XE_STATS) return launch_train_t<CC, EPI_RAW, XE_STATS>(in, wp, resid, out, M, ex, st); \
-        if (epi == EPI_RAW && xe == XE_BNBWD) return launch_train_t<CC, EPI_RAW, XE_BNBWD>(in, wp, resid, out, M, ex, st); \
-        if (epi == EPI_ADD && xe == XE_BNBWD) return launch_train_t<CC, EPI_ADD, XE_BNBWD>(in, wp, resid, out, M, ex, st); \
+        if (epi == EPI_RAW && xe == XE_STATS && px && px->res)                                     \
+            return launch_train_t<CC, EPI_RAW, XE_STATS, PRO_BN_RES>(in, wp, resid, out, M, ex, *px, fx, st); \
+        if (epi == EPI_RAW && xe == XE_STATS && px)                                                \
+            return launch_train_t<CC, EPI_RAW, XE_STATS, PRO_BN>(in, wp, resid, out, M, ex, *px, fx, st); \
+        if (epi == EPI_RAW && xe == XE_STATS) return launch_train_t<CC, EPI_RAW, XE_STATS>(in, wp, resid, out, M, ex, p0, fx, st); \
+        if (epi == EPI_RAW && xe == XE_BNBWD) return launch_train_t<CC, EPI_RAW, XE_BNBWD>(in, wp, resid, out, M, ex, p0, fx, st); \
+        if (epi == EPI_ADD && xe == XE_BNBWD) return launch_train_t<CC, EPI_ADD, XE_BNBWD>(in, wp, resid, out, M, ex, p0, fx, st); \
         return hipErrorInvalidValue;
     switch (C) {
         AZG_TRAIN_C(64)
@@ -928,6 +941,16 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     if (key == 21) {  // per-layer conv: last partial round of the 128x64 launch as 64x64 tiles (1) or not (0)
         const int prev = azg::g_conv_tail_split;
         azg::g_conv_tail_split = value ? 1 : 0;
+        return prev;
+    }
+    if (key == 24) {  // train: BN finalize fused into the producing conv's last workgroup (1, default) or separate (0)
+        const int prev = azg::g_train_fuse_fin;
+        if (value == 0 || value == 1) azg::g_train_fuse_fin = value;
+        return prev;
+    }
+    if (key == 23) {  // train: BN applies folded into the next conv's halo staging (1, default) or separate (0)
+        const int prev = azg::g_train_fuse_apply;
+        if (value == 0 || value == 1) azg::g_train_fuse_apply = value;
         return prev;
     }
     if (key == 18) {  // train: write-through outputs (bits: 1 convs, 2 BN apply, 4 wgrad slabs)

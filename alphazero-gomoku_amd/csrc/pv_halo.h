@@ -63,13 +63,14 @@ constexpr int halo_span(int BM)
 // LDS: halo rows [HR][32] + two weight chunks [2][BN][32] (register staging), or
 // two halo buffers [2][HRG][32] + [2][BN][32] (LDS-DMA staging, VAR bit 4); the
 // epilogue reuses it as a [BM][ELD] tile.
-template <int C, int BN, int WM, int TM, int NW, int VAR = 0>
+template <int C, int BN, int WM, int TM, int NW, int VAR = 0, int PRO = 0>
 constexpr int halo_lds_bytes()
 {
     using T = ConvTile<C, BN, WM, TM, NW>;
     const int hrg = (halo_span(T::BM) + 7) / 8 * 8;
     const int staging = (VAR & 4) ? (2 * hrg + ((VAR & 2) ? 3 : 2) * BN) * T::BK * 4
-                                  : ((halo_span(T::BM) + T::RPP - 1) / T::RPP * T::RPP + 2 * BN) * T::BK * 4;
+                                  : ((halo_span(T::BM) + T::RPP - 1) / T::RPP * T::RPP + 2 * BN) * T::BK * 4 +
+                                        (PRO ? 2 * C * 4 : 0);
     const int epilogue = T::BM * (BN + 8) * 4;
     return staging > epilogue ? staging : epilogue;
 }
@@ -98,6 +99,126 @@ struct EpiX {
     float* pb;           // [mtiles][C]
 };
 
+
+// BatchNorm finalize from per-tile partials (pa / pb [ntile][ldc]), shared by the
+// stand-alone finalize kernels (pv_train.hip) and the last-arriving workgroup of a
+// train conv (halo_epilogue, FinX): 8 consecutive lanes own one channel, lane j sums
+// tiles j, j+8, ... in fp64, then a fixed xor tree over the 8 lanes -- the same
+// order everywhere, so a fused and a separate finalize are bitwise identical.
+//   FWD (train-forward statistics; pa = tile mean, pb = tile M2, tile t holds
+//     min(prow, M - t*prow) rows): mean = S n_t m_t / N, var = (S (M2_t + n_t m_t^2)
+//     - N mean^2) / N in fp64; invstd / scale / shift and the running-stat update as
+//     ATen's CPU batch_norm (network.py:12-25 in train mode, momentum 0.1,
+//     unbiased running var);
+//   !FWD (BN backward; pa = S dy, pb = S (z - mean) dy): dgamma, dbeta and the
+//     bn_bwd_apply coefficients gm = S dy / N, k = S(z-mean)dy invstd^2 / N,
+//     iw = invstd * gamma.
+struct FinX {
+    unsigned* cnt = nullptr;     // fused: arrival counter per N tile (0 at launch; reset by the last arriver)
+    const float* gamma = nullptr;
+    const float* beta = nullptr;                            // FWD
+    float *rmean = nullptr, *rvar = nullptr;                // FWD running stats
+    float *mean_o = nullptr, *inv_o = nullptr, *scale_o = nullptr, *shift_o = nullptr;   // FWD outputs
+    const float* inv_i = nullptr;                           // !FWD: invstd of the layer
+    float *ggamma = nullptr, *gbeta = nullptr;              // !FWD: parameter grads
+    float *gm_o = nullptr, *k_o = nullptr, *iw_o = nullptr; // !FWD: bn_bwd_apply coefficients
+};
+// partial sums of tiles t = j, j+8, ... (the tile class j of 8) for channel c
+template <bool FWD>
+__device__ __forceinline__ void bn_fin_accum(const float* __restrict__ pa, const float* __restrict__ pb, int ldc,
+                                             int ntile, int prow, int M, int c, int j, double& v0, double& v1)
+{
+    v0 = 0.0;
+    v1 = 0.0;
+    // loads of up to 16 tiles issued back to back before their sums (one round trip
+    // per 16 tiles: unconditional loads from clamped rows, past-the-end tiles add an
+    // exact 0 -- no branch between a load and the next)
+    for (int t0 = j; t0 < ntile; t0 += 8 * 16) {
+        float a[16], b[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int t = min(t0 + 8 * k, ntile - 1);
+            a[k] = pa[(size_t)t * ldc + c];
+            b[k] = pb[(size_t)t * ldc + c];
+        }
+        __builtin_amdgcn_sched_barrier(0);   // hipcc otherwise interleaves each load with its wait
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int t = t0 + 8 * k;
+            const bool ok = t < ntile;
+            if (FWD) {
+                const double n = ok ? (double)min(prow, M - t * prow) : 0.0;
+                const double av = (double)a[k];
+                v0 += n * av;
+                v1 += (ok ? (double)b[k] : 0.0) + n * av * av;
+            } else {
+                v0 += ok ? (double)a[k] : 0.0;
+                v1 += ok ? (double)b[k] : 0.0;
+            }
+        }
+    }
+}
+// combine the 8 tile classes in the fixed order ((0+4)+(2+6))+((1+5)+(3+7)) and write
+// channel c's results
+template <bool FWD>
+__device__ __forceinline__ void bn_fin_out(double v0, double v1, int M, int c, const FinX& f)
+{
+    if (FWD) {
+        const double mean = v0 / (double)M;
+        double q = v1 - (double)M * mean * mean;     // S (z - mean)^2
+        q = q > 0.0 ? q : 0.0;
+        const double var = q / (double)M;
+        const float mean_f = (float)mean;
+        const float inv_f = (float)(1.0 / sqrt(var + (double)BN_EPS));
+        const float alpha = inv_f * f.gamma[c];
+        f.mean_o[c] = mean_f;
+        f.inv_o[c] = inv_f;
+        f.scale_o[c] = alpha;
+        f.shift_o[c] = fmaf(-mean_f, alpha, f.beta[c]);
+        const double unb = M > 1 ? q / (double)(M - 1) : var;
+        f.rmean[c] = (float)((double)BN_MOMENTUM * mean + (1.0 - (double)BN_MOMENTUM) * (double)f.rmean[c]);
+        f.rvar[c] = (float)((double)BN_MOMENTUM * unb + (1.0 - (double)BN_MOMENTUM) * (double)f.rvar[c]);
+    } else {
+        const double inv = (double)f.inv_i[c];
+        f.ggamma[c] = (float)(v1 * inv);
+        f.gbeta[c] = (float)v0;
+        f.gm_o[c] = (float)(v0 / (double)M);
+        f.k_o[c] = (float)(v1 * inv * inv / (double)M);
+        f.iw_o[c] = (float)inv * f.gamma[c];
+    }
+}
+// 8 consecutive lanes per channel (stand-alone kernels): xor tree 4, 2, 1 = the
+// fixed combine order above
+template <bool FWD>
+__device__ __forceinline__ void bn_fin_group8(const float* __restrict__ pa, const float* __restrict__ pb, int ldc,
+                                              int ntile, int prow, int M, int c, int j, const FinX& f)
+{
+    double v0, v1;
+    bn_fin_accum<FWD>(pa, pb, ldc, ntile, prow, M, c, j, v0, v1);
+#pragma unroll
+    for (int o = 4; o > 0; o >>= 1) {
+        v0 += __shfl_xor(v0, o, 64);
+        v1 += __shfl_xor(v1, o, 64);
+    }
+    if (j == 0) bn_fin_out<FWD>(v0, v1, M, c, f);
+}
+
+// Train-forward operand prologue (template PRO of halo_tile): the conv input is the
+// previous layer's RAW conv output z, and its BatchNorm (batch statistics) + ReLU
+// (+ the block's residual input) is applied while the halo rows are staged:
+//   a = relu(fma(z, scale[c], shift[c]) [+ res])   (padding rows stay 0)
+// so no separate bn_apply pass reads z and writes a; the tile's own pixel rows of
+// a (needed by the backward) are written once, by the N-tile-0 workgroups.
+constexpr int PRO_NONE = 0;
+constexpr int PRO_BN = 1;       // relu(bn(z))
+constexpr int PRO_BN_RES = 2;   // relu(bn(z) + res)
+struct ProX {
+    const float* res;     // PRO_BN_RES: residual input (padded NHWC)
+    const float* scale;   // [C] BN scale of the input layer (invstd * gamma)
+    const float* shift;   // [C] beta - mean * scale
+    float* aout;          // a (padded NHWC): own rows written when n0 == 0
+};
+
 // key of the 16-B slot swizzle of halo row `row` (padded-pixel index): the padded
 // board position v = yy*15 + xx (see halo_tile)
 __device__ __forceinline__ int halo_vkey(int row)
@@ -120,7 +241,7 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                                               const float* __restrict__ scale, const float* __restrict__ shift,
                                               const float* __restrict__ resid, float* __restrict__ out,
                                               __amdgpu_buffer_rsrc_t out_rs, int M, int m0, int n0, float* smem,
-                                              const EpiX& ex = EpiX{})
+                                              const EpiX& ex = EpiX{}, const FinX& fx = FinX{})
 {
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
     constexpr int BM = T::BM, BN = T::BN, WN = T::WN, TM = T::TM, TN = T::TN;
@@ -220,11 +341,17 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
     }
     if constexpr (XE != XE_NONE) {
         // fixed-order LDS reduction over the RPI row groups (bitwise reproducible)
-        static_assert(2 * RPI * BN + BN <= BM * ELD, "XE reduction scratch");
+        static_assert(2 * RPI * BN + BN + 1 <= BM * ELD, "XE reduction scratch (+ arrival flag)");
         float* R = smem;                       // [RPI][BN] partial a, then [RPI][BN] partial b
         float* Mu = smem + 2 * RPI * BN;       // [BN] tile mean (XE_STATS)
         const int mt = m0 / BM;
+        const int ntm = (M + BM - 1) / BM;
         const int rows = min(BM, M - m0);
+        // partials are stored write-through: a fused finalize (fx.cnt) reads them from
+        // another XCD after the arrival count
+        const __amdgpu_buffer_rsrc_t prs_a = wt_rsrc(ex.pa, (size_t)ntm * C * sizeof(float));
+        const __amdgpu_buffer_rsrc_t prs_b = wt_rsrc(ex.pb, (size_t)ntm * C * sizeof(float));
+        const int po = mt * C + n0 + tid;
         __syncthreads();                       // every thread is past its Es reads
         *(f32x4*)(R + er * BN + ec) = xa;
         if (XE == XE_BNBWD) *(f32x4*)(R + RPI * BN + er * BN + ec) = xb;
@@ -234,12 +361,12 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
             for (int r = 0; r < RPI; ++r) sa += R[r * BN + tid];
             if (XE == XE_BNBWD) {
                 for (int r = 0; r < RPI; ++r) sb += R[RPI * BN + r * BN + tid];
-                ex.pa[(size_t)mt * C + n0 + tid] = sa;
-                ex.pb[(size_t)mt * C + n0 + tid] = sb;
+                store1<true>(ex.pa, prs_a, po, sa);
+                store1<true>(ex.pb, prs_b, po, sb);
             } else {
                 const float mu = sa / (float)rows;
                 Mu[tid] = mu;
-                ex.pa[(size_t)mt * C + n0 + tid] = mu;
+                store1<true>(ex.pa, prs_a, po, mu);
             }
         }
         if constexpr (XE == XE_STATS) {
@@ -261,7 +388,44 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
             if (tid < BN) {
                 float sb = 0.f;
                 for (int r = 0; r < RPI; ++r) sb += R[RPI * BN + r * BN + tid];
-                ex.pb[(size_t)mt * C + n0 + tid] = sb;
+                store1<true>(ex.pb, prs_b, po, sb);
+            }
+        }
+        // fused finalize: the last workgroup of this N tile to publish its partials
+        // reduces all M tiles' partials of its BN channels (tower hand-off protocol:
+        // write-through stores, vmcnt(0), barrier, one agent-scope atomic; the last
+        // arriver acquires before reading)
+        if (fx.cnt) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            unsigned* flag = (unsigned*)(smem + 2 * RPI * BN + BN);
+            if (tid == 0) {
+                const unsigned old =
+                    __hip_atomic_fetch_add(fx.cnt + n0 / BN, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                *flag = old == (unsigned)(ntm - 1) ? 1u : 0u;
+            }
+            __syncthreads();
+            if (*flag) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                // wave w sums tile class w % 8 of channels n0 + lane (coalesced rows of
+                // the [tile][C] partials), the classes combine through LDS in the order
+                // of bn_fin_group8: bitwise equal to the stand-alone finalize
+                static_assert(T::NW == 8 && BN == 64, "fused finalize: 8 waves x 64 channels");
+                double* red = (double*)smem;   // [2][8][64]
+                const int wv = tid >> 6, ln = tid & 63;
+                double v0, v1;
+                bn_fin_accum<XE == XE_STATS>(ex.pa, ex.pb, C, ntm, BM, M, n0 + ln, wv, v0, v1);
+                red[wv * 64 + ln] = v0;
+                red[512 + wv * 64 + ln] = v1;
+                __syncthreads();
+                if (wv == 0) {
+                    auto comb = [&](const double* r) {
+                        return ((r[0 * 64 + ln] + r[4 * 64 + ln]) + (r[2 * 64 + ln] + r[6 * 64 + ln])) +
+                               ((r[1 * 64 + ln] + r[5 * 64 + ln]) + (r[3 * 64 + ln] + r[7 * 64 + ln]));
+                    };
+                    bn_fin_out<XE == XE_STATS>(comb(red), comb(red + 512), M, n0 + ln, fx);
+                    if (ln == 0) __hip_atomic_store(fx.cnt + n0 / BN, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
         }
     }
@@ -474,12 +638,13 @@ __device__ __forceinline__ void halo_mainloop_glds(const float* __restrict__ in,
 // barriers, bit 8 replaces LDS fragment reads by register values, bit 16 skips the
 // epilogue stores (kept live by a never-true compare).
 template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1 = false, int ABL = 0, int VAR = 0,
-          int XE = XE_NONE>
+          int XE = XE_NONE, int PRO = PRO_NONE>
 __device__ __forceinline__ void halo_tile(
     const float* __restrict__ in, const float* __restrict__ wp,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ resid, float* __restrict__ out, __amdgpu_buffer_rsrc_t out_rs,
-    int M, int m0, int n0, float* smem, const EpiX& ex = EpiX{})
+    int M, int m0, int n0, float* smem, const EpiX& ex = EpiX{}, const ProX& px = ProX{},
+    const FinX& fx = FinX{})
 {
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
     if constexpr ((VAR & 4) != 0) {   // LDS-DMA staging
@@ -498,6 +663,7 @@ __device__ __forceinline__ void halo_tile(
     constexpr int HR = H_LD * RPP;
     static_assert(RPP % 16 == 0, "halo staging rows must keep the row swizzle");
     static_assert(H_LD <= 9, "halo loads are spread over the 9 taps");
+    static_assert(PRO == PRO_NONE || (VAR == 0 && ABL == 0), "operand prologue: register staging only");
     // VAR (A/B studies; the product uses 0, measured fastest): bit 1 = halo rows
     // swizzled on the padded board position (conflict-free fragment reads) and an
     // unpadded epilogue tile; bit 2 = weights staged two chunks ahead; bit 4 = LDS-DMA
@@ -508,6 +674,7 @@ __device__ __forceinline__ void halo_tile(
 
     float* Ah = smem;                 // [HR][32]
     float* Bs = smem + HR * BK;       // [2][BN][32]
+    float* Ps = smem + (HR + 2 * BN) * BK;   // PRO: [2][C] input-layer BN scale / shift
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
@@ -524,15 +691,35 @@ __device__ __forceinline__ void halo_tile(
         hsrc[i] = r * C + sc;
     }
     const float* wsrc = wp + (size_t)(n0 + sr) * BK + sc;
+    // PRO: per staged row, interior (else the zero halo) / own pixel row (write a)
+    unsigned pint = 0, pown = 0;   // own rows are never clamped: their a offset is hsrc[i]
+    if constexpr (PRO != PRO_NONE) {
+        const int own_lo = pad_row(m0), own_hi = pad_row(mlast);
+#pragma unroll
+        for (int i = 0; i < H_LD; ++i) {
+            const int r = hbase + sr + RPP * i;
+            const int rb = r % PADPIX, yy = rb / PADW, xx = rb - yy * PADW;
+            const bool interior = yy >= 1 && yy <= BOARD && xx >= 1 && xx <= BOARD;
+            if (interior) pint |= 1u << i;
+            if (interior && n0 == 0 && r >= own_lo && r <= own_hi) pown |= 1u << i;
+        }
+        for (int c = tid; c < C; c += T::NT) {
+            Ps[c] = px.scale[c];
+            Ps[C + c] = px.shift[c];
+        }
+        __syncthreads();
+    }
 
     // weights: rb1 holds chunk j+1 (stored to LDS at the end of chunk j); with BPF2,
     // rb2 receives chunk j+2 at the top of chunk j, so a load has a whole chunk plus
     // the next chunk's MFMAs to land before the ds_write that waits on it (the loops
     // are fully unrolled: the rb1 = rb2 hand-over is a register renaming, not a move)
     f32x4 rh[H_LD], rb1[B_LD], rb2[B_LD];
+    f32x4 rr[PRO == PRO_BN_RES ? H_LD : 1];
     auto hload = [&](int cg, int i) {
         if (ABL & 2) return;
         rh[i] = *(const f32x4*)(in + hsrc[i] + cg * BK);
+        if constexpr (PRO == PRO_BN_RES) rr[i] = *(const f32x4*)(px.res + hsrc[i] + cg * BK);
     };
     auto bload = [&](f32x4 (&rb)[B_LD], int kc) {
         if (ABL & 1) return;
@@ -558,7 +745,29 @@ __device__ __forceinline__ void halo_tile(
 #pragma unroll
     for (int i = 0; i < H_LD; ++i)
         hwchunk[i] = VSWZ ? ((tid & 7) ^ ((vkey(hbase + sr + RPP * i) >> 1) & 7)) * 4 : wchunk;
-    auto hstore = [&]() {
+    // PRO: the BN / residual / ReLU of the input layer on the staged rows (same
+    // arithmetic as bn_apply_kernel), own rows of a written through
+    const __amdgpu_buffer_rsrc_t ars = wt_rsrc(px.aout, padded_bytes(M, C));
+    auto prologue = [&](int cg) {
+        if constexpr (PRO != PRO_NONE) {
+            const f32x4 s4 = *(const f32x4*)(Ps + cg * BK + sc);
+            const f32x4 t4 = *(const f32x4*)(Ps + C + cg * BK + sc);
+#pragma unroll
+            for (int i = 0; i < H_LD; ++i) {
+                f32x4 v = rh[i];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float y = fmaf(v[e], s4[e], t4[e]);
+                    if constexpr (PRO == PRO_BN_RES) y += rr[i][e];
+                    v[e] = (pint >> i) & 1 ? fmaxf(y, 0.f) : 0.f;
+                }
+                rh[i] = v;
+                if ((pown >> i) & 1) store4<true>(px.aout, ars, hsrc[i] + cg * BK, v);
+            }
+        }
+    };
+    auto hstore = [&](int cg) {
+        prologue(cg);
 #pragma unroll
         for (int i = 0; i < H_LD; ++i) *(f32x4*)(Ah + (sr + RPP * i) * BK + hwchunk[i]) = rh[i];
     };
@@ -599,7 +808,7 @@ __device__ __forceinline__ void halo_tile(
     } else {
         bload(rb1, kchunk(0));
     }
-    hstore();
+    hstore(0);
     if (BPF2) bstore(rb2, 0);
     else bstore(rb1, 0);
     __syncthreads();
@@ -669,7 +878,7 @@ __device__ __forceinline__ void halo_tile(
             }
             if (!(ABL & 4)) __syncthreads();
             if (tap == 8 && more) {
-                hstore();            // every wave is past its last read of this group's halo
+                hstore(cg + 1);      // every wave is past its last read of this group's halo
                 __syncthreads();
             }
         }
@@ -681,7 +890,7 @@ __device__ __forceinline__ void halo_tile(
 
     // the last chunk ended with a barrier: the staging buffers are free
     halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, (VSWZ ? BN : BN + 8), (VAR & 8) != 0, XE>(
-        acc, scale, shift, resid, out, out_rs, M, m0, n0, smem, ex);
+        acc, scale, shift, resid, out, out_rs, M, m0, n0, smem, ex, fx);
 }
 
 }  // namespace azg

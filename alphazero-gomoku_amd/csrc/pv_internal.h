@@ -34,14 +34,19 @@ struct BlockBn { int first, second; };
 hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, const float* scale,
                           const float* shift, const float* resid, float* out, int M, hipStream_t st);
 struct EpiX;
+struct ProX;
+struct FinX;
 constexpr int TRAIN_BM = 128;   // rows per M tile of conv3x3_train (BN partials granularity)
 hipError_t launch_conv3x3_train(int C, int epi, int xe, const float* in, const float* wp, const float* resid,
-                                float* out, int M, const EpiX& ex, hipStream_t st);
+                                float* out, int M, const EpiX& ex, hipStream_t st, const ProX* px = nullptr,
+                                const FinX* fx = nullptr);
 extern int g_tower_mode;
 extern int g_tower_shape;
 extern int g_tower_ablation;
 extern int g_tower_var;
 extern int g_wgrad_serial;
+extern int g_train_fuse_apply;
+extern int g_train_fuse_fin;
 extern int g_train_skip;
 extern int g_wgrad_bk;
 extern int g_wgrad_kernel;

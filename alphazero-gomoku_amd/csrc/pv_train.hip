@@ -48,6 +48,7 @@ struct TrainWS {
     float* spart = nullptr;                        // [B][27][C]
     float* slab = nullptr;                         // wgrad split-K slabs
     int S = 0, rps = 0;
+    unsigned* fincnt = nullptr;                    // fused BN finalize: arrival counters per N tile
     // heads
     float *zh = nullptr, *fp = nullptr, *fv = nullptr, *hv = nullptr, *dpre = nullptr;
     float *dlogits = nullptr, *dfp = nullptr, *dfv = nullptr, *dhv = nullptr, *dzh = nullptr, *lossb = nullptr;
@@ -171,7 +172,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
         if (RES) r = *(const f32x4*)(res + o);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            float y = v[k] * s[k] + t[k];
+            float y = fmaf(v[k], s[k], t[k]);   // same arithmetic as the conv staging prologue (ProX)
             if (RES) y += r[k];
             v[k] = fmaxf(y, 0.f);
         }
@@ -244,74 +245,24 @@ __device__ __forceinline__ void block_sum4_d(double (&v)[NV], double (*red)[4])
     for (int k = 0; k < NV; ++k) v[k] = ((red[k][0] + red[k][1]) + red[k][2]) + red[k][3];
 }
 
-// Batch statistics of one BN layer from per-tile (mean, M2) partials (tile t holds
-// min(prow, M - t*prow) rows), one workgroup per channel, every tile's partial
-// loaded by its own thread (all loads in flight at once: latency-bound, not a
-// loop), ONE fp64 block reduction: mean = S n_t m_t / N,
-// var = (S (M2_t + n_t m_t^2) - N mean^2) / N  (fp64: 53 bits, no cancellation at
-// fp32 precision).  Then the coefficients and the running-stat update as ATen's
-// CPU batch_norm (invstd in fp64 stored fp32, unbiased running var, momentum 0.1).
-__global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(
-    const float* __restrict__ pmean, const float* __restrict__ pm2, int ntile, int prow, int M, int C,
-    const BnDesc* desc, int layer, const float* __restrict__ params, float* __restrict__ stats,
-    float* __restrict__ bmean, float* __restrict__ binv, float* __restrict__ bscale, float* __restrict__ bshift)
+// Batch statistics / BN-backward sums of one BN layer from per-tile partials
+// (pv_halo.h bn_fin_group8: 8 lanes per channel, fp64, fixed order -- the same
+// reduction the last workgroup of a fused train conv runs, so both are bitwise
+// identical).  32 channels per workgroup.
+__global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(const float* __restrict__ pmean,
+                                                                const float* __restrict__ pm2, int ntile, int prow,
+                                                                int M, int C, int nch, FinX f)
 {
-    __shared__ double red[2][4];
-    const BnDesc d = desc[layer];
-    const int c = blockIdx.x;
-    double v[2] = {0.0, 0.0};
-    for (int t = threadIdx.x; t < ntile; t += 256) {
-        const double n = (double)min(prow, M - t * prow);
-        const double mt = (double)pmean[(size_t)t * C + c];
-        v[0] += n * mt;
-        v[1] += (double)pm2[(size_t)t * C + c] + n * mt * mt;
-    }
-    block_sum4_d<2>(v, red);
-    if (threadIdx.x == 0) {
-        const double mean = v[0] / (double)M;
-        double q = v[1] - (double)M * mean * mean;     // S (z - mean)^2
-        q = q > 0.0 ? q : 0.0;
-        const double var = q / (double)M;
-        const float mean_f = (float)mean;
-        const float inv_f = (float)(1.0 / sqrt(var + (double)BN_EPS));
-        const float alpha = inv_f * params[d.gamma_off + c];
-        bmean[d.out_off + c] = mean_f;
-        binv[d.out_off + c] = inv_f;
-        bscale[d.out_off + c] = alpha;
-        bshift[d.out_off + c] = params[d.beta_off + c] - mean_f * alpha;
-        const double unb = M > 1 ? q / (double)(M - 1) : var;
-        float* rm = stats + d.stat_off;
-        float* rv = stats + d.stat_off + d.c;
-        rm[c] = (float)((double)BN_MOMENTUM * mean + (1.0 - (double)BN_MOMENTUM) * (double)rm[c]);
-        rv[c] = (float)((double)BN_MOMENTUM * unb + (1.0 - (double)BN_MOMENTUM) * (double)rv[c]);
-    }
+    const int c = blockIdx.x * 32 + (threadIdx.x >> 3);
+    if (c < nch) bn_fin_group8<true>(pmean, pm2, C, ntile, prow, M, c, threadIdx.x & 7, f);
 }
 
-// BN-backward sums from per-tile partials (S dy, S (z-mean) dy), one workgroup per
-// channel, fp64 fixed-order block sum; dgamma = S(z-mean)dy * invstd, dbeta = S dy,
-// and for bn_bwd_apply gm = S dy / N, k = S(z-mean)dy invstd^2 / N, iw = invstd*gamma.
-__global__ __launch_bounds__(256) void bn_bwd_finalize_tiles_kernel(
-    const float* __restrict__ pa, const float* __restrict__ pb, int ntile, int M, int C, const BnDesc* desc,
-    int layer, const float* __restrict__ params, float* __restrict__ grads, const float* __restrict__ binv,
-    float* __restrict__ bgm, float* __restrict__ bk, float* __restrict__ biw)
+__global__ __launch_bounds__(256) void bn_bwd_finalize_tiles_kernel(const float* __restrict__ pa,
+                                                                    const float* __restrict__ pb, int ntile, int M,
+                                                                    int C, int nch, FinX f)
 {
-    __shared__ double red[2][4];
-    const BnDesc d = desc[layer];
-    const int c = blockIdx.x;
-    double v[2] = {0.0, 0.0};
-    for (int t = threadIdx.x; t < ntile; t += 256) {
-        v[0] += (double)pa[(size_t)t * C + c];
-        v[1] += (double)pb[(size_t)t * C + c];
-    }
-    block_sum4_d<2>(v, red);
-    if (threadIdx.x == 0) {
-        const double inv = (double)binv[d.out_off + c];
-        grads[d.gamma_off + c] = (float)(v[1] * inv);
-        grads[d.beta_off + c] = (float)v[0];
-        bgm[d.out_off + c] = (float)(v[0] / (double)M);
-        bk[d.out_off + c] = (float)(v[1] * inv * inv / (double)M);
-        biw[d.out_off + c] = (float)inv * params[d.gamma_off + c];
-    }
+    const int c = blockIdx.x * 32 + (threadIdx.x >> 3);
+    if (c < nch) bn_fin_group8<false>(pa, pb, C, ntile, 1, M, c, threadIdx.x & 7, f);
 }
 
 // dz = ((dy - gm) - (z - mean)*k) * invstd*gamma ; optional gres = dy
@@ -934,6 +885,11 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     A(np, 2 * 1024, false);
     w->npart = (double*)np;
     A(w->scal, 4, true);
+    {
+        float* fc = nullptr;
+        A(fc, 64, true);
+        w->fincnt = (unsigned*)fc;
+    }
     if (getenv("AZG_DEBUG_SNAP")) {
         w->snap.assign(NB + 1, nullptr);
         for (int i = 0; i <= NB; ++i) A(w->snap[i], act, true);
@@ -952,6 +908,8 @@ static inline int grid_for(int64_t total) { int64_t b = (total + 255) / 256; ret
     } while (0)
 
 int g_wgrad_serial = 0;   // 1: conv weight grads on the caller's stream (A/B timing)
+int g_train_fuse_apply = 1;   // key 23: 1 BN applies folded into the next conv's staging; 0 separate passes
+int g_train_fuse_fin = 1;     // key 24: 1 BN finalize by the last workgroup of the producing conv; 0 separate kernels
 int g_train_skip = 0;     // study build only (key 19): skip BN kernels to time them in situ (results invalid)
 
 template <int C>
@@ -969,13 +927,39 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     const int gM = grid_for((int64_t)M * C / 4);
 
     const int ntt = (M + TRAIN_BM - 1) / TRAIN_BM;   // M tiles of conv3x3_train (partials per tile)
+    // finalize arguments of one BN layer (forward statistics / backward sums)
+    auto fin_args = [&](int layer, bool fwd) -> FinX {
+        const BnDesc& d = bd[layer];
+        FinX f{};
+        f.gamma = P + d.gamma_off;
+        if (fwd) {
+            f.beta = P + d.beta_off;
+            f.rmean = h->bn + d.stat_off;
+            f.rvar = h->bn + d.stat_off + d.c;
+            f.mean_o = w->bmean + d.out_off;
+            f.inv_o = w->binv + d.out_off;
+            f.scale_o = w->bscale + d.out_off;
+            f.shift_o = w->bshift + d.out_off;
+        } else {
+            f.inv_i = w->binv + d.out_off;
+            f.ggamma = G + d.gamma_off;
+            f.gbeta = G + d.beta_off;
+            f.gm_o = w->bgm + d.out_off;
+            f.k_o = w->bk + d.out_off;
+            f.iw_o = w->biw + d.out_off;
+        }
+        return f;
+    };
     auto fin_fwd = [&](int layer, int prow, int nt) -> int32_t {
         if (g_train_skip & 2) return 0;
-        hipLaunchKernelGGL(bn_finalize_tiles_kernel, dim3(bd[layer].c), dim3(256), 0, st, w->part_a,
-                           w->part_b, nt, prow, M, C, bdd, layer, P, h->bn, w->bmean, w->binv, w->bscale, w->bshift);
+        hipLaunchKernelGGL(bn_finalize_tiles_kernel, dim3((bd[layer].c + 31) / 32), dim3(256), 0, st, w->part_a,
+                           w->part_b, nt, prow, M, C, bd[layer].c, fin_args(layer, true));
         AZG_CK(hipGetLastError(), "train: bn_finalize_tiles");
         return 0;
     };
+    // the conv3x3_train launch that produces a layer's partials also finalizes it
+    // (key 24; the fused and the separate finalize are bitwise identical)
+    const bool ffin = g_train_fuse_fin != 0 && !(g_train_skip & 10);
     // stem: separate column statistics (64-row tiles)
     auto stats = [&](const float* z, int layer) -> int32_t {
         int pr = prof_begin(h, AZG_PROF_TRAIN_OTHER, st);
@@ -1006,11 +990,18 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     };
     // train-mode conv: forward (z + BN tile statistics) or dgrad (+ BN-backward tile
     // sums of the layer below: act / z / layer `xl`); partials land in part_a / part_b
+    // fin >= 0: the BN layer this launch's partials belong to, finalized in-kernel
     auto conv = [&](int epi, int xe, const float* in, const float* wp, const float* res, float* out,
-                    const float* xact, const float* xz, int xl) -> int32_t {
+                    const float* xact, const float* xz, int xl, int fin = -1) -> int32_t {
         int pr = prof_begin(h, AZG_PROF_TRAIN_CONV, st, B);
         const EpiX ex{xact, xz, xl >= 0 ? w->bmean + bd[xl].out_off : nullptr, w->part_a, w->part_b};
-        AZG_CK(launch_conv3x3_train(C, epi, xe, in, wp, res, out, M, ex, st), "train: conv3x3");
+        FinX fx{};
+        if (fin >= 0) {
+            fx = fin_args(fin, xe == XE_STATS);
+            fx.cnt = w->fincnt;
+        }
+        AZG_CK(launch_conv3x3_train(C, epi, xe, in, wp, res, out, M, ex, st, nullptr, fin >= 0 ? &fx : nullptr),
+               "train: conv3x3");
         prof_end(h, pr, st);
         return 0;
     };
@@ -1022,8 +1013,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     };
     auto bwd_fin = [&](int layer, int nt) -> int32_t {
         if (g_train_skip & 8) return 0;
-        hipLaunchKernelGGL(bn_bwd_finalize_tiles_kernel, dim3(bd[layer].c), dim3(256), 0, st,
-                           w->part_a, w->part_b, nt, M, C, bdd, layer, P, G, w->binv, w->bgm, w->bk, w->biw);
+        hipLaunchKernelGGL(bn_bwd_finalize_tiles_kernel, dim3((bd[layer].c + 31) / 32), dim3(256), 0, st,
+                           w->part_a, w->part_b, nt, M, C, bd[layer].c, fin_args(layer, false));
         AZG_CK(hipGetLastError(), "train: bn_bwd_finalize_tiles");
         return 0;
     };
@@ -1082,17 +1073,48 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     // ---- forward (train-mode BN) ----
     AZG_CK(launch_stem(C, EPI_RAW, x, h->wstem, nullptr, nullptr, w->z0, B, st), "train: stem");
     R(stats(w->z0, h->bn_stem));
-    R(apply(w->z0, nullptr, h->bn_stem, w->a0));
     const float* X = w->a0;
-    for (int i = 0; i < NB; ++i) {
-        R(conv(EPI_RAW, XE_STATS, X, h->wpack + (size_t)(2 * i) * 9 * C * C, nullptr, w->z1[i], nullptr, nullptr, -1));
-        R(fin_fwd(h->bn_blk[i].first, TRAIN_BM, ntt));
-        R(apply(w->z1[i], nullptr, h->bn_blk[i].first, w->hh[i]));
-        R(conv(EPI_RAW, XE_STATS, w->hh[i], h->wpack + (size_t)(2 * i + 1) * 9 * C * C, nullptr, w->z2[i], nullptr,
-               nullptr, -1));
-        R(fin_fwd(h->bn_blk[i].second, TRAIN_BM, ntt));
-        R(apply(w->z2[i], X, h->bn_blk[i].second, w->xo[i]));
-        X = w->xo[i];
+    if (g_train_fuse_apply) {
+        // every BN apply but the last is done by the next conv's halo staging
+        // (pv_halo.h ProX): `pend` = the activation still to be formed from its raw z
+        struct Pend { const float* z; int layer; const float* res; float* out; };
+        Pend pend{w->z0, h->bn_stem, nullptr, w->a0};
+        auto fused_conv = [&](const Pend& p, const float* wpk, float* out, int fin) -> int32_t {
+            int pr = prof_begin(h, AZG_PROF_TRAIN_CONV, st, B);
+            const int o = bd[p.layer].out_off;
+            const EpiX ex{nullptr, nullptr, nullptr, w->part_a, w->part_b};
+            const ProX px{p.res, w->bscale + o, w->bshift + o, p.out};
+            FinX fx = fin_args(fin, true);
+            fx.cnt = w->fincnt;
+            AZG_CK(launch_conv3x3_train(C, EPI_RAW, XE_STATS, p.z, wpk, nullptr, out, M, ex, st, &px,
+                                        ffin ? &fx : nullptr),
+                   "train: conv3x3 (fused BN apply)");
+            prof_end(h, pr, st);
+            if (!ffin) return fin_fwd(fin, TRAIN_BM, ntt);
+            return 0;
+        };
+        for (int i = 0; i < NB; ++i) {
+            R(fused_conv(pend, h->wpack + (size_t)(2 * i) * 9 * C * C, w->z1[i], h->bn_blk[i].first));
+            pend = Pend{w->z1[i], h->bn_blk[i].first, nullptr, w->hh[i]};
+            R(fused_conv(pend, h->wpack + (size_t)(2 * i + 1) * 9 * C * C, w->z2[i], h->bn_blk[i].second));
+            pend = Pend{w->z2[i], h->bn_blk[i].second, X, w->xo[i]};
+            X = w->xo[i];
+        }
+        R(apply(pend.z, pend.res, pend.layer, pend.out));
+    } else {
+        R(apply(w->z0, nullptr, h->bn_stem, w->a0));
+        for (int i = 0; i < NB; ++i) {
+            const int l1 = h->bn_blk[i].first, l2 = h->bn_blk[i].second;
+            R(conv(EPI_RAW, XE_STATS, X, h->wpack + (size_t)(2 * i) * 9 * C * C, nullptr, w->z1[i], nullptr, nullptr,
+                   -1, ffin ? l1 : -1));
+            if (!ffin) R(fin_fwd(l1, TRAIN_BM, ntt));
+            R(apply(w->z1[i], nullptr, l1, w->hh[i]));
+            R(conv(EPI_RAW, XE_STATS, w->hh[i], h->wpack + (size_t)(2 * i + 1) * 9 * C * C, nullptr, w->z2[i],
+                   nullptr, nullptr, -1, ffin ? l2 : -1));
+            if (!ffin) R(fin_fwd(l2, TRAIN_BM, ntt));
+            R(apply(w->z2[i], X, h->bn_blk[i].second, w->xo[i]));
+            X = w->xo[i];
+        }
     }
     // ---- heads forward + loss + backward to the tower output ----
     {
@@ -1173,21 +1195,24 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         R(bwd_reduce(w->gX, w->xo[NB - 1], w->z2[NB - 1], h->bn_blk[NB - 1].second));
         bwd_nt = ntile;
     }
+    bool done_fin = false;   // the previous dgrad launch already finalized the next layer
     for (int i = NB - 1; i >= 0; --i) {
         const float* Xin = i == 0 ? w->a0 : w->xo[i - 1];
         const float* zin = i == 0 ? w->z0 : w->z2[i - 1];
         const int lin = i == 0 ? h->bn_stem : h->bn_blk[i - 1].second;
-        R(bwd_fin(h->bn_blk[i].second, bwd_nt));
+        if (!done_fin) R(bwd_fin(h->bn_blk[i].second, bwd_nt));
         R(reuse(0));
         R(bwd_apply(w->gX, w->xo[i], w->z2[i], h->bn_blk[i].second, dzbuf[0], w->GR));
         R(wgrad(0, w->hh[i], h->t_blk[i].w2));
         R(conv(EPI_RAW, XE_BNBWD, dzbuf[0], w->wdpack + (size_t)(2 * i + 1) * 9 * C * C, nullptr, w->DH, w->hh[i],
-               w->z1[i], h->bn_blk[i].first));
-        R(bwd_fin(h->bn_blk[i].first, ntt));
+               w->z1[i], h->bn_blk[i].first, ffin ? h->bn_blk[i].first : -1));
+        if (!ffin) R(bwd_fin(h->bn_blk[i].first, ntt));
         R(reuse(1));
         R(bwd_apply(w->DH, w->hh[i], w->z1[i], h->bn_blk[i].first, dzbuf[1], nullptr));
         R(wgrad(1, Xin, h->t_blk[i].w1));
-        R(conv(EPI_ADD, XE_BNBWD, dzbuf[1], w->wdpack + (size_t)(2 * i) * 9 * C * C, w->GR, w->gX, Xin, zin, lin));
+        R(conv(EPI_ADD, XE_BNBWD, dzbuf[1], w->wdpack + (size_t)(2 * i) * 9 * C * C, w->GR, w->gX, Xin, zin, lin,
+               ffin ? lin : -1));
+        done_fin = ffin;
         bwd_nt = ntt;
         R(snap(NB - i));
     }
@@ -1198,7 +1223,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         R(bwd_reduce(w->gX, w->a0, w->z0, h->bn_stem));
         bwd_nt = ntile;
     }
-    R(bwd_fin(h->bn_stem, bwd_nt));
+    if (!done_fin) R(bwd_fin(h->bn_stem, bwd_nt));
     R(bwd_apply(w->gX, w->a0, w->z0, h->bn_stem, w->DH, nullptr));
     hipLaunchKernelGGL((stem_wgrad_kernel<C>), dim3(B * STEM_WG_CHUNKS), dim3(256), 0, st, x, w->DH, w->spart);
     AZG_CK(hipGetLastError(), "train: stem_wgrad");
