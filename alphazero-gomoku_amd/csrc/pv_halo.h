@@ -124,7 +124,16 @@ struct FinX {
     float *gm_o = nullptr, *k_o = nullptr, *iw_o = nullptr; // !FWD: bn_bwd_apply coefficients
 };
 // partial sums of tiles t = j, j+8, ... (the tile class j of 8) for channel c
-template <bool FWD>
+// Agent-coherent load (relaxed atomic, agent scope: served from the device-coherent
+// level, never from a stale line of this XCD's L2) -- how a last-arriving workgroup
+// reads what other XCDs published write-through, WITHOUT an acquire fence: an acquire
+// invalidates the whole L2 of the XCD and every other workgroup running there then
+// re-fetches its halo rows and weights.
+__device__ __forceinline__ float coh_load(const float* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool FWD, bool COH = false>
 __device__ __forceinline__ void bn_fin_accum(const float* __restrict__ pa, const float* __restrict__ pb, int ldc,
                                              int ntile, int prow, int M, int c, int j, double& v0, double& v1)
 {
@@ -138,8 +147,8 @@ __device__ __forceinline__ void bn_fin_accum(const float* __restrict__ pa, const
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const int t = min(t0 + 8 * k, ntile - 1);
-            a[k] = pa[(size_t)t * ldc + c];
-            b[k] = pb[(size_t)t * ldc + c];
+            a[k] = COH ? coh_load(pa + (size_t)t * ldc + c) : pa[(size_t)t * ldc + c];
+            b[k] = COH ? coh_load(pb + (size_t)t * ldc + c) : pb[(size_t)t * ldc + c];
         }
         __builtin_amdgcn_sched_barrier(0);   // hipcc otherwise interleaves each load with its wait
 #pragma unroll
@@ -394,7 +403,7 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
         // fused finalize: the last workgroup of this N tile to publish its partials
         // reduces all M tiles' partials of its BN channels (tower hand-off protocol:
         // write-through stores, vmcnt(0), barrier, one agent-scope atomic; the last
-        // arriver acquires before reading)
+        // arriver reads them with agent-coherent loads, coh_load)
         if (fx.cnt) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
@@ -406,7 +415,6 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
             }
             __syncthreads();
             if (*flag) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 // wave w sums tile class w % 8 of channels n0 + lane (coalesced rows of
                 // the [tile][C] partials), the classes combine through LDS in the order
                 // of bn_fin_group8: bitwise equal to the stand-alone finalize
@@ -414,7 +422,7 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                 double* red = (double*)smem;   // [2][8][64]
                 const int wv = tid >> 6, ln = tid & 63;
                 double v0, v1;
-                bn_fin_accum<XE == XE_STATS>(ex.pa, ex.pb, C, ntm, BM, M, n0 + ln, wv, v0, v1);
+                bn_fin_accum<XE == XE_STATS, true>(ex.pa, ex.pb, C, ntm, BM, M, n0 + ln, wv, v0, v1);
                 red[wv * 64 + ln] = v0;
                 red[512 + wv * 64 + ln] = v1;
                 __syncthreads();

@@ -102,7 +102,9 @@ def gpu_masks(eng, blocks, B):
 
 
 @pytest.mark.parametrize("tag,blocks,ch,B", [("3x64", 3, 64, 128), ("6x128", 6, 128, 128), ("3x64", 3, 64, 37),
-                                             (None, 2, 128, 16), (None, 10, 256, 12)])
+                                             (None, 2, 128, 16), (None, 10, 256, 12),
+                                             # fused BN apply / finalize at 160 and 48 samples (C = 64 / 256)
+                                             (None, 2, 64, 160), (None, 2, 256, 48)])
 def test_gradients_match_oracle(tag, blocks, ch, B):
     """Gradients vs fp64 autograd with the GPU's ReLU masks (oracle.masked_grads_fp64):
     |g_gpu - g_64| <= 2e-5 * max|g_64| + 1e-8 per tensor.  The fp32 CPU oracle (own
@@ -348,3 +350,4 @@ def test_train_schedule_keys_bitwise(key, values):
                 assert all(torch.equal(a, c) for a, c in zip(ref, got)), (key, v)
     finally:
         lib.azg_pv_set_tuning(key, prev)
+
