@@ -671,6 +671,7 @@ __device__ __forceinline__ void halo_tile(
     constexpr int HR = H_LD * RPP;
     static_assert(RPP % 16 == 0, "halo staging rows must keep the row swizzle");
     static_assert(H_LD <= 9, "halo loads are spread over the 9 taps");
+    static_assert(PRO == PRO_NONE || H_LD <= 8, "the operand prologue of a row runs one tap after its load");
     static_assert(PRO == PRO_NONE || (VAR == 0 && ABL == 0), "operand prologue: register staging only");
     // VAR (A/B studies; the product uses 0, measured fastest): bit 1 = halo rows
     // swizzled on the padded board position (conflict-free fragment reads) and an
@@ -756,26 +757,25 @@ __device__ __forceinline__ void halo_tile(
     // PRO: the BN / residual / ReLU of the input layer on the staged rows (same
     // arithmetic as bn_apply_kernel), own rows of a written through
     const __amdgpu_buffer_rsrc_t ars = wt_rsrc(px.aout, padded_bytes(M, C));
-    auto prologue = [&](int cg) {
+    // per staged row i: applied one tap after its load was issued (the residual row
+    // dies there, keeping the PRO_BN_RES register peak low), to all rows of the first
+    // group before its store
+    auto pro_row = [&](int cg, int i) {
         if constexpr (PRO != PRO_NONE) {
             const f32x4 s4 = *(const f32x4*)(Ps + cg * BK + sc);
             const f32x4 t4 = *(const f32x4*)(Ps + C + cg * BK + sc);
+            f32x4 v = rh[i];
 #pragma unroll
-            for (int i = 0; i < H_LD; ++i) {
-                f32x4 v = rh[i];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    float y = fmaf(v[e], s4[e], t4[e]);
-                    if constexpr (PRO == PRO_BN_RES) y += rr[i][e];
-                    v[e] = (pint >> i) & 1 ? fmaxf(y, 0.f) : 0.f;
-                }
-                rh[i] = v;
-                if ((pown >> i) & 1) store4<true>(px.aout, ars, hsrc[i] + cg * BK, v);
+            for (int e = 0; e < 4; ++e) {
+                float y = fmaf(v[e], s4[e], t4[e]);
+                if constexpr (PRO == PRO_BN_RES) y += rr[i][e];
+                v[e] = (pint >> i) & 1 ? fmaxf(y, 0.f) : 0.f;
             }
+            rh[i] = v;
+            if ((pown >> i) & 1) store4<true>(px.aout, ars, hsrc[i] + cg * BK, v);
         }
     };
-    auto hstore = [&](int cg) {
-        prologue(cg);
+    auto hstore = [&]() {
 #pragma unroll
         for (int i = 0; i < H_LD; ++i) *(f32x4*)(Ah + (sr + RPP * i) * BK + hwchunk[i]) = rh[i];
     };
@@ -816,7 +816,9 @@ __device__ __forceinline__ void halo_tile(
     } else {
         bload(rb1, kchunk(0));
     }
-    hstore(0);
+#pragma unroll
+    for (int i = 0; i < H_LD; ++i) pro_row(0, i);
+    hstore();
     if (BPF2) bstore(rb2, 0);
     else bstore(rb1, 0);
     __syncthreads();
@@ -877,6 +879,8 @@ __device__ __forceinline__ void halo_tile(
                         for (int j = 0; j < TN; ++j)
                             at[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], at[i][j], 0, 0, 0);
             }
+            // the row loaded one tap ago gets its BN / ReLU now (PRO)
+            if (PRO != PRO_NONE && more && tap >= 1 && tap <= H_LD) pro_row(cg + 1, tap - 1);
             if (j + 1 < NCHK) {
                 bstore(rb1, cur ^ 1);
                 if (BPF2) {
@@ -886,7 +890,7 @@ __device__ __forceinline__ void halo_tile(
             }
             if (!(ABL & 4)) __syncthreads();
             if (tap == 8 && more) {
-                hstore(cg + 1);      // every wave is past its last read of this group's halo
+                hstore();            // every wave is past its last read of this group's halo
                 __syncthreads();
             }
         }
