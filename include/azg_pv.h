@@ -175,6 +175,12 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *   key 22: per-layer 128x64 conv tile body (1 = halo rows keyed on the board
  *          position, conflict-free fragment reads, default; 0 = row-keyed; 4 / 5 =
  *          LDS-DMA staging); bitwise identical;
+ *   key 23: train forward BN apply + ReLU (+ residual) folded into the next conv's
+ *          halo staging (1, default) or separate bn_apply passes (0); bitwise
+ *          identical;
+ *   key 24: train BN finalize run by the last workgroup of the conv producing the
+ *          layer's partials (1, default) or by separate finalize kernels (0); one
+ *          shared fp64 reduction order, bitwise identical;
  *   key 14: persistent-tower dependency spin bound (tests only: 0 makes every
  *          dependency wait time out at once, exercising the error path; -1
  *          restores the default).
