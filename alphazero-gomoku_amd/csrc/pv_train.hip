@@ -1074,7 +1074,10 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     AZG_CK(launch_stem(C, EPI_RAW, x, h->wstem, nullptr, nullptr, w->z0, B, st), "train: stem");
     R(stats(w->z0, h->bn_stem));
     const float* X = w->a0;
-    if (g_train_fuse_apply) {
+    // the staging prologue fits the 128-VGPR tile body at C <= 128; at C = 256 (eight
+    // channel groups unrolled) it spills 96 VGPRs and costs ~1 ms per 10x256 step
+    // (measured), so the separate apply passes stay there
+    if (g_train_fuse_apply && C <= 128) {
         // every BN apply but the last is done by the next conv's halo staging
         // (pv_halo.h ProX): `pend` = the activation still to be formed from its raw z
         struct Pend { const float* z; int layer; const float* res; float* out; };

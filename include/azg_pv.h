@@ -176,8 +176,9 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          position, conflict-free fragment reads, default; 0 = row-keyed; 4 / 5 =
  *          LDS-DMA staging); bitwise identical;
  *   key 23: train forward BN apply + ReLU (+ residual) folded into the next conv's
- *          halo staging (1, default) or separate bn_apply passes (0); bitwise
- *          identical;
+ *          halo staging (1, default; C <= 128 only: at C = 256 the prologue spills
+ *          and the separate passes are faster) or separate bn_apply passes (0);
+ *          bitwise identical;
  *   key 24: train BN finalize run by the last workgroup of the conv producing the
  *          layer's partials (1, default) or by separate finalize kernels (0); one
  *          shared fp64 reduction order, bitwise identical;

@@ -8,7 +8,7 @@
                                  excluded) against the bench JSON's hipEvent totals, and
                                  the train-step timeline of one step
 
-    python scripts/summarize_r2.py gpurun_out/prof_r2
+    python scripts/summarize_r2.py gpurun_out/prof_r2 [tag]
 """
 import csv
 import json
@@ -28,9 +28,10 @@ def rows(path):
 
 def main():
     root = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "gpurun_out", "prof_r2")
+    tag = sys.argv[2] if len(sys.argv) > 2 else "r2"
     sp_dir, tr_dir = os.path.join(root, "sp", "trace"), os.path.join(root, "train", "trace")
-    shutil.copy(os.path.join(sp_dir, "run_kernel_stats.csv"), os.path.join(PROF, "r2_selfplay_kernel_stats.csv"))
-    shutil.copy(os.path.join(tr_dir, "run_kernel_stats.csv"), os.path.join(PROF, "r2_train_kernel_stats.csv"))
+    shutil.copy(os.path.join(sp_dir, "run_kernel_stats.csv"), os.path.join(PROF, f"{tag}_selfplay_kernel_stats.csv"))
+    shutil.copy(os.path.join(tr_dir, "run_kernel_stats.csv"), os.path.join(PROF, f"{tag}_train_kernel_stats.csv"))
     bench = json.loads(open(os.path.join(root, "sp", "bench.json")).read().strip().splitlines()[-1])
     sp = bench["selfplay"]
     trace = rows(os.path.join(sp_dir, "run_kernel_trace.csv"))
@@ -50,7 +51,7 @@ def main():
     ev_ms = det["kernel_ms_rank0"].get("tower", 0) + det["kernel_ms_rank0"].get("conv3x3", 0)
     ev_n = det["kernel_launches_rank0"].get("tower", 0) + det["kernel_launches_rank0"].get("conv3x3", 0)
     roof = bench["roofline"]
-    L = ["# rocprofv3 evidence, round 2", "",
+    L = [f"# rocprofv3 evidence, {tag}", "",
          "## Headline: configs[2] self-play to game end (bench.py, this command under rocprofv3)", "",
          f"`rocprofv3 --kernel-trace --stats -- python3 bench.py --skip-forward --no-cpu-baseline --train-steps 0 "
          f"--big-steps 0` (scripts/gpu_profile_r2.sh): {bench['value']:.0f} leaf boards/s over "
@@ -85,7 +86,7 @@ def main():
         for k, (n, us) in sorted(agg.items(), key=lambda x: -x[1][1])[:16]:
             L.append(f"| `{k}` | {n} | {us:.0f} |")
         L.append("")
-    open(os.path.join(PROF, "r2_selfplay_summary.md"), "w").write("\n".join(L) + "\n")
+    open(os.path.join(PROF, f"{tag}_selfplay_summary.md"), "w").write("\n".join(L) + "\n")
     print("\n".join(L))
 
 

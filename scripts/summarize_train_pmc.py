@@ -35,9 +35,13 @@ def main():
     # kernels of one train step (between two stem launches): setup kernels excluded
     starts = [i for i, r in enumerate(trace) if "stem_mfma" in r[0]]
     in_step = collections.Counter(r[0].split("(")[0] for r in trace[starts[-3]:starts[-2]])
-    flops = {"conv3x3_wgrad_t": CONV_FLOP, "conv3x3_train": CONV_FLOP}
-    algo = {"conv3x3_train<128, 2, 1": 2 * ACT, "conv3x3_train<128, 2, 2": 4 * ACT, "conv3x3_train<128, 3, 2": 5 * ACT,
-            "conv3x3_wgrad_t": 2 * ACT, "bn_apply_kernel<128, false": 2 * ACT, "bn_apply_kernel<128, true": 3 * ACT,
+    flops = {"conv3x3_wgrad_t": CONV_FLOP, "conv3x3_wgrad_nat": CONV_FLOP, "conv3x3_train": CONV_FLOP}
+    # algorithmic bytes: forward z in + z out (+ PRO: own rows of a written, PRO_BN_RES:
+    # residual in); dgrad dZ in + out + act + z (+ residual grad); weight grad dZ + X
+    algo = {"conv3x3_train<128, 2, 1, true, 0>": 2 * ACT, "conv3x3_train<128, 2, 1, true, 1>": 3 * ACT,
+            "conv3x3_train<128, 2, 1, true, 2>": 4 * ACT, "conv3x3_train<128, 2, 2": 4 * ACT,
+            "conv3x3_train<128, 3, 2": 5 * ACT, "conv3x3_wgrad_t": 2 * ACT, "conv3x3_wgrad_nat": 2 * ACT,
+            "bn_apply_kernel<128, false": 2 * ACT, "bn_apply_kernel<128, true": 3 * ACT,
             "bn_bwd_apply_kernel<128, false": 4 * ACT, "bn_bwd_apply_kernel<128, true": 5 * ACT}
     rows = []
     for k, d in acc.items():
@@ -79,8 +83,9 @@ def main():
                  f"{r['hbm_mb']:.1f}{' (' + format(r['alg_mb'], '.1f') + ')' if r.get('alg_mb') else ''} | "
                  f"{r['gbs']:.0f} | {f('wait', '{:.1%}')} | {f('lds_wait', '{:.1%}')} | {r['conf']:.0f} | "
                  f"{f('valu_per_mfma', '{:.2f}')} |")
-    L += ["", "Reading: the convs are MFMA-bound at 64-68 % SQ busy inside an 88 % tile-quantization ceiling "
-              "(450 tiles of 128x64 on 256 CUs); the BN kernels are HBM passes at 3-6 TB/s; wgrad_reduce reads "
+    L += ["", "Reading: the convs are MFMA-bound inside an 88 % tile-quantization ceiling (450 tiles of "
+              "128x64 on 512 slots); the forward convs carry the previous layer's BN apply in their staging and "
+              "the BN finalize in their last workgroup; the BN kernels left are HBM passes; wgrad_reduce reads "
               "the split-K slabs (33 MB) the weight-grad kernel wrote.", ""]
     out = os.path.join(REPO, "profiles", f"{tag}_train_pmc.md")
     open(out, "w").write("\n".join(L) + "\n")
