@@ -139,20 +139,20 @@ __device__ __forceinline__ void bn_fin_accum(const float* __restrict__ pa, const
 {
     v0 = 0.0;
     v1 = 0.0;
-    // loads of up to 16 tiles issued back to back before their sums (one round trip
-    // per 16 tiles: unconditional loads from clamped rows, past-the-end tiles add an
+    // loads of up to 32 tiles issued back to back before their sums (one round trip
+    // per 32 tiles: unconditional loads from clamped rows, past-the-end tiles add an
     // exact 0 -- no branch between a load and the next)
-    for (int t0 = j; t0 < ntile; t0 += 8 * 16) {
-        float a[16], b[16];
+    for (int t0 = j; t0 < ntile; t0 += 8 * 32) {
+        float a[32], b[32];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
+        for (int k = 0; k < 32; ++k) {
             const int t = min(t0 + 8 * k, ntile - 1);
             a[k] = COH ? coh_load(pa + (size_t)t * ldc + c) : pa[(size_t)t * ldc + c];
             b[k] = COH ? coh_load(pb + (size_t)t * ldc + c) : pb[(size_t)t * ldc + c];
         }
         __builtin_amdgcn_sched_barrier(0);   // hipcc otherwise interleaves each load with its wait
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
+        for (int k = 0; k < 32; ++k) {
             const int t = t0 + 8 * k;
             const bool ok = t < ntile;
             if (FWD) {
