@@ -921,6 +921,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         azg::g_tower_spin_limit = value < 0 ? (1u << 22) : (unsigned)value;
         return prev;
     }
+    if (key == 31) {  // persistent tower: dependent halo / residual reads agent-coherent, no L2-invalidating acquire (1) or acquire (0)
+        const int prev = azg::g_tower_coh;
+        azg::g_tower_coh = value ? 1 : 0;
+        return prev;
+    }
     if (key == 17) {  // persistent tower claim granularity (0 one tile, 1 one M tile x all N tiles)
         const int prev = azg::g_tower_group;
         azg::g_tower_group = value ? 1 : 0;

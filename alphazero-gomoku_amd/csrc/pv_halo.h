@@ -245,7 +245,7 @@ __device__ __forceinline__ int halo_vkey(int row)
 // 16 pad_off divisions) per fragment.  Same per-element arithmetic.  The caller
 // guarantees every wave is past its last staging-buffer access (barrier).
 template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1, int ABL, int ELD, bool EARLY = false,
-          int XE = XE_NONE>
+          int XE = XE_NONE, bool COH = false>
 __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<C, BN_, WM_, TM_, NW_>::TN],
                                               const float* __restrict__ scale, const float* __restrict__ shift,
                                               const float* __restrict__ resid, float* __restrict__ out,
@@ -316,6 +316,11 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
             }
             f32x4 rv = {0.f, 0.f, 0.f, 0.f};
             if (EARLY) rv = rve[EARLY ? p : 0];
+            else if (has_res && COH)   // residual produced inside the launch (tower, VAR bit 16)
+                rv = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(resid), (short)0,
+                                                                                     0x7fffffff, 0x00020000),
+                                                   o * 4, 0, 16));
             else if (has_res) rv = *(const f32x4*)(resid + o);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -725,9 +730,17 @@ __device__ __forceinline__ void halo_tile(
     // are fully unrolled: the rb1 = rb2 hand-over is a register renaming, not a move)
     f32x4 rh[H_LD], rb1[B_LD], rb2[B_LD];
     f32x4 rr[PRO == PRO_BN_RES ? H_LD : 1];
+    // VAR bit 16 (persistent tower, key 31): halo rows are produced inside the launch by
+    // other XCDs; they are read with agent-coherent (sc1) loads instead of after an
+    // L2-invalidating acquire, so the weights stay in L2
+    const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in), (short)0,
+                                                                          0x7fffffff, 0x00020000);
     auto hload = [&](int cg, int i) {
         if (ABL & 2) return;
-        rh[i] = *(const f32x4*)(in + hsrc[i] + cg * BK);
+        if constexpr ((VAR & 16) != 0)
+            rh[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, (hsrc[i] + cg * BK) * 4, 0, 16));
+        else
+            rh[i] = *(const f32x4*)(in + hsrc[i] + cg * BK);
         if constexpr (PRO == PRO_BN_RES) rr[i] = *(const f32x4*)(px.res + hsrc[i] + cg * BK);
     };
     auto bload = [&](f32x4 (&rb)[B_LD], int kc) {
@@ -901,7 +914,7 @@ __device__ __forceinline__ void halo_tile(
     }
 
     // the last chunk ended with a barrier: the staging buffers are free
-    halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, (VSWZ ? BN : BN + 8), (VAR & 8) != 0, XE>(
+    halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, (VSWZ ? BN : BN + 8), (VAR & 8) != 0, XE, (VAR & 16) != 0>(
         acc, scale, shift, resid, out, out_rs, M, m0, n0, smem, ex, fx);
 }
 

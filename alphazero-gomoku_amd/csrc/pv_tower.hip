@@ -60,6 +60,7 @@ struct TowerArgs {
 constexpr unsigned kSpinLimit = 1u << 22;    // x s_sleep(2): seconds, far above any tile time
 unsigned g_tower_spin_limit = kSpinLimit;    // tuning key 14 (tests: 0 forces the timeout path)
 int g_tower_group = 1;                       // tuning key 17: 1 (default) = claim an M tile with all its N tiles
+int g_tower_coh = 1;                         // tuning key 31: 1 (default) = coherent dependent loads instead of an acquire
 
 // waves per SIMD the register budget is sized for: 4 (128 VGPRs) for the one-
 // accumulator tiles; 2 (256 VGPRs, one workgroup per CU) for 128-wide N tiles
@@ -113,7 +114,9 @@ __global__ __launch_bounds__(64 * NW_, tower_min_waves<BN_>()) void conv_tower(c
                         __builtin_amdgcn_s_sleep(2);
                     }
                 }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                // VAR bit 16: the dependent reads are agent-coherent loads, no acquire
+                // (an acquire invalidates the XCD's L2 and the weights are re-fetched)
+                if constexpr ((VAR & 16) == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
         }
@@ -206,7 +209,9 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     if (e != hipSuccess) return e;
 #define AZG_TOWER_C(CC)                                                                    \
     case CC:                                                                               \
+        if (shape == 8 && g_tower_coh) return launch_tower_t<CC, 64, 4, 1, 8, 16>(a, st, nullptr); \
         if (shape == 8) return launch_tower_t<CC, 64, 4, 1, 8>(a, st, nullptr);    \
+        if (g_tower_coh) return launch_tower_t<CC, 64, 2, 1, 4, 16>(a, st, nullptr); \
         return launch_tower_t<CC, 64, 2, 1, 4>(a, st, nullptr);
 #ifdef AZG_AB_STUDIES   // A/B tile-body variants and the 128x128 shape (make study)
     if (C == 128 && shape == 9) {   // 128x128 tiles, 2 accumulators per wave, LDS-DMA staging (A/B study)

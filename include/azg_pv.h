@@ -182,6 +182,10 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *   key 24: train BN finalize run by the last workgroup of the conv producing the
  *          layer's partials (1, default) or by separate finalize kernels (0); one
  *          shared fp64 reduction order, bitwise identical;
+ *   key 31: persistent tower: dependent halo / residual reads are agent-coherent
+ *          loads and the dependency wait has no L2-invalidating acquire (1,
+ *          default; 1.75x vs 2.08x algorithmic HBM bytes, +2.5 %) or an acquire
+ *          (0); bitwise identical;
  *   key 14: persistent-tower dependency spin bound (tests only: 0 makes every
  *          dependency wait time out at once, exercising the error path; -1
  *          restores the default).

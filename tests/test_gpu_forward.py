@@ -221,13 +221,15 @@ def test_persistent_tower_bitwise_equals_per_layer_launches(blocks, ch, batches)
             lib.azg_pv_set_tuning(5, 1)
             for shape in (5, 8):
                 lib.azg_pv_set_tuning(6, shape)
-                for group in (0, 1):                     # claim granularity (key 17)
+                for group, coh in ((0, 0), (1, 0), (1, 1), (0, 1)):   # claim granularity (key 17), coherent reads (31)
                     prev_group = lib.azg_pv_set_tuning(17, group)
+                    prev_coh = lib.azg_pv_set_tuning(31, coh)
                     for rep in range(3):
                         p1, v1, l1 = eng.forward(x, want_logits=True)
                         assert lib.azg_pv_tower_status(eng.h, stream) == 0
-                        assert torch.equal(l0, l1), (B, shape, group, rep, float((l0 - l1).abs().max()))
-                        assert torch.equal(p0, p1) and torch.equal(v0, v1), (B, shape, group, rep)
+                        assert torch.equal(l0, l1), (B, shape, group, coh, rep, float((l0 - l1).abs().max()))
+                        assert torch.equal(p0, p1) and torch.equal(v0, v1), (B, shape, group, coh, rep)
+                    lib.azg_pv_set_tuning(31, prev_coh)
                     lib.azg_pv_set_tuning(17, prev_group)
             if ch == 128 and lib.azg_pv_set_tuning(15, 0) == 1:   # study build: tile-body variants, same arithmetic
                 lib.azg_pv_set_tuning(6, 8)
