@@ -196,20 +196,25 @@ __device__ __forceinline__ void bn_fin_out(double v0, double v1, int M, int c, c
         f.iw_o[c] = (float)inv * f.gamma[c];
     }
 }
-// 8 consecutive lanes per channel (stand-alone kernels): xor tree 4, 2, 1 = the
-// fixed combine order above
+// 8 waves x 64 lanes: wave w holds tile class w of channel c (lane); the classes are
+// combined through LDS in the fixed order above by wave 0, which writes the results
+// (shared by the fused finalize of halo_epilogue and the stand-alone kernels).
+// Every thread of the 512-thread workgroup must call it (barrier).
 template <bool FWD>
-__device__ __forceinline__ void bn_fin_group8(const float* __restrict__ pa, const float* __restrict__ pb, int ldc,
-                                              int ntile, int prow, int M, int c, int j, const FinX& f)
+__device__ __forceinline__ void bn_fin_combine8(double v0, double v1, double* red, int M, int c, bool valid,
+                                                const FinX& f)
 {
-    double v0, v1;
-    bn_fin_accum<FWD>(pa, pb, ldc, ntile, prow, M, c, j, v0, v1);
-#pragma unroll
-    for (int o = 4; o > 0; o >>= 1) {
-        v0 += __shfl_xor(v0, o, 64);
-        v1 += __shfl_xor(v1, o, 64);
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    red[wv * 64 + ln] = v0;
+    red[512 + wv * 64 + ln] = v1;
+    __syncthreads();
+    if (wv == 0 && valid) {
+        auto comb = [&](const double* r) {
+            return ((r[0 * 64 + ln] + r[4 * 64 + ln]) + (r[2 * 64 + ln] + r[6 * 64 + ln])) +
+                   ((r[1 * 64 + ln] + r[5 * 64 + ln]) + (r[3 * 64 + ln] + r[7 * 64 + ln]));
+        };
+        bn_fin_out<FWD>(comb(red), comb(red + 512), M, c, f);
     }
-    if (j == 0) bn_fin_out<FWD>(v0, v1, M, c, f);
 }
 
 // Train-forward operand prologue (template PRO of halo_tile): the conv input is the
@@ -422,23 +427,14 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
             if (*flag) {
                 // wave w sums tile class w % 8 of channels n0 + lane (coalesced rows of
                 // the [tile][C] partials), the classes combine through LDS in the order
-                // of bn_fin_group8: bitwise equal to the stand-alone finalize
+                // of bn_fin_combine8: bitwise equal to the stand-alone finalize
                 static_assert(T::NW == 8 && BN == 64, "fused finalize: 8 waves x 64 channels");
                 double* red = (double*)smem;   // [2][8][64]
                 const int wv = tid >> 6, ln = tid & 63;
                 double v0, v1;
                 bn_fin_accum<XE == XE_STATS, true>(ex.pa, ex.pb, C, ntm, BM, M, n0 + ln, wv, v0, v1);
-                red[wv * 64 + ln] = v0;
-                red[512 + wv * 64 + ln] = v1;
-                __syncthreads();
-                if (wv == 0) {
-                    auto comb = [&](const double* r) {
-                        return ((r[0 * 64 + ln] + r[4 * 64 + ln]) + (r[2 * 64 + ln] + r[6 * 64 + ln])) +
-                               ((r[1 * 64 + ln] + r[5 * 64 + ln]) + (r[3 * 64 + ln] + r[7 * 64 + ln]));
-                    };
-                    bn_fin_out<XE == XE_STATS>(comb(red), comb(red + 512), M, n0 + ln, fx);
-                    if (ln == 0) __hip_atomic_store(fx.cnt + n0 / BN, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
+                bn_fin_combine8<XE == XE_STATS>(v0, v1, red, M, n0 + ln, true, fx);
+                if (tid == 0) __hip_atomic_store(fx.cnt + n0 / BN, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }

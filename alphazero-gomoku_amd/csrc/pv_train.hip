@@ -246,23 +246,19 @@ __device__ __forceinline__ void block_sum4_d(double (&v)[NV], double (*red)[4])
 }
 
 // Batch statistics / BN-backward sums of one BN layer from per-tile partials
-// (pv_halo.h bn_fin_group8: 8 lanes per channel, fp64, fixed order -- the same
-// reduction the last workgroup of a fused train conv runs, so both are bitwise
-// identical).  32 channels per workgroup.
-__global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(const float* __restrict__ pmean,
-                                                                const float* __restrict__ pm2, int ntile, int prow,
-                                                                int M, int C, int nch, FinX f)
+// (pv_halo.h bn_fin_accum + bn_fin_combine8: wave w sums tile class w % 8 of 64
+// channels in fp64, fixed combine order -- exactly what the last workgroup of a fused
+// train conv runs, so both are bitwise identical).  64 channels per workgroup.
+template <bool FWD>
+__global__ __launch_bounds__(512) void bn_fin_tiles_kernel(const float* __restrict__ pa, const float* __restrict__ pb,
+                                                          int ntile, int prow, int M, int C, int nch, FinX f)
 {
-    const int c = blockIdx.x * 32 + (threadIdx.x >> 3);
-    if (c < nch) bn_fin_group8<true>(pmean, pm2, C, ntile, prow, M, c, threadIdx.x & 7, f);
-}
-
-__global__ __launch_bounds__(256) void bn_bwd_finalize_tiles_kernel(const float* __restrict__ pa,
-                                                                    const float* __restrict__ pb, int ntile, int M,
-                                                                    int C, int nch, FinX f)
-{
-    const int c = blockIdx.x * 32 + (threadIdx.x >> 3);
-    if (c < nch) bn_fin_group8<false>(pa, pb, C, ntile, 1, M, c, threadIdx.x & 7, f);
+    __shared__ double red[2 * 8 * 64];
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const int c = blockIdx.x * 64 + ln;
+    double v0 = 0.0, v1 = 0.0;
+    if (c < nch) bn_fin_accum<FWD>(pa, pb, C, ntile, prow, M, c, wv, v0, v1);
+    bn_fin_combine8<FWD>(v0, v1, red, M, c, c < nch, f);
 }
 
 // dz = ((dy - gm) - (z - mean)*k) * invstd*gamma ; optional gres = dy
@@ -952,7 +948,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     };
     auto fin_fwd = [&](int layer, int prow, int nt) -> int32_t {
         if (g_train_skip & 2) return 0;
-        hipLaunchKernelGGL(bn_finalize_tiles_kernel, dim3((bd[layer].c + 31) / 32), dim3(256), 0, st, w->part_a,
+        hipLaunchKernelGGL(bn_fin_tiles_kernel<true>, dim3((bd[layer].c + 63) / 64), dim3(512), 0, st, w->part_a,
                            w->part_b, nt, prow, M, C, bd[layer].c, fin_args(layer, true));
         AZG_CK(hipGetLastError(), "train: bn_finalize_tiles");
         return 0;
@@ -1013,8 +1009,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     };
     auto bwd_fin = [&](int layer, int nt) -> int32_t {
         if (g_train_skip & 8) return 0;
-        hipLaunchKernelGGL(bn_bwd_finalize_tiles_kernel, dim3((bd[layer].c + 31) / 32), dim3(256), 0, st,
-                           w->part_a, w->part_b, nt, M, C, bd[layer].c, fin_args(layer, false));
+        hipLaunchKernelGGL(bn_fin_tiles_kernel<false>, dim3((bd[layer].c + 63) / 64), dim3(512), 0, st,
+                           w->part_a, w->part_b, nt, 1, M, C, bd[layer].c, fin_args(layer, false));
         AZG_CK(hipGetLastError(), "train: bn_bwd_finalize_tiles");
         return 0;
     };
