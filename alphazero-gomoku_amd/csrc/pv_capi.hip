@@ -496,10 +496,12 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
                     if (best_ms[c] < best_ms[b]) b = c;
                 // a preferred variant is kept unless another is > 2 % faster (single-
                 // round timings flip between near-equal variants): the 128x64
-                // persistent tower below 1536 boards, per-layer launches above (their
-                // 128x64 tiles measured ~1-2 % ahead of the tower at 2048-4096 boards,
-                // scripts/conv_shape_ab.py / conv_probe.py)
-                const int pref = batch >= 1536 ? 0 : 2;
+                // persistent tower at every batch since its dependency reads became
+                // agent-coherent loads (key 31: 87.9 / 88.4 / 88.7 % of peak at
+                // 1024 / 2048 / 4096 boards vs 84.3 / 86.2 / 87.8 % for the per-layer
+                // launches, scripts/tower_vs_layer.py); round 1-2 preferred per-layer
+                // launches from 1536 boards, when they were 1-2 % ahead
+                const int pref = (g_tower_coh || batch < 1536) ? 2 : 0;
                 if (best_ms[pref] <= 1.02f * best_ms[b]) b = pref;
                 choice = cand[b];
             }
