@@ -402,8 +402,9 @@ int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst)
     return 0;
 }
 
-// Stem + residual tower.  variant 0: one launch per conv; 5 / 8: the persistent
-// tower (pv_tower.hip) with 64x64 / 128x64 tiles.  All bitwise identical.
+// Stem + residual tower.  variant 0: one launch per conv; 5 / 8 / 10: the persistent
+// tower (pv_tower.hip) with 64x64 / 128x64 / 128x128 (16-wave) tiles.  All bitwise
+// identical.
 static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch, hipStream_t st,
                               const int8_t* boards, const int8_t* players, float** out)
 {
@@ -454,28 +455,34 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
 
 // Tower variant per (C, blocks, batch bucket): g_tower_mode 0 = per-layer launches,
 // 1 = persistent tower with shape g_tower_shape, 2 = timed on first use of the
-// bucket (stem + tower, every variant, best of 2 after a warm pass; the persistent
-// tower wins from ~128 to ~1024 boards, per-layer launches below and at the largest
-// batches).  While the stream is being captured the untuned default is used.
+// bucket (stem + tower, every variant, best of 2 after a warm pass).  Variants: 0
+// per-layer launches; 5 / 8 the tower with 64x64 / 128x64 tiles (2-4 workgroups per
+// CU, acquire hand-off); 10 (C = 128) the tower with 16-wave 128x128 tiles (one
+// workgroup per CU, sc1-load hand-off).  The preferred variant (10 where it exists,
+// else 8) is kept for batches >= 128 unless another is > 2 % faster, so timing noise
+// cannot flip near-equal choices.  While the stream is being captured the untuned
+// default is used.  All variants are bitwise identical.
 static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, const int8_t* boards,
                          const int8_t* players)
 {
     if (h->NB == 0 || h->NB > kTowerMaxBlocks) return 0;
     if ((size_t)batch * PADPIX * h->C * sizeof(float) >= (size_t)INT32_MAX) return 0;
     if (g_tower_mode == 0) return 0;
-    if (g_tower_mode == 1) return g_tower_shape;
+    if (g_tower_mode == 1) return (g_tower_shape == 10 && h->C != 128) ? 8 : g_tower_shape;
     const int bucket = conv_batch_bucket(batch * PIX);
     static std::map<std::tuple<int, int, int>, int> cache;
     const auto key = std::make_tuple(h->C, h->NB, bucket);
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
-    const int fallback = batch >= 128 ? 8 : 0;
+    const int wide = h->C == 128 ? 10 : 8;   // preferred tower shape
+    const int fallback = batch >= 128 ? wide : 0;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return fallback;
     const bool prof = h->prof_on;
     h->prof_on = false;
-    const int cand[3] = {0, 5, 8};
-    float best_ms[3] = {1e30f, 1e30f, 1e30f};
+    const int cand[4] = {0, 5, 8, 10};
+    const int ncand = h->C == 128 ? 4 : 3;
+    float best_ms[4] = {1e30f, 1e30f, 1e30f, 1e30f};
     hipEvent_t e0, e1;
     int choice = fallback;
     if (hipEventCreate(&e0) == hipSuccess) {
@@ -483,7 +490,7 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
             bool ok = true;
             float* out = nullptr;
             for (int r = 0; r < 3 && ok; ++r)
-                for (int c = 0; c < 3 && ok; ++c) {
+                for (int c = 0; c < ncand && ok; ++c) {
                     ok = hipEventRecord(e0, st) == hipSuccess &&
                          stem_and_tower(h, cand[c], x, batch, st, boards, players, &out) == 0 &&
                          hipEventRecord(e1, st) == hipSuccess && hipEventSynchronize(e1) == hipSuccess;
@@ -492,17 +499,12 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
                 }
             if (ok) {
                 int b = 0;
-                for (int c = 1; c < 3; ++c)
+                for (int c = 1; c < ncand; ++c)
                     if (best_ms[c] < best_ms[b]) b = c;
-                // a preferred variant is kept unless another is > 2 % faster (single-
-                // round timings flip between near-equal variants): the 128x64
-                // persistent tower at every batch since its dependency reads became
-                // agent-coherent loads (key 31: 87.9 / 88.4 / 88.7 % of peak at
-                // 1024 / 2048 / 4096 boards vs 84.3 / 86.2 / 87.8 % for the per-layer
-                // launches, scripts/tower_vs_layer.py); round 1-2 preferred per-layer
-                // launches from 1536 boards, when they were 1-2 % ahead
-                const int pref = (g_tower_coh || batch < 1536) ? 2 : 0;
-                if (best_ms[pref] <= 1.02f * best_ms[b]) b = pref;
+                if (batch >= 128) {
+                    const int pref = wide == 10 ? 3 : 2;
+                    if (best_ms[pref] <= 1.02f * best_ms[b]) b = pref;
+                }
                 choice = cand[b];
             }
             (void)hipEventDestroy(e1);

@@ -921,10 +921,14 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         azg::g_tower_spin_limit = value < 0 ? (1u << 22) : (unsigned)value;
         return prev;
     }
-    if (key == 31) {  // persistent tower: dependent halo / residual reads agent-coherent, no L2-invalidating acquire (1) or acquire (0)
+    if (key == 31) {  // study build only: 64x64 / 128x64 tower with sc1 dependent loads instead of the acquire
+#ifdef AZG_AB_STUDIES   // outside the guide's measured envelope (two or more workgroups per CU): never in the product
         const int prev = azg::g_tower_coh;
         azg::g_tower_coh = value ? 1 : 0;
         return prev;
+#else
+        return 0;
+#endif
     }
     if (key == 17) {  // persistent tower claim granularity (0 one tile, 1 one M tile x all N tiles)
         const int prev = azg::g_tower_group;
@@ -993,7 +997,7 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     if (key == 10) {  // persistent-tower tile body variant (A/B studies, bitwise identical)
         const int prev = azg::g_tower_var;
 #ifdef AZG_AB_STUDIES
-        if ((value >= 0 && value <= 8) || value == 12) azg::g_tower_var = value;
+        if ((value >= 0 && value <= 8) || value == 12 || value == 13) azg::g_tower_var = value;
 #else
         if (value == 0) azg::g_tower_var = value;
 #endif
@@ -1020,7 +1024,7 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     }
     if (key == 6) {   // persistent tower tile shape
         const int prev = azg::g_tower_shape;
-        if (value == 5 || value == 8) azg::g_tower_shape = value;
+        if (value == 5 || value == 8 || value == 10) azg::g_tower_shape = value;
 #ifdef AZG_AB_STUDIES
         if (value == 9) azg::g_tower_shape = value;
 #endif

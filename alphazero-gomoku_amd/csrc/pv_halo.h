@@ -123,12 +123,11 @@ struct FinX {
     float *ggamma = nullptr, *gbeta = nullptr;              // !FWD: parameter grads
     float *gm_o = nullptr, *k_o = nullptr, *iw_o = nullptr; // !FWD: bn_bwd_apply coefficients
 };
-// partial sums of tiles t = j, j+8, ... (the tile class j of 8) for channel c
-// Agent-coherent load (relaxed atomic, agent scope: served from the device-coherent
-// level, never from a stale line of this XCD's L2) -- how a last-arriving workgroup
-// reads what other XCDs published write-through, WITHOUT an acquire fence: an acquire
-// invalidates the whole L2 of the XCD and every other workgroup running there then
-// re-fetches its halo rows and weights.
+// partial sums of tiles t = j, j+8, ... (the tile class j of 8) for channel c.
+// COH: every load is an agent-scope relaxed atomic load (`global_load_dword sc1`,
+// L1 bypassed) -- the consumer form that may replace an acquire only inside the
+// microarch guide's measured one-workgroup-per-CU envelope; the product's fused
+// finalize runs at two workgroups per CU and uses an acquire + plain loads instead.
 __device__ __forceinline__ float coh_load(const float* p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -249,8 +248,10 @@ __device__ __forceinline__ int halo_vkey(int row)
 // scale/shift/residual, one 16-B store per run -- instead of 16 scalar stores (and
 // 16 pad_off divisions) per fragment.  Same per-element arithmetic.  The caller
 // guarantees every wave is past its last staging-buffer access (barrier).
+// RBUF: how the residual is read -- 0 plain pointer loads; 1 buffer loads (default
+// cache policy); 2 buffer loads with sc1 (the tower's one-workgroup-per-CU hand-off)
 template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1, int ABL, int ELD, bool EARLY = false,
-          int XE = XE_NONE, bool COH = false>
+          int XE = XE_NONE, int RBUF = 0>
 __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<C, BN_, WM_, TM_, NW_>::TN],
                                               const float* __restrict__ scale, const float* __restrict__ shift,
                                               const float* __restrict__ resid, float* __restrict__ out,
@@ -321,11 +322,11 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
             }
             f32x4 rv = {0.f, 0.f, 0.f, 0.f};
             if (EARLY) rv = rve[EARLY ? p : 0];
-            else if (has_res && COH)   // residual produced inside the launch (tower, VAR bit 16)
+            else if (has_res && RBUF)   // residual produced inside the launch (tower)
                 rv = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                    __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(resid), (short)0,
                                                                                      0x7fffffff, 0x00020000),
-                                                   o * 4, 0, 16));
+                                                   o * 4, 0, RBUF == 2 ? 16 : 0));
             else if (has_res) rv = *(const f32x4*)(resid + o);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -411,9 +412,12 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
             }
         }
         // fused finalize: the last workgroup of this N tile to publish its partials
-        // reduces all M tiles' partials of its BN channels (tower hand-off protocol:
-        // write-through stores, vmcnt(0), barrier, one agent-scope atomic; the last
-        // arriver reads them with agent-coherent loads, coh_load)
+        // reduces all M tiles' partials of its BN channels.  Hand-off (MI355X_MICROARCH
+        // "Valid forms", producer R1 + consumer acquire -- the form valid at any number
+        // of workgroups per CU; this launch runs two): write-through stores, every wave
+        // vmcnt(0), barrier, one agent-scope atomic add per workgroup; the workgroup
+        // whose add returns ntm - 1 runs ONE agent-scope acquire, vmcnt(0) and a barrier
+        // before its plain loads of the partials.
         if (fx.cnt) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
@@ -421,7 +425,12 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
             if (tid == 0) {
                 const unsigned old =
                     __hip_atomic_fetch_add(fx.cnt + n0 / BN, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                *flag = old == (unsigned)(ntm - 1) ? 1u : 0u;
+                const unsigned last = old == (unsigned)(ntm - 1) ? 1u : 0u;
+                if (last) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                *flag = last;
             }
             __syncthreads();
             if (*flag) {
@@ -432,7 +441,7 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                 double* red = (double*)smem;   // [2][8][64]
                 const int wv = tid >> 6, ln = tid & 63;
                 double v0, v1;
-                bn_fin_accum<XE == XE_STATS, true>(ex.pa, ex.pb, C, ntm, BM, M, n0 + ln, wv, v0, v1);
+                bn_fin_accum<XE == XE_STATS, false>(ex.pa, ex.pb, C, ntm, BM, M, n0 + ln, wv, v0, v1);
                 bn_fin_combine8<XE == XE_STATS>(v0, v1, red, M, n0 + ln, true, fx);
                 if (tid == 0) __hip_atomic_store(fx.cnt + n0 / BN, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -726,24 +735,50 @@ __device__ __forceinline__ void halo_tile(
     // are fully unrolled: the rb1 = rb2 hand-over is a register renaming, not a move)
     f32x4 rh[H_LD], rb1[B_LD], rb2[B_LD];
     f32x4 rr[PRO == PRO_BN_RES ? H_LD : 1];
-    // VAR bit 16 (persistent tower, key 31): halo rows are produced inside the launch by
-    // other XCDs; they are read with agent-coherent (sc1) loads instead of after an
-    // L2-invalidating acquire, so the weights stay in L2
+    // VAR bit 16 (persistent tower at ONE workgroup per CU): halo rows are produced
+    // inside the launch by other CUs; every load of them is an sc1 buffer load (L1
+    // bypassed) in place of the consumer's acquire -- row 1 of the microarch guide's
+    // measured hand-off table, valid only at one workgroup per CU (pv_tower.hip).
+    // VAR bit 32: the same buffer-resource addressing (32-bit offsets: fewer VGPRs than
+    // 64-bit pointers) with the default cache policy, behind the consumer's acquire.
     const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in), (short)0,
                                                                           0x7fffffff, 0x00020000);
+    // 1024-thread tiles stage 2 x 128 rows for a halo of at most HS rows: rows past the
+    // tile's last needed row (hmax) are not loaded (their LDS rows are never read)
+    constexpr bool HPRED = T::NT >= 1024 && H_LD * RPP - HS >= RPP / 4;
+    if constexpr (HPRED) {
+#pragma unroll
+        for (int i = 0; i < H_LD; ++i) rh[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     auto hload = [&](int cg, int i) {
         if (ABL & 2) return;
-        if constexpr ((VAR & 16) != 0)
-            rh[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, (hsrc[i] + cg * BK) * 4, 0, 16));
+        if constexpr (HPRED) {
+            if (hbase + sr + RPP * i > hmax) return;
+        }
+        if constexpr ((VAR & 48) != 0)
+            rh[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, (hsrc[i] + cg * BK) * 4, 0,
+                                                                                    (VAR & 16) ? 16 : 0));
         else
             rh[i] = *(const f32x4*)(in + hsrc[i] + cg * BK);
         if constexpr (PRO == PRO_BN_RES) rr[i] = *(const f32x4*)(px.res + hsrc[i] + cg * BK);
     };
+    // VAR 16 / 32: weights through a buffer resource too (SGPR base + one VGPR offset
+    // + per-chunk SGPR/immediate offsets, instead of a 64-bit address per chunk)
+    const __amdgpu_buffer_rsrc_t w_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wp), (short)0,
+                                                                         0x7fffffff, 0x00020000);
+    const int wvo = ((n0 + sr) * BK + sc) * 4;
     auto bload = [&](f32x4 (&rb)[B_LD], int kc) {
         if (ABL & 1) return;
-        const float* wk = wsrc + (size_t)kc * C * BK;
+        if constexpr ((VAR & 48) != 0) {
 #pragma unroll
-        for (int i = 0; i < B_LD; ++i) rb[i] = *(const f32x4*)(wk + RPP * i * BK);
+            for (int i = 0; i < B_LD; ++i)
+                rb[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                      w_rs, wvo, (kc * C * BK + RPP * i * BK) * 4, 0));
+        } else {
+            const float* wk = wsrc + (size_t)kc * C * BK;
+#pragma unroll
+            for (int i = 0; i < B_LD; ++i) rb[i] = *(const f32x4*)(wk + RPP * i * BK);
+        }
     };
     // K chunk j (0 .. 9*CG-1) = tap j%9 of channel group j/9 -> packed weight chunk
     auto kchunk = [](int j) { return (j % 9) * CG + j / 9; };
@@ -910,7 +945,8 @@ __device__ __forceinline__ void halo_tile(
     }
 
     // the last chunk ended with a barrier: the staging buffers are free
-    halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, (VSWZ ? BN : BN + 8), (VAR & 8) != 0, XE, (VAR & 16) != 0>(
+    halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, (VSWZ ? BN : BN + 8), (VAR & 8) != 0, XE,
+                  (VAR & 16) ? 2 : (VAR & 32) ? 1 : 0>(
         acc, scale, shift, resid, out, out_rs, M, m0, n0, smem, ex, fx);
 }
 

@@ -59,7 +59,9 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
                         hipStream_t st, float** result);
 extern unsigned g_tower_spin_limit;
 extern int g_tower_group;
+#ifdef AZG_AB_STUDIES
 extern int g_tower_coh;
+#endif
 hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const float* scale,
                        const float* shift, float* out, int B, hipStream_t st, const int8_t* boards = nullptr,
                        const int8_t* players = nullptr);

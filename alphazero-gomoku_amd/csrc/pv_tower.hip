@@ -11,13 +11,21 @@
 // Tile body: halo_tile (pv_halo.h), identical arithmetic to the per-layer kernel
 // (results are bitwise equal to the per-layer path).
 //
-// Hand-off protocol (cdna_hip_programming.md Guideline 16, R1 + acquire):
-//  * producer: every output element is stored write-through (buffer_store sc1);
-//    each wave drains (s_waitcnt vmcnt(0)); workgroup barrier; one lane adds 1 to
-//    the (layer, M tile) counter with an agent-scope atomic;
-//  * consumer: one lane polls the (up to) three counters with relaxed agent-scope
-//    loads until each equals the number of N tiles, then ONE agent-scope acquire
-//    (L1 invalidate), s_waitcnt vmcnt(0), workgroup barrier, then plain loads.
+// Hand-off protocol (cdna_hip_programming.md Guideline 16; MI355X_MICROARCH.md
+// "Valid forms"), producer side always R1: every output element is stored
+// write-through (16-B buffer_store sc1); each wave drains (s_waitcnt vmcnt(0));
+// workgroup barrier; one lane adds the tile count to the (layer, M tile) counter
+// with an agent-scope atomic.  Consumer: one lane polls the (up to) three counters
+// with relaxed agent-scope loads (global_load sc1) until each is complete, then
+//  * VAR bit 16 clear (64x64 / 128x64 tiles, 2-4 workgroups per CU): ONE agent-scope
+//    acquire, s_waitcnt vmcnt(0), workgroup barrier, plain loads -- the form valid at
+//    any occupancy;
+//  * VAR bit 16 set (the 16-wave 128x128 tile, exactly ONE workgroup per CU, checked
+//    at launch): s_waitcnt vmcnt(0), workgroup barrier, and EVERY load of handed-off
+//    bytes (halo rows, the epilogue's residual) is a 16-B sc1 buffer load -- row 1 of
+//    the guide's measured hand-off table, which requires one workgroup per CU in
+//    every cell; no LDS-DMA or early-epilogue path may be combined with it
+//    (static_assert below).
 // Deadlock freedom: a tile waits only on tiles claimed before it (all of layer
 // l-1 precedes layer l in claim order), and a claimed tile is always executed by a
 // running workgroup, so the oldest unfinished tile can always finish.  Spins are
@@ -60,17 +68,30 @@ struct TowerArgs {
 constexpr unsigned kSpinLimit = 1u << 22;    // x s_sleep(2): seconds, far above any tile time
 unsigned g_tower_spin_limit = kSpinLimit;    // tuning key 14 (tests: 0 forces the timeout path)
 int g_tower_group = 1;                       // tuning key 17: 1 (default) = claim an M tile with all its N tiles
-int g_tower_coh = 1;                         // tuning key 31: 1 (default) = coherent dependent loads instead of an acquire
+#ifdef AZG_AB_STUDIES
+int g_tower_coh = 0;   // study key 31: sc1 dependent loads with 64x64 / 128x64 tiles (OUTSIDE the guide's envelope)
+#endif
 
 // waves per SIMD the register budget is sized for: 4 (128 VGPRs) for the one-
-// accumulator tiles; 2 (256 VGPRs, one workgroup per CU) for 128-wide N tiles
-template <int BN_>
-constexpr int tower_min_waves() { return BN_ >= 128 ? 2 : 4; }
+// accumulator tiles (two 8-wave or four 4-wave workgroups per CU, or the one 16-wave
+// workgroup); 2 (256 VGPRs, one 8-wave workgroup per CU) for 128-wide N tiles of 8 waves
+template <int BN_, int NW_>
+constexpr int tower_min_waves() { return NW_ >= 16 ? 4 : BN_ >= 128 ? 2 : 4; }
+// dynamic LDS of a tower launch: the 16-wave tile asks for more than half of the CU's
+// 160 KiB so that one workgroup per CU is guaranteed by LDS alone (the sc1-load
+// hand-off is valid only there), whatever the register allocation
+template <int C, int BN, int WM, int TM, int NW, int VAR>
+constexpr int tower_lds_bytes()
+{
+    constexpr int need = halo_lds_bytes<C, BN, WM, TM, NW, VAR>() + 16;
+    return NW >= 16 && need <= 82 * 1024 ? 82 * 1024 : need;
+}
 
 template <int C, int BN_, int WM_, int TM_, int NW_, int VAR = 0>
-__global__ __launch_bounds__(64 * NW_, tower_min_waves<BN_>()) void conv_tower(const TowerArgs a)
+__global__ __launch_bounds__(64 * NW_, (tower_min_waves<BN_, NW_>())) void conv_tower(const TowerArgs a)
 {
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
+    static_assert(!((VAR & 48) && (VAR & 12)), "buffer halo / residual loads (VAR 16, 32) exclude LDS-DMA (4) and early epilogue loads (8)");
     constexpr int NTN = C / T::BN;
     constexpr int LDS_FLOATS = halo_lds_bytes<C, BN_, WM_, TM_, NW_, VAR>() / 4;
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -114,8 +135,8 @@ __global__ __launch_bounds__(64 * NW_, tower_min_waves<BN_>()) void conv_tower(c
                         __builtin_amdgcn_s_sleep(2);
                     }
                 }
-                // VAR bit 16: the dependent reads are agent-coherent loads, no acquire
-                // (an acquire invalidates the XCD's L2 and the weights are re-fetched)
+                // VAR bit 16 (one workgroup per CU): every dependent read is an sc1 load,
+                // no acquire; otherwise ONE agent-scope acquire (L1 invalidate) here
                 if constexpr ((VAR & 16) == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
@@ -141,7 +162,7 @@ __global__ __launch_bounds__(64 * NW_, tower_min_waves<BN_>()) void conv_tower(c
 template <int C, int BN, int WM, int TM, int NW, int VAR = 0>
 static hipError_t launch_tower_t(const TowerArgs& a, hipStream_t st, int* grid_out)
 {
-    constexpr int lds = halo_lds_bytes<C, BN, WM, TM, NW, VAR>() + 16;
+    constexpr int lds = tower_lds_bytes<C, BN, WM, TM, NW, VAR>();
     static int grid = 0;
     if (grid == 0) {
         hipError_t e = hipFuncSetAttribute((const void*)conv_tower<C, BN, WM, TM, NW, VAR>,
@@ -153,6 +174,9 @@ static hipError_t launch_tower_t(const TowerArgs& a, hipStream_t st, int* grid_o
         if (e != hipSuccess) return e;
         if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
         if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+        // the sc1-load hand-off (VAR 16) is valid at one workgroup per CU only: refuse
+        // to launch it at any other residency
+        if ((VAR & 16) && per_cu != 1) return hipErrorInvalidConfiguration;
         grid = max(1, per_cu) * cus;
     }
     if (grid_out) *grid_out = grid;
@@ -162,7 +186,8 @@ static hipError_t launch_tower_t(const TowerArgs& a, hipStream_t st, int* grid_o
 
 int g_tower_ablation = 0;
 int g_tower_var = 0;     // halo_tile VAR of the 128x64 C=128 tower (0 = product; 1..8, 12 A/B studies)
-int g_tower_shape = 8;   // forced shape when g_tower_mode == 1: 5 = 64x64 (4 waves), 8 = 128x64 (8 waves)
+int g_tower_shape = 8;   // forced shape when g_tower_mode == 1: 5 = 64x64 (4 waves), 8 = 128x64 (8 waves),
+                         // 10 = 128x128 (16 waves, one workgroup per CU; C = 128)
 
 size_t tower_sync_bytes(int nlayers, int M)
 {
@@ -189,6 +214,7 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     a.status = status;
     a.spin_limit = g_tower_spin_limit;
     a.group = g_tower_group ? C / (shape == 8 || shape == 5 ? 64 : 128) : 1;
+    if (shape == 10 && C != 128) return hipErrorInvalidValue;   // 16-wave tile: C = 128 only (C = 256 spills)
     a.abl = g_tower_ablation;
     float* X = act[0];
     float* H = act[1];
@@ -207,13 +233,11 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     *result = X;
     hipError_t e = hipMemsetAsync(sync, 0, tower_sync_bytes(2 * NB, M), st);
     if (e != hipSuccess) return e;
-#define AZG_TOWER_C(CC)                                                                    \
-    case CC:                                                                               \
-        if (shape == 8 && g_tower_coh) return launch_tower_t<CC, 64, 4, 1, 8, 16>(a, st, nullptr); \
-        if (shape == 8) return launch_tower_t<CC, 64, 4, 1, 8>(a, st, nullptr);    \
-        if (g_tower_coh) return launch_tower_t<CC, 64, 2, 1, 4, 16>(a, st, nullptr); \
-        return launch_tower_t<CC, 64, 2, 1, 4>(a, st, nullptr);
-#ifdef AZG_AB_STUDIES   // A/B tile-body variants and the 128x128 shape (make study)
+#ifdef AZG_AB_STUDIES
+    if (g_tower_coh && (shape == 8 || shape == 5)) {   // study only: sc1 loads at 2-4 workgroups per CU
+        if (C == 128 && shape == 8) return launch_tower_t<128, 64, 4, 1, 8, 16>(a, st, nullptr);
+        if (C == 128) return launch_tower_t<128, 64, 2, 1, 4, 16>(a, st, nullptr);
+    }
     if (C == 128 && shape == 9) {   // 128x128 tiles, 2 accumulators per wave, LDS-DMA staging (A/B study)
         if (g_tower_var == 5) return launch_tower_t<128, 128, 4, 1, 8, 5>(a, st, nullptr);
         return launch_tower_t<128, 128, 4, 1, 8, 4>(a, st, nullptr);
@@ -229,14 +253,24 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
         if (g_tower_var == 7) return launch_tower_t<128, 64, 4, 1, 8, 7>(a, st, nullptr);
         if (g_tower_var == 12) return launch_tower_t<128, 64, 4, 1, 8, 12>(a, st, nullptr);
     }
+    if (C == 128 && shape == 10 && g_tower_var == 1)   // 16-wave tile with the acquire instead of sc1 loads
+        return launch_tower_t<128, 128, 4, 1, 16, 32>(a, st, nullptr);
+    if (C == 128 && shape == 8 && g_tower_var == 13)   // round-2 acquire form: 64-bit pointer loads (VAR 0)
+        return launch_tower_t<128, 64, 4, 1, 8, 0>(a, st, nullptr);
 #endif
     switch (C) {
-        AZG_TOWER_C(64)
-        AZG_TOWER_C(128)
-        AZG_TOWER_C(256)
+        case 64:
+            if (shape == 8) return launch_tower_t<64, 64, 4, 1, 8, 32>(a, st, nullptr);
+            return launch_tower_t<64, 64, 2, 1, 4, 32>(a, st, nullptr);
+        case 128:
+            if (shape == 10) return launch_tower_t<128, 128, 4, 1, 16, 16>(a, st, nullptr);
+            if (shape == 8) return launch_tower_t<128, 64, 4, 1, 8, 32>(a, st, nullptr);
+            return launch_tower_t<128, 64, 2, 1, 4, 32>(a, st, nullptr);
+        case 256:
+            if (shape == 8) return launch_tower_t<256, 64, 4, 1, 8, 32>(a, st, nullptr);
+            return launch_tower_t<256, 64, 2, 1, 4, 32>(a, st, nullptr);
         default: return hipErrorInvalidValue;
     }
-#undef AZG_TOWER_C
 }
 
 }  // namespace azg

@@ -45,12 +45,19 @@ def init_from_env(backend: Optional[str] = None) -> tuple:
 
 
 def _on_host(t: torch.Tensor, fn) -> torch.Tensor:
-    """Run collective `fn` on `t`; a device tensor under gloo is staged through host
-    memory (gloo is the CPU test backend: world-size-2 DP tests of the HIP engine)."""
-    if t.is_cuda and dist.get_backend() != "nccl":
+    """Run collective `fn` on `t` where the backend can reach it: a device tensor
+    under gloo is staged through host memory (gloo is the CPU test backend:
+    world-size-2 DP tests of the HIP engine); a host tensor under RCCL ("nccl",
+    which has no CPU path) is staged through the current HIP device."""
+    nccl = dist.get_backend() == "nccl"
+    if t.is_cuda and not nccl:
         h = t.detach().to("cpu")
         fn(h)
         t.copy_(h)
+    elif not t.is_cuda and nccl:
+        d = t.detach().to(torch.device("cuda", torch.cuda.current_device()))
+        fn(d)
+        t.copy_(d.cpu())
     else:
         fn(t)
     return t
@@ -87,7 +94,7 @@ def allreduce_min_int(v: int, device) -> int:
     if world() == 1:
         return int(v)
     t = torch.tensor([int(v)], dtype=torch.int64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    _on_host(t, lambda x: dist.all_reduce(x, op=dist.ReduceOp.MIN))
     return int(t.item())
 
 
@@ -108,7 +115,8 @@ def broadcast_model(model, src: int = 0) -> None:
     broadcast_(opt.flat_exp_avg, src)
     broadcast_(opt.flat_exp_avg_sq, src)
     opt._ensure_state()
-    step = torch.tensor([float(opt.state[eng.params[0]]["step"])], dtype=torch.float64)
+    # on the engine's device: RCCL has no CPU tensors (gloo stages it through the host)
+    step = torch.tensor([float(opt.state[eng.params[0]]["step"])], dtype=torch.float64, device=eng.device)
     broadcast_(step, src)
     for p in eng.params:
         opt.state[p]["step"].fill_(float(step.item()))

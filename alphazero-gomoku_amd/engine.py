@@ -103,7 +103,10 @@ class PolicyValueEngine:
     def check_status(self):
         """Raise if any forward on this handle computed on stale inputs (sticky
         device status, include/azg_pv.h azg_pv_status).  A plain host load: call it
-        after synchronising with the forwards it should cover."""
+        after synchronising with the forwards it should cover.  The status stays set
+        (every later check raises) until clear_status(): a caller that handles the
+        failure clears it once reported (train.train_alphazero does so after a failed
+        evaluation, which the reference counts as a loss)."""
         s = int(self.lib.azg_pv_status(self.h))
         if s:
             raise RuntimeError(f"libazg_pv: persistent residual tower timed out waiting for its inputs "

@@ -206,6 +206,10 @@ def train_alphazero(game_name: str = "gomoku", board_size: int = 15, num_iterati
         except Exception as e:  # reference: evaluation failure counts as a loss (train.py:803-805)
             print(f"evaluation failed: {e}")
             new_wins, win_rate, draws = 0, 0.0, 0
+            # the failure is reported: clear the sticky tower status (engine.check_status)
+            # so the next generation's forwards are judged on their own
+            for mdl in (model_candidate, model_best):
+                mdl.engine.clear_status()
         if main:
             print(f"eval done: {(time.time() - te) / 60:.2f} min, win_rate={win_rate:.3f} "
                   f"({new_wins}/{eval_games}), draws={draws}")

@@ -25,8 +25,8 @@ those launches on the stream they ran on.
 Sub-legs (extra keys): `forward_b512` (configs[1]: K forwards of 512 boards in HBM,
 own roofline), `train` (configs[3] train step, 6x128, B=128/GPU, RCCL all-reduce
 at N>1), `pente_10x256` (configs[4]: Pente self-play with the 10x256 net at 800
-sims for a stated move window, its 10x256 forward at B=512 and train step at
-B=128), and `cpu_baseline` (rank 0 at N=1: the reference CPU path, i.e. the oracle
+sims, 32 games per GPU played to their end, its 10x256 forward at B=512 and train
+step at B=128), and `cpu_baseline` (rank 0 at N=1: the reference CPU path, i.e. the oracle
 restatement of network.py + the reference-semantics Python MCTS, on this host).
 """
 from __future__ import annotations
@@ -483,8 +483,9 @@ def train_leg(model, args, rank, world, dist, dev, local, blocks=BLOCKS, ch=CHAN
 
 
 def pente_leg(args, rank, world, dist, dev, local):
-    """configs[4] on one GPU: the 10x256 net -- Pente self-play at 800 sims/move for
-    a stated window of moves, the B=512 forward and the B=128 train step."""
+    """configs[4] on one GPU: the 10x256 net -- Pente self-play at 800 sims/move
+    (default: 32 games, every game to its end), the B=512 forward and the B=128 train
+    step."""
     from games.pente import Pente
     from network import PyTorchModel
     nb, ch = 10, 256
@@ -503,10 +504,16 @@ def pente_leg(args, rank, world, dist, dev, local):
         barrier_sync(dist, local)
         (nbd,) = reduce_(dist, dev, [float(sp.boards)])
         (dtm,) = reduce_(dist, dev, [dt], op="max")
+        lengths = np.asarray(sp.game_lengths)
+        span = ("every game played to its end (is_game_over(), max_moves 225; train.py:369-393)"
+                if args.pente_moves >= 225 else f"first {args.pente_moves} moves of every game (max_moves window)")
         out["selfplay"] = {
-            "config": f"Pente (capture rules), {G} concurrent games/GPU x {S} sims/move, first {args.pente_moves} "
-                      f"moves of every game (window; max_moves), native C++ search + batched HIP forward ({nb}x{ch})",
+            "config": f"Pente (capture rules), {G} concurrent games/GPU x {S} sims/move, {span}, __main__ settings, "
+                      f"native C++ search + batched HIP forward ({nb}x{ch})",
             "boards_per_s": round(nbd / dtm, 1), "leaf_boards": int(nbd), "seconds": round(dtm, 2),
+            "games": G, "rounds": int(sp.rounds), "moves": int(sp.moves),
+            "game_length_rank0": {"mean": round(float(lengths.mean()), 1), "min": int(lengths.min()),
+                                  "max": int(lengths.max())},
             "mean_batch_rank0": round(sp.boards / max(sp.forwards, 1), 1),
             "roofline": roofline_from_profile(prof, boards, nb, ch, f"azg::conv_tower<{ch},*>",
                                               f"azg::conv3x3_halo<{ch},*>")}
@@ -529,8 +536,9 @@ def main():
     ap.add_argument("--train-steps", type=int, default=20, help="steps of the configs[3] train leg (0: skip)")
     ap.add_argument("--big-steps", type=int, default=10, help="10x256 forwards (configs[4] net; 0: skip the leg)")
     ap.add_argument("--big-train-steps", type=int, default=5)
-    ap.add_argument("--pente-games", type=int, default=64)
-    ap.add_argument("--pente-moves", type=int, default=3, help="move window of the configs[4] Pente self-play")
+    ap.add_argument("--pente-games", type=int, default=32)
+    ap.add_argument("--pente-moves", type=int, default=225,
+                    help="max_moves of the configs[4] Pente self-play (225 = every game to its end)")
     ap.add_argument("--skip-forward", action="store_true", help="profiling runs: no configs[1] sub-leg")
     ap.add_argument("--tune", action="append", default=[], help="KEY=VALUE tuning key (A/B and profiling runs)")
     args = ap.parse_args()

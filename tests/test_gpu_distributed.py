@@ -10,7 +10,13 @@ Checked: params, Adam moments and step, BN running stats and counters bitwise
 identical across ranks, and equal (<= 2e-6) to a single-process run that evaluates
 both ranks' batches with azg_pv_train_backward, averages the two flat gradients,
 and applies clip + Adam once per step (BN running stats evolved per rank, then
-averaged -- what sync_bn_stats does)."""
+averaged -- what sync_bn_stats does).  Two shapes: 2x64 at B = 32/rank, and
+configs[3]'s per-rank shape, 6x128 at B = 128/rank (7.57 MB flat gradient; the
+reference step network.py:199-235 at train.py:849-889's batch).
+
+`test_collectives_see_device_tensors_under_rccl`: with the backend reported as
+"nccl" (RCCL has no CPU path), every tensor reaching a collective from
+broadcast_model / grad_hook / sync_bn_stats / allreduce_* is a HIP tensor."""
 import os
 import socket
 
@@ -23,7 +29,7 @@ from conftest import PKG, REPO, has_gpu
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")]
 
-K, B, BLOCKS, CH = 3, 32, 2, 64
+SHAPES = {"2x64_b32": (3, 32, 2, 64), "6x128_b128": (2, 128, 6, 128)}   # K steps, B per rank, blocks, channels
 
 
 def _free_port():
@@ -32,7 +38,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _batch(rank, step):
+def _batch(rank, step, B):
     from oracle.boards import encode_batch, synth_positions, synth_targets
     b, p = synth_positions(B, seed=1000 + 10 * step + rank)
     pi, z = synth_targets(B, seed=2000 + 10 * step + rank)
@@ -48,7 +54,8 @@ def _state(m):
             "step": np.array([float(opt.state[eng.params[0]]["step"])])}
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, shape):
+    K, B, BLOCKS, CH = SHAPES[shape]
     import sys
     sys.path[:0] = [REPO, PKG]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
@@ -60,12 +67,12 @@ def _worker(rank, world, port, out_dir):
     torch.manual_seed(rank)                              # replicas start DIFFERENT
     m = PyTorchModel(board_size=15, device="cuda:0", n_res_blocks=BLOCKS, channels=CH)
     if rank == 1:                                        # and a different Adam history
-        x, pi, z = _batch(7, 7)
+        x, pi, z = _batch(7, 7, B)
         m.train_batch(x, pi, z)
     D.broadcast_model(m, 0)
     m.grad_hook = D.grad_hook()
     for s in range(K):
-        x, pi, z = _batch(rank, s)
+        x, pi, z = _batch(rank, s, B)
         m.train_batch(x, pi, z)
     D.sync_bn_stats(m)
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **_state(m))
@@ -73,9 +80,11 @@ def _worker(rank, world, port, out_dir):
 
 
 @pytest.mark.timeout(300)
-def test_dp_train_through_hip_engine_world2(tmp_path):
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_dp_train_through_hip_engine_world2(tmp_path, shape):
+    K, B, BLOCKS, CH = SHAPES[shape]
     port = _free_port()
-    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, port, str(tmp_path), shape), nprocs=2, join=True)
     r0, r1 = (dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(2))
     for k in r0:
         assert np.array_equal(r0[k], r1[k]), k          # replicas bitwise identical
@@ -93,7 +102,7 @@ def test_dp_train_through_hip_engine_world2(tmp_path):
     for s in range(K):
         gs = []
         for r in range(2):
-            x, pi, z = (torch.from_numpy(np.asarray(a, np.float32)).to(eng.device) for a in _batch(r, s))
+            x, pi, z = (torch.from_numpy(np.asarray(a, np.float32)).to(eng.device) for a in _batch(r, s, B))
             with torch.no_grad():
                 eng.flat_bn.copy_(bn[r])
             eng.flat_nbt.copy_(nbt0)
@@ -110,6 +119,34 @@ def test_dp_train_through_hip_engine_world2(tmp_path):
     want = _state(m)
     for k in ("params", "m", "v", "bn"):
         d = float(np.abs(r0[k] - want[k]).max())
-        print(f"{k}: max |dp - single| = {d:.2e}")
+        print(f"{shape} {k}: max |dp - single| = {d:.2e}")
         assert d <= 2e-6, (k, d)
     assert np.array_equal(r0["nbt"], want["nbt"]) and r0["step"][0] == want["step"][0] == K
+
+
+def test_collectives_see_device_tensors_under_rccl(monkeypatch):
+    """under RCCL every collective operand must be a HIP tensor --
+    broadcast_model's Adam step counter used to be a CPU float64 tensor.  The backend
+    is reported as "nccl" and world size 2; the collectives record their operands."""
+    import distributed as D
+    import torch.distributed as dist
+    from network import PyTorchModel
+    seen = []
+
+    def rec(name):
+        def f(t, *a, **k):
+            seen.append((name, t.device.type, tuple(t.shape), t.dtype))
+        return f
+    monkeypatch.setattr(D, "world", lambda: 2)
+    monkeypatch.setattr(dist, "get_backend", lambda *a, **k: "nccl")
+    monkeypatch.setattr(dist, "broadcast", rec("broadcast"))
+    monkeypatch.setattr(dist, "all_reduce", rec("all_reduce"))
+    torch.manual_seed(0)
+    m = PyTorchModel(board_size=15, device="cuda:0", n_res_blocks=1, channels=64)
+    D.broadcast_model(m, 0)
+    D.grad_hook()(m.engine.flat_grads)
+    D.sync_bn_stats(m)
+    D.allreduce_sum_(torch.zeros(3, dtype=torch.int64))            # a host tensor: staged through the GPU
+    assert D.allreduce_min_int(5, "cpu") == 5
+    assert len(seen) >= 8
+    assert all(dev == "cuda" for _, dev, _, _ in seen), seen

@@ -202,9 +202,11 @@ def test_empty_batch():
                                                (10, 256, (96, 513))])
 def test_persistent_tower_bitwise_equals_per_layer_launches(blocks, ch, batches):
     """The persistent residual tower (one launch, tiles handed between workgroups
-    through counters + acquire) computes exactly the per-layer kernels' arithmetic:
-    outputs must be BITWISE equal.  Repeated runs (stale-line hazards show up
-    intermittently), with each tile shape, and the timeout word must stay 0."""
+    through counters: acquire + plain loads for the 64x64 / 128x64 tiles at 2-4
+    workgroups per CU, sc1 loads for the 16-wave 128x128 tile at one workgroup per
+    CU) computes exactly the per-layer kernels' arithmetic: outputs must be BITWISE
+    equal.  Repeated runs (stale-line hazards show up intermittently), with each tile
+    shape and claim granularity, and the timeout word must stay 0."""
     import _native
     from synth import synth_encoded
     lib = _native.load_library()
@@ -219,26 +221,26 @@ def test_persistent_tower_bitwise_equals_per_layer_launches(blocks, ch, batches)
             lib.azg_pv_set_tuning(5, 0)
             p0, v0, l0 = eng.forward(x, want_logits=True)
             lib.azg_pv_set_tuning(5, 1)
-            for shape in (5, 8):
+            for shape in ((5, 8, 10) if ch == 128 else (5, 8)):
                 lib.azg_pv_set_tuning(6, shape)
-                for group, coh in ((0, 0), (1, 0), (1, 1), (0, 1)):   # claim granularity (key 17), coherent reads (31)
+                for group in (0, 1):   # claim granularity (key 17)
                     prev_group = lib.azg_pv_set_tuning(17, group)
-                    prev_coh = lib.azg_pv_set_tuning(31, coh)
                     for rep in range(3):
                         p1, v1, l1 = eng.forward(x, want_logits=True)
                         assert lib.azg_pv_tower_status(eng.h, stream) == 0
-                        assert torch.equal(l0, l1), (B, shape, group, coh, rep, float((l0 - l1).abs().max()))
-                        assert torch.equal(p0, p1) and torch.equal(v0, v1), (B, shape, group, coh, rep)
-                    lib.azg_pv_set_tuning(31, prev_coh)
+                        assert torch.equal(l0, l1), (B, shape, group, rep, float((l0 - l1).abs().max()))
+                        assert torch.equal(p0, p1) and torch.equal(v0, v1), (B, shape, group, rep)
                     lib.azg_pv_set_tuning(17, prev_group)
             if ch == 128 and lib.azg_pv_set_tuning(15, 0) == 1:   # study build: tile-body variants, same arithmetic
-                lib.azg_pv_set_tuning(6, 8)
-                for var in (0, 1, 2, 3, 4, 5, 6, 7, 8, 12):
+                for shape, var, coh in [(8, v, 0) for v in (1, 2, 3, 4, 5, 6, 7, 8, 12, 13)] + [(8, 0, 1), (10, 1, 0)]:
+                    lib.azg_pv_set_tuning(6, shape)
                     prev_var = lib.azg_pv_set_tuning(10, var)
+                    prev_coh = lib.azg_pv_set_tuning(31, coh)
                     p1, v1, l1 = eng.forward(x, want_logits=True)
+                    lib.azg_pv_set_tuning(31, prev_coh)
                     lib.azg_pv_set_tuning(10, prev_var)
                     assert lib.azg_pv_tower_status(eng.h, stream) == 0
-                    assert torch.equal(l0, l1), ("var", var, B, float((l0 - l1).abs().max()))
+                    assert torch.equal(l0, l1), ("var", shape, var, coh, B, float((l0 - l1).abs().max()))
     finally:
         lib.azg_pv_set_tuning(6, prev_shape)
         lib.azg_pv_set_tuning(5, prev_mode)
@@ -274,8 +276,9 @@ def test_per_layer_variants_bitwise(blocks, ch, B):
 
 
 def test_persistent_tower_under_concurrent_load():
-    """Tower forwards on two streams at once (uneven load: a per-layer forward and
-    a tower forward of another model share the GPU) stay bitwise reproducible."""
+    """Tower forwards on two streams at once (uneven load: towers of two models with
+    different batches share the GPU) stay bitwise equal to per-layer launches, for
+    every tower tile shape."""
     import _native
     from synth import synth_encoded
     lib = _native.load_library()
@@ -283,19 +286,26 @@ def test_persistent_tower_under_concurrent_load():
     m2 = make_model(6, 128, seed=5)
     x1 = torch.from_numpy(synth_encoded(512, seed=11)).cuda()
     x2 = torch.from_numpy(synth_encoded(1024, seed=12)).cuda()
-    prev_mode = lib.azg_pv_set_tuning(5, 1)
-    r1 = m1.engine.forward(x1)[0].clone()
-    r2 = m2.engine.forward(x2)[0].clone()
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-    torch.cuda.synchronize()
-    for _ in range(4):
-        with torch.cuda.stream(s1):
-            a = m1.engine.forward(x1)[0]
-        with torch.cuda.stream(s2):
-            b = m2.engine.forward(x2)[0]
+    prev_mode = lib.azg_pv_set_tuning(5, 0)
+    prev_shape = lib.azg_pv_set_tuning(6, 8)
+    try:
+        r1 = m1.engine.forward(x1)[0].clone()
+        r2 = m2.engine.forward(x2)[0].clone()
+        lib.azg_pv_set_tuning(5, 1)
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
         torch.cuda.synchronize()
-        assert torch.equal(a, r1) and torch.equal(b, r2)
-    lib.azg_pv_set_tuning(5, prev_mode)
+        for shape in (8, 10, 5):
+            lib.azg_pv_set_tuning(6, shape)
+            for _ in range(4):
+                with torch.cuda.stream(s1):
+                    a = m1.engine.forward(x1)[0]
+                with torch.cuda.stream(s2):
+                    b = m2.engine.forward(x2)[0]
+                torch.cuda.synchronize()
+                assert torch.equal(a, r1) and torch.equal(b, r2), shape
+    finally:
+        lib.azg_pv_set_tuning(6, prev_shape)
+        lib.azg_pv_set_tuning(5, prev_mode)
 
 
 def test_tower_timeout_is_a_hard_error():
