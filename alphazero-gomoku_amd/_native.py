@@ -49,7 +49,7 @@ _SIGS = {
     "azg_pv_debug_copy": (ctypes.c_int32, [_P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32, _P]),
 }
 EXPORTS = tuple(_SIGS)
-PROF_CLASSES = ("conv3x3", "stem", "heads", "train_conv", "train_wgrad", "train_other", "tower", "r7")
+PROF_CLASSES = ("conv3x3", "stem", "heads", "train_conv", "train_wgrad", "train_other", "tower", "tower16")
 ABI_VERSION = 1
 
 _lib = None

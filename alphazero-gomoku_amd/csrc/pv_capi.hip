@@ -426,7 +426,7 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
             out_off[2 * i] = bd[h->bn_blk[i].first].out_off;
             out_off[2 * i + 1] = bd[h->bn_blk[i].second].out_off;
         }
-        pr = prof_begin(h, AZG_PROF_TOWER, st, batch);
+        pr = prof_begin(h, variant == 10 ? AZG_PROF_TOWER_WIDE : AZG_PROF_TOWER, st, batch);
         AZG_TRY(launch_tower(C, h->NB, variant, h->act, h->wpack, h->scale, h->shift, out_off, M, h->tower_sync,
                              h->status_dev, st, &X),
                 "forward: tower");

@@ -225,7 +225,7 @@ __global__ __launch_bounds__(64 * NW_, 2) void conv3x3_halo(
 // WT: outputs stored write-through (no dirty L2 lines at the kernel boundary).
 // PRO (forward only): the input is the previous layer's raw output z and its BN +
 // ReLU (+ residual) is applied in the halo staging (pv_halo.h ProX).
-template <int C, int EPI, int XE, bool WT, int PRO = PRO_NONE>
+template <int C, int EPI, int XE, bool WT, int PRO = PRO_NONE, int VAR = 32>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv3x3_train(
     const float* __restrict__ in, const float* __restrict__ wp, const float* __restrict__ resid,
     float* __restrict__ out, int M, EpiX ex, ProX px, FinX fx)
@@ -236,9 +236,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
     const int L = blockIdx.x, nt = gridDim.x;
     const int xcd = L & 7, q8 = nt >> 3, r8 = nt & 7;
     const int t = xcd * q8 + min(xcd, r8) + (L >> 3);
-    halo_tile<C, 64, 4, 1, 8, EPI, WT, 0, 0, XE, PRO>(in, wp, nullptr, nullptr, resid, out,
-                                                   wt_rsrc(out, padded_bytes(M, C)), M, (t / NTN) * T::BM,
-                                                   (t % NTN) * T::BN, smem, ex, px, fx);
+    halo_tile<C, 64, 4, 1, 8, EPI, WT, 0, VAR, XE, PRO>(in, wp, nullptr, nullptr, resid, out,
+                                                     wt_rsrc(out, padded_bytes(M, C)), M, (t / NTN) * T::BM,
+                                                     (t % NTN) * T::BN, smem, ex, px, fx);
 }
 
 // Stem conv 3->C (K = 27) on the VALU: 0.2 % of the forward FLOPs.  One
@@ -784,30 +784,36 @@ hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, cons
 
 int g_train_wt = 7;   // key 18 bits: 1 train conv outputs, 2 BN apply outputs, 4 wgrad slabs write-through
 
-template <int C, int EPI, int XE, int PRO = PRO_NONE>
-static hipError_t launch_train_t(const float* in, const float* wp, const float* resid, float* out, int M,
+int g_train_var = 32;  // key 25: halo_tile VAR of the train convs (32 buffer-resource addressing, default; 0 64-bit pointers)
+
+template <int C, int EPI, int XE, int PRO, bool WT, int VAR>
+static hipError_t launch_train_v(const float* in, const float* wp, const float* resid, float* out, int M,
                                  const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st)
 {
     using T = ConvTile<C, 64, 4, 1, 8>;
     constexpr int lds = halo_lds_bytes<C, 64, 4, 1, 8, 0, PRO>();
     static bool attr_done = false;
     if (!attr_done) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, false, PRO>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, WT, PRO, VAR>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, true, PRO>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
         attr_done = true;
     }
     dim3 grid(((M + T::BM - 1) / T::BM) * (C / T::BN));
-    if (g_train_wt & 1)
-        hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, true, PRO>), grid, dim3(T::NT), lds, st, in, wp, resid, out, M,
-                           ex, px, fx);
-    else
-        hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, false, PRO>), grid, dim3(T::NT), lds, st, in, wp, resid, out,
-                           M, ex, px, fx);
+    hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, WT, PRO, VAR>), grid, dim3(T::NT), lds, st, in, wp, resid, out, M,
+                       ex, px, fx);
     return hipGetLastError();
+}
+
+template <int C, int EPI, int XE, int PRO = PRO_NONE>
+static hipError_t launch_train_t(const float* in, const float* wp, const float* resid, float* out, int M,
+                                 const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st)
+{
+#ifdef AZG_AB_STUDIES   // plain (write-back) output stores: A/B only
+    if (!(g_train_wt & 1)) return launch_train_v<C, EPI, XE, PRO, false, 32>(in, wp, resid, out, M, ex, px, fx, st);
+#endif
+    if (g_train_var == 0) return launch_train_v<C, EPI, XE, PRO, true, 0>(in, wp, resid, out, M, ex, px, fx, st);
+    return launch_train_v<C, EPI, XE, PRO, true, 32>(in, wp, resid, out, M, ex, px, fx, st);
 }
 
 // Train conv with fused BN partials: (EPI_RAW, XE_STATS) forward, optionally with
@@ -955,6 +961,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     if (key == 24) {  // train: BN finalize fused into the producing conv's last workgroup (1, default) or separate (0)
         const int prev = azg::g_train_fuse_fin;
         if (value == 0 || value == 1) azg::g_train_fuse_fin = value;
+        return prev;
+    }
+    if (key == 25) {  // train convs: halo_tile VAR (32 buffer-resource addressing, default; 0 64-bit pointers); bitwise identical
+        const int prev = azg::g_train_var;
+        if (value == 0 || value == 32) azg::g_train_var = value;
         return prev;
     }
     if (key == 23) {  // train: BN applies folded into the next conv's halo staging (1, default) or separate (0)

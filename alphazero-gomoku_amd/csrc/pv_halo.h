@@ -682,7 +682,7 @@ __device__ __forceinline__ void halo_tile(
     static_assert(RPP % 16 == 0, "halo staging rows must keep the row swizzle");
     static_assert(H_LD <= 9, "halo loads are spread over the 9 taps");
     static_assert(PRO == PRO_NONE || H_LD <= 8, "the operand prologue of a row runs one tap after its load");
-    static_assert(PRO == PRO_NONE || (VAR == 0 && ABL == 0), "operand prologue: register staging only");
+    static_assert(PRO == PRO_NONE || ((VAR == 0 || VAR == 32) && ABL == 0), "operand prologue: register staging only");
     // VAR (A/B studies; the product uses 0, measured fastest): bit 1 = halo rows
     // swizzled on the padded board position (conflict-free fragment reads) and an
     // unpadded epilogue tile; bit 2 = weights staged two chunks ahead; bit 4 = LDS-DMA
@@ -743,6 +743,8 @@ __device__ __forceinline__ void halo_tile(
     // 64-bit pointers) with the default cache policy, behind the consumer's acquire.
     const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in), (short)0,
                                                                           0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t res_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(px.res), (short)0,
+                                                                           0x7fffffff, 0x00020000);
     // 1024-thread tiles stage 2 x 128 rows for a halo of at most HS rows: rows past the
     // tile's last needed row (hmax) are not loaded (their LDS rows are never read)
     constexpr bool HPRED = T::NT >= 1024 && H_LD * RPP - HS >= RPP / 4;
@@ -760,7 +762,12 @@ __device__ __forceinline__ void halo_tile(
                                                                                     (VAR & 16) ? 16 : 0));
         else
             rh[i] = *(const f32x4*)(in + hsrc[i] + cg * BK);
-        if constexpr (PRO == PRO_BN_RES) rr[i] = *(const f32x4*)(px.res + hsrc[i] + cg * BK);
+        if constexpr (PRO == PRO_BN_RES) {
+            if constexpr ((VAR & 32) != 0)
+                rr[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(res_rs, (hsrc[i] + cg * BK) * 4, 0, 0));
+            else
+                rr[i] = *(const f32x4*)(px.res + hsrc[i] + cg * BK);
+        }
     };
     // VAR 16 / 32: weights through a buffer resource too (SGPR base + one VGPR offset
     // + per-chunk SGPR/immediate offsets, instead of a 64-bit address per chunk)

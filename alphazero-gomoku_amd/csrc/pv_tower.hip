@@ -174,9 +174,14 @@ static hipError_t launch_tower_t(const TowerArgs& a, hipStream_t st, int* grid_o
         if (e != hipSuccess) return e;
         if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
         if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
-        // the sc1-load hand-off (VAR 16) is valid at one workgroup per CU only: refuse
-        // to launch it at any other residency
+        // the sc1-load hand-off (VAR 16) is valid at one workgroup per CU only: the
+        // product refuses to launch it at any other residency (the study build runs the
+        // round-2 two-per-CU form on purpose, key 31)
+#ifndef AZG_AB_STUDIES
         if ((VAR & 16) && per_cu != 1) return hipErrorInvalidConfiguration;
+#else
+        if ((VAR & 16) && NW >= 16 && per_cu != 1) return hipErrorInvalidConfiguration;
+#endif
         grid = max(1, per_cu) * cus;
     }
     if (grid_out) *grid_out = grid;

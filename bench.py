@@ -257,7 +257,7 @@ def cpu_baseline(game_seconds: float) -> dict:
 # --------------------------------------------------------------------- GPU legs
 def traffic_records():
     """HBM-traffic records of the residual-conv kernels from the committed PMC passes
-    (profiles/conv_traffic.json: scripts/summarize_profile.py, summarize_conv_pmc.py)."""
+    (profiles/conv_traffic.json: scripts/summarize_pmc_r3.py, summarize_conv_pmc.py)."""
     try:
         d = json.load(open(os.path.join(REPO, "profiles", "conv_traffic.json")))
         return d.get("records", [d])
@@ -265,20 +265,27 @@ def traffic_records():
         return []
 
 
-def roofline_from_profile(prof, boards, blocks, ch, kname_tower, kname_layer, traffic=True):
+# profile class -> (convs per launch as a multiple of blocks (0: one conv), PMC record shape prefix)
+TOWER_CLASSES = {"tower16": (2, "conv_tower<128, 128, 4, 1, 16"), "tower": (2, "conv_tower<"), "conv3x3": (0, None)}
+
+
+def roofline_from_profile(prof, boards, blocks, ch, knames, traffic=True):
     """Residual-conv roofline from hipEvent-timed launches.  The kernel is the
-    DOMINANT class by device time: the persistent tower (`tower`) or the per-layer
-    conv3x3 launches (`conv3x3`); the other class is reported beside it.  traffic:
-    HBM bytes per launch from the committed PMC record of that kernel, scaled per
-    board to this run's average launch (6x128 only)."""
+    DOMINANT class by device time: the persistent tower with 16-wave tiles
+    (`tower16`), with 64x64 / 128x64 tiles (`tower`), or per-layer conv3x3 launches
+    (`conv3x3`); the other classes are reported beside it.  traffic: HBM bytes per
+    launch from the committed PMC record of that kernel and net at the batch closest
+    to this run's average launch, scaled per board to it."""
     cf = conv_flop(ch)
     cls = {}
-    for k, convs, name in (("tower", 2 * blocks, kname_tower), ("conv3x3", 1, kname_layer)):
+    for k, (mult, _) in TOWER_CLASSES.items():
         ms, n = prof.get(k, (0.0, 0))
         if n:
+            convs = mult * blocks if mult else 1
             flop = cf * convs * boards.get(k, 0)
-            cls[k] = {"kernel": name, "launches": n, "device_ms": round(ms, 1), "avg_launch_us": round(ms / n * 1e3, 2),
-                      "flop_per_launch": round(flop / n), "boards_per_launch": round(boards.get(k, 0) / n, 1),
+            cls[k] = {"kernel": knames.get(k, k), "launches": n, "device_ms": round(ms, 1),
+                      "avg_launch_us": round(ms / n * 1e3, 2), "flop_per_launch": round(flop / n),
+                      "boards_per_launch": round(boards.get(k, 0) / n, 1),
                       "frac": round(flop / (ms / 1e3) / PEAK_F32_MFMA, 4), "_flop": flop, "_ms": ms}
     if not cls:
         return None
@@ -288,18 +295,20 @@ def roofline_from_profile(prof, boards, blocks, ch, kname_tower, kname_layer, tr
     out = {"bound": "mfma", "achieved": round(achieved / 1e12, 3), "peak": PEAK_F32_MFMA / 1e12,
            "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA, 4), "traffic": None}
     out.update({k: v for k, v in d.items() if not k.startswith("_") and k != "frac"})
-    if traffic and (blocks, ch) == (BLOCKS, CHANNELS):
-        recs = [r for r in traffic_records() if r.get("kernel") == dom]
+    pref = TOWER_CLASSES[dom][1]
+    if traffic and pref:
+        net = f"{blocks}x{ch}_B"
+        recs = [r for r in traffic_records() if r.get("kernel") == "tower" and r.get("config", "").startswith(net)
+                and r.get("shape", "").startswith(pref) and (dom != "tower" or "16>" not in r["shape"])]
         if recs:
-            # per board over the record's launches (both epilogues of the per-layer
-            # conv alternate: mean of the two records)
-            per_board = sum(r["hbm_bytes_per_launch"] / r["boards_per_launch"] for r in recs) / len(recs)
-            out["traffic"] = round(per_board * d["boards_per_launch"])
-            out["traffic_basis"] = "; ".join(
-                f"PMC FETCH_SIZE x2 + WRITE_SIZE of {r['kernel']} ({r.get('epilogue', 'all convs')}) at "
-                f"{r['config']} ({r['tag']}): {r['hbm_bytes_per_launch'] / 1e6:.1f} MB per launch, "
-                f"{r.get('traffic_over_algorithmic', 0)}x algorithmic" for r in recs) + \
-                "; scaled per board to this run's average launch"
+            bpl = d["boards_per_launch"]
+            r = min(recs, key=lambda r: abs(r["boards_per_launch"] - bpl))
+            out["traffic"] = round(r["hbm_bytes_per_launch"] / r["boards_per_launch"] * bpl)
+            out["traffic_over_algorithmic"] = r["traffic_over_algorithmic"]
+            out["traffic_basis"] = (f"PMC FETCH_SIZE x2 + WRITE_SIZE of {r['shape']} at {r['config']} ({r['tag']}): "
+                                    f"{r['hbm_bytes_per_launch'] / 1e6:.1f} MB per launch, "
+                                    f"{r['traffic_over_algorithmic']}x algorithmic; scaled per board to this run's "
+                                    f"average launch ({bpl} boards)")
     others = [k for k in cls if k != dom]
     if others:
         tot_f = sum(c["_flop"] for c in cls.values())
@@ -307,6 +316,15 @@ def roofline_from_profile(prof, boards, blocks, ch, kname_tower, kname_layer, tr
         out["all_residual_convs_frac"] = round(tot_f / (tot_ms / 1e3) / PEAK_F32_MFMA, 4)
         out["other_classes"] = {k: {kk: vv for kk, vv in cls[k].items() if not kk.startswith("_")} for k in others}
     return out
+
+
+def tower_knames(ch, blocks):
+    n = 2 * blocks
+    return {"tower16": f"azg::conv_tower<{ch},128,4,1,16,16> (persistent residual tower, 16-wave 128x128 tiles, one "
+                       f"workgroup per CU: {n} fused 3x3 conv + BN (+ residual) + ReLU layers per launch)",
+            "tower": f"azg::conv_tower<{ch},64,*> (persistent residual tower, 64x64 / 128x64 tiles: {n} fused layers "
+                     f"per launch)",
+            "conv3x3": f"azg::conv3x3_halo<{ch},*> (per-layer fused 3x3 conv + BN (+ residual) + ReLU)"}
 
 
 def batch_buckets(top):
@@ -380,10 +398,7 @@ def selfplay_leg(model, args, rank, world, dist, dev, local):
     dt_max, rounds_max = reduce_(dist, dev, [dt, float(sp.rounds)], op="max")
     winners = {w: sum(1 for _, x in results if x == w) for w in (0, 1, 2)}
     lengths = np.asarray(sp.game_lengths)
-    roof = roofline_from_profile(prof, boards, BLOCKS, CHANNELS,
-                                 "azg::conv_tower<128,64,4,1,8> (persistent residual tower: 12 fused 3x3 conv + "
-                                 "BN + residual + ReLU layers per launch; launches inside the self-play run)",
-                                 "azg::conv3x3_halo<128,*> (fused 3x3 conv + BN + residual + ReLU)")
+    roof = roofline_from_profile(prof, boards, BLOCKS, CHANNELS, tower_knames(CHANNELS, BLOCKS))
     nn_ms = sum(v[0] for v in prof.values())
     return {
         "boards": n_boards, "seconds": dt_max, "rounds": int(rounds_max),
@@ -436,9 +451,7 @@ def forward_leg(model, args, rank, world, dist, dev, local, blocks=BLOCKS, ch=CH
     eng.check_status()
     assert torch.isfinite(probs).all() and torch.isfinite(values).all()
     (elapsed,) = reduce_(dist, dev, [elapsed], op="max")
-    roof = roofline_from_profile(prof, boards, blocks, ch,
-                                 f"azg::conv_tower<{ch},*> (persistent residual tower, {2 * blocks} convs per launch)",
-                                 f"azg::conv3x3_halo<{ch},*>")
+    roof = roofline_from_profile(prof, boards, blocks, ch, tower_knames(ch, blocks))
     return {"config": f"{blocks}x{ch} ResNet, batch {B}/GPU eval forward (BN running stats, softmax + tanh), "
                       f"inputs resident in HBM",
             "boards_per_s": round(B * steps * world / elapsed, 1), "ms_per_step": round(elapsed / steps * 1e3, 4),
@@ -515,8 +528,7 @@ def pente_leg(args, rank, world, dist, dev, local):
             "game_length_rank0": {"mean": round(float(lengths.mean()), 1), "min": int(lengths.min()),
                                   "max": int(lengths.max())},
             "mean_batch_rank0": round(sp.boards / max(sp.forwards, 1), 1),
-            "roofline": roofline_from_profile(prof, boards, nb, ch, f"azg::conv_tower<{ch},*>",
-                                              f"azg::conv3x3_halo<{ch},*>")}
+            "roofline": roofline_from_profile(prof, boards, nb, ch, tower_knames(ch, nb))}
     del m
     torch.cuda.empty_cache()
     return out

@@ -126,7 +126,9 @@ enum {
     AZG_PROF_TRAIN_CONV = 3, /* train-mode 3x3 conv fwd + dgrad        */
     AZG_PROF_TRAIN_WGRAD = 4,
     AZG_PROF_TRAIN_OTHER = 5,
-    AZG_PROF_TOWER = 6,      /* persistent residual tower (all 2*NB convs, one launch) */
+    AZG_PROF_TOWER = 6,      /* persistent residual tower (all 2*NB convs, one launch),
+                                64x64 / 128x64 tiles, 2-4 workgroups per CU          */
+    AZG_PROF_TOWER_WIDE = 7, /* the same with 16-wave 128x128 tiles, 1 workgroup per CU */
     AZG_PROF_NCLASS = 8
 };
 int32_t azg_pv_profile_enable(azg_pv* h, int32_t enable);
@@ -148,7 +150,7 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          (shape from key 6), 2 (default) chosen per (C, blocks, batch bucket) by
  *          timing every variant on first use -- all bitwise identical;
  *   key 6: persistent-tower tile shape for key 5 = 1 (8: 128x64 / 8 waves, default;
- *          5: 64x64 / 4 waves);
+ *          5: 64x64 / 4 waves; 10: 128x128 / 16 waves, one workgroup per CU, C = 128);
  *   keys 3, 7, 8: timing-only ablation switches (results invalid while set);
  *   key 10: tile-body variant of the C=128 128x64 persistent tower (0 = default;
  *          1..5 = swizzle / prefetch / LDS-DMA staging variants for A/B timing, all
@@ -166,9 +168,9 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          tiles, run back to back by the claiming workgroup, default: the second
  *          tile's halo rows hit the XCD's L2, +2 % at B = 512 and 4096, measured;
  *          0 = one 128x64 tile per claim); bitwise identical results;
- *   key 18: train write-through stores (bits: 1 conv outputs, 2 BN-apply outputs,
- *          4 weight-grad slabs; default 7): no dirty L2 lines at the kernel
- *          boundaries; bitwise identical;
+ *   key 18: train write-through stores (bits: 1 conv outputs -- study build only,
+ *          2 BN-apply outputs, 4 weight-grad slabs; default 7): no dirty L2 lines at
+ *          the kernel boundaries; bitwise identical;
  *   key 19: study build only: skip train BN kernels (timing, results invalid);
  *   key 21: per-layer 128x64 conv: the last partial round of workgroups runs as a
  *          second launch of 64x64 tiles (1, default) or not (0); bitwise identical;
@@ -182,10 +184,13 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *   key 24: train BN finalize run by the last workgroup of the conv producing the
  *          layer's partials (1, default) or by separate finalize kernels (0); one
  *          shared fp64 reduction order, bitwise identical;
- *   key 31: persistent tower: dependent halo / residual reads are agent-coherent
- *          loads and the dependency wait has no L2-invalidating acquire (1,
- *          default; 1.75x vs 2.08x algorithmic HBM bytes, +2.5 %) or an acquire
- *          (0); bitwise identical;
+ *   key 25: train convs: operand addressing through buffer resources (32,
+ *          default) or 64-bit pointers (0); bitwise identical;
+ *   key 31: study build only: the 64x64 / 128x64 towers with sc1 dependent loads
+ *          and no acquire (two or more workgroups per CU: outside the microarch
+ *          guide's measured envelope; the product uses the acquire there and the
+ *          sc1 form only for the one-workgroup-per-CU 16-wave tile); returns 0 in
+ *          the product library;
  *   key 14: persistent-tower dependency spin bound (tests only: 0 makes every
  *          dependency wait time out at once, exercising the error path; -1
  *          restores the default).

@@ -1,9 +1,9 @@
-"""Eval forward of the 6x128 net at one batch with the residual convs forced to
-per-layer launches (key 5 = 0) or the persistent tower (key 5 = 1): the probe the
-PMC passes for the self-play roofline's traffic run on (the self-play forwards are
-dominated by per-layer conv3x3_halo<128,64,4,1,8> launches at B ~ 4096).
+"""Eval forward of the 6x128 (or --blocks x --channels) net at one batch with the
+residual convs forced to per-layer launches (key 5 = 0) or the persistent tower
+(key 5 = 1, tile shape --tower-shape: 10 = 16-wave 128x128, 8 = 128x64, 5 = 64x64):
+the probe the PMC passes for the rooflines' traffic run on.
 
-    python scripts/conv_probe.py --batch 4096 --tower 0 --steps 3
+    python scripts/conv_probe.py --batch 3456 --tower 1 --tower-shape 10 --steps 3
 """
 import argparse
 import json
@@ -23,16 +23,24 @@ def main():
     ap.add_argument("--tower", type=int, default=0)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--shape", type=int, default=-1, help="force the per-layer tile shape (key 0)")
+    ap.add_argument("--tower-shape", type=int, default=8, help="persistent tower tile shape (key 6)")
+    ap.add_argument("--var", type=int, default=0, help="study build: tower tile-body variant (key 10)")
+    ap.add_argument("--coh", type=int, default=0, help="study build: round-2 sc1 tower hand-off at 2 WG/CU (key 31)")
+    ap.add_argument("--blocks", type=int, default=6)
+    ap.add_argument("--channels", type=int, default=128)
     args = ap.parse_args()
     import _native
     lib = _native.load_library()
     lib.azg_pv_set_tuning(5, args.tower)
+    lib.azg_pv_set_tuning(6, args.tower_shape)
     lib.azg_pv_set_tuning(0, args.shape)
+    lib.azg_pv_set_tuning(10, args.var)
+    lib.azg_pv_set_tuning(31, args.coh)
     from network import PyTorchModel
     from synth import synth_encoded
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    m = PyTorchModel(board_size=15, device=str(dev), n_res_blocks=6, channels=128)
+    m = PyTorchModel(board_size=15, device=str(dev), n_res_blocks=args.blocks, channels=args.channels)
     m.net.eval()
     B = args.batch
     x = torch.from_numpy(synth_encoded(B, seed=3)).to(dev)
@@ -50,12 +58,14 @@ def main():
     prof = eng.profile_read()
     eng.profile_enable(False)
     eng.check_status()
-    flop = 2 * 225 * 128 * 9 * 128 * B
-    out = {"batch": B, "tower": args.tower, "ms_per_forward": round(dt / args.steps * 1e3, 3)}
+    ch = args.channels
+    flop = 2 * 225 * ch * 9 * ch * B
+    out = {"net": f"{args.blocks}x{ch}", "batch": B, "tower": args.tower, "tower_shape": args.tower_shape,
+           "ms_per_forward": round(dt / args.steps * 1e3, 3)}
     for k, (ms, n) in prof.items():
         out[k] = {"launches": n, "avg_us": round(ms / n * 1e3, 1)}
-        if k in ("conv3x3", "tower"):
-            per = flop * (12 if k == "tower" else 1)
+        if k in ("conv3x3", "tower", "tower16"):
+            per = flop * (2 * args.blocks if k.startswith("tower") else 1)
             out[k]["mfma_frac"] = round(per / (ms / n / 1e3) / 157.3e12, 4)
     print(json.dumps(out), flush=True)
 

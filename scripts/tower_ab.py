@@ -70,7 +70,7 @@ def main():
                 wall = (time.perf_counter() - t0) / args.steps
                 prof = eng.profile_read()
                 eng.profile_enable(False)
-                dev = (prof.get("tower", (0.0, 0))[0] + prof.get("conv3x3", (0.0, 0))[0]) / args.steps
+                dev = sum(prof.get(c, (0.0, 0))[0] for c in ("tower", "tower16", "conv3x3")) / args.steps
                 best_dev = dev if best_dev is None else min(best_dev, dev)
                 best_wall = wall if best_wall is None else min(best_wall, wall)
             row[name] = {"tower_ms": round(best_dev, 4), "frac": round(flop / (best_dev * 1e-3) / 157.3e12, 4),

@@ -81,7 +81,7 @@ def main():
                     eng.forward(x)
                 prof = eng.profile_read()
                 eng.profile_enable(False)
-                ms = prof.get("tower", prof.get("conv3x3", (0.0, 0)))[0]
+                ms = sum(prof.get(c, (0.0, 0))[0] for c in ("tower", "tower16", "conv3x3"))
                 res[name].append(ms / args.steps)
         eng.check_status()
         flop = 12 * 2 * 225 * 128 * 9 * 128 * B

@@ -48,7 +48,7 @@ def main():
                 torch.cuda.synchronize()
                 prof = eng.profile_read()
                 eng.profile_enable(False)
-                ms = sum(prof.get(c, (0.0, 0))[0] for c in ("tower", "conv3x3")) / args.steps
+                ms = sum(prof.get(c, (0.0, 0))[0] for c in ("tower", "tower16", "conv3x3")) / args.steps
                 res[name].append(ms)
         flop = 12 * 2 * 225 * 128 * 9 * 128 * B
         print(json.dumps({"batch": B, **{k: {"ms": round(min(v), 4), "frac": round(flop / (min(v) / 1e3) / 157.3e12, 4)}

@@ -6,7 +6,8 @@
   * graph: backward + clip/Adam captured once in a HIP graph and replayed (fixed step
     count inside, timing only) -- the device-bound floor without launch gaps;
   * key 24 = 0 / 1: BN finalize in separate kernels vs fused into the producing conv's
-    last workgroup (acquire hand-off).
+    last workgroup (acquire hand-off); key 25 = 32 / 0: train convs with buffer-
+    resource addressing vs 64-bit pointers.
 
     python scripts/train_r3_probe.py [--steps 30]
 """
@@ -54,18 +55,22 @@ def main():
     for _ in range(5):
         step()
     torch.cuda.synchronize()
-    for key24 in (1, 0, 1):
-        lib.azg_pv_set_tuning(24, key24)
-        for _ in range(3):
-            step()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(K):
-            step()
-        torch.cuda.synchronize()
-        ms = (time.perf_counter() - t0) / K * 1e3
-        out.setdefault(f"pipelined_ms_key24_{key24}", []).append(round(ms, 4))
+    for rnd in range(2):
+        for key25 in (32, 0):
+            for key24 in (1, 0):
+                lib.azg_pv_set_tuning(24, key24)
+                lib.azg_pv_set_tuning(25, key25)
+                for _ in range(3):
+                    step()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(K):
+                    step()
+                torch.cuda.synchronize()
+                ms = (time.perf_counter() - t0) / K * 1e3
+                out.setdefault(f"pipelined_ms_key24_{key24}_key25_{key25}", []).append(round(ms, 4))
     lib.azg_pv_set_tuning(24, 1)
+    lib.azg_pv_set_tuning(25, 32)
     if hasattr(torch.cuda, "_sleep"):
         torch.cuda.synchronize()
         torch.cuda._sleep(int(2.4e9 * 0.5))        # ~0.5 s spin ahead of the queue
@@ -106,7 +111,7 @@ def main():
             out.setdefault("graph_ms", []).append(round((time.perf_counter() - t0) / K * 1e3, 4))
     except Exception as e:  # noqa: BLE001 -- a probe: report, do not fail the run
         out["graph_error"] = repr(e)[:300]
-    best = min(min(out.get("pipelined_ms_key24_1", [1e9])), min(out.get("pipelined_ms_key24_0", [1e9])))
+    best = min(min(v) for k, v in out.items() if k.startswith("pipelined_ms"))
     out["best_pipelined_mfma_frac"] = round(flop / (best * 1e-3) / 157.3e12, 4)
     print(json.dumps(out), flush=True)
 

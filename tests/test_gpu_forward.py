@@ -236,9 +236,11 @@ def test_persistent_tower_bitwise_equals_per_layer_launches(blocks, ch, batches)
                     lib.azg_pv_set_tuning(6, shape)
                     prev_var = lib.azg_pv_set_tuning(10, var)
                     prev_coh = lib.azg_pv_set_tuning(31, coh)
-                    p1, v1, l1 = eng.forward(x, want_logits=True)
-                    lib.azg_pv_set_tuning(31, prev_coh)
-                    lib.azg_pv_set_tuning(10, prev_var)
+                    try:
+                        p1, v1, l1 = eng.forward(x, want_logits=True)
+                    finally:
+                        lib.azg_pv_set_tuning(31, prev_coh)
+                        lib.azg_pv_set_tuning(10, prev_var)
                     assert lib.azg_pv_tower_status(eng.h, stream) == 0
                     assert torch.equal(l0, l1), ("var", shape, var, coh, B, float((l0 - l1).abs().max()))
     finally:
