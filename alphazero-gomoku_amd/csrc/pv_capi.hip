@@ -455,13 +455,16 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
 
 // Tower variant per (C, blocks, batch bucket): g_tower_mode 0 = per-layer launches,
 // 1 = persistent tower with shape g_tower_shape, 2 = timed on first use of the
-// bucket (stem + tower, every variant, best of 2 after a warm pass).  Variants: 0
+// bucket (stem + tower, every variant, best of 2 after a warm pass).  Candidates: 0
 // per-layer launches; 5 / 8 the tower with 64x64 / 128x64 tiles (2-4 workgroups per
-// CU, acquire hand-off); 10 (C = 128) the tower with 16-wave 128x128 tiles (one
-// workgroup per CU, sc1-load hand-off).  The preferred variant (10 where it exists,
-// else 8) is kept for batches >= 128 unless another is > 2 % faster, so timing noise
-// cannot flip near-equal choices.  While the stream is being captured the untuned
-// default is used.  All variants are bitwise identical.
+// CU, acquire hand-off, buffer-resource addressing).  The 128x64 tower is preferred
+// for batches >= 128 (round 3, scripts/tower_r3_ab.py: 87.0 / 90.2 / 91.0 / 91.2 % of
+// peak at 512 / 1024 / 2048 / 4096 boards vs 80.7 / 84.1 / 86.4 / 87.8 % per-layer) and
+// kept unless another candidate is > 2 % faster, so timing noise cannot flip
+// near-equal choices.  Shape 10 (16-wave 128x128 tiles, one workgroup per CU: 1.30x
+// algorithmic HBM bytes instead of 1.76x) is measured slower at every batch (83.6 %)
+// and is not a candidate; key 6 = 10 forces it.  While the stream is being captured
+// the untuned default is used.  All variants are bitwise identical.
 static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, const int8_t* boards,
                          const int8_t* players)
 {
@@ -474,15 +477,14 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
     const auto key = std::make_tuple(h->C, h->NB, bucket);
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
-    const int wide = h->C == 128 ? 10 : 8;   // preferred tower shape
-    const int fallback = batch >= 128 ? wide : 0;
+    const int fallback = batch >= 128 ? 8 : 0;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return fallback;
     const bool prof = h->prof_on;
     h->prof_on = false;
-    const int cand[4] = {0, 5, 8, 10};
-    const int ncand = h->C == 128 ? 4 : 3;
-    float best_ms[4] = {1e30f, 1e30f, 1e30f, 1e30f};
+    const int cand[3] = {0, 5, 8};
+    const int ncand = 3;
+    float best_ms[3] = {1e30f, 1e30f, 1e30f};
     hipEvent_t e0, e1;
     int choice = fallback;
     if (hipEventCreate(&e0) == hipSuccess) {
@@ -501,10 +503,7 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
                 int b = 0;
                 for (int c = 1; c < ncand; ++c)
                     if (best_ms[c] < best_ms[b]) b = c;
-                if (batch >= 128) {
-                    const int pref = wide == 10 ? 3 : 2;
-                    if (best_ms[pref] <= 1.02f * best_ms[b]) b = pref;
-                }
+                if (batch >= 128 && best_ms[2] <= 1.02f * best_ms[b]) b = 2;   // the 128x64 tower
                 choice = cand[b];
             }
             (void)hipEventDestroy(e1);

@@ -220,25 +220,31 @@ __global__ __launch_bounds__(64 * NW_, 2) void conv3x3_halo(
 }
 // Train-step conv (forward z = conv(a), dgrad = conv(dZ, flipped W) [+ resid]) with
 // the BatchNorm partial sums fused into the epilogue (pv_halo.h XE_STATS / XE_BNBWD):
-// one fixed tile shape (128 x 64, 8 waves; the shape autotuning picked at B = 128)
-// so the partials are per 128-row M tile.  Same XCD-aware tile order as above.
-// WT: outputs stored write-through (no dirty L2 lines at the kernel boundary).
-// PRO (forward only): the input is the previous layer's raw output z and its BN +
-// ReLU (+ residual) is applied in the halo staging (pv_halo.h ProX).
-template <int C, int EPI, int XE, bool WT, int PRO = PRO_NONE, int VAR = 32>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv3x3_train(
+// 128-row M tiles (the partials are per 128-row tile), either 128 x 64 with 8 waves
+// (two workgroups per CU; NWT 8) or 128 x 128 with 16 waves (one workgroup per CU, the
+// halo staged once for all 128 output channels; NWT 16, C = 128).  Same XCD-aware tile
+// order as above.  WT: outputs stored write-through (no dirty L2 lines at the kernel
+// boundary).  PRO (forward only): the input is the previous layer's raw output z and
+// its BN + ReLU (+ residual) is applied in the halo staging (pv_halo.h ProX).
+template <int C, int NWT>
+struct TrainTile {
+    static constexpr int BN = NWT >= 16 ? 128 : 64;
+    using T = ConvTile<C, BN, 4, 1, NWT>;
+};
+template <int C, int EPI, int XE, bool WT, int PRO = PRO_NONE, int VAR = 32, int NWT = 8>
+__global__ __launch_bounds__(64 * NWT) __attribute__((amdgpu_waves_per_eu(4))) void conv3x3_train(
     const float* __restrict__ in, const float* __restrict__ wp, const float* __restrict__ resid,
     float* __restrict__ out, int M, EpiX ex, ProX px, FinX fx)
 {
-    using T = ConvTile<C, 64, 4, 1, 8>;
+    using T = typename TrainTile<C, NWT>::T;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int NTN = C / T::BN;
     const int L = blockIdx.x, nt = gridDim.x;
     const int xcd = L & 7, q8 = nt >> 3, r8 = nt & 7;
     const int t = xcd * q8 + min(xcd, r8) + (L >> 3);
-    halo_tile<C, 64, 4, 1, 8, EPI, WT, 0, VAR, XE, PRO>(in, wp, nullptr, nullptr, resid, out,
-                                                     wt_rsrc(out, padded_bytes(M, C)), M, (t / NTN) * T::BM,
-                                                     (t % NTN) * T::BN, smem, ex, px, fx);
+    halo_tile<C, T::BN, 4, 1, NWT, EPI, WT, 0, VAR, XE, PRO>(in, wp, nullptr, nullptr, resid, out,
+                                                          wt_rsrc(out, padded_bytes(M, C)), M, (t / NTN) * T::BM,
+                                                          (t % NTN) * T::BN, smem, ex, px, fx);
 }
 
 // Stem conv 3->C (K = 27) on the VALU: 0.2 % of the forward FLOPs.  One
@@ -786,22 +792,24 @@ int g_train_wt = 7;   // key 18 bits: 1 train conv outputs, 2 BN apply outputs, 
 
 int g_train_var = 32;  // key 25: halo_tile VAR of the train convs (32 buffer-resource addressing, default; 0 64-bit pointers)
 
-template <int C, int EPI, int XE, int PRO, bool WT, int VAR>
+int g_train_tile = 8;  // key 26: train conv tile (8: 128x64 / 8 waves; 16: 128x128 / 16 waves, C = 128)
+
+template <int C, int EPI, int XE, int PRO, bool WT, int VAR, int NWT>
 static hipError_t launch_train_v(const float* in, const float* wp, const float* resid, float* out, int M,
                                  const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st)
 {
-    using T = ConvTile<C, 64, 4, 1, 8>;
-    constexpr int lds = halo_lds_bytes<C, 64, 4, 1, 8, 0, PRO>();
+    using T = typename TrainTile<C, NWT>::T;
+    constexpr int lds = halo_lds_bytes<C, T::BN, 4, 1, NWT, 0, PRO>();
     static bool attr_done = false;
     if (!attr_done) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, WT, PRO, VAR>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, WT, PRO, VAR, NWT>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
         attr_done = true;
     }
     dim3 grid(((M + T::BM - 1) / T::BM) * (C / T::BN));
-    hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, WT, PRO, VAR>), grid, dim3(T::NT), lds, st, in, wp, resid, out, M,
-                       ex, px, fx);
+    hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, WT, PRO, VAR, NWT>), grid, dim3(T::NT), lds, st, in, wp, resid,
+                       out, M, ex, px, fx);
     return hipGetLastError();
 }
 
@@ -810,10 +818,13 @@ static hipError_t launch_train_t(const float* in, const float* wp, const float* 
                                  const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st)
 {
 #ifdef AZG_AB_STUDIES   // plain (write-back) output stores: A/B only
-    if (!(g_train_wt & 1)) return launch_train_v<C, EPI, XE, PRO, false, 32>(in, wp, resid, out, M, ex, px, fx, st);
+    if (!(g_train_wt & 1)) return launch_train_v<C, EPI, XE, PRO, false, 32, 8>(in, wp, resid, out, M, ex, px, fx, st);
 #endif
-    if (g_train_var == 0) return launch_train_v<C, EPI, XE, PRO, true, 0>(in, wp, resid, out, M, ex, px, fx, st);
-    return launch_train_v<C, EPI, XE, PRO, true, 32>(in, wp, resid, out, M, ex, px, fx, st);
+    if constexpr (C == 128) {
+        if (g_train_tile == 16) return launch_train_v<C, EPI, XE, PRO, true, 32, 16>(in, wp, resid, out, M, ex, px, fx, st);
+    }
+    if (g_train_var == 0) return launch_train_v<C, EPI, XE, PRO, true, 0, 8>(in, wp, resid, out, M, ex, px, fx, st);
+    return launch_train_v<C, EPI, XE, PRO, true, 32, 8>(in, wp, resid, out, M, ex, px, fx, st);
 }
 
 // Train conv with fused BN partials: (EPI_RAW, XE_STATS) forward, optionally with
@@ -966,6 +977,21 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     if (key == 25) {  // train convs: halo_tile VAR (32 buffer-resource addressing, default; 0 64-bit pointers); bitwise identical
         const int prev = azg::g_train_var;
         if (value == 0 || value == 32) azg::g_train_var = value;
+        return prev;
+    }
+    if (key == 28) {  // train head chain: 1 fused (3 launches, default), 0 the 18-launch chain (A/B; same math, other sum orders)
+        const int prev = azg::g_train_fuse_heads;
+        if (value == 0 || value == 1) azg::g_train_fuse_heads = value;
+        return prev;
+    }
+    if (key == 27) {  // train wgrad split-K count (0 automatic; 8..64, multiple of 8); bitwise NOT identical across values
+        const int prev = azg::g_wgrad_splits;
+        if (value == 0 || (value >= 8 && value <= 64 && value % 8 == 0)) azg::g_wgrad_splits = value;
+        return prev;
+    }
+    if (key == 26) {  // train conv tile: 8 (128x64, 8 waves, default) or 16 (128x128, 16 waves, C = 128); bitwise identical
+        const int prev = azg::g_train_tile;
+        if (value == 8 || value == 16) azg::g_train_tile = value;
         return prev;
     }
     if (key == 23) {  // train: BN applies folded into the next conv's halo staging (1, default) or separate (0)

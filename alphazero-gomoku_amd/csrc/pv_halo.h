@@ -198,21 +198,23 @@ __device__ __forceinline__ void bn_fin_out(double v0, double v1, int M, int c, c
 // 8 waves x 64 lanes: wave w holds tile class w of channel c (lane); the classes are
 // combined through LDS in the fixed order above by wave 0, which writes the results
 // (shared by the fused finalize of halo_epilogue and the stand-alone kernels).
-// Every thread of the 512-thread workgroup must call it (barrier).
+// Every thread of the workgroup must call it (barrier).  A 16-wave workgroup runs two
+// such groups side by side (waves 8-15: the next 64 channels, `grp` 1): same order.
 template <bool FWD>
 __device__ __forceinline__ void bn_fin_combine8(double v0, double v1, double* red, int M, int c, bool valid,
                                                 const FinX& f)
 {
-    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-    red[wv * 64 + ln] = v0;
-    red[512 + wv * 64 + ln] = v1;
+    const int wv = (threadIdx.x >> 6) & 7, ln = threadIdx.x & 63, grp = threadIdx.x >> 9;
+    double* r0 = red + grp * 1024;
+    r0[wv * 64 + ln] = v0;
+    r0[512 + wv * 64 + ln] = v1;
     __syncthreads();
     if (wv == 0 && valid) {
         auto comb = [&](const double* r) {
             return ((r[0 * 64 + ln] + r[4 * 64 + ln]) + (r[2 * 64 + ln] + r[6 * 64 + ln])) +
                    ((r[1 * 64 + ln] + r[5 * 64 + ln]) + (r[3 * 64 + ln] + r[7 * 64 + ln]));
         };
-        bn_fin_out<FWD>(comb(red), comb(red + 512), M, c, f);
+        bn_fin_out<FWD>(comb(r0), comb(r0 + 512), M, c, f);
     }
 }
 
@@ -437,12 +439,15 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                 // wave w sums tile class w % 8 of channels n0 + lane (coalesced rows of
                 // the [tile][C] partials), the classes combine through LDS in the order
                 // of bn_fin_combine8: bitwise equal to the stand-alone finalize
-                static_assert(T::NW == 8 && BN == 64, "fused finalize: 8 waves x 64 channels");
-                double* red = (double*)smem;   // [2][8][64]
-                const int wv = tid >> 6, ln = tid & 63;
+                // (16 waves x 128 channels: waves 8-15 do channels n0 + 64 + lane)
+                static_assert((T::NW == 8 && BN == 64) || (T::NW == 16 && BN == 128),
+                              "fused finalize: 8 waves per 64 channels");
+                static_assert(2 * 1024 * 8 <= BM * ELD * 4, "fused finalize: LDS for the combine");
+                double* red = (double*)smem;   // [groups][2][8][64]
+                const int wv = (tid >> 6) & 7, ln = tid & 63, ch = n0 + (tid >> 9) * 64 + ln;
                 double v0, v1;
-                bn_fin_accum<XE == XE_STATS, false>(ex.pa, ex.pb, C, ntm, BM, M, n0 + ln, wv, v0, v1);
-                bn_fin_combine8<XE == XE_STATS>(v0, v1, red, M, n0 + ln, true, fx);
+                bn_fin_accum<XE == XE_STATS, false>(ex.pa, ex.pb, C, ntm, BM, M, ch, wv, v0, v1);
+                bn_fin_combine8<XE == XE_STATS>(v0, v1, red, M, ch, true, fx);
                 if (tid == 0) __hip_atomic_store(fx.cnt + n0 / BN, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }

@@ -47,9 +47,11 @@ extern int g_tower_var;
 extern int g_wgrad_serial;
 extern int g_train_fuse_apply;
 extern int g_train_fuse_fin;
+extern int g_train_fuse_heads;
 extern int g_train_skip;
 extern int g_wgrad_bk;
 extern int g_wgrad_kernel;
+extern int g_wgrad_splits;
 extern int g_train_wt;
 constexpr int kTowerMaxBlocks = 32;
 int conv_batch_bucket(int M);

@@ -16,6 +16,7 @@
 //    grads *= coef (always).
 #include "pv_internal.h"
 #include "pv_halo.h"
+#include "pv_train_heads.h"
 
 #include <cmath>
 #include <cstdlib>
@@ -54,6 +55,11 @@ struct TrainWS {
     float *dlogits = nullptr, *dfp = nullptr, *dfv = nullptr, *dhv = nullptr, *dzh = nullptr, *lossb = nullptr;
     float *lpre = nullptr, *hpre = nullptr, *hbw = nullptr;   // FC pre-activations, head BN bwd coefficients
     double* hspart = nullptr;                                 // head BN (channel, chunk) partials
+    // fused head chain (pv_train_heads.hip): per-workgroup partials + arrival counters
+    double* hsp1 = nullptr;      // head_proj_stats_kernel [groups][6]
+    double* hpd = nullptr;       // head_board_kernel [groups][head_board_pd()]
+    float* hpf = nullptr;        // head_board_kernel [groups][head_board_pf()]
+    unsigned* hcnt = nullptr;    // [2] arrival counters (0 between launches)
     // optimizer
     double* npart = nullptr;     // grad sq-sum partials
     float* scal = nullptr;       // [0] total norm, [1] clip coef
@@ -885,6 +891,15 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
         float* fc = nullptr;
         A(fc, 64, true);
         w->fincnt = (unsigned*)fc;
+        float* hc = nullptr;
+        A(hc, 16, true);
+        w->hcnt = (unsigned*)hc;
+        float* t = nullptr;
+        A(t, (size_t)head_proj_stats_groups(M) * 6 * 2, false);
+        w->hsp1 = (double*)t;
+        A(t, (size_t)head_board_groups(cap) * head_board_pd() * 2, false);
+        w->hpd = (double*)t;
+        A(w->hpf, (size_t)head_board_groups(cap) * head_board_pf(), false);
     }
     if (getenv("AZG_DEBUG_SNAP")) {
         w->snap.assign(NB + 1, nullptr);
@@ -907,6 +922,7 @@ int g_wgrad_serial = 0;   // 1: conv weight grads on the caller's stream (A/B ti
 int g_train_fuse_apply = 1;   // key 23: 1 BN applies folded into the next conv's staging; 0 separate passes
 int g_train_fuse_fin = 1;     // key 24: 1 BN finalize by the last workgroup of the producing conv; 0 separate kernels
 int g_train_skip = 0;     // study build only (key 19): skip BN kernels to time them in situ (results invalid)
+int g_train_fuse_heads = 1;   // key 28: 1 fused head chain (pv_train_heads.hip, 3 launches); 0 the 18-launch chain
 
 template <int C>
 static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, const float* zs, int B,
@@ -1067,6 +1083,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
 #define R(x) if ((r = (x))) return r
 
     // ---- forward (train-mode BN) ----
+    bool last_apply = false;   // the last block's BN apply is left to the fused head kernel
+    struct LastApply { const float* z; const float* res; int layer; float* out; } lastp{nullptr, nullptr, 0, nullptr};
     AZG_CK(launch_stem(C, EPI_RAW, x, h->wstem, nullptr, nullptr, w->z0, B, st), "train: stem");
     R(stats(w->z0, h->bn_stem));
     const float* X = w->a0;
@@ -1099,7 +1117,12 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             pend = Pend{w->z2[i], h->bn_blk[i].second, X, w->xo[i]};
             X = w->xo[i];
         }
-        R(apply(pend.z, pend.res, pend.layer, pend.out));
+        if (g_train_fuse_heads && pend.res) {
+            last_apply = true;   // the head kernel applies bn2 + residual + ReLU of the last block
+            lastp = {pend.z, pend.res, pend.layer, pend.out};
+        } else {
+            R(apply(pend.z, pend.res, pend.layer, pend.out));
+        }
     } else {
         R(apply(w->z0, nullptr, h->bn_stem, w->a0));
         for (int i = 0; i < NB; ++i) {
@@ -1116,7 +1139,107 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         }
     }
     // ---- heads forward + loss + backward to the tower output ----
-    {
+    const int hntile = (M + HROWS - 1) / HROWS;
+    if (g_train_fuse_heads) {
+        // three launches (pv_train_heads.hip) + the fc weight-grad GEMM and the head
+        // 1x1 weight-grad reduction
+        int pr = prof_begin(h, AZG_PROF_TRAIN_OTHER, st);
+        const int ho = bd[h->bn_pol].out_off;   // policy ch0, ch1, value: contiguous
+        HeadStatsArgs hs{};
+        hs.z = last_apply ? lastp.z : X;
+        if (last_apply) {
+            const int o = bd[lastp.layer].out_off;
+            hs.res = lastp.res;
+            hs.scale = w->bscale + o;
+            hs.shift = w->bshift + o;
+            hs.aout = lastp.out;
+        }
+        hs.wpc = P + h->poff[h->t_pc_w];
+        hs.wvc = P + h->poff[h->t_vc_w];
+        hs.zh = w->zh;
+        hs.part = w->hsp1;
+        hs.cnt = w->hcnt;
+        hs.M = M;
+        hs.desc = bdd;
+        hs.pol_layer = h->bn_pol;
+        hs.val_layer = h->bn_val;
+        hs.params = P;
+        hs.stats = h->bn;
+        hs.bmean = w->bmean;
+        hs.binv = w->binv;
+        hs.bscale = w->bscale;
+        hs.bshift = w->bshift;
+        hs.nbt = h->nbt;
+        hs.nbn = (int)h->bn_desc.size();
+        AZG_CK(launch_head_proj_stats(C, last_apply, hs, st), "train: head_proj_stats");
+        HeadBoardArgs hb{};
+        hb.zh = w->zh;
+        hb.hmean = w->bmean + ho;
+        hb.hscale = w->bscale + ho;
+        hb.hshift = w->bshift + ho;
+        hb.hinv = w->binv + ho;
+        hb.wpf = P + h->poff[h->t_pfc_w];
+        hb.bpf = P + h->poff[h->t_pfc_b];
+        hb.wv1 = P + h->poff[h->t_vfc1_w];
+        hb.bv1 = P + h->poff[h->t_vfc1_b];
+        hb.wv2 = P + h->poff[h->t_vfc2_w];
+        hb.bv2 = P + h->poff[h->t_vfc2_b];
+        hb.pis = pis;
+        hb.zs = zs;
+        hb.fp = w->fp;
+        hb.fv = w->fv;
+        hb.hv = w->hv;
+        hb.dlogits = w->dlogits;
+        hb.dhv = w->dhv;
+        hb.dfp = w->dfp;
+        hb.dfv = w->dfv;
+        hb.pd = w->hpd;
+        hb.pf = w->hpf;
+        hb.cnt = w->hcnt + 1;
+        hb.B = B;
+        hb.desc = bdd;
+        hb.pol_layer = h->bn_pol;
+        hb.val_layer = h->bn_val;
+        hb.params = P;
+        hb.grads = G;
+        hb.hb = w->hbw;
+        hb.g_pfb = G + h->poff[h->t_pfc_b];
+        hb.g_v1b = G + h->poff[h->t_vfc1_b];
+        hb.g_v2w = G + h->poff[h->t_vfc2_w];
+        hb.g_v2b = G + h->poff[h->t_vfc2_b];
+        hb.losses = losses;
+        AZG_CK(launch_head_board(hb, st), "train: head_board");
+        {   // weight grads: dWpf = dlogits^T . fp, dWv1 = dhv^T . fv
+            GemmProb a{w->dlogits, 1, ACTIONS, w->fp, 2 * PIX, 1, G + h->poff[h->t_pfc_w], 2 * PIX, 1, nullptr, 0, 0,
+                       ACTIONS, 2 * PIX, B};
+            GemmProb b{w->dhv, 1, VHID, w->fv, PIX, 1, G + h->poff[h->t_vfc1_w], PIX, 1, nullptr, 0, 0, VHID, PIX, B};
+            AZG_CK(launch_small_gemm(a, &b, st), "train: head fc wgrad");
+        }
+        HeadBwdArgs hw{};
+        hw.act = X;
+        hw.zh = w->zh;
+        hw.dfp = w->dfp;
+        hw.dfv = w->dfv;
+        hw.hmean = w->bmean + ho;
+        hw.hb = w->hbw;
+        hw.wpc = P + h->poff[h->t_pc_w];
+        hw.wvc = P + h->poff[h->t_vc_w];
+        hw.gx = w->gX;
+        hw.hpart = w->hpart;
+        if (NB > 0) {
+            hw.z2 = w->z2[NB - 1];
+            hw.mean2 = w->bmean + bd[h->bn_blk[NB - 1].second].out_off;
+            hw.pa = w->part_a;
+            hw.pb = w->part_b;
+        }
+        hw.M = M;
+        AZG_CK(launch_heads_bwd_fused(C, NB > 0, hw, st), "train: heads_bwd_fused");
+        // policy_conv.weight [2][C] then value_conv.weight [C]: partial layout [t][3][C]
+        hipLaunchKernelGGL(reduce_partials_kernel, dim3((3 * C + 15) / 16), dim3(256), 0, st, w->hpart, hntile, 3 * C,
+                           G + h->poff[h->t_pc_w], G + h->poff[h->t_vc_w], 2 * C, 0, C);
+        AZG_CK(hipGetLastError(), "train: heads proj wgrad");
+        prof_end(h, pr, st);
+    } else {
         int pr = prof_begin(h, AZG_PROF_TRAIN_OTHER, st);
         AZG_CK(launch_heads_project(C, false, X, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], nullptr, nullptr,
                                     w->zh, M, st),
@@ -1190,7 +1313,9 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     // epilogue of the dgrad conv that produces its gradient (XE_BNBWD, per 128-row
     // tile); the last block's gradient comes from the heads (separate reduction).
     int bwd_nt = ntt;
-    if (NB > 0) {
+    if (NB > 0 && g_train_fuse_heads) {
+        bwd_nt = hntile;   // S dy, S (z - mean) dy per 128-row tile from heads_bwd_fused_kernel
+    } else if (NB > 0) {
         R(bwd_reduce(w->gX, w->xo[NB - 1], w->z2[NB - 1], h->bn_blk[NB - 1].second));
         bwd_nt = ntile;
     }

@@ -1,0 +1,86 @@
+// Argument blocks and launchers of the fused train-step head chain
+// (pv_train_heads.hip), shared with the train-step orchestration (pv_train.hip).
+#pragma once
+#include "pv_internal.h"
+
+namespace azg {
+
+struct HeadStatsArgs {
+    const float* z;        // APPLY: last block's raw bn2 input z2; else the tower output
+    const float* res;      // APPLY: residual (block input)
+    const float* scale;    // APPLY: bn2 scale / shift (batch statistics, finalized)
+    const float* shift;
+    float* aout;           // APPLY: tower output a = relu(z*s + t + res) (padded NHWC)
+    const float* wpc;      // policy_conv.weight [2][C]
+    const float* wvc;      // value_conv.weight [C]
+    float* zh;             // [B][3][225]
+    double* part;          // [nwg][6]
+    unsigned* cnt;
+    int M;
+    // finalize (reference BatchNorm2d train-mode forward of policy_bn / value_bn)
+    const BnDesc* desc;
+    int pol_layer, val_layer;
+    const float* params;
+    float* stats;          // running stats
+    float *bmean, *binv, *bscale, *bshift;
+    int64_t* nbt;
+    int nbn;
+};
+
+struct HeadBoardArgs {
+    const float* zh;       // [B][3][225]
+    const float* hmean;    // head BN mean / scale / shift / invstd (policy ch 0, 1, value)
+    const float* hscale;
+    const float* hshift;
+    const float* hinv;
+    const float* wpf;      // policy_fc.weight [225][450], bias [225]
+    const float* bpf;
+    const float* wv1;      // value_fc1.weight [64][225], bias [64]
+    const float* bv1;
+    const float* wv2;      // value_fc2.weight [64], bias [1]
+    const float* bv2;
+    const float* pis;      // [B][225]
+    const float* zs;       // [B]
+    float *fp, *fv, *hv, *dlogits, *dhv, *dfp, *dfv;
+    double* pd;            // [nwg][HB_PD]
+    float* pf;             // [nwg][HB_PF]
+    unsigned* cnt;
+    int B;
+    // finalize
+    const BnDesc* desc;
+    int pol_layer, val_layer;
+    const float* params;
+    float* grads;
+    float* hb;             // [3][3] head-BN backward coefficients (S dy / N, k, invstd*gamma)
+    float *g_pfb, *g_v1b, *g_v2w, *g_v2b;
+    float* losses;
+};
+
+struct HeadBwdArgs {
+    const float* act;      // tower output a (padded NHWC)
+    const float* zh;       // [B][3][225]
+    const float* dfp;      // [B][450]
+    const float* dfv;      // [B][225]
+    const float* hmean;    // head BN mean (3)
+    const float* hb;       // [3][3] head-BN backward coefficients
+    const float* wpc;      // policy_conv.weight [2][C]
+    const float* wvc;      // value_conv.weight [C]
+    float* gx;             // gradient of the tower output (padded NHWC)
+    float* hpart;          // [tile][3][C] head 1x1 weight-grad partials
+    // last block's bn2 backward partials (NB > 0): dy = gx * (act > 0)
+    const float* z2;       // raw bn2 input
+    const float* mean2;    // bn2 batch mean
+    float* pa;             // [tile][C]: S dy
+    float* pb;             // [tile][C]: S (z - mean) dy
+    int M;
+};
+
+int head_proj_stats_groups(int M);
+int head_board_groups(int B);
+int head_board_pd();
+int head_board_pf();
+hipError_t launch_head_proj_stats(int C, bool apply, const HeadStatsArgs& a, hipStream_t st);
+hipError_t launch_head_board(const HeadBoardArgs& a, hipStream_t st);
+hipError_t launch_heads_bwd_fused(int C, bool bnx, const HeadBwdArgs& a, hipStream_t st);
+
+}  // namespace azg

@@ -1,0 +1,522 @@
+// Train-step head chain (reference network.py:101-115 forward in train mode, the
+// loss of network.py:216-221 and its backward down to the tower output), as three
+// launches on the critical path instead of eighteen:
+//
+//   head_proj_stats_kernel  the last block's BN2 + residual + ReLU (the tower output
+//       a = relu(z*s + t + x), written for the backward) fused with the three 1x1
+//       head projections (policy_conv C->2, value_conv C->1: zh[b][3][225]) and the
+//       head BatchNorms' batch statistics: per-workgroup fp64 sums, finalized by the
+//       last workgroup to arrive (mean / invstd / folded scale+shift, running stats,
+//       every BN layer's num_batches_tracked += 1);
+//   head_board_kernel  one wave per board, four boards per workgroup: head BN + ReLU
+//       (fp [450], fv [225]), policy_fc / value_fc1 forward (fp32 VALU dot products,
+//       weights streamed from L2), log_softmax + KLDiv(batchmean) + MSE and their
+//       gradients, the masked fc data gradients dfp / dfv, and per-workgroup partials
+//       of the head-BN backward sums, the fc bias grads, value_fc2 grads and the loss
+//       means -- finalized by the last workgroup (head-BN dgamma / dbeta and the
+//       backward-apply coefficients, bias grads, losses);
+//   heads_bwd_fused_kernel  the head-BN backward apply computed per pixel on the fly,
+//       the projections' data gradient gX = sum_ch dzh * Wh and weight-grad partials,
+//       and the BatchNorm-backward partial sums of the last block's bn2 (dy = gX * (a
+//       > 0), S dy, S (z - mean) dy per 128-row tile) for the next finalize.
+//
+// The fc weight gradients (dW = dlogits^T fp, dW1 = dhv^T fv) are a separate small
+// GEMM off the critical path.  Hand-offs to the last-arriving workgroups follow the
+// microarch guide's R1 producer + consumer acquire (valid at any occupancy):
+// write-through stores, s_waitcnt vmcnt(0), barrier, one relaxed agent-scope atomic
+// per workgroup; the workgroup whose add returns n - 1 runs an agent acquire before
+// its plain loads.
+#include "pv_train_heads.h"
+
+namespace azg {
+
+constexpr int HP_ROWS = 64;     // pixels per workgroup of head_proj_stats_kernel
+constexpr int HB_BOARDS = 4;    // boards per workgroup of head_board_kernel (one wave each)
+// per-workgroup partials of head_board_kernel: doubles [6 head-BN sums | 2 losses],
+// floats [225 policy bias | 64 value_fc1 bias | 64 value_fc2 weight | 1 value_fc2 bias]
+constexpr int HB_PD = 8;
+constexpr int HB_PF = ACTIONS + 2 * VHID + 1;
+
+// relaxed agent-scope arrival count, the last workgroup learns it is last (R1 + acquire)
+__device__ __forceinline__ bool last_arrival(unsigned* cnt, unsigned n, unsigned* flag)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned last = old == n - 1 ? 1u : 0u;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-armed for the next step
+        }
+        *flag = last;
+    }
+    __syncthreads();
+    return *flag != 0;
+}
+
+__device__ __forceinline__ void st_wt_d(double* p, double v)
+{
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v),
+                                          wt_rsrc(p, 8), 0, 0, 16);
+}
+__device__ __forceinline__ void st_wt_f(float* p, float v)
+{
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), wt_rsrc(p, 4), 0, 0, 16);
+}
+
+__device__ __forceinline__ double wsum_d(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int C, bool APPLY>
+__global__ __launch_bounds__(256) void head_proj_stats_kernel(const HeadStatsArgs a)
+{
+    constexpr int Q = C / 4;   // channels per thread (4 threads per pixel)
+    __shared__ float w[3][C];
+    __shared__ float ss[2][C];
+    __shared__ double red[4][6];
+    __shared__ unsigned flag;
+    for (int i = threadIdx.x; i < 3 * C; i += 256) w[i / C][i % C] = i < 2 * C ? a.wpc[i] : a.wvc[i - 2 * C];
+    if (APPLY)
+        for (int i = threadIdx.x; i < C; i += 256) {
+            ss[0][i] = a.scale[i];
+            ss[1][i] = a.shift[i];
+        }
+    __syncthreads();
+    const int q = threadIdx.x & 3;
+    const int m = blockIdx.x * HP_ROWS + (threadIdx.x >> 2);
+    float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+    if (m < a.M) {
+        const int o = pad_off(m, C) + q * Q;
+        const __amdgpu_buffer_rsrc_t ars = wt_rsrc(a.aout, padded_bytes(a.M, C));
+#pragma unroll
+        for (int c = 0; c < Q; c += 4) {
+            f32x4 v = *(const f32x4*)(a.z + o + c);
+            if (APPLY) {   // = bn_apply_kernel<C, true>: relu(z * scale + shift + res)
+                const f32x4 r = *(const f32x4*)(a.res + o + c);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k] * ss[0][q * Q + c + k] + ss[1][q * Q + c + k] + r[k], 0.f);
+                store4<true>(a.aout, ars, o + c, v);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                d0 = fmaf(v[k], w[0][q * Q + c + k], d0);
+                d1 = fmaf(v[k], w[1][q * Q + c + k], d1);
+                d2 = fmaf(v[k], w[2][q * Q + c + k], d2);
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 1; o < 4; o <<= 1) {   // = heads_project's reduction order
+        d0 += __shfl_xor(d0, o, 64);
+        d1 += __shfl_xor(d1, o, 64);
+        d2 += __shfl_xor(d2, o, 64);
+    }
+    const bool own = m < a.M && q == 0;
+    if (own) {
+        const int b = m / PIX, p = m - b * PIX;
+        float* hb = a.zh + (size_t)b * 3 * PIX;
+        hb[p] = d0;
+        hb[PIX + p] = d1;
+        hb[2 * PIX + p] = d2;
+    }
+    // per-workgroup fp64 sums S z, S z^2 of the three head channels
+    double v[6] = {own ? (double)d0 : 0.0, own ? (double)d0 * d0 : 0.0, own ? (double)d1 : 0.0,
+                   own ? (double)d1 * d1 : 0.0, own ? (double)d2 : 0.0, own ? (double)d2 * d2 : 0.0};
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) v[k] = wsum_d(v[k]);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) red[wid][k] = v[k];
+    __syncthreads();
+    if (threadIdx.x < 6)
+        st_wt_d(a.part + (size_t)blockIdx.x * 6 + threadIdx.x,
+                (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]));
+    if (!last_arrival(a.cnt, gridDim.x, &flag)) return;
+    // finalize: every workgroup's sums in workgroup order (lane j: workgroups j, j+64, ...)
+    const int nwg = gridDim.x;
+    if (wid == 0) {
+        double s[6] = {0, 0, 0, 0, 0, 0};
+        for (int g = lane; g < nwg; g += 64)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) s[k] += a.part[(size_t)g * 6 + k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) s[k] = wsum_d(s[k]);
+        if (lane < 3) {   // = head_stats_finalize_kernel
+            const int ch = lane;
+            const BnDesc d = a.desc[ch < 2 ? a.pol_layer : a.val_layer];
+            const int c = ch < 2 ? ch : 0;
+            const double N = (double)a.M;
+            const double sm = ch == 0 ? s[0] : ch == 1 ? s[2] : s[4];
+            const double sq = ch == 0 ? s[1] : ch == 1 ? s[3] : s[5];
+            const double mean = sm / N;
+            double qv = sq - sm * mean;
+            qv = qv > 0.0 ? qv : 0.0;
+            const double var = qv / N;
+            const float mean_f = (float)mean;
+            const float inv_f = (float)(1.0 / sqrt(var + (double)BN_EPS));
+            const float alpha = inv_f * a.params[d.gamma_off + c];
+            a.bmean[d.out_off + c] = mean_f;
+            a.binv[d.out_off + c] = inv_f;
+            a.bscale[d.out_off + c] = alpha;
+            a.bshift[d.out_off + c] = a.params[d.beta_off + c] - mean_f * alpha;
+            const double unb = N > 1 ? qv / (N - 1.0) : var;
+            float* rm = a.stats + d.stat_off;
+            float* rv = a.stats + d.stat_off + d.c;
+            rm[c] = (float)((double)BN_MOMENTUM * mean + (1.0 - (double)BN_MOMENTUM) * (double)rm[c]);
+            rv[c] = (float)((double)BN_MOMENTUM * unb + (1.0 - (double)BN_MOMENTUM) * (double)rv[c]);
+        }
+    }
+    if (a.nbt)
+        for (int i = threadIdx.x; i < a.nbn; i += 256) a.nbt[i] += 1;
+}
+
+__global__ __launch_bounds__(256) void head_board_kernel(const HeadBoardArgs a)
+{
+    __shared__ float fps[HB_BOARDS][2 * PIX];
+    __shared__ float fvs[HB_BOARDS][PIX];
+    __shared__ float lgs[HB_BOARDS][ACTIONS];
+    __shared__ float dls[HB_BOARDS][ACTIONS];
+    __shared__ float hps[HB_BOARDS][VHID];
+    __shared__ float dhs[HB_BOARDS][VHID];
+    __shared__ float hvs[HB_BOARDS][VHID];
+    __shared__ float dps[HB_BOARDS];
+    __shared__ double lss[HB_BOARDS][2];
+    __shared__ double red[4][6];
+    __shared__ unsigned flag;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int b0 = blockIdx.x * HB_BOARDS;
+    const int nb = min(HB_BOARDS, a.B - b0);
+    // head BN + ReLU (= head_bn_apply_kernel)
+    for (int i = tid; i < HB_BOARDS * 3 * PIX; i += 256) {
+        const int bb = i / (3 * PIX), k = i - bb * 3 * PIX, ch = k / PIX;
+        float y = 0.f;
+        if (bb < nb) y = fmaxf(a.zh[(size_t)(b0 + bb) * 3 * PIX + k] * a.hscale[ch] + a.hshift[ch], 0.f);
+        if (ch < 2) {
+            fps[bb][k] = y;
+            if (bb < nb) a.fp[(size_t)(b0 + bb) * 2 * PIX + k] = y;
+        } else {
+            fvs[bb][k - 2 * PIX] = y;
+            if (bb < nb) a.fv[(size_t)(b0 + bb) * PIX + k - 2 * PIX] = y;
+        }
+    }
+    __syncthreads();
+    // policy_fc / value_fc1 forward: wave w takes output rows w, w+4, ...; lanes split K
+    for (int j = wid; j < ACTIONS + VHID; j += 4) {
+        const bool pol = j < ACTIONS;
+        const float* wr = pol ? a.wpf + (size_t)j * 2 * PIX : a.wv1 + (size_t)(j - ACTIONS) * PIX;
+        const int K = pol ? 2 * PIX : PIX;
+        float s[HB_BOARDS] = {0.f, 0.f, 0.f, 0.f};
+        for (int k = lane; k < K; k += 64) {
+            const float wk = wr[k];
+#pragma unroll
+            for (int bb = 0; bb < HB_BOARDS; ++bb) s[bb] = fmaf(pol ? fps[bb][k] : fvs[bb][k], wk, s[bb]);
+        }
+#pragma unroll
+        for (int bb = 0; bb < HB_BOARDS; ++bb) s[bb] = wave_sum(s[bb]);
+        if (lane == 0)
+#pragma unroll
+            for (int bb = 0; bb < HB_BOARDS; ++bb) {
+                if (pol) lgs[bb][j] = s[bb];
+                else hps[bb][j - ACTIONS] = s[bb];
+            }
+    }
+    __syncthreads();
+    // loss and output gradients, one wave per board (= heads_loss_kernel)
+    {
+        const int bb = wid, b = b0 + bb;
+        const bool ok = bb < nb;
+        float lg[4];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int j = lane + 64 * t;
+            lg[t] = j < ACTIONS ? lgs[bb][j] + a.bpf[j] : -INFINITY;
+            mx = fmaxf(mx, lg[t]);
+        }
+        mx = wave_max(mx);
+        float se = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (lane + 64 * t < ACTIONS) se += expf(lg[t] - mx);
+        se = wave_sum(se);
+        const float lse = logf(se);
+        float kl = 0.f, st = 0.f, tv[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int j = lane + 64 * t;
+            tv[t] = (ok && j < ACTIONS) ? a.pis[(size_t)b * ACTIONS + j] : 0.f;
+            if (j < ACTIONS) {
+                const float lp = (lg[t] - mx) - lse;
+                if (tv[t] > 0.f) kl += tv[t] * (logf(tv[t]) - lp);
+                st += tv[t];
+            }
+        }
+        kl = wave_sum(kl);
+        st = wave_sum(st);
+        const float invB = 1.f / (float)a.B;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int j = lane + 64 * t;
+            if (j < ACTIONS) {
+                const float lp = (lg[t] - mx) - lse;
+                const float dl = ok ? (expf(lp) * st - tv[t]) * invB : 0.f;
+                dls[bb][j] = dl;
+                if (ok) a.dlogits[(size_t)b * ACTIONS + j] = dl;
+            }
+        }
+        const float hid = fmaxf(hps[bb][lane] + a.bv1[lane], 0.f);
+        const float pre = wave_sum(a.wv2[lane] * hid) + a.bv2[0];
+        const float v = tanhf(pre);
+        const float z = ok ? a.zs[b] : 0.f;
+        const float dv = 2.f * (v - z) / (float)a.B;
+        const float dp = ok ? dv * (1.f - v * v) : 0.f;
+        const float dh = hid > 0.f ? dp * a.wv2[lane] : 0.f;
+        hvs[bb][lane] = ok ? hid : 0.f;
+        dhs[bb][lane] = dh;
+        if (ok) {
+            a.hv[(size_t)b * VHID + lane] = hid;
+            a.dhv[(size_t)b * VHID + lane] = dh;
+        }
+        if (lane == 0) {
+            dps[bb] = dp;
+            lss[bb][0] = ok ? (double)kl : 0.0;
+            lss[bb][1] = ok ? (double)((v - z) * (v - z)) : 0.0;
+        }
+    }
+    __syncthreads();
+    // fc data gradients with the ReLU masks (= small_gemm dgrad): thread k of the
+    // 450 policy features and 225 value features; head-BN backward partials
+    double hs[6] = {0, 0, 0, 0, 0, 0};   // (S dy, S (z - mean) dy) for ch 0, 1, 2
+    for (int k = tid; k < 2 * PIX + PIX; k += 256) {
+        const bool pol = k < 2 * PIX;
+        const int kk = pol ? k : k - 2 * PIX;
+        float s[HB_BOARDS] = {0.f, 0.f, 0.f, 0.f};
+        if (pol) {
+            for (int j = 0; j < ACTIONS; ++j) {
+                const float wjk = a.wpf[(size_t)j * 2 * PIX + kk];
+#pragma unroll
+                for (int bb = 0; bb < HB_BOARDS; ++bb) s[bb] = fmaf(dls[bb][j], wjk, s[bb]);
+            }
+        } else {
+            for (int u = 0; u < VHID; ++u) {
+                const float wuk = a.wv1[(size_t)u * PIX + kk];
+#pragma unroll
+                for (int bb = 0; bb < HB_BOARDS; ++bb) s[bb] = fmaf(dhs[bb][u], wuk, s[bb]);
+            }
+        }
+        const int ch = pol ? kk / PIX : 2;
+        const int p = pol ? kk - ch * PIX : kk;
+        const double mu = (double)a.hmean[ch];
+#pragma unroll
+        for (int bb = 0; bb < HB_BOARDS; ++bb) {
+            if (bb >= nb) continue;
+            const float f = pol ? fps[bb][kk] : fvs[bb][kk];
+            const float d = f > 0.f ? s[bb] : 0.f;
+            const int b = b0 + bb;
+            if (pol) a.dfp[(size_t)b * 2 * PIX + kk] = d;
+            else a.dfv[(size_t)b * PIX + kk] = d;
+            const double zz = (double)a.zh[(size_t)b * 3 * PIX + ch * PIX + p];
+            hs[2 * ch] += (double)d;
+            hs[2 * ch + 1] += (zz - mu) * (double)d;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) hs[k] = wsum_d(hs[k]);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) red[wid][k] = hs[k];
+    __syncthreads();
+    double* pd = a.pd + (size_t)blockIdx.x * HB_PD;
+    float* pf = a.pf + (size_t)blockIdx.x * HB_PF;
+    if (tid < 6) st_wt_d(pd + tid, (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]));
+    if (tid == 6) st_wt_d(pd + 6, (lss[0][0] + lss[1][0]) + (lss[2][0] + lss[3][0]));
+    if (tid == 7) st_wt_d(pd + 7, (lss[0][1] + lss[1][1]) + (lss[2][1] + lss[3][1]));
+    for (int o = tid; o < HB_PF; o += 256) {   // bias / value_fc2 partials over this group's boards
+        float s = 0.f;
+#pragma unroll
+        for (int bb = 0; bb < HB_BOARDS; ++bb) {
+            if (o < ACTIONS) s += dls[bb][o];
+            else if (o < ACTIONS + VHID) s += dhs[bb][o - ACTIONS];
+            else if (o < ACTIONS + 2 * VHID) s = fmaf(dps[bb], hvs[bb][o - ACTIONS - VHID], s);
+            else s += dps[bb];
+        }
+        st_wt_f(pf + o, s);
+    }
+    if (!last_arrival(a.cnt, gridDim.x, &flag)) return;
+    // finalize over workgroups in order
+    const int nwg = gridDim.x;
+    if (wid == 0) {
+        double s[HB_PD];
+#pragma unroll
+        for (int k = 0; k < HB_PD; ++k) s[k] = 0.0;
+        for (int g = lane; g < nwg; g += 64)
+#pragma unroll
+            for (int k = 0; k < HB_PD; ++k) s[k] += a.pd[(size_t)g * HB_PD + k];
+#pragma unroll
+        for (int k = 0; k < HB_PD; ++k) s[k] = wsum_d(s[k]);
+        if (lane < 3) {   // = head_bn_bwd_finalize_kernel
+            const int ch = lane;
+            const BnDesc d = a.desc[ch < 2 ? a.pol_layer : a.val_layer];
+            const int c = ch < 2 ? ch : 0;
+            const double N = (double)a.B * PIX;
+            const double sd = ch == 0 ? s[0] : ch == 1 ? s[2] : s[4];
+            const double qd = ch == 0 ? s[1] : ch == 1 ? s[3] : s[5];
+            const float inv = a.hinv[ch];
+            const double invd = (double)inv;
+            a.grads[d.gamma_off + c] = (float)(qd * invd);
+            a.grads[d.beta_off + c] = (float)sd;
+            a.hb[ch * 3 + 0] = (float)(sd / N);
+            a.hb[ch * 3 + 1] = (float)(qd * invd * invd / N);
+            a.hb[ch * 3 + 2] = inv * a.params[d.gamma_off + c];
+        }
+        if (lane == 0) {   // = heads_small_grads_kernel's loss means
+            const float plf = (float)(s[6] / (double)a.B), vlf = (float)(s[7] / (double)a.B);
+            a.losses[0] = plf;
+            a.losses[1] = vlf;
+            a.losses[2] = plf + vlf;
+        }
+    }
+    for (int o = tid; o < HB_PF; o += 256) {
+        float s = 0.f;
+        for (int g = 0; g < nwg; ++g) s += a.pf[(size_t)g * HB_PF + o];
+        if (o < ACTIONS) a.g_pfb[o] = s;
+        else if (o < ACTIONS + VHID) a.g_v1b[o - ACTIONS] = s;
+        else if (o < ACTIONS + 2 * VHID) a.g_v2w[o - ACTIONS - VHID] = s;
+        else a.g_v2b[0] = s;
+    }
+}
+
+// = head_bn_bwd_apply_kernel (dzh on the fly) + heads_bwd_proj_kernel, and the last
+// block's bn_bwd_reduce partials per 128-row tile (HROWS), same thread layout as
+// heads_bwd_proj_kernel: float4 over channels, RG row groups, UNR rows in flight
+template <int C, bool BNX>
+__global__ __launch_bounds__(256) void heads_bwd_fused_kernel(const HeadBwdArgs a)
+{
+    constexpr int HROWS = 128;
+    constexpr int Q = C / 4, RG = 256 / Q, UNR = 4;
+    __shared__ f32x4 red[5][RG][Q];
+    const int q = threadIdx.x % Q, rg = threadIdx.x / Q;
+    const int c = 4 * q;
+    const int m0 = blockIdx.x * HROWS;
+    const int rows = min(HROWS, a.M - m0);
+    const f32x4 w0 = *(const f32x4*)(a.wpc + c), w1 = *(const f32x4*)(a.wpc + C + c), w2 = *(const f32x4*)(a.wvc + c);
+    f32x4 mu2 = {0.f, 0.f, 0.f, 0.f};
+    if (BNX) mu2 = *(const f32x4*)(a.mean2 + c);
+    float hm[3], hk[3][3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        hm[ch] = a.hmean[ch];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) hk[ch][k] = a.hb[ch * 3 + k];
+    }
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, xa = s0, xb = s0;
+    for (int r0 = rg; r0 < rows; r0 += RG * UNR) {
+        f32x4 xv[UNR], zv[UNR];
+        float d0[UNR], d1[UNR], d2[UNR];
+        int o[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const int r = r0 + RG * u;
+            const int m = m0 + min(r, rows - 1);
+            const int b = m / PIX, p = m - b * PIX;
+            const float* zb = a.zh + (size_t)b * 3 * PIX;
+            const float y0 = a.dfp[(size_t)b * 2 * PIX + p], y1 = a.dfp[(size_t)b * 2 * PIX + PIX + p];
+            const float y2 = a.dfv[(size_t)b * PIX + p];
+            d0[u] = ((y0 - hk[0][0]) - (zb[p] - hm[0]) * hk[0][1]) * hk[0][2];
+            d1[u] = ((y1 - hk[1][0]) - (zb[PIX + p] - hm[1]) * hk[1][1]) * hk[1][2];
+            d2[u] = ((y2 - hk[2][0]) - (zb[2 * PIX + p] - hm[2]) * hk[2][1]) * hk[2][2];
+            o[u] = pad_off(m, C) + c;
+            xv[u] = *(const f32x4*)(a.act + o[u]);
+            if (BNX) zv[u] = *(const f32x4*)(a.z2 + o[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            if (r0 + RG * u < rows) {
+                f32x4 g;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    s0[e] = fmaf(d0[u], xv[u][e], s0[e]);
+                    s1[e] = fmaf(d1[u], xv[u][e], s1[e]);
+                    s2[e] = fmaf(d2[u], xv[u][e], s2[e]);
+                    g[e] = d0[u] * w0[e] + d1[u] * w1[e] + d2[u] * w2[e];
+                    if (BNX) {   // = bn_bwd_reduce_kernel: dy = g * (act > 0)
+                        const float dy = xv[u][e] > 0.f ? g[e] : 0.f;
+                        xa[e] += dy;
+                        xb[e] = fmaf(zv[u][e] - mu2[e], dy, xb[e]);
+                    }
+                }
+                *(f32x4*)(a.gx + o[u]) = g;
+            }
+        }
+    }
+    red[0][rg][q] = s0;
+    red[1][rg][q] = s1;
+    red[2][rg][q] = s2;
+    red[3][rg][q] = xa;
+    red[4][rg][q] = xb;
+    __syncthreads();
+    if (rg == 0) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            if (!BNX && k >= 3) break;
+            f32x4 v = red[k][0][q];
+            for (int g = 1; g < RG; ++g) v += red[k][g][q];
+            if (k < 3) *(f32x4*)(a.hpart + ((size_t)blockIdx.x * 3 + k) * C + c) = v;
+            else *(f32x4*)((k == 3 ? a.pa : a.pb) + (size_t)blockIdx.x * C + c) = v;
+        }
+    }
+}
+
+hipError_t launch_head_proj_stats(int C, bool apply, const HeadStatsArgs& a, hipStream_t st)
+{
+    dim3 grid((a.M + HP_ROWS - 1) / HP_ROWS);
+#define AZG_HPS(CC)                                                                                     \
+    case CC:                                                                                            \
+        if (apply) hipLaunchKernelGGL((head_proj_stats_kernel<CC, true>), grid, dim3(256), 0, st, a);  \
+        else hipLaunchKernelGGL((head_proj_stats_kernel<CC, false>), grid, dim3(256), 0, st, a);       \
+        return hipGetLastError();
+    switch (C) {
+        AZG_HPS(64)
+        AZG_HPS(128)
+        AZG_HPS(256)
+        default: return hipErrorInvalidValue;
+    }
+#undef AZG_HPS
+}
+
+int head_proj_stats_groups(int M) { return (M + HP_ROWS - 1) / HP_ROWS; }
+int head_board_groups(int B) { return (B + HB_BOARDS - 1) / HB_BOARDS; }
+int head_board_pd() { return HB_PD; }
+int head_board_pf() { return HB_PF; }
+
+hipError_t launch_head_board(const HeadBoardArgs& a, hipStream_t st)
+{
+    hipLaunchKernelGGL(head_board_kernel, dim3(head_board_groups(a.B)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_heads_bwd_fused(int C, bool bnx, const HeadBwdArgs& a, hipStream_t st)
+{
+    dim3 grid((a.M + 127) / 128);
+#define AZG_HBF(CC)                                                                                     \
+    case CC:                                                                                            \
+        if (bnx) hipLaunchKernelGGL((heads_bwd_fused_kernel<CC, true>), grid, dim3(256), 0, st, a);    \
+        else hipLaunchKernelGGL((heads_bwd_fused_kernel<CC, false>), grid, dim3(256), 0, st, a);       \
+        return hipGetLastError();
+    switch (C) {
+        AZG_HBF(64)
+        AZG_HBF(128)
+        AZG_HBF(256)
+        default: return hipErrorInvalidValue;
+    }
+#undef AZG_HBF
+}
+
+}  // namespace azg

@@ -532,8 +532,16 @@ static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, f
 // every split keeps >= 2 whole 32-pixel chunks.
 int g_wgrad_bk = 32;   // pixels per K chunk of the row-staging tile (32 default; 16 = A/B study)
 
+int g_wgrad_splits = 0;   // key 27: split-K count override (multiple of 8, <= 64; 0 = automatic)
+
 int wgrad_splits(int C, int M)
 {
+    if (g_wgrad_splits > 0) {
+        int S = g_wgrad_splits;
+        const int nch = (M + 31) / 32;
+        while (S > 8 && nch < 2 * S) S -= 8;
+        return S;
+    }
     const int bt = C < 128 ? C : 128;
     const int tiles = 9 * (C / bt) * (C / bt);
     const int lds = 2 * 2 * bt * (g_wgrad_bk + 4) * 4;   // largest variant (K-contiguous staging)

@@ -16,7 +16,7 @@ run() {   # tag, probe args
     s=$?; echo "$tag pmc $pmc exit $s"; [ $s -eq 0 ] || exit $s
   done
 }
-mkdir -p $OUT/t10_b3456 $OUT/t10_b512 $OUT/t8_256_b512
-run t10_b3456 --batch 3456 --tower 1 --tower-shape ${SHAPE_128:-10} || exit 1
-run t10_b512 --batch 512 --tower 1 --tower-shape ${SHAPE_128:-10} || exit 1
-run t8_256_b512 --batch 512 --tower 1 --tower-shape 8 --blocks 10 --channels 256 || exit 1
+mkdir -p $OUT/t_b3456 $OUT/t_b512 $OUT/t_256_b512
+run t_b3456 --batch 3456 --tower 1 --tower-shape ${SHAPE_128:-8} || exit 1
+run t_b512 --batch 512 --tower 1 --tower-shape ${SHAPE_128:-8} || exit 1
+run t_256_b512 --batch 512 --tower 1 --tower-shape 8 --blocks 10 --channels 256 || exit 1

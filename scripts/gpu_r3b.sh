@@ -7,6 +7,8 @@ O=gpurun_out/r3b
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 STUDY=alphazero-gomoku_amd/libazg_pv_study.so
+timeout -k 10 300 python -u -m pytest tests/test_gpu_train.py -m gpu -v -k "schedule_keys" --timeout 240 --timeout-method thread > $O/pytest_keys.log 2>&1
+s=$?; echo "keys rc $s"; tail -3 $O/pytest_keys.log; [ $s -le 1 ] || exit $s
 AZG_PV_LIB=$STUDY timeout -k 10 300 python -u -m pytest tests/test_gpu_forward.py -m gpu -v -k "tower" --timeout 240 --timeout-method thread > $O/pytest_study.log 2>&1
 s=$?; echo "study pytest rc $s"; tail -5 $O/pytest_study.log; [ $s -le 1 ] || exit $s
 AZG_PV_LIB=$STUDY timeout -k 10 400 python -u scripts/tower_r3_ab.py > $O/tower_ab.log 2>&1 || { echo "tower ab failed"; tail -30 $O/tower_ab.log; exit 1; }

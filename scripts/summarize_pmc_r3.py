@@ -18,9 +18,9 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TAGS = {   # dir: (blocks, channels, batch)
-    "t10_b3456": (6, 128, 3456),
-    "t10_b512": (6, 128, 512),
-    "t8_256_b512": (10, 256, 512),
+    "t_b3456": (6, 128, 3456),
+    "t_b512": (6, 128, 512),
+    "t_256_b512": (10, 256, 512),
 }
 
 
@@ -49,8 +49,7 @@ def main():
             continue
         fetch = means(os.path.join(base, "pmc_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE")
         write = means(os.path.join(base, "pmc_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE")
-        mp = os.path.join(base, "pmc_SQ_VALU_MFMA_BUSY_CYCLES_GRBM_GUI_ACTIVE_SQ_BUSY_CYCLES",
-                          "run_counter_collection.csv")
+        mp = os.path.join(base, "pmc_SQ_VALU_MFMA_BUSY_CYCLES_GRBM_GUI_ACTIVE", "run_counter_collection.csv")
         mf, gr = means(mp, "SQ_VALU_MFMA_BUSY_CYCLES"), means(mp, "GRBM_GUI_ACTIVE")
         for k in fetch:
             f, w = fetch[k] * 2 * 1024, write.get(k, 0.0) * 1024

@@ -7,7 +7,8 @@
     count inside, timing only) -- the device-bound floor without launch gaps;
   * key 24 = 0 / 1: BN finalize in separate kernels vs fused into the producing conv's
     last workgroup (acquire hand-off); key 25 = 32 / 0: train convs with buffer-
-    resource addressing vs 64-bit pointers.
+    resource addressing vs 64-bit pointers; key 26 = 8 / 16: 128x64 tiles with 8 waves
+    vs 128x128 tiles with 16 waves (one workgroup per CU).
 
     python scripts/train_r3_probe.py [--steps 30]
 """
@@ -30,6 +31,10 @@ def main():
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--channels", type=int, default=128)
     ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--splits", default="", help="comma list of wgrad split counts to time (key 27; 0 = auto)")
+    ap.add_argument("--only-splits", action="store_true")
+    ap.add_argument("--ab", default="26=8,25=32,24=1;26=8,25=32,24=0;26=8,25=0,24=1;26=16,25=32,24=1",
+                    help="';'-separated sets of comma-separated KEY=VALUE tuning keys to time against each other")
     args = ap.parse_args()
     import _native
     from network import PyTorchModel
@@ -55,23 +60,33 @@ def main():
     for _ in range(5):
         step()
     torch.cuda.synchronize()
-    for rnd in range(2):
-        for key25 in (32, 0):
-            for key24 in (1, 0):
-                lib.azg_pv_set_tuning(24, key24)
-                lib.azg_pv_set_tuning(25, key25)
-                for _ in range(3):
-                    step()
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                for _ in range(K):
-                    step()
-                torch.cuda.synchronize()
-                ms = (time.perf_counter() - t0) / K * 1e3
-                out.setdefault(f"pipelined_ms_key24_{key24}_key25_{key25}", []).append(round(ms, 4))
-    lib.azg_pv_set_tuning(24, 1)
-    lib.azg_pv_set_tuning(25, 32)
-    if hasattr(torch.cuda, "_sleep"):
+    def timed(tag):
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(K):
+            step()
+        torch.cuda.synchronize()
+        out.setdefault(tag, []).append(round((time.perf_counter() - t0) / K * 1e3, 4))
+
+    if args.splits:
+        for rnd in range(2):
+            for S in (int(v) for v in args.splits.split(",")):
+                lib.azg_pv_set_tuning(27, S)
+                timed(f"pipelined_ms_splits_{S}")
+        lib.azg_pv_set_tuning(27, 0)
+    # A/B of tuning-key sets, interleaved rounds (default: the round-3 train keys)
+    for rnd in range(0 if args.only_splits else 2):
+        for cfg in args.ab.split(";"):
+            kv = [tuple(int(t) for t in item.split("=")) for item in cfg.split(",") if item]
+            if any(k == 26 and v == 16 for k, v in kv) and args.channels != 128:
+                continue
+            prev = [(k, lib.azg_pv_set_tuning(k, v)) for k, v in kv]
+            timed("pipelined_ms_" + (cfg.replace("=", "_").replace(",", "__") or "default"))
+            for k, v in reversed(prev):
+                lib.azg_pv_set_tuning(k, v)
+    if hasattr(torch.cuda, "_sleep") and not args.only_splits:
         torch.cuda.synchronize()
         torch.cuda._sleep(int(2.4e9 * 0.5))        # ~0.5 s spin ahead of the queue
         t0 = time.perf_counter()
@@ -91,6 +106,8 @@ def main():
         eng.lib.azg_pv_train_apply(eng.h, opt.flat_exp_avg.data_ptr(), opt.flat_exp_avg_sq.data_ptr(), 7,
                                    float(g["lr"]), 0.9, 0.999, 1e-8, float(g["weight_decay"]), 3.0, None, s)
     try:
+        if args.only_splits:
+            raise RuntimeError("skipped")
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):

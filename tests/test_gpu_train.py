@@ -323,14 +323,15 @@ def test_train_then_predict_uses_new_weights():
 
 
 @pytest.mark.parametrize("key,values", [(18, (0, 1, 2, 4, 7)), (12, (0, 1)), (16, (3, 0, 1, 2)), (23, (1, 0)), (24, (1, 0)),
-                                        (25, (32, 0))])
+                                        (25, (32, 0)), (26, (8, 16))])
 def test_train_schedule_keys_bitwise(key, values):
     """Train-step tuning keys change cache policy (18: write-through stores), stream
     schedule (12: weight grads overlapped or serial) or the weight-grad staging (16: LDS-DMA
     natural rows, register K-contiguous, two chunks ahead, row staging) or where the forward
     BN applies run (23: folded into the next conv's halo staging, or separate passes) and
     the BN finalizes (24: by the producing conv's last workgroup, or separate kernels)
-    or the train convs' operand addressing (25: buffer resources or 64-bit pointers):
+    or the train convs' operand addressing (25: buffer resources or 64-bit pointers) or
+    tile (26: 128x64 with 8 waves, or 128x128 with 16 waves at one workgroup per CU):
     two steps from one state must give bitwise-identical params, grads, BN buffers
     and Adam moments under every value."""
     import _native
