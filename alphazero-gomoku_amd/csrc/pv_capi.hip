@@ -389,7 +389,7 @@ int32_t ensure_eval_workspace(azg_pv* h, int batch, hipStream_t st)
     return 0;
 }
 
-int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst)
+int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst, int part)
 {
     const int C = h->C;
     const float* P = h->params;
@@ -397,7 +397,7 @@ int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst)
     // the eval BN fold: one launch
     AZG_TRY(launch_repack_all(P, h->conv_off_dev, 2 * h->NB, h->wpack, dgrad_dst, C, P + h->poff[h->t_stem_w],
                               h->wstem, P + h->poff[h->t_pfc_w], P + h->poff[h->t_vfc1_w], h->wfc, h->bn,
-                              h->bn_desc_dev, (int)h->bn_desc.size(), h->scale, h->shift, st),
+                              h->bn_desc_dev, (int)h->bn_desc.size(), h->scale, h->shift, st, part),
             "repack");
     return 0;
 }

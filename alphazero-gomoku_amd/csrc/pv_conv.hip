@@ -979,9 +979,19 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         if (value == 0 || value == 32) azg::g_train_var = value;
         return prev;
     }
-    if (key == 28) {  // train head chain: 1 fused (3 launches, default), 0 the 18-launch chain (A/B; same math, other sum orders)
+    if (key == 30) {  // train: split repack at the start of a step (1, default) or one launch on the stream (0); bitwise identical
+        const int prev = azg::g_train_split_pack;
+        if (value == 0 || value == 1) azg::g_train_split_pack = value;
+        return prev;
+    }
+    if (key == 29) {  // train: BN-backward apply of residual-free layers masks from z (1, default) or reads act (0); bitwise identical
+        const int prev = azg::g_train_maskz;
+        if (value == 0 || value == 1) azg::g_train_maskz = value;
+        return prev;
+    }
+    if (key == 28) {  // train head chain: bit mask of the fused stages (include/azg_pv.h), 0 the 18-launch chain (other sum orders)
         const int prev = azg::g_train_fuse_heads;
-        if (value == 0 || value == 1) azg::g_train_fuse_heads = value;
+        if (value >= 0 && value <= 7) azg::g_train_fuse_heads = value;
         return prev;
     }
     if (key == 27) {  // train wgrad split-K count (0 automatic; 8..64, multiple of 8); bitwise NOT identical across values

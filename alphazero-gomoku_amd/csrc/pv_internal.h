@@ -48,6 +48,8 @@ extern int g_wgrad_serial;
 extern int g_train_fuse_apply;
 extern int g_train_fuse_fin;
 extern int g_train_fuse_heads;
+extern int g_train_maskz;
+extern int g_train_split_pack;
 extern int g_train_skip;
 extern int g_wgrad_bk;
 extern int g_wgrad_kernel;
@@ -85,7 +87,7 @@ hipError_t launch_transpose(const float* src, float* dst, int R, int Cc, hipStre
 hipError_t launch_repack_all(const float* params, const int64_t* conv_offs, int nl, float* wp, float* wd, int C,
                              const float* stem_w, float* ws, const float* wpf, const float* wv1, float* wfc,
                              const float* stats, const void* desc, int nbn, float* scale, float* shift,
-                             hipStream_t st);
+                             hipStream_t st, int part = 0);
 hipError_t launch_fold_bn(const float* params, const float* stats, const void* desc, int nlayers,
                           float* scale, float* shift, hipStream_t st);
 
@@ -151,7 +153,7 @@ void build_layout(azg_pv* h);
 void free_workspace(azg_pv* h);
 void free_train_workspace(azg_pv* h);
 int32_t ensure_eval_workspace(azg_pv* h, int batch, hipStream_t st);
-int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst = nullptr);   // dgrad_dst: also pack dgrad weights
+int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst = nullptr, int part = 0);   // dgrad_dst: also pack dgrad weights
 int prof_begin(azg_pv* h, int cls, hipStream_t st, int64_t boards = 0);   // returns pair index or -1
 hipError_t prof_harvest(azg_pv* h);
 void prof_end(azg_pv* h, int pair, hipStream_t st);

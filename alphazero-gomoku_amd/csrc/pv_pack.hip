@@ -88,11 +88,14 @@ struct RepackArgs {
     int nbn;
     float* scale;
     float* shift;
+    int y0;       // first section of this launch (grid.y covers y0 .. y0 + grid.y - 1)
+    int skip;     // a section to skip (-1: none)
 };
 
 __global__ __launch_bounds__(256) void repack_all_kernel(const RepackArgs a)
 {
-    const int y = blockIdx.y;
+    const int y = a.y0 + (int)blockIdx.y;
+    if (y == a.skip) return;
     const int C = a.C;
     const int stride = gridDim.x * blockDim.x;
     const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -131,17 +134,21 @@ __global__ __launch_bounds__(256) void repack_all_kernel(const RepackArgs a)
     }
 }
 
+// part: 0 every section; 1 the stem only (y = nl); 2 the residual convs (+ dgrad packs)
+// and the head FCs -- neither the stem nor the eval BN fold (the train step's split
+// repack: part 1 on the caller's stream, part 2 on the side stream)
 hipError_t launch_repack_all(const float* params, const int64_t* conv_offs, int nl, float* wp, float* wd, int C,
                              const float* stem_w, float* ws, const float* wpf, const float* wv1, float* wfc,
                              const float* stats, const void* desc, int nbn, float* scale, float* shift,
-                             hipStream_t st)
+                             hipStream_t st, int part)
 {
     RepackArgs a{params, conv_offs, wp, wd, C, nl, stem_w, ws, wpf, wv1, wfc, stats, (const BnDesc*)desc, nbn,
-                 scale, shift};
+                 scale, shift, part == 1 ? nl : 0, part == 2 ? nl : -1};
     int nb = (9 * C * C + 255) / 256;
     nb = nb > 256 ? 256 : nb;
     nb = nb < nbn ? nbn : nb;
-    hipLaunchKernelGGL(repack_all_kernel, dim3(nb, nl + 3), dim3(256), 0, st, a);
+    if (part == 1) nb = (27 * C + 255) / 256;
+    hipLaunchKernelGGL(repack_all_kernel, dim3(nb, part == 1 ? 1 : part == 2 ? nl + 2 : nl + 3), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

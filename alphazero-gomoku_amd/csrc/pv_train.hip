@@ -72,6 +72,10 @@ struct TrainWS {
     float* DZ2 = nullptr;
     hipStream_t side = nullptr;
     hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+    // split repack at the start of a step: the stem on the caller's stream, the rest on
+    // `side` (ev_pack_in: the step's inputs are ready; ev_pack: the packs are written)
+    hipEvent_t ev_pack_in = nullptr, ev_pack = nullptr;
+    bool pack_pending = false;
 };
 
 static TrainWS* ws_of(azg_pv* h) { return (TrainWS*)h->train; }
@@ -86,6 +90,8 @@ void free_train_workspace(azg_pv* h)
         if (w->ev_ready[i]) (void)hipEventDestroy(w->ev_ready[i]);
         if (w->ev_done[i]) (void)hipEventDestroy(w->ev_done[i]);
     }
+    if (w->ev_pack_in) (void)hipEventDestroy(w->ev_pack_in);
+    if (w->ev_pack) (void)hipEventDestroy(w->ev_pack);
     if (w->side) (void)hipStreamDestroy(w->side);
     delete w;
     h->train = nullptr;
@@ -267,12 +273,17 @@ __global__ __launch_bounds__(512) void bn_fin_tiles_kernel(const float* __restri
     bn_fin_combine8<FWD>(v0, v1, red, M, c, c < nch, f);
 }
 
-// dz = ((dy - gm) - (z - mean)*k) * invstd*gamma ; optional gres = dy
-template <int C, bool GRES, bool WT = false>
+// dz = ((dy - gm) - (z - mean)*k) * invstd*gamma ; optional gres = dy.
+// dy = g * (act > 0).  MZ (a layer without a residual input: act = relu(fma(z, scale,
+// shift)), the same expression as the forward's apply): the mask is formed from z and
+// the layer's folded scale / shift instead of reading act -- bitwise the same mask,
+// one 4-B-per-channel tensor less to read.
+template <int C, bool GRES, bool WT = false, bool MZ = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* __restrict__ g, const float* __restrict__ act, const float* __restrict__ z,
     const float* __restrict__ mean, const float* __restrict__ gm, const float* __restrict__ kk,
-    const float* __restrict__ iw, float* __restrict__ dz, float* __restrict__ gres, int M)
+    const float* __restrict__ iw, float* __restrict__ dz, float* __restrict__ gres, int M,
+    const float* __restrict__ fscale = nullptr, const float* __restrict__ fshift = nullptr)
 {
     constexpr int F4 = C / 4;
     const int total = M * F4;
@@ -282,8 +293,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
         const int m = i / F4, c = (i - m * F4) * 4;
         const int o = pad_off(m, C) + c;
         const f32x4 gv = *(const f32x4*)(g + o);
-        const f32x4 av = *(const f32x4*)(act + o);
         const f32x4 zv = *(const f32x4*)(z + o);
+        f32x4 av;
+        if constexpr (MZ) {
+            const f32x4 sc = *(const f32x4*)(fscale + c), sh = *(const f32x4*)(fshift + c);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) av[q] = fmaf(zv[q], sc[q], sh[q]);
+        } else {
+            av = *(const f32x4*)(act + o);
+        }
         const f32x4 mu = *(const f32x4*)(mean + c);
         const f32x4 g_ = *(const f32x4*)(gm + c);
         const f32x4 k_ = *(const f32x4*)(kk + c);
@@ -754,30 +772,29 @@ __global__ __launch_bounds__(256) void grad_sqsum_kernel(const float* __restrict
     if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
-__global__ __launch_bounds__(256) void grad_norm_finalize_kernel(const double* __restrict__ part, int nb,
-                                                                 float max_norm, float* __restrict__ scal,
-                                                                 float* __restrict__ total_norm)
+// Adam with the clip_grad_norm_ finalize in its prologue: every workgroup reduces the
+// grad_sqsum partials itself (one fixed-order block reduction, the same in every workgroup, so all
+// workgroups hold the same coefficient, bitwise) and workgroup 0 publishes the norm --
+// one launch boundary less on the step's critical path.
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                   const double* __restrict__ part, int nb, float max_norm,
+                                                   float* __restrict__ scal, float* __restrict__ total_norm,
+                                                   float lr_bc1, float b1w, float b2, float one_m_b2, float bc2_sqrt,
+                                                   float eps, float wd)
 {
     __shared__ double red[8];
     double s = 0.0;
     for (int i = threadIdx.x; i < nb; i += blockDim.x) s += part[i];
     s = block_sum_d(s, red);
-    if (threadIdx.x == 0) {
-        const float tn = (float)sqrt(s);
-        float coef = max_norm / (tn + 1e-6f);
-        coef = coef < 1.f ? coef : 1.f;
+    const float tn = (float)sqrt(s);
+    float coef = max_norm / (tn + 1e-6f);
+    coef = coef < 1.f ? coef : 1.f;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
         scal[0] = tn;
         scal[1] = coef;
         if (total_norm) total_norm[0] = tn;
     }
-}
-
-__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g,
-                                                   float* __restrict__ m, float* __restrict__ v, int64_t n,
-                                                   const float* __restrict__ scal, float lr_bc1, float b1w,
-                                                   float b2, float one_m_b2, float bc2_sqrt, float eps, float wd)
-{
-    const float coef = scal[1];
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         float gi = g[i] * coef;
         g[i] = gi;
@@ -851,6 +868,8 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
             e = hipEventCreateWithFlags(&w->ev_ready[i], hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&w->ev_done[i], hipEventDisableTiming);
         }
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&w->ev_pack_in, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&w->ev_pack, hipEventDisableTiming);
         if (e != hipSuccess) return set_error("train: side stream / events", e);
     }
     A(w->wdpack, (size_t)(2 * NB > 0 ? 2 * NB : 1) * 9 * C * C, false);
@@ -922,7 +941,9 @@ int g_wgrad_serial = 0;   // 1: conv weight grads on the caller's stream (A/B ti
 int g_train_fuse_apply = 1;   // key 23: 1 BN applies folded into the next conv's staging; 0 separate passes
 int g_train_fuse_fin = 1;     // key 24: 1 BN finalize by the last workgroup of the producing conv; 0 separate kernels
 int g_train_skip = 0;     // study build only (key 19): skip BN kernels to time them in situ (results invalid)
-int g_train_fuse_heads = 1;   // key 28: 1 fused head chain (pv_train_heads.hip, 3 launches); 0 the 18-launch chain
+int g_train_split_pack = 1;   // key 30: 1 split repack (stem on the stream, the rest on the side stream); 0 one launch
+int g_train_maskz = 1;   // key 29: 1 BN-backward apply of residual-free layers forms its ReLU mask from z (default); 0 reads act
+int g_train_fuse_heads = 4;   // key 28: bit mask of the fused head stages (pv_train_heads.hip); 0 the 18-launch chain
 
 template <int C>
 static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, const float* zs, int B,
@@ -1030,18 +1051,23 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         AZG_CK(hipGetLastError(), "train: bn_bwd_finalize_tiles");
         return 0;
     };
+    // mz: the layer has no residual input -- its ReLU mask comes from z (bn_bwd_apply MZ)
     auto bwd_apply = [&](const float* g, const float* act, const float* z, int layer, float* dz,
-                         float* gres) -> int32_t {
+                         float* gres, bool mz = false) -> int32_t {
         if (g_train_skip & 4) return 0;
         const int o = bd[layer].out_off;
         const bool wt = (g_train_wt & 2) != 0;
-#define AZG_BWD_APPLY(GR, W)                                                                                  \
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<C, GR, W>), dim3(gM), dim3(256), 0, st, g, act, z, w->bmean + o, \
-                           w->bgm + o, w->bk + o, w->biw + o, dz, gres, M)
-        if (gres && wt) AZG_BWD_APPLY(true, true);
-        else if (gres) AZG_BWD_APPLY(true, false);
-        else if (wt) AZG_BWD_APPLY(false, true);
-        else AZG_BWD_APPLY(false, false);
+        mz = mz && g_train_maskz;
+#define AZG_BWD_APPLY(GR, W, MZ)                                                                              \
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<C, GR, W, MZ>), dim3(gM), dim3(256), 0, st, g, act, z,        \
+                           w->bmean + o, w->bgm + o, w->bk + o, w->biw + o, dz, gres, M, w->bscale + o,         \
+                           w->bshift + o)
+        if (gres && wt) AZG_BWD_APPLY(true, true, false);
+        else if (gres) AZG_BWD_APPLY(true, false, false);
+        else if (wt && mz) AZG_BWD_APPLY(false, true, true);
+        else if (wt) AZG_BWD_APPLY(false, true, false);
+        else if (mz) AZG_BWD_APPLY(false, false, true);
+        else AZG_BWD_APPLY(false, false, false);
 #undef AZG_BWD_APPLY
         AZG_CK(hipGetLastError(), "train: bn_bwd_apply");
         return 0;
@@ -1087,6 +1113,10 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     struct LastApply { const float* z; const float* res; int layer; float* out; } lastp{nullptr, nullptr, 0, nullptr};
     AZG_CK(launch_stem(C, EPI_RAW, x, h->wstem, nullptr, nullptr, w->z0, B, st), "train: stem");
     R(stats(w->z0, h->bn_stem));
+    if (w->pack_pending) {   // the residual convs' packs (split repack, train_backward)
+        AZG_CK(hipStreamWaitEvent(st, w->ev_pack, 0), "train: stream wait");
+        w->pack_pending = false;
+    }
     const float* X = w->a0;
     // the staging prologue fits the 128-VGPR tile body at C <= 128; at C = 256 (eight
     // channel groups unrolled) it spills 96 VGPRs and costs ~1 ms per 10x256 step
@@ -1117,7 +1147,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             pend = Pend{w->z2[i], h->bn_blk[i].second, X, w->xo[i]};
             X = w->xo[i];
         }
-        if (g_train_fuse_heads && pend.res) {
+        if ((g_train_fuse_heads & 1) && pend.res) {
             last_apply = true;   // the head kernel applies bn2 + residual + ReLU of the last block
             lastp = {pend.z, pend.res, pend.layer, pend.out};
         } else {
@@ -1139,12 +1169,18 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         }
     }
     // ---- heads forward + loss + backward to the tower output ----
+    // key 28 bit 0: head 1x1 projections + BN statistics + finalize in one launch
+    // (head_proj_stats, also applying the last block's bn2 + residual + ReLU); bit 1: head
+    // BN apply + FCs + loss + fc data grads + head BN-backward sums in one launch per 4
+    // boards (head_board); bit 2: head BN-backward apply + 1x1 data/weight-grad partials +
+    // the last block's BN-backward partials in one launch (heads_bwd_fused)
     const int hntile = (M + HROWS - 1) / HROWS;
-    if (g_train_fuse_heads) {
-        // three launches (pv_train_heads.hip) + the fc weight-grad GEMM and the head
-        // 1x1 weight-grad reduction
-        int pr = prof_begin(h, AZG_PROF_TRAIN_OTHER, st);
-        const int ho = bd[h->bn_pol].out_off;   // policy ch0, ch1, value: contiguous
+    const int fh = g_train_fuse_heads;
+    const int ho = bd[h->bn_pol].out_off;   // policy ch0, ch1, value: contiguous
+    const float* wpf = P + h->poff[h->t_pfc_w];
+    const float* wv1 = P + h->poff[h->t_vfc1_w];
+    int pr = prof_begin(h, AZG_PROF_TRAIN_OTHER, st);
+    if (fh & 1) {
         HeadStatsArgs hs{};
         hs.z = last_apply ? lastp.z : X;
         if (last_apply) {
@@ -1172,15 +1208,29 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         hs.nbt = h->nbt;
         hs.nbn = (int)h->bn_desc.size();
         AZG_CK(launch_head_proj_stats(C, last_apply, hs, st), "train: head_proj_stats");
+    } else {
+        AZG_CK(launch_heads_project(C, false, X, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], nullptr, nullptr,
+                                    w->zh, M, st),
+               "train: heads_project");
+        hipLaunchKernelGGL(head_stats_partial_kernel, dim3(3, HSC), dim3(256), 0, st, w->zh, B, w->hspart);
+        AZG_CK(hipGetLastError(), "train: head_stats_partial");
+        hipLaunchKernelGGL(head_stats_finalize_kernel, dim3(1), dim3(64), 0, st, w->hspart, B, bdd, h->bn_pol,
+                           h->bn_val, P, h->bn, w->bmean, w->binv, w->bscale, w->bshift, h->nbt,
+                           (int)h->bn_desc.size());
+        AZG_CK(hipGetLastError(), "train: head_stats_finalize");
+    }
+    const int gH = grid_for((int64_t)B * 3 * PIX);
+    if (fh & 2) {
         HeadBoardArgs hb{};
         hb.zh = w->zh;
         hb.hmean = w->bmean + ho;
         hb.hscale = w->bscale + ho;
         hb.hshift = w->bshift + ho;
         hb.hinv = w->binv + ho;
-        hb.wpf = P + h->poff[h->t_pfc_w];
+        hb.wfc = h->wfc;   // packed by this step's repack
+        hb.wpf = wpf;
         hb.bpf = P + h->poff[h->t_pfc_b];
-        hb.wv1 = P + h->poff[h->t_vfc1_w];
+        hb.wv1 = wv1;
         hb.bv1 = P + h->poff[h->t_vfc1_b];
         hb.wv2 = P + h->poff[h->t_vfc2_w];
         hb.bv2 = P + h->poff[h->t_vfc2_b];
@@ -1215,48 +1265,10 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             GemmProb b{w->dhv, 1, VHID, w->fv, PIX, 1, G + h->poff[h->t_vfc1_w], PIX, 1, nullptr, 0, 0, VHID, PIX, B};
             AZG_CK(launch_small_gemm(a, &b, st), "train: head fc wgrad");
         }
-        HeadBwdArgs hw{};
-        hw.act = X;
-        hw.zh = w->zh;
-        hw.dfp = w->dfp;
-        hw.dfv = w->dfv;
-        hw.hmean = w->bmean + ho;
-        hw.hb = w->hbw;
-        hw.wpc = P + h->poff[h->t_pc_w];
-        hw.wvc = P + h->poff[h->t_vc_w];
-        hw.gx = w->gX;
-        hw.hpart = w->hpart;
-        if (NB > 0) {
-            hw.z2 = w->z2[NB - 1];
-            hw.mean2 = w->bmean + bd[h->bn_blk[NB - 1].second].out_off;
-            hw.pa = w->part_a;
-            hw.pb = w->part_b;
-        }
-        hw.M = M;
-        AZG_CK(launch_heads_bwd_fused(C, NB > 0, hw, st), "train: heads_bwd_fused");
-        // policy_conv.weight [2][C] then value_conv.weight [C]: partial layout [t][3][C]
-        hipLaunchKernelGGL(reduce_partials_kernel, dim3((3 * C + 15) / 16), dim3(256), 0, st, w->hpart, hntile, 3 * C,
-                           G + h->poff[h->t_pc_w], G + h->poff[h->t_vc_w], 2 * C, 0, C);
-        AZG_CK(hipGetLastError(), "train: heads proj wgrad");
-        prof_end(h, pr, st);
     } else {
-        int pr = prof_begin(h, AZG_PROF_TRAIN_OTHER, st);
-        AZG_CK(launch_heads_project(C, false, X, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], nullptr, nullptr,
-                                    w->zh, M, st),
-               "train: heads_project");
-        hipLaunchKernelGGL(head_stats_partial_kernel, dim3(3, HSC), dim3(256), 0, st, w->zh, B, w->hspart);
-        AZG_CK(hipGetLastError(), "train: head_stats_partial");
-        hipLaunchKernelGGL(head_stats_finalize_kernel, dim3(1), dim3(64), 0, st, w->hspart, B, bdd, h->bn_pol,
-                           h->bn_val, P, h->bn, w->bmean, w->binv, w->bscale, w->bshift, h->nbt,
-                           (int)h->bn_desc.size());
-        AZG_CK(hipGetLastError(), "train: head_stats_finalize");
-        const int ho = bd[h->bn_pol].out_off;   // policy ch0, ch1, value: contiguous
-        const int gH = grid_for((int64_t)B * 3 * PIX);
         hipLaunchKernelGGL(head_bn_apply_kernel, dim3(gH), dim3(256), 0, st, w->zh, w->bscale + ho, w->bshift + ho,
                            w->fp, w->fv, B);
         AZG_CK(hipGetLastError(), "train: head_bn_apply");
-        const float* wpf = P + h->poff[h->t_pfc_w];
-        const float* wv1 = P + h->poff[h->t_vfc1_w];
         {   // logits / value hidden pre-activations
             GemmProb a{w->fp, 2 * PIX, 1, wpf, 1, 2 * PIX, w->lpre, ACTIONS, 1, nullptr, 0, 0, B, ACTIONS, 2 * PIX};
             GemmProb b{w->fv, PIX, 1, wv1, 1, PIX, w->hpre, VHID, 1, nullptr, 0, 0, B, VHID, PIX};
@@ -1288,19 +1300,40 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         hipLaunchKernelGGL(head_bn_bwd_finalize_kernel, dim3(1), dim3(64), 0, st, w->hspart, B, bdd, h->bn_pol,
                            h->bn_val, P, G, w->binv, w->hbw);
         AZG_CK(hipGetLastError(), "train: head_bn_bwd_finalize");
+    }
+    if (fh & 4) {
+        HeadBwdArgs hw{};
+        hw.act = X;
+        hw.zh = w->zh;
+        hw.dfp = w->dfp;
+        hw.dfv = w->dfv;
+        hw.hmean = w->bmean + ho;
+        hw.hb = w->hbw;
+        hw.wpc = P + h->poff[h->t_pc_w];
+        hw.wvc = P + h->poff[h->t_vc_w];
+        hw.gx = w->gX;
+        hw.hpart = w->hpart;
+        if (NB > 0) {
+            hw.z2 = w->z2[NB - 1];
+            hw.mean2 = w->bmean + bd[h->bn_blk[NB - 1].second].out_off;
+            hw.pa = w->part_a;
+            hw.pb = w->part_b;
+        }
+        hw.M = M;
+        AZG_CK(launch_heads_bwd_fused(C, NB > 0, hw, st), "train: heads_bwd_fused");
+    } else {
         hipLaunchKernelGGL(head_bn_bwd_apply_kernel, dim3(gH), dim3(256), 0, st, w->zh, w->dfp, w->dfv, w->bmean + ho,
                            w->hbw, w->dzh, B);
         AZG_CK(hipGetLastError(), "train: head_bn_bwd_apply");
-        const int hntile = (M + HROWS - 1) / HROWS;
         hipLaunchKernelGGL((heads_bwd_proj_kernel<C>), dim3(hntile), dim3(256), 0, st, X, w->dzh,
                            P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], w->gX, w->hpart, M);
         AZG_CK(hipGetLastError(), "train: heads_bwd_proj");
-        // policy_conv.weight [2][C] then value_conv.weight [C]: partial layout [t][3][C]
-        hipLaunchKernelGGL(reduce_partials_kernel, dim3((3 * C + 15) / 16), dim3(256), 0, st, w->hpart, hntile, 3 * C,
-                           G + h->poff[h->t_pc_w], G + h->poff[h->t_vc_w], 2 * C, 0, C);
-        AZG_CK(hipGetLastError(), "train: heads proj wgrad");
-        prof_end(h, pr, st);
     }
+    // policy_conv.weight [2][C] then value_conv.weight [C]: partial layout [t][3][C]
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3((3 * C + 15) / 16), dim3(256), 0, st, w->hpart, hntile, 3 * C,
+                       G + h->poff[h->t_pc_w], G + h->poff[h->t_vc_w], 2 * C, 0, C);
+    AZG_CK(hipGetLastError(), "train: heads proj wgrad");
+    prof_end(h, pr, st);
     auto snap = [&](int k) -> int32_t {
         if (!w->snap.empty())
             AZG_CK(hipMemcpyAsync(w->snap[k], w->gX, (size_t)B * PADPIX * C * sizeof(float), hipMemcpyDeviceToDevice, st),
@@ -1313,7 +1346,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     // epilogue of the dgrad conv that produces its gradient (XE_BNBWD, per 128-row
     // tile); the last block's gradient comes from the heads (separate reduction).
     int bwd_nt = ntt;
-    if (NB > 0 && g_train_fuse_heads) {
+    if (NB > 0 && (g_train_fuse_heads & 4)) {
         bwd_nt = hntile;   // S dy, S (z - mean) dy per 128-row tile from heads_bwd_fused_kernel
     } else if (NB > 0) {
         R(bwd_reduce(w->gX, w->xo[NB - 1], w->z2[NB - 1], h->bn_blk[NB - 1].second));
@@ -1332,7 +1365,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
                w->z1[i], h->bn_blk[i].first, ffin ? h->bn_blk[i].first : -1));
         if (!ffin) R(bwd_fin(h->bn_blk[i].first, ntt));
         R(reuse(1));
-        R(bwd_apply(w->DH, w->hh[i], w->z1[i], h->bn_blk[i].first, dzbuf[1], nullptr));
+        R(bwd_apply(w->DH, w->hh[i], w->z1[i], h->bn_blk[i].first, dzbuf[1], nullptr, true));
         R(wgrad(1, Xin, h->t_blk[i].w1));
         R(conv(EPI_ADD, XE_BNBWD, dzbuf[1], w->wdpack + (size_t)(2 * i) * 9 * C * C, w->GR, w->gX, Xin, zin, lin,
                ffin ? lin : -1));
@@ -1348,7 +1381,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         bwd_nt = ntile;
     }
     if (!done_fin) R(bwd_fin(h->bn_stem, bwd_nt));
-    R(bwd_apply(w->gX, w->a0, w->z0, h->bn_stem, w->DH, nullptr));
+    R(bwd_apply(w->gX, w->a0, w->z0, h->bn_stem, w->DH, nullptr, true));
     hipLaunchKernelGGL((stem_wgrad_kernel<C>), dim3(B * STEM_WG_CHUNKS), dim3(256), 0, st, x, w->DH, w->spart);
     AZG_CK(hipGetLastError(), "train: stem_wgrad");
     hipLaunchKernelGGL(reduce_partials_kernel, dim3((27 * C + 15) / 16), dim3(256), 0, st, w->spart, B * STEM_WG_CHUNKS, 27 * C,
@@ -1365,7 +1398,19 @@ int32_t train_backward(azg_pv* h, const float* x, const float* pis, const float*
 {
     if (int32_t r = ensure_train_ws(h, B, st)) return r;
     TrainWS* w = ws_of(h);
-    if (int32_t r = repack(h, st, w->wdpack)) return r;
+    if (g_train_split_pack && !g_wgrad_serial) {
+        // the stem's pack on this stream; the residual convs' forward + dgrad packs and
+        // the head FCs on the side stream, overlapping the stem and its statistics (the
+        // first residual conv waits for them, train_backward_t)
+        AZG_CK(hipEventRecord(w->ev_pack_in, st), "train: event record");
+        AZG_CK(hipStreamWaitEvent(w->side, w->ev_pack_in, 0), "train: stream wait");
+        if (int32_t r = repack(h, st, w->wdpack, 1)) return r;
+        if (int32_t r = repack(h, w->side, w->wdpack, 2)) return r;
+        AZG_CK(hipEventRecord(w->ev_pack, w->side), "train: event record");
+        w->pack_pending = true;
+    } else if (int32_t r = repack(h, st, w->wdpack)) {
+        return r;
+    }
     const int C = h->C;
     int32_t r;
     switch (C) {
@@ -1388,16 +1433,14 @@ int32_t train_apply(azg_pv* h, float* exp_avg, float* exp_avg_sq, int64_t step, 
     int pr = prof_begin(h, AZG_PROF_TRAIN_OTHER, st);
     hipLaunchKernelGGL(grad_sqsum_kernel, dim3(nb), dim3(256), 0, st, h->grads, n, w->npart);
     AZG_CK(hipGetLastError(), "apply: grad_sqsum");
-    hipLaunchKernelGGL(grad_norm_finalize_kernel, dim3(1), dim3(256), 0, st, w->npart, nb, max_norm, w->scal,
-                       total_norm);
-    AZG_CK(hipGetLastError(), "apply: grad_norm_finalize");
     const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
     const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
     const float lr_bc1 = (float)((double)lr / bc1);
     const float bc2_sqrt = (float)std::sqrt(bc2);
-    hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, st, h->params, h->grads, exp_avg, exp_avg_sq,
-                       n, w->scal, lr_bc1, (float)(1.0 - (double)beta1), beta2, (float)(1.0 - (double)beta2),
-                       bc2_sqrt, eps, wd);
+    // 1024 workgroups, grid-stride: each reduces the 1024 norm partials (8 KB) itself
+    hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n) < 1024 ? grid_for(n) : 1024), dim3(256), 0, st, h->params,
+                       h->grads, exp_avg, exp_avg_sq, n, w->npart, nb, max_norm, w->scal, total_norm, lr_bc1,
+                       (float)(1.0 - (double)beta1), beta2, (float)(1.0 - (double)beta2), bc2_sqrt, eps, wd);
     AZG_CK(hipGetLastError(), "apply: adam");
     prof_end(h, pr, st);
     h->dirty = true;

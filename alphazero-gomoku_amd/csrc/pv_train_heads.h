@@ -33,6 +33,7 @@ struct HeadBoardArgs {
     const float* hscale;
     const float* hshift;
     const float* hinv;
+    const float* wfc;      // packed policy_fc + value_fc1 rows [289][456] (pv_pack.hip), zero-padded
     const float* wpf;      // policy_fc.weight [225][450], bias [225]
     const float* bpf;
     const float* wv1;      // value_fc1.weight [64][225], bias [64]

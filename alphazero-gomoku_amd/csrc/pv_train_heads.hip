@@ -28,6 +28,21 @@
 // its plain loads.
 #include "pv_train_heads.h"
 
+#ifdef AZG_HB_TIMING   // ad-hoc phase timing (wall clock, 100 MHz), never in the product
+#define HBT_DECL unsigned long long hbt_[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define HBT(i) do { if (threadIdx.x == 0) hbt_[i] = wall_clock64(); } while (0)
+#define HBT_MID(n) do { if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1)) \
+    printf("HBT %s blk %d mid %llu | %llu %llu %llu %llu %llu %llu %llu\n", n, (int)blockIdx.x, hbt_[0], \
+           hbt_[1] - hbt_[0], hbt_[2] - hbt_[0], hbt_[3] - hbt_[0], hbt_[4] - hbt_[0], hbt_[5] - hbt_[0], \
+           hbt_[6] - hbt_[0], hbt_[7] - hbt_[0]); } while (0)
+#define HBT_END(n) do { if (threadIdx.x == 0) printf("HBT %s last %d start %llu end %llu\n", n, \
+    (int)blockIdx.x, hbt_[0], wall_clock64() - hbt_[0]); } while (0)
+#else
+#define HBT_DECL
+#define HBT(i)
+#define HBT_MID(n)
+#define HBT_END(n)
+#endif
 namespace azg {
 
 constexpr int HP_ROWS = 64;     // pixels per workgroup of head_proj_stats_kernel
@@ -87,6 +102,7 @@ __global__ __launch_bounds__(256) void head_proj_stats_kernel(const HeadStatsArg
             ss[0][i] = a.scale[i];
             ss[1][i] = a.shift[i];
         }
+    HBT_DECL; HBT(0);
     __syncthreads();
     const int q = threadIdx.x & 3;
     const int m = blockIdx.x * HP_ROWS + (threadIdx.x >> 2);
@@ -94,14 +110,20 @@ __global__ __launch_bounds__(256) void head_proj_stats_kernel(const HeadStatsArg
     if (m < a.M) {
         const int o = pad_off(m, C) + q * Q;
         const __amdgpu_buffer_rsrc_t ars = wt_rsrc(a.aout, padded_bytes(a.M, C));
+        // every load of the row issued before the first store (stores may alias them)
+        f32x4 zv[Q / 4], rv[APPLY ? Q / 4 : 1];
 #pragma unroll
         for (int c = 0; c < Q; c += 4) {
-            f32x4 v = *(const f32x4*)(a.z + o + c);
-            if (APPLY) {   // = bn_apply_kernel<C, true>: relu(z * scale + shift + res)
-                const f32x4 r = *(const f32x4*)(a.res + o + c);
+            zv[c / 4] = *(const f32x4*)(a.z + o + c);
+            if (APPLY) rv[c / 4] = *(const f32x4*)(a.res + o + c);
+        }
 #pragma unroll
-                for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k] * ss[0][q * Q + c + k] + ss[1][q * Q + c + k] + r[k], 0.f);
-                store4<true>(a.aout, ars, o + c, v);
+        for (int c = 0; c < Q; c += 4) {
+            f32x4 v = zv[c / 4];
+            if (APPLY) {   // = bn_apply_kernel<C, true>: relu(z * scale + shift + res)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    v[k] = fmaxf(v[k] * ss[0][q * Q + c + k] + ss[1][q * Q + c + k] + rv[c / 4][k], 0.f);
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -109,7 +131,11 @@ __global__ __launch_bounds__(256) void head_proj_stats_kernel(const HeadStatsArg
                 d1 = fmaf(v[k], w[1][q * Q + c + k], d1);
                 d2 = fmaf(v[k], w[2][q * Q + c + k], d2);
             }
+            zv[c / 4] = v;
         }
+        if (APPLY)
+#pragma unroll
+            for (int c = 0; c < Q; c += 4) store4<true>(a.aout, ars, o + c, zv[c / 4]);
     }
 #pragma unroll
     for (int o = 1; o < 4; o <<= 1) {   // = heads_project's reduction order
@@ -135,19 +161,37 @@ __global__ __launch_bounds__(256) void head_proj_stats_kernel(const HeadStatsArg
 #pragma unroll
         for (int k = 0; k < 6; ++k) red[wid][k] = v[k];
     __syncthreads();
+    HBT(1);
     if (threadIdx.x < 6)
         st_wt_d(a.part + (size_t)blockIdx.x * 6 + threadIdx.x,
                 (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]));
+    HBT(7); HBT_MID("proj");
     if (!last_arrival(a.cnt, gridDim.x, &flag)) return;
-    // finalize: every workgroup's sums in workgroup order (lane j: workgroups j, j+64, ...)
+    // finalize: thread t sums workgroups t, t + 256, ... (all loads issued first), then a
+    // fixed-order block reduction
     const int nwg = gridDim.x;
+    double s[6] = {0, 0, 0, 0, 0, 0};
+    for (int g0 = threadIdx.x; g0 < nwg; g0 += 512) {
+        double x0[6], x1[6];
+        const bool two = g0 + 256 < nwg;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            x0[k] = a.part[(size_t)g0 * 6 + k];
+            x1[k] = two ? a.part[(size_t)(g0 + 256) * 6 + k] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) s[k] += x0[k] + x1[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s[k] = wsum_d(s[k]);
+    __syncthreads();
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) red[wid][k] = s[k];
+    __syncthreads();
     if (wid == 0) {
-        double s[6] = {0, 0, 0, 0, 0, 0};
-        for (int g = lane; g < nwg; g += 64)
 #pragma unroll
-            for (int k = 0; k < 6; ++k) s[k] += a.part[(size_t)g * 6 + k];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) s[k] = wsum_d(s[k]);
+        for (int k = 0; k < 6; ++k) s[k] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
         if (lane < 3) {   // = head_stats_finalize_kernel
             const int ch = lane;
             const BnDesc d = a.desc[ch < 2 ? a.pol_layer : a.val_layer];
@@ -175,12 +219,13 @@ __global__ __launch_bounds__(256) void head_proj_stats_kernel(const HeadStatsArg
     }
     if (a.nbt)
         for (int i = threadIdx.x; i < a.nbn; i += 256) a.nbt[i] += 1;
+    HBT_END("proj");
 }
 
-__global__ __launch_bounds__(256) void head_board_kernel(const HeadBoardArgs a)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void head_board_kernel(const HeadBoardArgs a)
 {
-    __shared__ float fps[HB_BOARDS][2 * PIX];
-    __shared__ float fvs[HB_BOARDS][PIX];
+    constexpr int FK = 512;   // feature row: policy 450 (zero pads to 512) | value 225 (zero pads to 512)
+    __shared__ __attribute__((aligned(16))) float fb[HB_BOARDS][2][FK];
     __shared__ float lgs[HB_BOARDS][ACTIONS];
     __shared__ float dls[HB_BOARDS][ACTIONS];
     __shared__ float hps[HB_BOARDS][VHID];
@@ -190,44 +235,125 @@ __global__ __launch_bounds__(256) void head_board_kernel(const HeadBoardArgs a)
     __shared__ double lss[HB_BOARDS][2];
     __shared__ double red[4][6];
     __shared__ unsigned flag;
+    constexpr int KC = 64, LDW = KC + 4;                         // fc weight chunk [289][64 + 4]
+    __shared__ __attribute__((aligned(16))) float lwbuf[FC_OUT * LDW];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int b0 = blockIdx.x * HB_BOARDS;
+    HBT_DECL; HBT(0);
     const int nb = min(HB_BOARDS, a.B - b0);
-    // head BN + ReLU (= head_bn_apply_kernel)
-    for (int i = tid; i < HB_BOARDS * 3 * PIX; i += 256) {
-        const int bb = i / (3 * PIX), k = i - bb * 3 * PIX, ch = k / PIX;
-        float y = 0.f;
-        if (bb < nb) y = fmaxf(a.zh[(size_t)(b0 + bb) * 3 * PIX + k] * a.hscale[ch] + a.hshift[ch], 0.f);
-        if (ch < 2) {
-            fps[bb][k] = y;
-            if (bb < nb) a.fp[(size_t)(b0 + bb) * 2 * PIX + k] = y;
-        } else {
-            fvs[bb][k - 2 * PIX] = y;
-            if (bb < nb) a.fv[(size_t)(b0 + bb) * PIX + k - 2 * PIX] = y;
-        }
-    }
-    __syncthreads();
-    // policy_fc / value_fc1 forward: wave w takes output rows w, w+4, ...; lanes split K
-    for (int j = wid; j < ACTIONS + VHID; j += 4) {
-        const bool pol = j < ACTIONS;
-        const float* wr = pol ? a.wpf + (size_t)j * 2 * PIX : a.wv1 + (size_t)(j - ACTIONS) * PIX;
-        const int K = pol ? 2 * PIX : PIX;
-        float s[HB_BOARDS] = {0.f, 0.f, 0.f, 0.f};
-        for (int k = lane; k < K; k += 64) {
-            const float wk = wr[k];
+    // head BN + ReLU (= head_bn_apply_kernel); feature pads and absent boards are 0.
+    // Every zh load of the thread first (the feature stores may alias them)
+    constexpr int NA = (HB_BOARDS * 2 * FK) / 256;   // 16 items per thread
+    {
+        const float hs0 = a.hscale[0], hs1 = a.hscale[1], hs2 = a.hscale[2];
+        const float ht0 = a.hshift[0], ht1 = a.hshift[1], ht2 = a.hshift[2];
+        float zv[NA];
 #pragma unroll
-            for (int bb = 0; bb < HB_BOARDS; ++bb) s[bb] = fmaf(pol ? fps[bb][k] : fvs[bb][k], wk, s[bb]);
+        for (int u = 0; u < NA; ++u) {
+            const int i = tid + 256 * u;
+            const int bb = i / (2 * FK), pol = ((i / FK) & 1) == 0, kk = i & (FK - 1);
+            const bool in = bb < nb && kk < (pol ? 2 * PIX : PIX);
+            zv[u] = in ? a.zh[(size_t)(b0 + bb) * 3 * PIX + (pol ? kk : 2 * PIX + kk)] : 0.f;
         }
 #pragma unroll
-        for (int bb = 0; bb < HB_BOARDS; ++bb) s[bb] = wave_sum(s[bb]);
-        if (lane == 0)
+        for (int u = 0; u < NA; ++u) {
+            const int i = tid + 256 * u;
+            const int bb = i / (2 * FK), pol = ((i / FK) & 1) == 0, kk = i & (FK - 1);
+            const bool in = bb < nb && kk < (pol ? 2 * PIX : PIX);
+            const int ch = pol ? (kk < PIX ? 0 : 1) : 2;
+            const float sc = ch == 0 ? hs0 : ch == 1 ? hs1 : hs2, sh = ch == 0 ? ht0 : ch == 1 ? ht1 : ht2;
+            const float y = in ? fmaxf(zv[u] * sc + sh, 0.f) : 0.f;
+            fb[bb][pol ? 0 : 1][kk] = y;
+            zv[u] = y;
+        }
 #pragma unroll
-            for (int bb = 0; bb < HB_BOARDS; ++bb) {
-                if (pol) lgs[bb][j] = s[bb];
-                else hps[bb][j - ACTIONS] = s[bb];
+        for (int u = 0; u < NA; ++u) {
+            const int i = tid + 256 * u;
+            const int bb = i / (2 * FK), pol = ((i / FK) & 1) == 0, kk = i & (FK - 1);
+            if (bb < nb && kk < (pol ? 2 * PIX : PIX)) {
+                if (pol) a.fp[(size_t)(b0 + bb) * 2 * PIX + kk] = zv[u];
+                else a.fv[(size_t)(b0 + bb) * PIX + kk] = zv[u];
             }
+        }
+    }
+    HBT(1);
+    // policy_fc / value_fc1 forward on the packed rows wfc[289][456] (16-B aligned, zero
+    // pads), staged through LDS in K chunks of 64: every thread issues its share of a
+    // chunk's 289 x 64 floats (19 float4, coalesced 256-B row pieces) at once, the next
+    // chunk's loads are issued before the current chunk's FMAs.  Thread t owns output row
+    // t (wave 0 also row t + 256); the features are LDS broadcasts, the K loop is fully
+    // unrolled (the last chunk's columns past 456 are zero weights and zero features)
+    {
+        constexpr int NCH = (FC_KP + KC - 1) / KC;            // 8 chunks
+        constexpr int NV4 = (FC_OUT * KC / 4 + 255) / 256;    // float4 loads per thread per chunk (19)
+        float* wl = lwbuf;
+        f32x4 wv[NV4];
+        auto load = [&](int c) {
+            const int k0 = c * KC;
+#pragma unroll
+            for (int u = 0; u < NV4; ++u) {
+                const int e = tid + 256 * u;                  // float4 index in the chunk
+                const int r = e / (KC / 4), q = e - r * (KC / 4);
+                wv[u] = (r < FC_OUT && k0 + 4 * q < FC_KP)
+                            ? *(const f32x4*)(a.wfc + (size_t)r * FC_KP + k0 + 4 * q)
+                            : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        };
+        float s0[HB_BOARDS] = {0.f, 0.f, 0.f, 0.f}, s1[HB_BOARDS] = {0.f, 0.f, 0.f, 0.f};
+        const int j0 = tid, j1 = tid + 256;                   // j1 < 289 only in wave 0
+        const float* f0 = &fb[0][j0 < ACTIONS ? 0 : 1][0];    // policy rows: policy features
+        const float* f1 = &fb[0][1][0];
+        const float* w0p = wl + j0 * LDW;
+        const float* w1p = wl + min(j1, FC_OUT - 1) * LDW;
+        load(0);
+        for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+            for (int u = 0; u < NV4; ++u) {
+                const int e = tid + 256 * u;
+                const int r = e / (KC / 4), q = e - r * (KC / 4);
+                if (r < FC_OUT) *(f32x4*)(wl + r * LDW + 4 * q) = wv[u];
+            }
+            __syncthreads();
+            if (c + 1 < NCH) load(c + 1);
+            const int k0 = c * KC;
+            if (wid == 0) {
+#pragma unroll
+                for (int k = 0; k < KC; k += 4) {
+                    const f32x4 w0 = *(const f32x4*)(w0p + k), w1 = *(const f32x4*)(w1p + k);
+#pragma unroll
+                    for (int bb = 0; bb < HB_BOARDS; ++bb) {
+                        const f32x4 x0 = *(const f32x4*)(f0 + bb * 2 * FK + k0 + k);
+                        const f32x4 x1 = *(const f32x4*)(f1 + bb * 2 * FK + k0 + k);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            s0[bb] = fmaf(x0[e], w0[e], s0[bb]);
+                            s1[bb] = fmaf(x1[e], w1[e], s1[bb]);
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < KC; k += 4) {
+                    const f32x4 w0 = *(const f32x4*)(w0p + k);
+#pragma unroll
+                    for (int bb = 0; bb < HB_BOARDS; ++bb) {
+                        const f32x4 x0 = *(const f32x4*)(f0 + bb * 2 * FK + k0 + k);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) s0[bb] = fmaf(x0[e], w0[e], s0[bb]);
+                    }
+                }
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int bb = 0; bb < HB_BOARDS; ++bb) {
+            if (j0 < ACTIONS) lgs[bb][j0] = s0[bb];
+            else hps[bb][j0 - ACTIONS] = s0[bb];
+            if (j1 < FC_OUT) hps[bb][j1 - ACTIONS] = s1[bb];
+        }
     }
     __syncthreads();
+    HBT(2);
     // loss and output gradients, one wave per board (= heads_loss_kernel)
     {
         const int bb = wid, b = b0 + bb;
@@ -291,40 +417,128 @@ __global__ __launch_bounds__(256) void head_board_kernel(const HeadBoardArgs a)
         }
     }
     __syncthreads();
-    // fc data gradients with the ReLU masks (= small_gemm dgrad): thread k of the
-    // 450 policy features and 225 value features; head-BN backward partials
+    HBT(3);
+    // fc data gradients with the ReLU masks (= small_gemm dgrad) on the packed rows:
+    // thread t owns the float4 column group cg = t & 127 (< 114) of wfc and the row half
+    // h = t >> 7: policy rows [113 h, 113 h + 113) (-> policy features 4 cg .. 4 cg + 3)
+    // and, for cg < 57, value rows [32 h, 32 h + 32) (-> value features 4 cg ..).  Rows in
+    // batches of 16 float4 loads, the next batch issued before the current one's FMAs;
+    // the two halves are added in LDS (half 0 + half 1)
     double hs[6] = {0, 0, 0, 0, 0, 0};   // (S dy, S (z - mean) dy) for ch 0, 1, 2
-    for (int k = tid; k < 2 * PIX + PIX; k += 256) {
-        const bool pol = k < 2 * PIX;
-        const int kk = pol ? k : k - 2 * PIX;
-        float s[HB_BOARDS] = {0.f, 0.f, 0.f, 0.f};
-        if (pol) {
-            for (int j = 0; j < ACTIONS; ++j) {
-                const float wjk = a.wpf[(size_t)j * 2 * PIX + kk];
-#pragma unroll
-                for (int bb = 0; bb < HB_BOARDS; ++bb) s[bb] = fmaf(dls[bb][j], wjk, s[bb]);
-            }
-        } else {
-            for (int u = 0; u < VHID; ++u) {
-                const float wuk = a.wv1[(size_t)u * PIX + kk];
-#pragma unroll
-                for (int bb = 0; bb < HB_BOARDS; ++bb) s[bb] = fmaf(dhs[bb][u], wuk, s[bb]);
-            }
-        }
-        const int ch = pol ? kk / PIX : 2;
-        const int p = pol ? kk - ch * PIX : kk;
-        const double mu = (double)a.hmean[ch];
+    {
+        constexpr int NCG = FC_KP / 4, NCV = (PIX + 3) / 4;     // 114 policy, 57 value column groups
+        constexpr int PH = (ACTIONS + 1) / 2, VH = VHID / 2;     // 113 / 32 rows per half
+        constexpr int RB = 16;
+        const int cg = tid & 127, h = tid >> 7;
+        const bool act = cg < NCG, vact = cg < NCV;
+        const int pr0 = h * PH, pr1 = min(ACTIONS, pr0 + PH);    // policy rows of this half
+        const int np = pr1 - pr0;                                // 113 or 112
+        const int nrows = np + (vact ? VH : 0);                  // this thread's rows: policy then value
+        f32x4 ap[HB_BOARDS], av[HB_BOARDS];
 #pragma unroll
         for (int bb = 0; bb < HB_BOARDS; ++bb) {
-            if (bb >= nb) continue;
-            const float f = pol ? fps[bb][kk] : fvs[bb][kk];
-            const float d = f > 0.f ? s[bb] : 0.f;
-            const int b = b0 + bb;
-            if (pol) a.dfp[(size_t)b * 2 * PIX + kk] = d;
-            else a.dfv[(size_t)b * PIX + kk] = d;
-            const double zz = (double)a.zh[(size_t)b * 3 * PIX + ch * PIX + p];
-            hs[2 * ch] += (double)d;
-            hs[2 * ch + 1] += (zz - mu) * (double)d;
+            ap[bb] = f32x4{0.f, 0.f, 0.f, 0.f};
+            av[bb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        // row r of this thread: r < np -> wfc row pr0 + r (policy, d = dls), else value
+        // row ACTIONS + 32 h + (r - np) (d = dhs)
+        auto wrow = [&](int r) {
+            return r < np ? pr0 + r : ACTIONS + VH * h + (r - np);
+        };
+        f32x4 wa[RB], wb[RB];
+#define HB_LD(W, R0)                                                                                    \
+    _Pragma("unroll") for (int u = 0; u < RB; ++u) {                                                    \
+        const int r = (R0) + u;                                                                         \
+        W[u] = (act && r < nrows) ? *(const f32x4*)(a.wfc + (size_t)wrow(r) * FC_KP + 4 * cg)           \
+                                  : f32x4{0.f, 0.f, 0.f, 0.f};                                          \
+    }
+#define HB_USE(W, R0)                                                                                   \
+    _Pragma("unroll") for (int u = 0; u < RB; ++u) {                                                    \
+        const int r = (R0) + u;                                                                         \
+        if (r < np) {                                                                                   \
+            const int j = pr0 + r;                                                                      \
+            _Pragma("unroll") for (int bb = 0; bb < HB_BOARDS; ++bb) {                                  \
+                const float d = dls[bb][j];                                                             \
+                _Pragma("unroll") for (int e = 0; e < 4; ++e) ap[bb][e] = fmaf(d, W[u][e], ap[bb][e]);  \
+            }                                                                                           \
+        } else if (r < nrows) {                                                                         \
+            const int jv = VH * h + (r - np);                                                           \
+            _Pragma("unroll") for (int bb = 0; bb < HB_BOARDS; ++bb) {                                  \
+                const float d = dhs[bb][jv];                                                            \
+                _Pragma("unroll") for (int e = 0; e < 4; ++e) av[bb][e] = fmaf(d, W[u][e], av[bb][e]);  \
+            }                                                                                           \
+        }                                                                                               \
+    }
+        constexpr int MAXR = PH + VH;                            // 145 rows at most
+        HB_LD(wa, 0)
+        for (int r0 = 0; r0 < MAXR; r0 += 2 * RB) {
+            HB_LD(wb, r0 + RB)
+            HB_USE(wa, r0)
+            if (r0 + 2 * RB < MAXR) {
+                HB_LD(wa, r0 + 2 * RB)
+            }
+            HB_USE(wb, r0 + RB)
+        }
+#undef HB_LD
+#undef HB_USE
+        // halves: half 1 parks its sums in the (free) weight-chunk LDS, half 0 adds them
+        f32x4* park = (f32x4*)lwbuf;                             // [2][HB_BOARDS][128]
+        if (h == 1)
+#pragma unroll
+            for (int bb = 0; bb < HB_BOARDS; ++bb) {
+                park[(0 * HB_BOARDS + bb) * 128 + cg] = ap[bb];
+                park[(1 * HB_BOARDS + bb) * 128 + cg] = av[bb];
+            }
+        __syncthreads();
+        if (h == 0 && act) {
+#pragma unroll
+            for (int bb = 0; bb < HB_BOARDS; ++bb) {
+                const f32x4 p1 = park[(0 * HB_BOARDS + bb) * 128 + cg], v1 = park[(1 * HB_BOARDS + bb) * 128 + cg];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    ap[bb][e] += p1[e];
+                    av[bb][e] += v1[e];
+                }
+            }
+            // masks, stores and the head BN-backward sums: policy features k = 4 cg + e
+            // (k < 450: channel k / 225), value features k = 4 cg + e (k < 225: channel 2)
+            float zp[HB_BOARDS][4], zq[HB_BOARDS][4];
+#pragma unroll
+            for (int bb = 0; bb < HB_BOARDS; ++bb)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int k = 4 * cg + e;
+                    const bool ok = bb < nb;
+                    zp[bb][e] = ok && k < 2 * PIX ? a.zh[(size_t)(b0 + bb) * 3 * PIX + k] : 0.f;
+                    zq[bb][e] = ok && vact && k < PIX ? a.zh[(size_t)(b0 + bb) * 3 * PIX + 2 * PIX + k] : 0.f;
+                }
+            const double mu0 = (double)a.hmean[0], mu1 = (double)a.hmean[1], mu2 = (double)a.hmean[2];
+#pragma unroll
+            for (int bb = 0; bb < HB_BOARDS; ++bb) {
+                if (bb >= nb) continue;
+                const int b = b0 + bb;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int k = 4 * cg + e;
+                    if (k < 2 * PIX) {
+                        const float d = fb[bb][0][k] > 0.f ? ap[bb][e] : 0.f;
+                        a.dfp[(size_t)b * 2 * PIX + k] = d;
+                        if (k < PIX) {
+                            hs[0] += (double)d;
+                            hs[1] += ((double)zp[bb][e] - mu0) * (double)d;
+                        } else {
+                            hs[2] += (double)d;
+                            hs[3] += ((double)zp[bb][e] - mu1) * (double)d;
+                        }
+                    }
+                    if (vact && k < PIX) {
+                        const float d = fb[bb][1][k] > 0.f ? av[bb][e] : 0.f;
+                        a.dfv[(size_t)b * PIX + k] = d;
+                        hs[4] += (double)d;
+                        hs[5] += ((double)zq[bb][e] - mu2) * (double)d;
+                    }
+                }
+            }
         }
     }
 #pragma unroll
@@ -333,6 +547,7 @@ __global__ __launch_bounds__(256) void head_board_kernel(const HeadBoardArgs a)
 #pragma unroll
         for (int k = 0; k < 6; ++k) red[wid][k] = hs[k];
     __syncthreads();
+    HBT(6);
     double* pd = a.pd + (size_t)blockIdx.x * HB_PD;
     float* pf = a.pf + (size_t)blockIdx.x * HB_PF;
     if (tid < 6) st_wt_d(pd + tid, (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]));
@@ -349,8 +564,9 @@ __global__ __launch_bounds__(256) void head_board_kernel(const HeadBoardArgs a)
         }
         st_wt_f(pf + o, s);
     }
+    HBT(7); HBT_MID("board");
     if (!last_arrival(a.cnt, gridDim.x, &flag)) return;
-    // finalize over workgroups in order
+    // finalize over workgroups in order; every load of a group issued before its sums
     const int nwg = gridDim.x;
     if (wid == 0) {
         double s[HB_PD];
@@ -383,14 +599,23 @@ __global__ __launch_bounds__(256) void head_board_kernel(const HeadBoardArgs a)
             a.losses[2] = plf + vlf;
         }
     }
+    constexpr int UG = 8;
     for (int o = tid; o < HB_PF; o += 256) {
         float s = 0.f;
-        for (int g = 0; g < nwg; ++g) s += a.pf[(size_t)g * HB_PF + o];
+        for (int g0 = 0; g0 < nwg; g0 += UG) {
+            float v[UG];
+#pragma unroll
+            for (int u = 0; u < UG; ++u) v[u] = g0 + u < nwg ? a.pf[(size_t)(g0 + u) * HB_PF + o] : 0.f;
+#pragma unroll
+            for (int u = 0; u < UG; ++u)
+                if (g0 + u < nwg) s += v[u];
+        }
         if (o < ACTIONS) a.g_pfb[o] = s;
         else if (o < ACTIONS + VHID) a.g_v1b[o - ACTIONS] = s;
         else if (o < ACTIONS + 2 * VHID) a.g_v2w[o - ACTIONS - VHID] = s;
         else a.g_v2b[0] = s;
     }
+    HBT_END("board");
 }
 
 // = head_bn_bwd_apply_kernel (dzh on the fly) + heads_bwd_proj_kernel, and the last

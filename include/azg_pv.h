@@ -186,6 +186,19 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          shared fp64 reduction order, bitwise identical;
  *   key 25: train convs: operand addressing through buffer resources (32,
  *          default) or 64-bit pointers (0); bitwise identical;
+ *   key 26: train conv tile (8: 128x64 with 8 waves, default; 16: 128x128 with 16
+ *          waves, one workgroup per CU); bitwise identical;
+ *   key 27: train conv weight-grad pixel splits (0 = automatic, default); bitwise
+ *          identical only at a fixed value;
+ *   key 28: train head chain, bit mask of the fused stages (bit 0 head projections +
+ *          BN statistics + finalize, also applying the last block's bn2; bit 1 head BN
+ *          apply + FCs + loss + fc data grads per 4 boards; bit 2 head BN-backward +
+ *          1x1 backward + the last block's BN-backward partials); 0 = the 18-launch
+ *          chain; fp32 sums in another order (within the oracle tolerance);
+ *   key 29: train BN-backward ReLU mask formed from z with the layer's scale and
+ *          shift (1, default) or read from the stored activation (0); bitwise identical;
+ *   key 30: train weight repack split over the two streams (1, default) or one launch
+ *          on the caller's stream (0); bitwise identical;
  *   key 31: study build only: the 64x64 / 128x64 towers with sc1 dependent loads
  *          and no acquire (two or more workgroups per CU: outside the microarch
  *          guide's measured envelope; the product uses the acquire there and the

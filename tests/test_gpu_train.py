@@ -166,6 +166,22 @@ def test_gradients_match_oracle(tag, blocks, ch, B):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("fuse", [0, 1, 2, 4, 7])
+@pytest.mark.parametrize("tag,blocks,ch,B", [("3x64", 3, 64, 37), ("6x128", 6, 128, 128)])
+def test_head_chain_variants_match_oracle(fuse, tag, blocks, ch, B):
+    """Every fused head stage (key 28 bits: projections + statistics, per-board FCs +
+    loss, head BN-backward + 1x1 backward) and the 18-launch chain hold the oracle
+    tolerance of test_gradients_match_oracle, at a ragged batch (37: a partial 4-board
+    group) and at the bench's train shape."""
+    import _native
+    lib = _native.load_library()
+    prev = lib.azg_pv_set_tuning(28, fuse)
+    try:
+        test_gradients_match_oracle(tag, blocks, ch, B)
+    finally:
+        lib.azg_pv_set_tuning(28, prev)
+
+
 def fp32_masks(st, blocks, ch, x):
     """The fp32 CPU oracle's own ReLU masks (train-mode forward), NCHW / [B, n]."""
     net = RefModel(blocks, ch).net
@@ -323,7 +339,7 @@ def test_train_then_predict_uses_new_weights():
 
 
 @pytest.mark.parametrize("key,values", [(18, (0, 1, 2, 4, 7)), (12, (0, 1)), (16, (3, 0, 1, 2)), (23, (1, 0)), (24, (1, 0)),
-                                        (25, (32, 0)), (26, (8, 16))])
+                                        (25, (32, 0)), (26, (8, 16)), (29, (1, 0)), (30, (1, 0))])
 def test_train_schedule_keys_bitwise(key, values):
     """Train-step tuning keys change cache policy (18: write-through stores), stream
     schedule (12: weight grads overlapped or serial) or the weight-grad staging (16: LDS-DMA
@@ -331,7 +347,10 @@ def test_train_schedule_keys_bitwise(key, values):
     BN applies run (23: folded into the next conv's halo staging, or separate passes) and
     the BN finalizes (24: by the producing conv's last workgroup, or separate kernels)
     or the train convs' operand addressing (25: buffer resources or 64-bit pointers) or
-    tile (26: 128x64 with 8 waves, or 128x128 with 16 waves at one workgroup per CU):
+    tile (26: 128x64 with 8 waves, or 128x128 with 16 waves at one workgroup per CU) or
+    the BN-backward apply's ReLU mask (29: formed from z with the layer's scale / shift,
+    or read from the stored activation) or the step's weight repack (30: split across
+    the two streams, or one launch):
     two steps from one state must give bitwise-identical params, grads, BN buffers
     and Adam moments under every value."""
     import _native
