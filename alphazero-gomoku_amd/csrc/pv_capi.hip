@@ -132,6 +132,7 @@ int32_t azg_pv_bind(azg_pv* h, float* params, float* grads, float* bn_stats)
     h->grads = grads;
     h->bn = bn_stats;
     h->dirty = true;
+    h->train_packs = false;
     return 0;
 }
 
@@ -148,6 +149,7 @@ int32_t azg_pv_mark_dirty(azg_pv* h)
 {
     if (!h) return fail("azg_pv_mark_dirty: null handle");
     h->dirty = true;
+    h->train_packs = false;
     return 0;
 }
 

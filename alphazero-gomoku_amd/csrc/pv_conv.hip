@@ -991,7 +991,27 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     }
     if (key == 28) {  // train head chain: bit mask of the fused stages (include/azg_pv.h), 0 the 18-launch chain (other sum orders)
         const int prev = azg::g_train_fuse_heads;
-        if (value >= 0 && value <= 7) azg::g_train_fuse_heads = value;
+        if (value >= 0 && value <= 31) azg::g_train_fuse_heads = value;
+        return prev;
+    }
+    if (key == 36) {  // train: next step's weight packs right after Adam (1, default) or at the step start (0); bitwise identical
+        const int prev = azg::g_train_pack_after;
+        if (value == 0 || value == 1) azg::g_train_pack_after = value;
+        return prev;
+    }
+    if (key == 34) {  // train: one dZ buffer per backward conv (1, default) or two alternating + reuse waits (0); bitwise identical
+        const int prev = azg::g_train_dz_all;
+        if (value == 0 || value == 1) azg::g_train_dz_all = value;
+        return prev;
+    }
+    if (key == 33) {  // train: stream hand-off events with a device-scope release (1, default) or system scope (0); bitwise identical
+        const int prev = azg::g_train_ev_device;
+        if (value == 0 || value == 1) azg::g_train_ev_device = value;
+        return prev;
+    }
+    if (key == 32) {  // train: head weight-grad reductions on the side stream (1, default) or the caller's (0); bitwise identical
+        const int prev = azg::g_train_side_heads;
+        if (value == 0 || value == 1) azg::g_train_side_heads = value;
         return prev;
     }
     if (key == 27) {  // train wgrad split-K count (0 automatic; 8..64, multiple of 8); bitwise NOT identical across values
@@ -1016,7 +1036,7 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     }
     if (key == 16) {  // train: wgrad kernel (3 LDS-DMA natural rows, default; 1 K-contiguous, 2 same 2 ahead, 0 row staging; bitwise identical)
         const int prev = azg::g_wgrad_kernel;
-        if (value >= 0 && value <= 3) azg::g_wgrad_kernel = value;
+        if (value >= 0 && value <= 4) azg::g_wgrad_kernel = value;
         return prev;
     }
     if (key == 13) {  // train: wgrad K chunk (32 default, 16 A/B)

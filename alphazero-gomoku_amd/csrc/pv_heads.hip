@@ -182,6 +182,14 @@ hipError_t launch_heads_project(int C, bool bn, const float* act, const float* w
 #undef AZG_PROJ_CASE
 }
 
+// the fc forward alone (train step, key 28 bit 3): feat [B][FC_FS] -> pre [B][FC_OUT]
+hipError_t launch_heads_fc(const float* feat, const float* wfc, float* pre, int B, hipStream_t st)
+{
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(heads_fc, dim3((B + 31) / 32, 10), dim3(256), 0, st, feat, wfc, pre, B);
+    return hipGetLastError();
+}
+
 hipError_t launch_heads_fwd(int C, const float* act, const float* wpc, const float* wvc, const float* hscale,
                             const float* hshift, const float* wfc, const float* bpf,
                             const float* bv1, const float* wv2, const float* bv2, float* hbuf, float* probs,

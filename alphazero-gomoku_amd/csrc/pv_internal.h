@@ -48,6 +48,10 @@ extern int g_wgrad_serial;
 extern int g_train_fuse_apply;
 extern int g_train_fuse_fin;
 extern int g_train_fuse_heads;
+extern int g_train_side_heads;
+extern int g_train_ev_device;
+extern int g_train_dz_all;
+extern int g_train_pack_after;
 extern int g_train_maskz;
 extern int g_train_split_pack;
 extern int g_train_skip;
@@ -75,6 +79,7 @@ hipError_t launch_heads_fwd(int C, const float* act, const float* wpc, const flo
                             const float* wv2, const float* bv2, float* hbuf, float* probs,
                             float* values, float* logits, int B, hipStream_t st,
                             const int8_t* boards = nullptr, float* priors = nullptr);
+hipError_t launch_heads_fc(const float* feat, const float* wfc, float* pre, int B, hipStream_t st);
 hipError_t launch_heads_project(int C, bool bn, const float* act, const float* wpc, const float* wvc,
                                 const float* hscale, const float* hshift, float* hout, int M, hipStream_t st,
                                 int fs = 3 * PIX, int voff = 2 * PIX);
@@ -117,6 +122,7 @@ struct azg_pv {
     float* bn = nullptr;
     int64_t* nbt = nullptr;   // optional: num_batches_tracked per BN layer (azg_pv_bind_counters)
     bool dirty = true;
+    bool train_packs = false;   // wpack / wdpack / wstem / wfc hold the current parameters (train_apply, key 36)
 
     // packed / derived weights (one allocation)
     float* wbase = nullptr;

@@ -59,7 +59,10 @@ struct TrainWS {
     double* hsp1 = nullptr;      // head_proj_stats_kernel [groups][6]
     double* hpd = nullptr;       // head_board_kernel [groups][head_board_pd()]
     float* hpf = nullptr;        // head_board_kernel [groups][head_board_pf()]
-    unsigned* hcnt = nullptr;    // [2] arrival counters (0 between launches)
+    unsigned* hcnt = nullptr;    // [3] arrival counters (0 between launches)
+    double* hdp = nullptr;       // head_dgrad_kernel [groups][6]
+    float* feat = nullptr;       // [B][FC_FS] head features, eval row layout (zero pads)
+    float* pre = nullptr;        // [B][FC_OUT] fc pre-activations (logits | value hidden)
     // optimizer
     double* npart = nullptr;     // grad sq-sum partials
     float* scal = nullptr;       // [0] total norm, [1] clip coef
@@ -70,13 +73,46 @@ struct TrainWS {
     // alternates between DZ and DZ2 so the next BN backward never overwrites a dZ a
     // pending wgrad still reads (ev_ready: dZ written; ev_done: its wgrad finished)
     float* DZ2 = nullptr;
+    // key 34: one dZ buffer per conv (no reuse waits on the caller's stream: every
+    // stream wait is a ~6 us bubble there, measured)
+    std::vector<float*> dzs;
     hipStream_t side = nullptr;
     hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
     // split repack at the start of a step: the stem on the caller's stream, the rest on
     // `side` (ev_pack_in: the step's inputs are ready; ev_pack: the packs are written)
     hipEvent_t ev_pack_in = nullptr, ev_pack = nullptr;
     bool pack_pending = false;
+    // off-critical-path head weight grads moved to `side` (ev_heads), and the join of
+    // everything `side` ran before the optimizer (ev_join)
+    hipEvent_t ev_heads = nullptr, ev_join = nullptr;
+    int ev_flags = -1;           // flags the hand-off events were created with (key 33)
 };
+
+int g_train_dz_all = 1;     // key 34: 1 one dZ buffer per conv (default); 0 two alternating buffers + reuse waits
+int g_train_pack_after = 1; // key 36: 1 the next step's weight packs right after Adam (same stream, no hand-off); 0 at the step start
+int g_train_ev_device = 1;   // key 33: 1 stream hand-off events release at device scope (default); 0 system scope
+
+// (re)create the stream hand-off events: they only order work between two streams of
+// one device, so a device-scope release is enough (hipEventReleaseToDevice); the
+// default system-scope release adds an L2 writeback + invalidate per record
+static hipError_t make_events(TrainWS* w)
+{
+    const int flags = hipEventDisableTiming | (g_train_ev_device ? hipEventReleaseToDevice : 0);
+    if (w->ev_flags == flags) return hipSuccess;
+    hipEvent_t* evs[] = {&w->ev_ready[0], &w->ev_ready[1], &w->ev_done[0], &w->ev_done[1], &w->ev_pack_in,
+                         &w->ev_pack, &w->ev_heads, &w->ev_join};
+    if (w->side) (void)hipStreamSynchronize(w->side);
+    for (hipEvent_t* e : evs) {
+        if (*e) (void)hipEventDestroy(*e);
+        *e = nullptr;
+    }
+    for (hipEvent_t* e : evs) {
+        hipError_t r = hipEventCreateWithFlags(e, flags);
+        if (r != hipSuccess) return r;
+    }
+    w->ev_flags = flags;
+    return hipSuccess;
+}
 
 static TrainWS* ws_of(azg_pv* h) { return (TrainWS*)h->train; }
 
@@ -92,6 +128,8 @@ void free_train_workspace(azg_pv* h)
     }
     if (w->ev_pack_in) (void)hipEventDestroy(w->ev_pack_in);
     if (w->ev_pack) (void)hipEventDestroy(w->ev_pack);
+    if (w->ev_heads) (void)hipEventDestroy(w->ev_heads);
+    if (w->ev_join) (void)hipEventDestroy(w->ev_join);
     if (w->side) (void)hipStreamDestroy(w->side);
     delete w;
     h->train = nullptr;
@@ -412,7 +450,8 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(
     const float* __restrict__ lpre, const float* __restrict__ bpf, const float* __restrict__ hpre,
     const float* __restrict__ bv1, const float* __restrict__ wv2, const float* __restrict__ bv2,
     const float* __restrict__ pis, const float* __restrict__ zs, float* __restrict__ dlogits,
-    float* __restrict__ hv, float* __restrict__ dhv, float* __restrict__ dpre, float* __restrict__ lossb, int B)
+    float* __restrict__ hv, float* __restrict__ dhv, float* __restrict__ dpre, float* __restrict__ lossb, int B,
+    int lps = ACTIONS, int hps = VHID)
 {
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -422,7 +461,7 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         const int j = lane + 64 * t;
-        lg[t] = j < ACTIONS ? lpre[(size_t)b * ACTIONS + j] + bpf[j] : -INFINITY;
+        lg[t] = j < ACTIONS ? lpre[(size_t)b * lps + j] + bpf[j] : -INFINITY;
         mx = fmaxf(mx, lg[t]);
     }
     mx = wave_max(mx);
@@ -455,7 +494,7 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(
             dlogits[(size_t)b * ACTIONS + j] = (expf(lp) * st - tv[t]) * invB;
         }
     }
-    const float hid = fmaxf(hpre[(size_t)b * VHID + lane] + bv1[lane], 0.f);
+    const float hid = fmaxf(hpre[(size_t)b * hps + lane] + bv1[lane], 0.f);
     const float pre = wave_sum(wv2[lane] * hid) + bv2[0];
     const float v = tanhf(pre);
     const float z = zs[b];
@@ -836,6 +875,7 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     while (cap < B) cap *= 2;
     w = new TrainWS();
     h->train = w;
+    h->train_packs = false;   // a fresh dgrad pack buffer
     w->cap = cap;
     const int C = h->C, NB = h->NB;
     const size_t act = (size_t)cap * PADPIX * C;
@@ -857,6 +897,9 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     A(w->DH, act, true);
     A(w->GR, act, true);
     A(w->DZ2, act, true);
+    w->dzs.assign(2 * NB, nullptr);
+    for (int k = 0; k < 2 * NB; ++k) A(w->dzs[k], act, true);
+
     {
         // the weight grads are off the critical path: their stream gets the LOWEST
         // priority so the dependent chain on the caller's stream (BN kernels, dgrad)
@@ -864,12 +907,7 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
         int least = 0, greatest = 0;
         hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
         if (e == hipSuccess) e = hipStreamCreateWithPriority(&w->side, hipStreamNonBlocking, least);
-        for (int i = 0; i < 2 && e == hipSuccess; ++i) {
-            e = hipEventCreateWithFlags(&w->ev_ready[i], hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&w->ev_done[i], hipEventDisableTiming);
-        }
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&w->ev_pack_in, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&w->ev_pack, hipEventDisableTiming);
+        if (e == hipSuccess) e = make_events(w);
         if (e != hipSuccess) return set_error("train: side stream / events", e);
     }
     A(w->wdpack, (size_t)(2 * NB > 0 ? 2 * NB : 1) * 9 * C * C, false);
@@ -919,6 +957,10 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
         A(t, (size_t)head_board_groups(cap) * head_board_pd() * 2, false);
         w->hpd = (double*)t;
         A(w->hpf, (size_t)head_board_groups(cap) * head_board_pf(), false);
+        A(t, (size_t)head_dgrad_groups(cap) * 6 * 2, false);
+        w->hdp = (double*)t;
+        A(w->feat, (size_t)cap * FC_FS, true);
+        A(w->pre, (size_t)cap * FC_OUT, false);
     }
     if (getenv("AZG_DEBUG_SNAP")) {
         w->snap.assign(NB + 1, nullptr);
@@ -943,7 +985,8 @@ int g_train_fuse_fin = 1;     // key 24: 1 BN finalize by the last workgroup of 
 int g_train_skip = 0;     // study build only (key 19): skip BN kernels to time them in situ (results invalid)
 int g_train_split_pack = 1;   // key 30: 1 split repack (stem on the stream, the rest on the side stream); 0 one launch
 int g_train_maskz = 1;   // key 29: 1 BN-backward apply of residual-free layers forms its ReLU mask from z (default); 0 reads act
-int g_train_fuse_heads = 4;   // key 28: bit mask of the fused head stages (pv_train_heads.hip); 0 the 18-launch chain
+int g_train_fuse_heads = 28;   // key 28: bit mask of the fused head stages (pv_train_heads.hip); 0 the 18-launch chain
+int g_train_side_heads = 1;   // key 32: 1 the head weight-grad reductions on the side stream; 0 on the caller's
 
 template <int C>
 static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, const float* zs, int B,
@@ -1072,16 +1115,20 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         AZG_CK(hipGetLastError(), "train: bn_bwd_apply");
         return 0;
     };
-    // weight gradient of one conv on the side stream, after dZ (slot) is ready
+    // weight gradient of one conv on the side stream, after dZ is ready
     bool pending[2] = {false, false};
     float* dzbuf[2] = {w->DZ, w->DZ2};
-    auto wgrad = [&](int slot, const float* xin, int tensor) -> int32_t {
+    const bool dz_all = g_train_dz_all != 0 && !g_wgrad_serial;
+    bool side_used = false;
+    // dZ of backward conv k (2i+1: conv2 of block i, 2i: conv1): its own buffer (key 34)
+    // or the alternating slot
+    auto dzb = [&](int k, int slot) -> float* { return dz_all ? w->dzs[k] : dzbuf[slot]; };
+    auto wgrad = [&](int slot, const float* dz, const float* xin, int tensor) -> int32_t {
         if (g_wgrad_serial) {   // A/B: weight grads on the caller's stream, no overlap
             int pr = prof_begin(h, AZG_PROF_TRAIN_WGRAD, st);
             const int S = wgrad_splits(C, M);
             if (S > w->S) return set_error("train: wgrad splits exceed the slab workspace", hipErrorInvalidValue);
-            AZG_CK(launch_wgrad(C, dzbuf[slot], xin, w->slab, G + h->poff[tensor], M, S, st),
-                   "train: wgrad");
+            AZG_CK(launch_wgrad(C, dz, xin, w->slab, G + h->poff[tensor], M, S, st), "train: wgrad");
             prof_end(h, pr, st);
             return 0;
         }
@@ -1090,11 +1137,13 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         int pr = prof_begin(h, AZG_PROF_TRAIN_WGRAD, w->side);
         const int S = wgrad_splits(C, M);
         if (S > w->S) return set_error("train: wgrad splits exceed the slab workspace", hipErrorInvalidValue);
-        AZG_CK(launch_wgrad(C, dzbuf[slot], xin, w->slab, G + h->poff[tensor], M, S, w->side),
-               "train: wgrad");
+        AZG_CK(launch_wgrad(C, dz, xin, w->slab, G + h->poff[tensor], M, S, w->side), "train: wgrad");
         prof_end(h, pr, w->side);
-        AZG_CK(hipEventRecord(w->ev_done[slot], w->side), "train: event record");
-        pending[slot] = true;
+        side_used = true;
+        if (!dz_all) {
+            AZG_CK(hipEventRecord(w->ev_done[slot], w->side), "train: event record");
+            pending[slot] = true;
+        }
         return 0;
     };
     // the caller's stream may overwrite dZ (slot) only after its wgrad has read it
@@ -1147,7 +1196,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             pend = Pend{w->z2[i], h->bn_blk[i].second, X, w->xo[i]};
             X = w->xo[i];
         }
-        if ((g_train_fuse_heads & 1) && pend.res) {
+        if ((g_train_fuse_heads & 17) && pend.res) {
             last_apply = true;   // the head kernel applies bn2 + residual + ReLU of the last block
             lastp = {pend.z, pend.res, pend.layer, pend.out};
         } else {
@@ -1180,7 +1229,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     const float* wpf = P + h->poff[h->t_pfc_w];
     const float* wv1 = P + h->poff[h->t_vfc1_w];
     int pr = prof_begin(h, AZG_PROF_TRAIN_OTHER, st);
-    if (fh & 1) {
+    if (fh & 17) {
         HeadStatsArgs hs{};
         hs.z = last_apply ? lastp.z : X;
         if (last_apply) {
@@ -1207,7 +1256,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         hs.bshift = w->bshift;
         hs.nbt = h->nbt;
         hs.nbn = (int)h->bn_desc.size();
-        AZG_CK(launch_head_proj_stats(C, last_apply, hs, st), "train: head_proj_stats");
+        if (fh & 16) AZG_CK(launch_head_proj_split(C, last_apply, hs, st), "train: head_proj_split");
+        else AZG_CK(launch_head_proj_stats(C, last_apply, hs, st), "train: head_proj_stats");
     } else {
         AZG_CK(launch_heads_project(C, false, X, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], nullptr, nullptr,
                                     w->zh, M, st),
@@ -1220,7 +1270,64 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         AZG_CK(hipGetLastError(), "train: head_stats_finalize");
     }
     const int gH = grid_for((int64_t)B * 3 * PIX);
-    if (fh & 2) {
+    // head weight-grad work only Adam reads goes to the side stream (key 32)
+    const bool side_heads = g_train_side_heads && !g_wgrad_serial;
+    auto to_side = [&]() -> int32_t {
+        AZG_CK(hipEventRecord(w->ev_heads, st), "train: event record");
+        AZG_CK(hipStreamWaitEvent(w->side, w->ev_heads, 0), "train: stream wait");
+        side_used = true;
+        return 0;
+    };
+    // the fc weight grads, their biases / value_fc2 and the loss means (key 28 bit 3)
+    auto fc_wgrads = [&](hipStream_t ws) -> int32_t {
+        {   // weight grads: dWpf = dlogits^T . fp, dWv1 = dhv^T . fv
+            GemmProb a{w->dlogits, 1, ACTIONS, w->fp, 2 * PIX, 1, G + h->poff[h->t_pfc_w], 2 * PIX, 1, nullptr, 0, 0,
+                       ACTIONS, 2 * PIX, B};
+            GemmProb b{w->dhv, 1, VHID, w->fv, PIX, 1, G + h->poff[h->t_vfc1_w], PIX, 1, nullptr, 0, 0, VHID, PIX, B};
+            AZG_CK(launch_small_gemm(a, &b, ws), "train: head fc wgrad");
+        }
+        hipLaunchKernelGGL(heads_small_grads_kernel, dim3((HSG_OUT + 3) / 4), dim3(256), 0, ws, w->dlogits, w->dhv,
+                           w->dpre, w->hv, w->lossb, B, G + h->poff[h->t_pfc_b], G + h->poff[h->t_vfc1_b],
+                           G + h->poff[h->t_vfc2_w], G + h->poff[h->t_vfc2_b], losses);
+        AZG_CK(hipGetLastError(), "train: heads_small_grads");
+        return 0;
+    };
+    if (fh & 8) {
+        // short, wide launches: features in the eval row layout -> heads_fc (MFMA) ->
+        // heads_loss -> masked fc dgrad + head-BN backward partials -> one-wave finalize;
+        // the weight grads of the fcs and their biases / value_fc2 (and the loss means) on
+        // the side stream
+        AZG_CK(launch_head_bn_apply_feat(w->zh, w->bscale + ho, w->bshift + ho, w->fp, w->fv, w->feat, B, st),
+               "train: head_bn_apply_feat");
+        AZG_CK(launch_heads_fc(w->feat, h->wfc, w->pre, B, st), "train: heads_fc");
+        hipLaunchKernelGGL(heads_loss_kernel, dim3((B + 3) / 4), dim3(256), 0, st, w->pre, P + h->poff[h->t_pfc_b],
+                           w->pre + ACTIONS, P + h->poff[h->t_vfc1_b], P + h->poff[h->t_vfc2_w],
+                           P + h->poff[h->t_vfc2_b], pis, zs, w->dlogits, w->hv, w->dhv, w->dpre, w->lossb, B,
+                           FC_OUT, FC_OUT);
+        AZG_CK(hipGetLastError(), "train: heads_loss");
+        HeadDgradArgs hd{};
+        hd.dlogits = w->dlogits;
+        hd.dhv = w->dhv;
+        hd.wpf = wpf;
+        hd.wv1 = wv1;
+        hd.fp = w->fp;
+        hd.fv = w->fv;
+        hd.zh = w->zh;
+        hd.hmean = w->bmean + ho;
+        hd.dfp = w->dfp;
+        hd.dfv = w->dfv;
+        hd.part = w->hdp;
+        hd.B = B;
+        hd.desc = bdd;
+        hd.pol_layer = h->bn_pol;
+        hd.val_layer = h->bn_val;
+        hd.params = P;
+        hd.grads = G;
+        hd.hinv = w->binv + ho;
+        hd.hb = w->hbw;
+        AZG_CK(launch_head_dgrad(hd, st), "train: head_dgrad");
+        if (!side_heads) R(fc_wgrads(st));   // else after the 1x1 backward, with one hand-off
+    } else if (fh & 2) {
         HeadBoardArgs hb{};
         hb.zh = w->zh;
         hb.hmean = w->bmean + ho;
@@ -1330,8 +1437,16 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         AZG_CK(hipGetLastError(), "train: heads_bwd_proj");
     }
     // policy_conv.weight [2][C] then value_conv.weight [C]: partial layout [t][3][C]
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3((3 * C + 15) / 16), dim3(256), 0, st, w->hpart, hntile, 3 * C,
-                       G + h->poff[h->t_pc_w], G + h->poff[h->t_vc_w], 2 * C, 0, C);
+    {
+        hipStream_t ws = st;
+        if (side_heads && (fh & 8)) {   // one hand-off: the fc weight grads and this reduction
+            if (int32_t r2 = to_side()) return r2;
+            ws = w->side;
+            R(fc_wgrads(ws));
+        }
+        hipLaunchKernelGGL(reduce_partials_kernel, dim3((3 * C + 15) / 16), dim3(256), 0, ws, w->hpart, hntile, 3 * C,
+                           G + h->poff[h->t_pc_w], G + h->poff[h->t_vc_w], 2 * C, 0, C);
+    }
     AZG_CK(hipGetLastError(), "train: heads proj wgrad");
     prof_end(h, pr, st);
     auto snap = [&](int k) -> int32_t {
@@ -1359,15 +1474,17 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         const int lin = i == 0 ? h->bn_stem : h->bn_blk[i - 1].second;
         if (!done_fin) R(bwd_fin(h->bn_blk[i].second, bwd_nt));
         R(reuse(0));
-        R(bwd_apply(w->gX, w->xo[i], w->z2[i], h->bn_blk[i].second, dzbuf[0], w->GR));
-        R(wgrad(0, w->hh[i], h->t_blk[i].w2));
-        R(conv(EPI_RAW, XE_BNBWD, dzbuf[0], w->wdpack + (size_t)(2 * i + 1) * 9 * C * C, nullptr, w->DH, w->hh[i],
+        float* dz2 = dzb(2 * i + 1, 0);
+        R(bwd_apply(w->gX, w->xo[i], w->z2[i], h->bn_blk[i].second, dz2, w->GR));
+        R(wgrad(0, dz2, w->hh[i], h->t_blk[i].w2));
+        R(conv(EPI_RAW, XE_BNBWD, dz2, w->wdpack + (size_t)(2 * i + 1) * 9 * C * C, nullptr, w->DH, w->hh[i],
                w->z1[i], h->bn_blk[i].first, ffin ? h->bn_blk[i].first : -1));
         if (!ffin) R(bwd_fin(h->bn_blk[i].first, ntt));
         R(reuse(1));
-        R(bwd_apply(w->DH, w->hh[i], w->z1[i], h->bn_blk[i].first, dzbuf[1], nullptr, true));
-        R(wgrad(1, Xin, h->t_blk[i].w1));
-        R(conv(EPI_ADD, XE_BNBWD, dzbuf[1], w->wdpack + (size_t)(2 * i) * 9 * C * C, w->GR, w->gX, Xin, zin, lin,
+        float* dz1 = dzb(2 * i, 1);
+        R(bwd_apply(w->DH, w->hh[i], w->z1[i], h->bn_blk[i].first, dz1, nullptr, true));
+        R(wgrad(1, dz1, Xin, h->t_blk[i].w1));
+        R(conv(EPI_ADD, XE_BNBWD, dz1, w->wdpack + (size_t)(2 * i) * 9 * C * C, w->GR, w->gX, Xin, zin, lin,
                ffin ? lin : -1));
         done_fin = ffin;
         bwd_nt = ntt;
@@ -1389,6 +1506,10 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     AZG_CK(hipGetLastError(), "train: stem_wgrad_reduce");
     R(reuse(0));
     R(reuse(1));                 // joins the side stream: every conv weight grad is done
+    if (side_used) {             // (and the head weight grads when no conv weight grad follows them)
+        AZG_CK(hipEventRecord(w->ev_join, w->side), "train: event record");
+        AZG_CK(hipStreamWaitEvent(st, w->ev_join, 0), "train: stream wait");
+    }
 #undef R
     return 0;
 }
@@ -1398,7 +1519,11 @@ int32_t train_backward(azg_pv* h, const float* x, const float* pis, const float*
 {
     if (int32_t r = ensure_train_ws(h, B, st)) return r;
     TrainWS* w = ws_of(h);
-    if (g_train_split_pack && !g_wgrad_serial) {
+    AZG_CK(make_events(w), "train: events");
+    if (h->train_packs) {
+        // the packs were refreshed right after the last Adam step (train_apply, key 36) and
+        // no parameter changed since (azg_pv_mark_dirty / bind clear the flag)
+    } else if (g_train_split_pack && !g_wgrad_serial) {
         // the stem's pack on this stream; the residual convs' forward + dgrad packs and
         // the head FCs on the side stream, overlapping the stem and its statistics (the
         // first residual conv waits for them, train_backward_t)
@@ -1411,6 +1536,7 @@ int32_t train_backward(azg_pv* h, const float* x, const float* pis, const float*
     } else if (int32_t r = repack(h, st, w->wdpack)) {
         return r;
     }
+    h->train_packs = true;
     const int C = h->C;
     int32_t r;
     switch (C) {
@@ -1442,8 +1568,18 @@ int32_t train_apply(azg_pv* h, float* exp_avg, float* exp_avg_sq, int64_t step, 
                        h->grads, exp_avg, exp_avg_sq, n, w->npart, nb, max_norm, w->scal, total_norm, lr_bc1,
                        (float)(1.0 - (double)beta1), beta2, (float)(1.0 - (double)beta2), bc2_sqrt, eps, wd);
     AZG_CK(hipGetLastError(), "apply: adam");
+    h->train_packs = false;   // the parameters changed
+    if (g_train_pack_after) {
+        // every pack of the next step (and the eval BN fold) from the new parameters, on
+        // this stream right behind Adam: the next train step starts without a repack and
+        // without the cross-stream hand-off of the split repack (key 30)
+        if (int32_t r = repack(h, st, w->wdpack)) return r;
+        h->train_packs = true;
+        h->dirty = false;
+    } else {
+        h->dirty = true;
+    }
     prof_end(h, pr, st);
-    h->dirty = true;
     return 0;
 }
 
@@ -1477,7 +1613,7 @@ extern "C" int32_t azg_pv_debug_copy(azg_pv* h, int32_t which, int32_t index, fl
         case 4: src = w->z2[index]; break;
         case 5: src = w->xo[index]; break;
         case 6: src = w->gX; break;
-        case 7: src = w->DZ; break;
+        case 7: src = (g_train_dz_all && !w->dzs.empty()) ? w->dzs[0] : w->DZ; break;   // the last backward conv's dZ
         case 8: src = w->DH; break;
         case 9: src = w->GR; break;
         case 10:

@@ -76,6 +76,34 @@ struct HeadBwdArgs {
     int M;
 };
 
+// key 28 bit 3: the fc stage as short, wide launches (pv_train_heads.hip)
+struct HeadDgradArgs {
+    const float* dlogits;  // [B][225]
+    const float* dhv;      // [B][64]
+    const float* wpf;      // policy_fc.weight [225][450]
+    const float* wv1;      // value_fc1.weight [64][225]
+    const float* fp;       // features [B][450] / [B][225] (ReLU masks)
+    const float* fv;
+    const float* zh;       // [B][3][225]
+    const float* hmean;    // head BN mean (3)
+    float *dfp, *dfv;      // masked fc data gradients
+    double* part;          // [groups][6] head-BN backward sums per workgroup
+    int B;
+    // finalize (head_bn_bwd_fin_kernel)
+    const BnDesc* desc;
+    int pol_layer, val_layer;
+    const float* params;
+    float* grads;
+    const float* hinv;     // head BN invstd (3)
+    float* hb;             // [3][3] head-BN backward coefficients
+};
+int head_dgrad_groups(int B);
+hipError_t launch_head_dgrad(const HeadDgradArgs& a, hipStream_t st);
+hipError_t launch_head_bn_apply_feat(const float* zh, const float* hscale, const float* hshift, float* fp, float* fv,
+                                     float* feat, int B, hipStream_t st);
+// key 28 bit 4: head_proj_stats_kernel's partials finalized by a one-workgroup kernel
+hipError_t launch_head_proj_split(int C, bool apply, const HeadStatsArgs& a, hipStream_t st);
+
 int head_proj_stats_groups(int M);
 int head_board_groups(int B);
 int head_board_pd();

@@ -28,6 +28,8 @@
 // its plain loads.
 #include "pv_train_heads.h"
 
+#include <type_traits>
+
 #ifdef AZG_HB_TIMING   // ad-hoc phase timing (wall clock, 100 MHz), never in the product
 #define HBT_DECL unsigned long long hbt_[8] = {0, 0, 0, 0, 0, 0, 0, 0}
 #define HBT(i) do { if (threadIdx.x == 0) hbt_[i] = wall_clock64(); } while (0)
@@ -88,88 +90,13 @@ __device__ __forceinline__ double wsum_d(double v)
     return v;
 }
 
-template <int C, bool APPLY>
-__global__ __launch_bounds__(256) void head_proj_stats_kernel(const HeadStatsArgs a)
+// finalize of the head BN statistics from nwg per-workgroup fp64 partials [nwg][6]:
+// thread t sums workgroups t, t + 256, ... (all loads issued first), then a fixed-order
+// block reduction (256 threads; red: [4][6]); shared by the last-arriving workgroup of
+// head_proj_stats_kernel and the one-workgroup head_proj_fin_kernel (bitwise equal)
+__device__ __forceinline__ void head_stats_fin(const HeadStatsArgs& a, int nwg, double (*red)[6])
 {
-    constexpr int Q = C / 4;   // channels per thread (4 threads per pixel)
-    __shared__ float w[3][C];
-    __shared__ float ss[2][C];
-    __shared__ double red[4][6];
-    __shared__ unsigned flag;
-    for (int i = threadIdx.x; i < 3 * C; i += 256) w[i / C][i % C] = i < 2 * C ? a.wpc[i] : a.wvc[i - 2 * C];
-    if (APPLY)
-        for (int i = threadIdx.x; i < C; i += 256) {
-            ss[0][i] = a.scale[i];
-            ss[1][i] = a.shift[i];
-        }
-    HBT_DECL; HBT(0);
-    __syncthreads();
-    const int q = threadIdx.x & 3;
-    const int m = blockIdx.x * HP_ROWS + (threadIdx.x >> 2);
-    float d0 = 0.f, d1 = 0.f, d2 = 0.f;
-    if (m < a.M) {
-        const int o = pad_off(m, C) + q * Q;
-        const __amdgpu_buffer_rsrc_t ars = wt_rsrc(a.aout, padded_bytes(a.M, C));
-        // every load of the row issued before the first store (stores may alias them)
-        f32x4 zv[Q / 4], rv[APPLY ? Q / 4 : 1];
-#pragma unroll
-        for (int c = 0; c < Q; c += 4) {
-            zv[c / 4] = *(const f32x4*)(a.z + o + c);
-            if (APPLY) rv[c / 4] = *(const f32x4*)(a.res + o + c);
-        }
-#pragma unroll
-        for (int c = 0; c < Q; c += 4) {
-            f32x4 v = zv[c / 4];
-            if (APPLY) {   // = bn_apply_kernel<C, true>: relu(z * scale + shift + res)
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    v[k] = fmaxf(v[k] * ss[0][q * Q + c + k] + ss[1][q * Q + c + k] + rv[c / 4][k], 0.f);
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                d0 = fmaf(v[k], w[0][q * Q + c + k], d0);
-                d1 = fmaf(v[k], w[1][q * Q + c + k], d1);
-                d2 = fmaf(v[k], w[2][q * Q + c + k], d2);
-            }
-            zv[c / 4] = v;
-        }
-        if (APPLY)
-#pragma unroll
-            for (int c = 0; c < Q; c += 4) store4<true>(a.aout, ars, o + c, zv[c / 4]);
-    }
-#pragma unroll
-    for (int o = 1; o < 4; o <<= 1) {   // = heads_project's reduction order
-        d0 += __shfl_xor(d0, o, 64);
-        d1 += __shfl_xor(d1, o, 64);
-        d2 += __shfl_xor(d2, o, 64);
-    }
-    const bool own = m < a.M && q == 0;
-    if (own) {
-        const int b = m / PIX, p = m - b * PIX;
-        float* hb = a.zh + (size_t)b * 3 * PIX;
-        hb[p] = d0;
-        hb[PIX + p] = d1;
-        hb[2 * PIX + p] = d2;
-    }
-    // per-workgroup fp64 sums S z, S z^2 of the three head channels
-    double v[6] = {own ? (double)d0 : 0.0, own ? (double)d0 * d0 : 0.0, own ? (double)d1 : 0.0,
-                   own ? (double)d1 * d1 : 0.0, own ? (double)d2 : 0.0, own ? (double)d2 * d2 : 0.0};
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) v[k] = wsum_d(v[k]);
-    if (lane == 0)
-#pragma unroll
-        for (int k = 0; k < 6; ++k) red[wid][k] = v[k];
-    __syncthreads();
-    HBT(1);
-    if (threadIdx.x < 6)
-        st_wt_d(a.part + (size_t)blockIdx.x * 6 + threadIdx.x,
-                (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]));
-    HBT(7); HBT_MID("proj");
-    if (!last_arrival(a.cnt, gridDim.x, &flag)) return;
-    // finalize: thread t sums workgroups t, t + 256, ... (all loads issued first), then a
-    // fixed-order block reduction
-    const int nwg = gridDim.x;
     double s[6] = {0, 0, 0, 0, 0, 0};
     for (int g0 = threadIdx.x; g0 < nwg; g0 += 512) {
         double x0[6], x1[6];
@@ -219,6 +146,96 @@ __global__ __launch_bounds__(256) void head_proj_stats_kernel(const HeadStatsArg
     }
     if (a.nbt)
         for (int i = threadIdx.x; i < a.nbn; i += 256) a.nbt[i] += 1;
+}
+
+// LAST: the last-arriving workgroup finalizes (key 28 bit 0); otherwise the partials
+// are left to head_proj_fin_kernel (key 28 bit 4)
+template <int C, bool APPLY, bool LAST = true>
+__global__ __launch_bounds__(256) void head_proj_stats_kernel(const HeadStatsArgs a)
+{
+    // C/4 consecutive threads own one pixel (4 channels each: 16-B runs, every wave
+    // instruction reads whole 128-B lines), 256*4/C pixels per pass; every load of the
+    // workgroup's 64 rows is issued before the first store (the stores may alias them)
+    constexpr int TPP = C / 4, PPP = 256 / TPP, NP = HP_ROWS / PPP;
+    static_assert(TPP <= 64 && 64 % TPP == 0 && HP_ROWS % PPP == 0, "pixel layout");
+    __shared__ double red[4][6];
+    __shared__ unsigned flag;
+    const int tid = threadIdx.x;
+    const int c = (tid % TPP) * 4, pp = tid / TPP;
+    const f32x4 w0 = *(const f32x4*)(a.wpc + c), w1 = *(const f32x4*)(a.wpc + C + c), w2 = *(const f32x4*)(a.wvc + c);
+    f32x4 s4 = {1.f, 1.f, 1.f, 1.f}, t4 = {0.f, 0.f, 0.f, 0.f};
+    if (APPLY) {
+        s4 = *(const f32x4*)(a.scale + c);
+        t4 = *(const f32x4*)(a.shift + c);
+    }
+    HBT_DECL; HBT(0);
+    const int mb = blockIdx.x * HP_ROWS;
+    f32x4 zv[NP], rv[APPLY ? NP : 1];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const int m = mb + pp + p * PPP;
+        zv[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (APPLY) rv[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (m < a.M) {
+            const int o = pad_off(m, C) + c;
+            zv[p] = *(const f32x4*)(a.z + o);
+            if (APPLY) rv[p] = *(const f32x4*)(a.res + o);
+        }
+    }
+    const __amdgpu_buffer_rsrc_t ars = wt_rsrc(a.aout, padded_bytes(a.M, C));
+    double v[6] = {0, 0, 0, 0, 0, 0};   // S z, S z^2 of the three head channels (owner lanes)
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const int m = mb + pp + p * PPP;
+        f32x4 x = zv[p];
+        if (APPLY) {   // = bn_apply_kernel<C, true>: relu(fma(z, scale, shift) + res)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x[k] = fmaxf(fmaf(x[k], s4[k], t4[k]) + rv[p][k], 0.f);
+            if (m < a.M) store4<true>(a.aout, ars, pad_off(m, C) + c, x);
+        }
+        float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            d0 = fmaf(x[k], w0[k], d0);
+            d1 = fmaf(x[k], w1[k], d1);
+            d2 = fmaf(x[k], w2[k], d2);
+        }
+#pragma unroll
+        for (int o = 1; o < TPP; o <<= 1) {
+            d0 += __shfl_xor(d0, o, 64);
+            d1 += __shfl_xor(d1, o, 64);
+            d2 += __shfl_xor(d2, o, 64);
+        }
+        if (tid % TPP == 0 && m < a.M) {
+            const int b = m / PIX, px = m - b * PIX;
+            float* hb = a.zh + (size_t)b * 3 * PIX;
+            hb[px] = d0;
+            hb[PIX + px] = d1;
+            hb[2 * PIX + px] = d2;
+            v[0] += (double)d0;
+            v[1] += (double)d0 * d0;
+            v[2] += (double)d1;
+            v[3] += (double)d1 * d1;
+            v[4] += (double)d2;
+            v[5] += (double)d2 * d2;
+        }
+    }
+    // per-workgroup fp64 sums S z, S z^2 of the three head channels
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) v[k] = wsum_d(v[k]);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) red[wid][k] = v[k];
+    __syncthreads();
+    HBT(1);
+    if (threadIdx.x < 6)
+        st_wt_d(a.part + (size_t)blockIdx.x * 6 + threadIdx.x,
+                (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]));
+    HBT(7); HBT_MID("proj");
+    if constexpr (!LAST) return;
+    if (!last_arrival(a.cnt, gridDim.x, &flag)) return;
+    head_stats_fin(a, gridDim.x, red);
     HBT_END("proj");
 }
 
@@ -697,6 +714,201 @@ __global__ __launch_bounds__(256) void heads_bwd_fused_kernel(const HeadBwdArgs 
             else *(f32x4*)((k == 3 ? a.pa : a.pb) + (size_t)blockIdx.x * C + c) = v;
         }
     }
+}
+
+// ---- key 28 bits 3 / 4: short, wide launches for the latency-bound head chain -----
+
+__global__ __launch_bounds__(256) void head_proj_fin_kernel(const HeadStatsArgs a, int nwg)
+{
+    __shared__ double red[4][6];
+    head_stats_fin(a, nwg, red);
+}
+
+// = head_bn_apply_kernel, also writing the features in the eval forward's padded row
+// layout feat[b][FC_FS] (policy 450 -> FC_KP, value 225 at FC_KP; the zero pads are set
+// at allocation) so the fc forward runs on heads_fc's 16-B operand loads
+__global__ __launch_bounds__(256) void head_bn_apply_feat_kernel(const float* __restrict__ zh,
+                                                                 const float* __restrict__ hscale,
+                                                                 const float* __restrict__ hshift,
+                                                                 float* __restrict__ fp, float* __restrict__ fv,
+                                                                 float* __restrict__ feat, int B)
+{
+    const int total = B * 3 * PIX;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const int b = i / (3 * PIX), k = i - b * 3 * PIX;
+        const int ch = k / PIX;
+        const float y = fmaxf(zh[i] * hscale[ch] + hshift[ch], 0.f);
+        if (ch < 2) {
+            fp[(size_t)b * 2 * PIX + k] = y;
+            feat[(size_t)b * FC_FS + k] = y;
+        } else {
+            fv[(size_t)b * PIX + k - 2 * PIX] = y;
+            feat[(size_t)b * FC_FS + FC_KP + k - 2 * PIX] = y;
+        }
+    }
+}
+
+// fc data gradients with the feature ReLU masks (= the masked small_gemm dgrad) and the
+// head BN-backward partial sums (= head_bn_bwd_partial_kernel), one workgroup per 32
+// boards x 32 features (grid.y: 15 policy then 8 value feature tiles):
+//   out[b][f] = S_k d[b][k] W[k][f],  d = dlogits (K = 225, W = policy_fc [225][450])
+//                                     or dhv (K = 64, W = value_fc1 [64][225])
+// The group's d rows are staged into LDS with coalesced loads (odd row stride: the
+// MFMA's column reads spread over the banks); W is read straight into registers,
+// W[k = 2s + h][f0 + lane] (128-B rows per half-wave), all of a wave's loads issued
+// before the staging.  K split over the four waves, partial tiles summed in fixed wave
+// order; per workgroup fp64 S dy, S (z - mean) dy of its head channel.
+constexpr int HD_PT = (2 * PIX + 31) / 32;   // 15 policy feature tiles
+constexpr int HD_VT = (PIX + 31) / 32;       // 8 value feature tiles
+constexpr int HD_LDA = ACTIONS + 4;          // 229
+
+__global__ __launch_bounds__(256) void head_dgrad_kernel(const HeadDgradArgs a)
+{
+    __shared__ float As[32][HD_LDA];
+    __shared__ float red[4][16][64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int r32 = lane & 31, h = lane >> 5;
+    const int i0 = blockIdx.x * 32, ft = blockIdx.y;
+    const bool val = ft >= HD_PT;
+    const int f0 = val ? (ft - HD_PT) * 32 : ft * 32;
+    const int F = val ? PIX : 2 * PIX;
+    const int K = val ? VHID : ACTIONS;
+    const float* W = val ? a.wv1 : a.wpf;
+    const int f = f0 + r32;
+    const bool fok = f < F;
+    const int steps = (K + 1) / 2;
+    const int s0 = wid * steps / 4, s1 = (wid + 1) * steps / 4;
+    constexpr int SMAX = (ACTIONS + 1) / 2 / 4 + 1;   // 29
+    float bw[SMAX];
+#pragma unroll
+    for (int u = 0; u < SMAX; ++u) {
+        const int k = 2 * (s0 + u) + h;
+        bw[u] = (s0 + u < s1 && k < K && fok) ? W[(size_t)k * F + f] : 0.f;
+    }
+    // every staging load of the thread in flight before its LDS stores
+    auto stage = [&](const float* src, auto kc) {
+        constexpr int KK = decltype(kc)::value, NE = (32 * KK + 255) / 256;
+        float v[NE];
+#pragma unroll
+        for (int u = 0; u < NE; ++u) {
+            const int e = tid + 256 * u, bb = e / KK;
+            v[u] = (e < 32 * KK && i0 + bb < a.B) ? src[(size_t)i0 * KK + e] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < NE; ++u) {
+            const int e = tid + 256 * u, bb = e / KK, k = e - bb * KK;
+            if (e < 32 * KK) As[bb][k] = v[u];
+        }
+    };
+    if (val) stage(a.dhv, std::integral_constant<int, VHID>{});
+    else stage(a.dlogits, std::integral_constant<int, ACTIONS>{});
+    __syncthreads();
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int u = 0; u < SMAX; ++u)
+        if (s0 + u < s1) {
+            const int k = 2 * (s0 + u) + h;
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(k < K ? As[r32][k] : 0.f, bw[u], acc, 0, 0, 0);
+        }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wid][r][lane] = acc[r];
+    __syncthreads();
+    if (wid != 0) return;
+    double hs[6] = {0, 0, 0, 0, 0, 0};   // (S dy, S (z - mean) dy) of head channels 0, 1, 2
+    if (fok) {
+        const int ch = val ? 2 : f < PIX ? 0 : 1;
+        const double mu = (double)a.hmean[ch];
+        double sd = 0.0, sq = 0.0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int b = i0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (b >= a.B) continue;
+            const float v = ((red[0][r][lane] + red[1][r][lane]) + red[2][r][lane]) + red[3][r][lane];
+            const float fe = val ? a.fv[(size_t)b * PIX + f] : a.fp[(size_t)b * 2 * PIX + f];
+            const float zz = a.zh[(size_t)b * 3 * PIX + (val ? 2 * PIX : 0) + f];
+            const float d = fe > 0.f ? v : 0.f;
+            if (val) a.dfv[(size_t)b * PIX + f] = d;
+            else a.dfp[(size_t)b * 2 * PIX + f] = d;
+            sd += (double)d;
+            sq += ((double)zz - mu) * (double)d;
+        }
+        hs[2 * ch] = sd;
+        hs[2 * ch + 1] = sq;
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) hs[k] = wsum_d(hs[k]);
+    if (lane < 6) a.part[(size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 6 + lane] = hs[lane];
+}
+
+// = head_bn_bwd_finalize_kernel over head_dgrad_kernel's per-workgroup partials (one
+// wave: lane g sums workgroups g, g + 64, ..., then a fixed xor tree)
+__global__ __launch_bounds__(64) void head_bn_bwd_fin_kernel(const HeadDgradArgs a, int nwg)
+{
+    const int lane = threadIdx.x;
+    double sm[6] = {0, 0, 0, 0, 0, 0};
+    for (int g = lane; g < nwg; g += 64)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) sm[k] += a.part[(size_t)g * 6 + k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) sm[k] = wsum_d(sm[k]);
+    if (lane < 3) {
+        const int ch = lane;
+        const BnDesc d = a.desc[ch < 2 ? a.pol_layer : a.val_layer];
+        const int c = ch < 2 ? ch : 0;
+        const double N = (double)a.B * PIX;
+        const double sd = sm[2 * ch], qd = sm[2 * ch + 1];
+        const float inv = a.hinv[ch];
+        const double invd = (double)inv;
+        a.grads[d.gamma_off + c] = (float)(qd * invd);
+        a.grads[d.beta_off + c] = (float)sd;
+        a.hb[ch * 3 + 0] = (float)(sd / N);
+        a.hb[ch * 3 + 1] = (float)(qd * invd * invd / N);
+        a.hb[ch * 3 + 2] = inv * a.params[d.gamma_off + c];
+    }
+}
+
+int head_dgrad_groups(int B) { return ((B + 31) / 32) * (HD_PT + HD_VT); }
+
+hipError_t launch_head_proj_split(int C, bool apply, const HeadStatsArgs& a, hipStream_t st)
+{
+    const int nwg = head_proj_stats_groups(a.M);
+#define AZG_HPP(CC)                                                                                          \
+    case CC:                                                                                                 \
+        if (apply) hipLaunchKernelGGL((head_proj_stats_kernel<CC, true, false>), dim3(nwg), dim3(256), 0, st, a); \
+        else hipLaunchKernelGGL((head_proj_stats_kernel<CC, false, false>), dim3(nwg), dim3(256), 0, st, a);      \
+        break;
+    switch (C) {
+        AZG_HPP(64)
+        AZG_HPP(128)
+        AZG_HPP(256)
+        default: return hipErrorInvalidValue;
+    }
+#undef AZG_HPP
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(head_proj_fin_kernel, dim3(1), dim3(256), 0, st, a, nwg);
+    return hipGetLastError();
+}
+
+hipError_t launch_head_bn_apply_feat(const float* zh, const float* hscale, const float* hshift, float* fp, float* fv,
+                                     float* feat, int B, hipStream_t st)
+{
+    const int total = B * 3 * PIX;
+    int nb = (total + 255) / 256;
+    nb = nb > 8192 ? 8192 : nb;
+    hipLaunchKernelGGL(head_bn_apply_feat_kernel, dim3(nb), dim3(256), 0, st, zh, hscale, hshift, fp, fv, feat, B);
+    return hipGetLastError();
+}
+
+hipError_t launch_head_dgrad(const HeadDgradArgs& a, hipStream_t st)
+{
+    hipLaunchKernelGGL(head_dgrad_kernel, dim3((a.B + 31) / 32, HD_PT + HD_VT), dim3(256), 0, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(head_bn_bwd_fin_kernel, dim3(1), dim3(64), 0, st, a, head_dgrad_groups(a.B));
+    return hipGetLastError();
 }
 
 hipError_t launch_head_proj_stats(int C, bool apply, const HeadStatsArgs& a, hipStream_t st)

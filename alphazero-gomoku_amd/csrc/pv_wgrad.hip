@@ -328,22 +328,26 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_t(
 // read land on disjoint bank halves.  Rows past the split read padded pixel 0 (the
 // zero halo).  Measured at 6x128, B = 128 (scripts/wgrad_lab.hip): 74.0 vs 89.2 us
 // (hipEvent incl. launch) for the K-contiguous kernel.
-template <int C, bool WT = true>
-__global__ __launch_bounds__(256, 2) void conv3x3_wgrad_nat(
+template <int C, bool WT = true, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, 2) void conv3x3_wgrad_nat(
     const float* __restrict__ dz, const float* __restrict__ x, float* __restrict__ slab, int M, int S)
 {
-    constexpr int BT = C < 128 ? C : 128, BK = 32, NT = C / BT, W = BT / 2, TT = BT / 64;
+    // NWV = 4: 2 x 2 waves of (BT/2) x (BT/2); NWV = 8 (BT = 128): 2 x 4 waves of 64 co x
+    // 32 ci (two accumulators each: four waves per SIMD at two workgroups per CU)
+    constexpr int BT = C < 128 ? C : 128, BK = 32, NT = C / BT;
+    constexpr int WNW = NWV == 8 ? 4 : 2;           // waves along ci
+    constexpr int TA = BT / 64, TB = BT / (32 * WNW); // accumulators along co / ci per wave
     constexpr int RPI = 256 / BT;      // pixel rows per wave-instruction (1 KiB)
     constexpr int CPR = BT / 4;        // 16-B chunks per row
-    constexpr int IPW = BK / RPI / 4;  // instructions per wave per operand per chunk
-    static_assert(IPW >= 1 && CPR >= 16, "tile");
+    constexpr int IPW = BK / RPI / NWV;  // instructions per wave per operand per chunk
+    static_assert(IPW >= 1 && CPR >= 16 && TB >= 1, "tile");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* As = smem;                  // [2][BK][BT]  dz rows (co)
     float* Bs = smem + 2 * BK * BT;    // [2][BK][BT]  x rows (ci, tap-shifted)
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wid >> 1, wn = wid & 1;
+    const int wm = wid / WNW, wn = wid % WNW;
     constexpr int TILES = 9 * NT * NT;
     const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;   // XCD-aware order, see conv3x3_wgrad_mfma
     const int split = (k / TILES) * 8 + xcd;
@@ -376,19 +380,23 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_nat(
         }
     };
     const int r32 = lane & 31, h = lane >> 5;
-    int aoff[TT], boff[TT];
+    int aoff[TA], boff[TB];
 #pragma unroll
-    for (int i = 0; i < TT; ++i) {
-        const int ca = wm * W + i * 32 + r32, cb = wn * W + i * 32 + r32;
+    for (int i = 0; i < TA; ++i) {
+        const int ca = wm * (BT / 2) + i * 32 + r32;
         aoff[i] = 16 * h * BT + (((ca >> 2) ^ (h << 3)) << 2) + (ca & 3);
-        boff[i] = 16 * h * BT + (((cb >> 2) ^ (h << 3)) << 2) + (cb & 3);
+    }
+#pragma unroll
+    for (int j = 0; j < TB; ++j) {
+        const int cb = wn * (BT / WNW) + j * 32 + r32;
+        boff[j] = 16 * h * BT + (((cb >> 2) ^ (h << 3)) << 2) + (cb & 3);
     }
 
-    f32x16 acc[TT][TT];
+    f32x16 acc[TA][TB];
 #pragma unroll
-    for (int i = 0; i < TT; ++i)
+    for (int i = 0; i < TA; ++i)
 #pragma unroll
-        for (int j = 0; j < TT; ++j)
+        for (int j = 0; j < TB; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -404,15 +412,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_nat(
         const float* Bb = Bs + cur * BK * BT;
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
-            float a[TT], b[TT];
+            float a[TA], b[TB];
 #pragma unroll
-            for (int i = 0; i < TT; ++i) a[i] = Ab[s * BT + aoff[i]];
+            for (int i = 0; i < TA; ++i) a[i] = Ab[s * BT + aoff[i]];
 #pragma unroll
-            for (int j = 0; j < TT; ++j) b[j] = Bb[s * BT + boff[j]];
+            for (int j = 0; j < TB; ++j) b[j] = Bb[s * BT + boff[j]];
 #pragma unroll
-            for (int i = 0; i < TT; ++i)
+            for (int i = 0; i < TA; ++i)
 #pragma unroll
-                for (int j = 0; j < TT; ++j)
+                for (int j = 0; j < TB; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of chunk kc+1 retired
@@ -422,13 +430,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_nat(
     float* out = slab + ((size_t)split * 9 + tap) * C * C;
     const __amdgpu_buffer_rsrc_t rs = wt_rsrc(out, (size_t)C * C * sizeof(float));
 #pragma unroll
-    for (int i = 0; i < TT; ++i)
+    for (int i = 0; i < TA; ++i)
 #pragma unroll
-        for (int j = 0; j < TT; ++j)
+        for (int j = 0; j < TB; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int co = co0 + wm * W + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const int ci = ci0 + wn * W + j * 32 + r32;
+                const int co = co0 + wm * (BT / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int ci = ci0 + wn * (BT / WNW) + j * 32 + r32;
                 store1<WT>(out, rs, co * C + ci, acc[i][j][r]);
             }
 }
@@ -471,7 +479,7 @@ static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, f
     using T = WgTile<C, BK>;
     if (S % 8) return hipErrorInvalidValue;           // wgrad_splits guarantees S % 8 == 0
     dim3 grid(S * 9 * T::NT * T::NT);
-    if (g_wgrad_kernel == 3 && BK == 32) {
+    if (g_wgrad_kernel >= 3 && BK == 32) {
         constexpr int lds = 2 * 2 * 32 * T::BT * 4;
         static bool attr_n = false;
         if (!attr_n) {
@@ -480,8 +488,22 @@ static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, f
             if (e == hipSuccess)
                 e = hipFuncSetAttribute((const void*)conv3x3_wgrad_nat<C, false>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            if constexpr (T::BT == 128)
+                if (e == hipSuccess)
+                    e = hipFuncSetAttribute((const void*)conv3x3_wgrad_nat<C, true, 8>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
             if (e != hipSuccess) return e;
             attr_n = true;
+        }
+        if constexpr (T::BT == 128) {
+            if (g_wgrad_kernel == 4 && (g_train_wt & 4)) {   // 8 waves per 128x128 tile
+                hipLaunchKernelGGL((conv3x3_wgrad_nat<C, true, 8>), grid, dim3(512), lds, st, dz, x, slab, M, S);
+                hipError_t e = hipGetLastError();
+                if (e != hipSuccess) return e;
+                const int total = 9 * C * C;
+                hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, dw, C, S);
+                return hipGetLastError();
+            }
         }
         if (g_train_wt & 4)
             hipLaunchKernelGGL((conv3x3_wgrad_nat<C, true>), grid, dim3(256), lds, st, dz, x, slab, M, S);

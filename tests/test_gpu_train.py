@@ -166,7 +166,7 @@ def test_gradients_match_oracle(tag, blocks, ch, B):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("fuse", [0, 1, 2, 4, 7])
+@pytest.mark.parametrize("fuse", [0, 1, 2, 4, 7, 8, 12, 16, 20, 28])
 @pytest.mark.parametrize("tag,blocks,ch,B", [("3x64", 3, 64, 37), ("6x128", 6, 128, 128)])
 def test_head_chain_variants_match_oracle(fuse, tag, blocks, ch, B):
     """Every fused head stage (key 28 bits: projections + statistics, per-board FCs +
@@ -338,8 +338,8 @@ def test_train_then_predict_uses_new_weights():
     np.testing.assert_allclose(v1, rv, atol=1e-5)
 
 
-@pytest.mark.parametrize("key,values", [(18, (0, 1, 2, 4, 7)), (12, (0, 1)), (16, (3, 0, 1, 2)), (23, (1, 0)), (24, (1, 0)),
-                                        (25, (32, 0)), (26, (8, 16)), (29, (1, 0)), (30, (1, 0))])
+@pytest.mark.parametrize("key,values", [(18, (0, 1, 2, 4, 7)), (12, (0, 1)), (16, (3, 0, 1, 2, 4)), (23, (1, 0)), (24, (1, 0)),
+                                        (25, (32, 0)), (26, (8, 16)), (29, (1, 0)), (30, (1, 0)), (32, (1, 0)), (33, (1, 0)), (34, (1, 0)), (36, (1, 0))])
 def test_train_schedule_keys_bitwise(key, values):
     """Train-step tuning keys change cache policy (18: write-through stores), stream
     schedule (12: weight grads overlapped or serial) or the weight-grad staging (16: LDS-DMA
