@@ -329,11 +329,16 @@ __global__ __launch_bounds__(256) void stem_conv(
 constexpr int STEM_CW = 64;   // channels per wave (2 accumulators): twice the waves of 128
 // ABL (timing studies only, results invalid when set): 1 no stores, 2 no input
 // loads, 4 no weight loads, 8 no MFMA.
-template <int C, int EPI, bool BOARDS, int ABL = 0>
+// STATS (train forward, EPI_RAW): per 128-row tile (the workgroup's 4 waves) and channel
+// the mean and M2 of the raw stem output straight from the accumulators (two-pass, fp32)
+// -> pa / pb [tile][C], combined exactly in fp64 by bn_fin_tiles_kernel (prow 128): the
+// col_stats pass over z0 disappears.  Waves past M stay (barriers) but store nothing.
+template <int C, int EPI, bool BOARDS, int ABL = 0, bool STATS = false>
 __global__ __launch_bounds__(256) void stem_mfma(const float* __restrict__ x, const int8_t* __restrict__ boards,
                                                  const int8_t* __restrict__ players, const float* __restrict__ ws,
                                                  const float* __restrict__ scale, const float* __restrict__ shift,
-                                                 float* __restrict__ out, int M)
+                                                 float* __restrict__ out, int M, float* __restrict__ pa = nullptr,
+                                                 float* __restrict__ pb = nullptr)
 {
     constexpr int CW = C < STEM_CW ? C : STEM_CW;
     constexpr int NJ = CW / 32;
@@ -342,7 +347,7 @@ __global__ __launch_bounds__(256) void stem_mfma(const float* __restrict__ x, co
     const int wid = threadIdx.x >> 6;
     const int r32 = lane & 31, h = lane >> 5;
     const int m0 = (blockIdx.x * 4 + wid) * 32;
-    if (m0 >= M) return;                         // wave-uniform; the kernel has no barrier
+    if (!STATS && m0 >= M) return;               // wave-uniform; no barrier without STATS
     const int c0 = blockIdx.y * CW;
 
     float bw[NJ][KS];
@@ -442,6 +447,44 @@ __global__ __launch_bounds__(256) void stem_mfma(const float* __restrict__ x, co
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if constexpr (STATS) {
+        __shared__ float sred[4][CW];
+        __shared__ float smean[CW];
+        const int rows_w = m0 < M ? min(32, M - m0) : 0;      // valid rows of this wave
+        const int tile = blockIdx.x, rows = min(128, M - tile * 128);
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            float sv = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if ((r & 3) + 8 * (r >> 2) + 4 * h < rows_w) sv += acc[j][r];
+            sv += __shfl_xor(sv, 32, 64);
+            if (h == 0) sred[wid][32 * j + r32] = sv;
+        }
+        __syncthreads();
+        if (tid < CW) {
+            const float mu = (((sred[0][tid] + sred[1][tid]) + sred[2][tid]) + sred[3][tid]) / (float)rows;
+            smean[tid] = mu;
+            pa[(size_t)tile * C + c0 + tid] = mu;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const float mu = smean[32 * j + r32];
+            float q = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if ((r & 3) + 8 * (r >> 2) + 4 * h < rows_w) {
+                    const float d = acc[j][r] - mu;
+                    q = fmaf(d, d, q);
+                }
+            q += __shfl_xor(q, 32, 64);
+            if (h == 0) sred[wid][32 * j + r32] = q;
+        }
+        __syncthreads();
+        if (tid < CW) pb[(size_t)tile * C + c0 + tid] = ((sred[0][tid] + sred[1][tid]) + sred[2][tid]) + sred[3][tid];
     }
 }
 
@@ -861,6 +904,23 @@ int conv_tuned_shape(int C, int M)
     return it == tune_cache().end() ? -1 : it->second;
 }
 
+// train-forward stem with its BN statistics partials per 128-row tile (STATS)
+hipError_t launch_stem_stats(int C, const float* x, const float* ws, float* out, int B, float* pa, float* pb,
+                             hipStream_t st)
+{
+    if (B <= 0) return hipSuccess;
+    const int M = B * PIX;
+    const int cw = C < STEM_CW ? C : STEM_CW;
+    const dim3 grid((M + 127) / 128, C / cw);
+    switch (C) {
+        case 64: hipLaunchKernelGGL((stem_mfma<64, EPI_RAW, false, 0, true>), grid, dim3(256), 0, st, x, nullptr, nullptr, ws, nullptr, nullptr, out, M, pa, pb); break;
+        case 128: hipLaunchKernelGGL((stem_mfma<128, EPI_RAW, false, 0, true>), grid, dim3(256), 0, st, x, nullptr, nullptr, ws, nullptr, nullptr, out, M, pa, pb); break;
+        case 256: hipLaunchKernelGGL((stem_mfma<256, EPI_RAW, false, 0, true>), grid, dim3(256), 0, st, x, nullptr, nullptr, ws, nullptr, nullptr, out, M, pa, pb); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 int g_stem_variant = 1;   // 1: fp32-MFMA stem (product); 0: VALU stem_conv (bitwise reference)
 int g_stem_ablation = 0;  // timing studies only (C = 128 float-plane stem)
 
@@ -994,6 +1054,16 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         if (value >= 0 && value <= 31) azg::g_train_fuse_heads = value;
         return prev;
     }
+    if (key == 38) {  // train: stem BN statistics from the stem's accumulators (1, default) or a col_stats pass (0)
+        const int prev = azg::g_train_stem_stats;
+        if (value == 0 || value == 1) azg::g_train_stem_stats = value;
+        return prev;
+    }
+    if (key == 37) {  // train: weight-grad stream priority, 0 lowest (default) or 1 highest; bitwise identical
+        const int prev = azg::g_train_side_prio;
+        if (value == 0 || value == 1) azg::g_train_side_prio = value;
+        return prev;
+    }
     if (key == 36) {  // train: next step's weight packs right after Adam (1, default) or at the step start (0); bitwise identical
         const int prev = azg::g_train_pack_after;
         if (value == 0 || value == 1) azg::g_train_pack_after = value;
@@ -1009,7 +1079,7 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         if (value == 0 || value == 1) azg::g_train_ev_device = value;
         return prev;
     }
-    if (key == 32) {  // train: head weight-grad reductions on the side stream (1, default) or the caller's (0); bitwise identical
+    if (key == 32) {  // train: head weight-grad work deferred to the end of the tower backward (1, default) or in the head chain (0); bitwise identical
         const int prev = azg::g_train_side_heads;
         if (value == 0 || value == 1) azg::g_train_side_heads = value;
         return prev;

@@ -52,6 +52,10 @@ extern int g_train_side_heads;
 extern int g_train_ev_device;
 extern int g_train_dz_all;
 extern int g_train_pack_after;
+extern int g_train_side_prio;
+extern int g_train_stem_stats;
+hipError_t launch_stem_stats(int C, const float* x, const float* ws, float* out, int B, float* pa, float* pb,
+                             hipStream_t st);
 extern int g_train_maskz;
 extern int g_train_split_pack;
 extern int g_train_skip;

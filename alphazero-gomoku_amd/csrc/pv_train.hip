@@ -82,25 +82,43 @@ struct TrainWS {
     // `side` (ev_pack_in: the step's inputs are ready; ev_pack: the packs are written)
     hipEvent_t ev_pack_in = nullptr, ev_pack = nullptr;
     bool pack_pending = false;
-    // off-critical-path head weight grads moved to `side` (ev_heads), and the join of
-    // everything `side` ran before the optimizer (ev_join)
-    hipEvent_t ev_heads = nullptr, ev_join = nullptr;
+    // the join of everything `side` ran before the optimizer (ev_join)
+    hipEvent_t ev_join = nullptr;
     int ev_flags = -1;           // flags the hand-off events were created with (key 33)
+    int side_prio = -1;          // priority class `side` was created with (key 37)
 };
 
 int g_train_dz_all = 1;     // key 34: 1 one dZ buffer per conv (default); 0 two alternating buffers + reuse waits
 int g_train_pack_after = 1; // key 36: 1 the next step's weight packs right after Adam (same stream, no hand-off); 0 at the step start
+int g_train_stem_stats = 1;  // key 38: 1 stem BN statistics from the stem's accumulators (default); 0 col_stats pass
+int g_train_side_prio = 0;   // key 37: priority of the weight-grad stream: 0 lowest (default), 1 highest
 int g_train_ev_device = 1;   // key 33: 1 stream hand-off events release at device scope (default); 0 system scope
 
 // (re)create the stream hand-off events: they only order work between two streams of
 // one device, so a device-scope release is enough (hipEventReleaseToDevice); the
 // default system-scope release adds an L2 writeback + invalidate per record
+static hipError_t make_side_stream(TrainWS* w)
+{
+    if (w->side && w->side_prio == g_train_side_prio) return hipSuccess;
+    int least = 0, greatest = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e != hipSuccess) return e;
+    if (w->side) {
+        (void)hipStreamSynchronize(w->side);
+        (void)hipStreamDestroy(w->side);
+        w->side = nullptr;
+    }
+    e = hipStreamCreateWithPriority(&w->side, hipStreamNonBlocking, g_train_side_prio ? greatest : least);
+    if (e == hipSuccess) w->side_prio = g_train_side_prio;
+    return e;
+}
+
 static hipError_t make_events(TrainWS* w)
 {
     const int flags = hipEventDisableTiming | (g_train_ev_device ? hipEventReleaseToDevice : 0);
     if (w->ev_flags == flags) return hipSuccess;
     hipEvent_t* evs[] = {&w->ev_ready[0], &w->ev_ready[1], &w->ev_done[0], &w->ev_done[1], &w->ev_pack_in,
-                         &w->ev_pack, &w->ev_heads, &w->ev_join};
+                         &w->ev_pack, &w->ev_join};
     if (w->side) (void)hipStreamSynchronize(w->side);
     for (hipEvent_t* e : evs) {
         if (*e) (void)hipEventDestroy(*e);
@@ -128,7 +146,6 @@ void free_train_workspace(azg_pv* h)
     }
     if (w->ev_pack_in) (void)hipEventDestroy(w->ev_pack_in);
     if (w->ev_pack) (void)hipEventDestroy(w->ev_pack);
-    if (w->ev_heads) (void)hipEventDestroy(w->ev_heads);
     if (w->ev_join) (void)hipEventDestroy(w->ev_join);
     if (w->side) (void)hipStreamDestroy(w->side);
     delete w;
@@ -904,9 +921,7 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
         // the weight grads are off the critical path: their stream gets the LOWEST
         // priority so the dependent chain on the caller's stream (BN kernels, dgrad)
         // is dispatched first whenever workgroup slots free up
-        int least = 0, greatest = 0;
-        hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-        if (e == hipSuccess) e = hipStreamCreateWithPriority(&w->side, hipStreamNonBlocking, least);
+        hipError_t e = make_side_stream(w);
         if (e == hipSuccess) e = make_events(w);
         if (e != hipSuccess) return set_error("train: side stream / events", e);
     }
@@ -986,7 +1001,7 @@ int g_train_skip = 0;     // study build only (key 19): skip BN kernels to time 
 int g_train_split_pack = 1;   // key 30: 1 split repack (stem on the stream, the rest on the side stream); 0 one launch
 int g_train_maskz = 1;   // key 29: 1 BN-backward apply of residual-free layers forms its ReLU mask from z (default); 0 reads act
 int g_train_fuse_heads = 28;   // key 28: bit mask of the fused head stages (pv_train_heads.hip); 0 the 18-launch chain
-int g_train_side_heads = 1;   // key 32: 1 the head weight-grad reductions on the side stream; 0 on the caller's
+int g_train_side_heads = 1;   // key 32: 1 the head weight-grad work deferred to the end of the tower backward; 0 in the head chain
 
 template <int C>
 static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, const float* zs, int B,
@@ -1160,8 +1175,15 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     // ---- forward (train-mode BN) ----
     bool last_apply = false;   // the last block's BN apply is left to the fused head kernel
     struct LastApply { const float* z; const float* res; int layer; float* out; } lastp{nullptr, nullptr, 0, nullptr};
-    AZG_CK(launch_stem(C, EPI_RAW, x, h->wstem, nullptr, nullptr, w->z0, B, st), "train: stem");
-    R(stats(w->z0, h->bn_stem));
+    if (g_train_stem_stats && !(g_train_skip & 2)) {
+        int pr0 = prof_begin(h, AZG_PROF_TRAIN_OTHER, st);
+        AZG_CK(launch_stem_stats(C, x, h->wstem, w->z0, B, w->part_a, w->part_b, st), "train: stem + statistics");
+        R(fin_fwd(h->bn_stem, 128, (M + 127) / 128));
+        prof_end(h, pr0, st);
+    } else {
+        AZG_CK(launch_stem(C, EPI_RAW, x, h->wstem, nullptr, nullptr, w->z0, B, st), "train: stem");
+        R(stats(w->z0, h->bn_stem));
+    }
     if (w->pack_pending) {   // the residual convs' packs (split repack, train_backward)
         AZG_CK(hipStreamWaitEvent(st, w->ev_pack, 0), "train: stream wait");
         w->pack_pending = false;
@@ -1229,8 +1251,11 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     const float* wpf = P + h->poff[h->t_pfc_w];
     const float* wv1 = P + h->poff[h->t_vfc1_w];
     int pr = prof_begin(h, AZG_PROF_TRAIN_OTHER, st);
+    // key 28 bits 3 + 4: both head finalizes folded into their consumer kernels
+    const bool fold_fin = (fh & 8) && (fh & 16);
+    HeadStatsArgs hs{};
+    HeadDgradArgs hd{};
     if (fh & 17) {
-        HeadStatsArgs hs{};
         hs.z = last_apply ? lastp.z : X;
         if (last_apply) {
             const int o = bd[lastp.layer].out_off;
@@ -1256,7 +1281,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         hs.bshift = w->bshift;
         hs.nbt = h->nbt;
         hs.nbn = (int)h->bn_desc.size();
-        if (fh & 16) AZG_CK(launch_head_proj_split(C, last_apply, hs, st), "train: head_proj_split");
+        if (fold_fin) AZG_CK(launch_head_proj_partials(C, last_apply, hs, st), "train: head_proj_partials");
+        else if (fh & 16) AZG_CK(launch_head_proj_split(C, last_apply, hs, st), "train: head_proj_split");
         else AZG_CK(launch_head_proj_stats(C, last_apply, hs, st), "train: head_proj_stats");
     } else {
         AZG_CK(launch_heads_project(C, false, X, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], nullptr, nullptr,
@@ -1270,22 +1296,16 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         AZG_CK(hipGetLastError(), "train: head_stats_finalize");
     }
     const int gH = grid_for((int64_t)B * 3 * PIX);
-    // head weight-grad work only Adam reads goes to the side stream (key 32)
-    const bool side_heads = g_train_side_heads && !g_wgrad_serial;
-    auto to_side = [&]() -> int32_t {
-        AZG_CK(hipEventRecord(w->ev_heads, st), "train: event record");
-        AZG_CK(hipStreamWaitEvent(w->side, w->ev_heads, 0), "train: stream wait");
-        side_used = true;
-        return 0;
-    };
+    // head weight-grad work only Adam reads waits for the end of the tower backward (key
+    // 32): the side stream is the backward's bottleneck (it ends after the caller's),
+    // while the caller's stream idles there
+    const bool defer_heads = g_train_side_heads && (fh & 8);
     // the fc weight grads, their biases / value_fc2 and the loss means (key 28 bit 3)
     auto fc_wgrads = [&](hipStream_t ws) -> int32_t {
-        {   // weight grads: dWpf = dlogits^T . fp, dWv1 = dhv^T . fv
-            GemmProb a{w->dlogits, 1, ACTIONS, w->fp, 2 * PIX, 1, G + h->poff[h->t_pfc_w], 2 * PIX, 1, nullptr, 0, 0,
-                       ACTIONS, 2 * PIX, B};
-            GemmProb b{w->dhv, 1, VHID, w->fv, PIX, 1, G + h->poff[h->t_vfc1_w], PIX, 1, nullptr, 0, 0, VHID, PIX, B};
-            AZG_CK(launch_small_gemm(a, &b, ws), "train: head fc wgrad");
-        }
+        // weight grads: dWpf = dlogits^T . fp, dWv1 = dhv^T . fv
+        AZG_CK(launch_head_fc_wgrad(w->dlogits, w->fp, w->dhv, w->fv, G + h->poff[h->t_pfc_w], G + h->poff[h->t_vfc1_w],
+                                    B, ws),
+               "train: head fc wgrad");
         hipLaunchKernelGGL(heads_small_grads_kernel, dim3((HSG_OUT + 3) / 4), dim3(256), 0, ws, w->dlogits, w->dhv,
                            w->dpre, w->hv, w->lossb, B, G + h->poff[h->t_pfc_b], G + h->poff[h->t_vfc1_b],
                            G + h->poff[h->t_vfc2_w], G + h->poff[h->t_vfc2_b], losses);
@@ -1297,7 +1317,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         // heads_loss -> masked fc dgrad + head-BN backward partials -> one-wave finalize;
         // the weight grads of the fcs and their biases / value_fc2 (and the loss means) on
         // the side stream
-        AZG_CK(launch_head_bn_apply_feat(w->zh, w->bscale + ho, w->bshift + ho, w->fp, w->fv, w->feat, B, st),
+        AZG_CK(launch_head_bn_apply_feat(w->zh, w->bscale + ho, w->bshift + ho, w->fp, w->fv, w->feat, B, st,
+                                         fold_fin ? &hs : nullptr),
                "train: head_bn_apply_feat");
         AZG_CK(launch_heads_fc(w->feat, h->wfc, w->pre, B, st), "train: heads_fc");
         hipLaunchKernelGGL(heads_loss_kernel, dim3((B + 3) / 4), dim3(256), 0, st, w->pre, P + h->poff[h->t_pfc_b],
@@ -1305,7 +1326,6 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
                            P + h->poff[h->t_vfc2_b], pis, zs, w->dlogits, w->hv, w->dhv, w->dpre, w->lossb, B,
                            FC_OUT, FC_OUT);
         AZG_CK(hipGetLastError(), "train: heads_loss");
-        HeadDgradArgs hd{};
         hd.dlogits = w->dlogits;
         hd.dhv = w->dhv;
         hd.wpf = wpf;
@@ -1325,8 +1345,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         hd.grads = G;
         hd.hinv = w->binv + ho;
         hd.hb = w->hbw;
-        AZG_CK(launch_head_dgrad(hd, st), "train: head_dgrad");
-        if (!side_heads) R(fc_wgrads(st));   // else after the 1x1 backward, with one hand-off
+        AZG_CK(launch_head_dgrad(hd, st, !fold_fin), "train: head_dgrad");
+        if (!defer_heads) R(fc_wgrads(st));   // else after the tower backward
     } else if (fh & 2) {
         HeadBoardArgs hb{};
         hb.zh = w->zh;
@@ -1427,6 +1447,10 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             hw.pb = w->part_b;
         }
         hw.M = M;
+        if (fold_fin) {
+            hw.dg = hd;
+            hw.dg_nwg = head_dgrad_groups(B);
+        }
         AZG_CK(launch_heads_bwd_fused(C, NB > 0, hw, st), "train: heads_bwd_fused");
     } else {
         hipLaunchKernelGGL(head_bn_bwd_apply_kernel, dim3(gH), dim3(256), 0, st, w->zh, w->dfp, w->dfv, w->bmean + ho,
@@ -1437,17 +1461,13 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         AZG_CK(hipGetLastError(), "train: heads_bwd_proj");
     }
     // policy_conv.weight [2][C] then value_conv.weight [C]: partial layout [t][3][C]
-    {
-        hipStream_t ws = st;
-        if (side_heads && (fh & 8)) {   // one hand-off: the fc weight grads and this reduction
-            if (int32_t r2 = to_side()) return r2;
-            ws = w->side;
-            R(fc_wgrads(ws));
-        }
-        hipLaunchKernelGGL(reduce_partials_kernel, dim3((3 * C + 15) / 16), dim3(256), 0, ws, w->hpart, hntile, 3 * C,
+    auto head_proj_wgrad = [&]() -> int32_t {
+        hipLaunchKernelGGL(reduce_partials_kernel, dim3((3 * C + 15) / 16), dim3(256), 0, st, w->hpart, hntile, 3 * C,
                            G + h->poff[h->t_pc_w], G + h->poff[h->t_vc_w], 2 * C, 0, C);
-    }
-    AZG_CK(hipGetLastError(), "train: heads proj wgrad");
+        AZG_CK(hipGetLastError(), "train: heads proj wgrad");
+        return 0;
+    };
+    if (!defer_heads) R(head_proj_wgrad());
     prof_end(h, pr, st);
     auto snap = [&](int k) -> int32_t {
         if (!w->snap.empty())
@@ -1490,6 +1510,10 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         bwd_nt = ntt;
         R(snap(NB - i));
     }
+    if (defer_heads) {   // the head weight grads (Adam's inputs only)
+        R(fc_wgrads(st));
+        R(head_proj_wgrad());
+    }
     // ---- stem backward ----
     // overlaps the last conv weight grads still on the side stream: its dz goes to
     // DH (no pending weight grad reads DH), the join comes after it
@@ -1519,6 +1543,7 @@ int32_t train_backward(azg_pv* h, const float* x, const float* pis, const float*
 {
     if (int32_t r = ensure_train_ws(h, B, st)) return r;
     TrainWS* w = ws_of(h);
+    AZG_CK(make_side_stream(w), "train: side stream");
     AZG_CK(make_events(w), "train: events");
     if (h->train_packs) {
         // the packs were refreshed right after the last Adam step (train_apply, key 36) and

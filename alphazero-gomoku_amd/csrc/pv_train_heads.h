@@ -57,26 +57,6 @@ struct HeadBoardArgs {
     float* losses;
 };
 
-struct HeadBwdArgs {
-    const float* act;      // tower output a (padded NHWC)
-    const float* zh;       // [B][3][225]
-    const float* dfp;      // [B][450]
-    const float* dfv;      // [B][225]
-    const float* hmean;    // head BN mean (3)
-    const float* hb;       // [3][3] head-BN backward coefficients
-    const float* wpc;      // policy_conv.weight [2][C]
-    const float* wvc;      // value_conv.weight [C]
-    float* gx;             // gradient of the tower output (padded NHWC)
-    float* hpart;          // [tile][3][C] head 1x1 weight-grad partials
-    // last block's bn2 backward partials (NB > 0): dy = gx * (act > 0)
-    const float* z2;       // raw bn2 input
-    const float* mean2;    // bn2 batch mean
-    float* pa;             // [tile][C]: S dy
-    float* pb;             // [tile][C]: S (z - mean) dy
-    int M;
-};
-
-// key 28 bit 3: the fc stage as short, wide launches (pv_train_heads.hip)
 struct HeadDgradArgs {
     const float* dlogits;  // [B][225]
     const float* dhv;      // [B][64]
@@ -97,10 +77,38 @@ struct HeadDgradArgs {
     const float* hinv;     // head BN invstd (3)
     float* hb;             // [3][3] head-BN backward coefficients
 };
+
+struct HeadBwdArgs {
+    const float* act;      // tower output a (padded NHWC)
+    const float* zh;       // [B][3][225]
+    const float* dfp;      // [B][450]
+    const float* dfv;      // [B][225]
+    const float* hmean;    // head BN mean (3)
+    const float* hb;       // [3][3] head-BN backward coefficients
+    const float* wpc;      // policy_conv.weight [2][C]
+    const float* wvc;      // value_conv.weight [C]
+    float* gx;             // gradient of the tower output (padded NHWC)
+    float* hpart;          // [tile][3][C] head 1x1 weight-grad partials
+    // last block's bn2 backward partials (NB > 0): dy = gx * (act > 0)
+    const float* z2;       // raw bn2 input
+    const float* mean2;    // bn2 batch mean
+    float* pa;             // [tile][C]: S dy
+    float* pb;             // [tile][C]: S (z - mean) dy
+    int M;
+    // key 28 bit 4: the head-BN backward finalize folded in (every workgroup reduces
+    // head_dgrad_kernel's partials itself; null: read hb)
+    HeadDgradArgs dg;
+    int dg_nwg;            // 0: read hb
+};
+
+// key 28 bit 3: the fc stage as short, wide launches (pv_train_heads.hip)
 int head_dgrad_groups(int B);
-hipError_t launch_head_dgrad(const HeadDgradArgs& a, hipStream_t st);
+hipError_t launch_head_dgrad(const HeadDgradArgs& a, hipStream_t st, bool fin);
 hipError_t launch_head_bn_apply_feat(const float* zh, const float* hscale, const float* hshift, float* fp, float* fv,
-                                     float* feat, int B, hipStream_t st);
+                                     float* feat, int B, hipStream_t st, const HeadStatsArgs* fin);
+hipError_t launch_head_fc_wgrad(const float* dlogits, const float* fp, const float* dhv, const float* fv, float* gpf,
+                                float* gv1, int B, hipStream_t st);
+hipError_t launch_head_proj_partials(int C, bool apply, const HeadStatsArgs& a, hipStream_t st);
 // key 28 bit 4: head_proj_stats_kernel's partials finalized by a one-workgroup kernel
 hipError_t launch_head_proj_split(int C, bool apply, const HeadStatsArgs& a, hipStream_t st);
 

@@ -94,7 +94,11 @@ __device__ __forceinline__ double wsum_d(double v)
 // thread t sums workgroups t, t + 256, ... (all loads issued first), then a fixed-order
 // block reduction (256 threads; red: [4][6]); shared by the last-arriving workgroup of
 // head_proj_stats_kernel and the one-workgroup head_proj_fin_kernel (bitwise equal)
-__device__ __forceinline__ void head_stats_fin(const HeadStatsArgs& a, int nwg, double (*red)[6])
+// coef (LDS, optional): the folded scale / shift of the three channels for the caller's
+// own use; write: publish mean / invstd / scale / shift, the running stats and the
+// num_batches_tracked increments (exactly one workgroup per step may write)
+__device__ __forceinline__ void head_stats_fin(const HeadStatsArgs& a, int nwg, double (*red)[6],
+                                               float* coef = nullptr, bool write = true)
 {
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double s[6] = {0, 0, 0, 0, 0, 0};
@@ -133,18 +137,25 @@ __device__ __forceinline__ void head_stats_fin(const HeadStatsArgs& a, int nwg, 
             const float mean_f = (float)mean;
             const float inv_f = (float)(1.0 / sqrt(var + (double)BN_EPS));
             const float alpha = inv_f * a.params[d.gamma_off + c];
-            a.bmean[d.out_off + c] = mean_f;
-            a.binv[d.out_off + c] = inv_f;
-            a.bscale[d.out_off + c] = alpha;
-            a.bshift[d.out_off + c] = a.params[d.beta_off + c] - mean_f * alpha;
-            const double unb = N > 1 ? qv / (N - 1.0) : var;
-            float* rm = a.stats + d.stat_off;
-            float* rv = a.stats + d.stat_off + d.c;
-            rm[c] = (float)((double)BN_MOMENTUM * mean + (1.0 - (double)BN_MOMENTUM) * (double)rm[c]);
-            rv[c] = (float)((double)BN_MOMENTUM * unb + (1.0 - (double)BN_MOMENTUM) * (double)rv[c]);
+            const float shift = a.params[d.beta_off + c] - mean_f * alpha;
+            if (coef) {
+                coef[ch] = alpha;
+                coef[3 + ch] = shift;
+            }
+            if (write) {
+                a.bmean[d.out_off + c] = mean_f;
+                a.binv[d.out_off + c] = inv_f;
+                a.bscale[d.out_off + c] = alpha;
+                a.bshift[d.out_off + c] = shift;
+                const double unb = N > 1 ? qv / (N - 1.0) : var;
+                float* rm = a.stats + d.stat_off;
+                float* rv = a.stats + d.stat_off + d.c;
+                rm[c] = (float)((double)BN_MOMENTUM * mean + (1.0 - (double)BN_MOMENTUM) * (double)rm[c]);
+                rv[c] = (float)((double)BN_MOMENTUM * unb + (1.0 - (double)BN_MOMENTUM) * (double)rv[c]);
+            }
         }
     }
-    if (a.nbt)
+    if (write && a.nbt)
         for (int i = threadIdx.x; i < a.nbn; i += 256) a.nbt[i] += 1;
 }
 
@@ -638,6 +649,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 // = head_bn_bwd_apply_kernel (dzh on the fly) + heads_bwd_proj_kernel, and the last
 // block's bn_bwd_reduce partials per 128-row tile (HROWS), same thread layout as
 // heads_bwd_proj_kernel: float4 over channels, RG row groups, UNR rows in flight
+__device__ __forceinline__ void head_bwd_fin_wave(const HeadDgradArgs& a, int nwg, float* hk, bool write);
+
 template <int C, bool BNX>
 __global__ __launch_bounds__(256) void heads_bwd_fused_kernel(const HeadBwdArgs a)
 {
@@ -651,12 +664,22 @@ __global__ __launch_bounds__(256) void heads_bwd_fused_kernel(const HeadBwdArgs 
     const f32x4 w0 = *(const f32x4*)(a.wpc + c), w1 = *(const f32x4*)(a.wpc + C + c), w2 = *(const f32x4*)(a.wvc + c);
     f32x4 mu2 = {0.f, 0.f, 0.f, 0.f};
     if (BNX) mu2 = *(const f32x4*)(a.mean2 + c);
+    // head-BN backward coefficients: from head_bn_bwd_fin_kernel (a.dg_nwg == 0) or
+    // finalized here by every workgroup from head_dgrad_kernel's partials (workgroup 0
+    // publishes the BN grads): the same wave reduction, bitwise equal
+    __shared__ float shk[9];
+    const float* hbp = a.hb;
+    if (a.dg_nwg) {
+        if (threadIdx.x < 64) head_bwd_fin_wave(a.dg, a.dg_nwg, shk, blockIdx.x == 0);
+        __syncthreads();
+        hbp = shk;
+    }
     float hm[3], hk[3][3];
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
         hm[ch] = a.hmean[ch];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) hk[ch][k] = a.hb[ch * 3 + k];
+        for (int k = 0; k < 3; ++k) hk[ch][k] = hbp[ch * 3 + k];
     }
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, xa = s0, xb = s0;
     for (int r0 = rg; r0 < rows; r0 += RG * UNR) {
@@ -727,12 +750,26 @@ __global__ __launch_bounds__(256) void head_proj_fin_kernel(const HeadStatsArgs 
 // = head_bn_apply_kernel, also writing the features in the eval forward's padded row
 // layout feat[b][FC_FS] (policy 450 -> FC_KP, value 225 at FC_KP; the zero pads are set
 // at allocation) so the fc forward runs on heads_fc's 16-B operand loads
+// FIN (key 28 bit 4): the head BN statistics are finalized by every workgroup from
+// head_proj_stats_kernel's nwg partials (the same fixed-order reduction as
+// head_proj_fin_kernel, which this replaces: bitwise equal coefficients); workgroup 0
+// publishes them with the running stats
+template <bool FIN>
 __global__ __launch_bounds__(256) void head_bn_apply_feat_kernel(const float* __restrict__ zh,
                                                                  const float* __restrict__ hscale,
                                                                  const float* __restrict__ hshift,
                                                                  float* __restrict__ fp, float* __restrict__ fv,
-                                                                 float* __restrict__ feat, int B)
+                                                                 float* __restrict__ feat, int B,
+                                                                 const HeadStatsArgs fa, int nwg)
 {
+    __shared__ double red[4][6];
+    __shared__ float coef[6];
+    if (FIN) {
+        head_stats_fin(fa, nwg, red, coef, blockIdx.x == 0);
+        __syncthreads();
+        hscale = coef;
+        hshift = coef + 3;
+    }
     const int total = B * 3 * PIX;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
         const int b = i / (3 * PIX), k = i - b * 3 * PIX;
@@ -844,9 +881,11 @@ __global__ __launch_bounds__(256) void head_dgrad_kernel(const HeadDgradArgs a)
 
 // = head_bn_bwd_finalize_kernel over head_dgrad_kernel's per-workgroup partials (one
 // wave: lane g sums workgroups g, g + 64, ..., then a fixed xor tree)
-__global__ __launch_bounds__(64) void head_bn_bwd_fin_kernel(const HeadDgradArgs a, int nwg)
+// one wave: lane g sums workgroups g, g + 64, ..., then a fixed xor tree; hk (optional):
+// the [3][3] coefficients for the caller's own use; write: publish grads and hb
+__device__ __forceinline__ void head_bwd_fin_wave(const HeadDgradArgs& a, int nwg, float* hk, bool write)
 {
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     double sm[6] = {0, 0, 0, 0, 0, 0};
     for (int g = lane; g < nwg; g += 64)
 #pragma unroll
@@ -861,12 +900,95 @@ __global__ __launch_bounds__(64) void head_bn_bwd_fin_kernel(const HeadDgradArgs
         const double sd = sm[2 * ch], qd = sm[2 * ch + 1];
         const float inv = a.hinv[ch];
         const double invd = (double)inv;
-        a.grads[d.gamma_off + c] = (float)(qd * invd);
-        a.grads[d.beta_off + c] = (float)sd;
-        a.hb[ch * 3 + 0] = (float)(sd / N);
-        a.hb[ch * 3 + 1] = (float)(qd * invd * invd / N);
-        a.hb[ch * 3 + 2] = inv * a.params[d.gamma_off + c];
+        const float k0 = (float)(sd / N), k1 = (float)(qd * invd * invd / N), k2 = inv * a.params[d.gamma_off + c];
+        if (hk) {
+            hk[ch * 3 + 0] = k0;
+            hk[ch * 3 + 1] = k1;
+            hk[ch * 3 + 2] = k2;
+        }
+        if (write) {
+            a.grads[d.gamma_off + c] = (float)(qd * invd);
+            a.grads[d.beta_off + c] = (float)sd;
+            a.hb[ch * 3 + 0] = k0;
+            a.hb[ch * 3 + 1] = k1;
+            a.hb[ch * 3 + 2] = k2;
+        }
     }
+}
+
+__global__ __launch_bounds__(64) void head_bn_bwd_fin_kernel(const HeadDgradArgs a, int nwg)
+{
+    head_bwd_fin_wave(a, nwg, nullptr, true);
+}
+
+// fc weight gradients dWpf[j][k] = S_b dlogits[b][j] fp[b][k] (225 x 450) and dWv1[u][k]
+// = S_b dhv[b][u] fv[b][k] (64 x 225), K = the batch: one 32 x 32 output tile per
+// workgroup (grid.x: 8 x 15 policy tiles, then 2 x 8 value tiles), K split over the
+// four waves, both operands read straight into registers (A[j][b] = d[b][j] and
+// B[b][k] = f[b][k]: 128-B row pieces per half-wave), partial tiles summed in fixed wave
+// order through 16 KB of LDS -- small enough to share a CU with the conv weight-grad
+// workgroups at the end of the step (small_gemm stages K in 131 KB and waits for a free CU)
+constexpr int HW_PJ = (ACTIONS + 31) / 32, HW_PK = (2 * PIX + 31) / 32;   // 8 x 15 policy tiles
+constexpr int HW_VJ = VHID / 32, HW_VK = (PIX + 31) / 32;                 // 2 x 8 value tiles
+
+__global__ __launch_bounds__(256) void head_fc_wgrad_kernel(const float* __restrict__ dlogits,
+                                                            const float* __restrict__ fp,
+                                                            const float* __restrict__ dhv,
+                                                            const float* __restrict__ fv, float* __restrict__ gpf,
+                                                            float* __restrict__ gv1, int B)
+{
+    __shared__ float red[4][16][64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int r32 = lane & 31, h = lane >> 5;
+    int t = blockIdx.x;
+    const bool val = t >= HW_PJ * HW_PK;
+    if (val) t -= HW_PJ * HW_PK;
+    const int nk = val ? HW_VK : HW_PK;
+    const int j0 = (t / nk) * 32, k0 = (t % nk) * 32;
+    const int J = val ? VHID : ACTIONS, Kf = val ? PIX : 2 * PIX;
+    const float* D = val ? dhv : dlogits;   // [B][J]
+    const float* Fm = val ? fv : fp;        // [B][Kf]
+    const int j = j0 + r32, k = k0 + r32;
+    const bool jok = j < J, kok = k < Kf;
+    const int steps = (B + 1) / 2;
+    const int s0 = wid * steps / 4, s1 = (wid + 1) * steps / 4;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    constexpr int U = 16;   // steps per batch of loads
+    for (int sb = s0; sb < s1; sb += U) {
+        float av[U], bv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int b = 2 * (sb + u) + h;
+            const bool ok = sb + u < s1 && b < B;
+            av[u] = ok && jok ? D[(size_t)b * J + j] : 0.f;
+            bv[u] = ok && kok ? Fm[(size_t)b * Kf + k] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (sb + u < s1) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wid][r][lane] = acc[r];
+    __syncthreads();
+    if (wid == 0) {
+        float* G = val ? gv1 : gpf;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float v = ((red[0][r][lane] + red[1][r][lane]) + red[2][r][lane]) + red[3][r][lane];
+            const int jj = j0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (jj < J && kok) G[(size_t)jj * Kf + k] = v;
+        }
+    }
+}
+
+hipError_t launch_head_fc_wgrad(const float* dlogits, const float* fp, const float* dhv, const float* fv, float* gpf,
+                                float* gv1, int B, hipStream_t st)
+{
+    hipLaunchKernelGGL(head_fc_wgrad_kernel, dim3(HW_PJ * HW_PK + HW_VJ * HW_VK), dim3(256), 0, st, dlogits, fp, dhv,
+                       fv, gpf, gv1, B);
+    return hipGetLastError();
 }
 
 int head_dgrad_groups(int B) { return ((B + 31) / 32) * (HD_PT + HD_VT); }
@@ -893,20 +1015,45 @@ hipError_t launch_head_proj_split(int C, bool apply, const HeadStatsArgs& a, hip
 }
 
 hipError_t launch_head_bn_apply_feat(const float* zh, const float* hscale, const float* hshift, float* fp, float* fv,
-                                     float* feat, int B, hipStream_t st)
+                                     float* feat, int B, hipStream_t st, const HeadStatsArgs* fin)
 {
     const int total = B * 3 * PIX;
     int nb = (total + 255) / 256;
     nb = nb > 8192 ? 8192 : nb;
-    hipLaunchKernelGGL(head_bn_apply_feat_kernel, dim3(nb), dim3(256), 0, st, zh, hscale, hshift, fp, fv, feat, B);
+    if (fin)
+        hipLaunchKernelGGL(head_bn_apply_feat_kernel<true>, dim3(nb), dim3(256), 0, st, zh, hscale, hshift, fp, fv,
+                           feat, B, *fin, head_proj_stats_groups(fin->M));
+    else
+        hipLaunchKernelGGL(head_bn_apply_feat_kernel<false>, dim3(nb), dim3(256), 0, st, zh, hscale, hshift, fp, fv,
+                           feat, B, HeadStatsArgs{}, 0);
     return hipGetLastError();
 }
 
-hipError_t launch_head_dgrad(const HeadDgradArgs& a, hipStream_t st)
+// the projections + statistics partials alone (key 28 bit 4 with the finalize folded
+// into the feature kernel)
+hipError_t launch_head_proj_partials(int C, bool apply, const HeadStatsArgs& a, hipStream_t st)
+{
+    const int nwg = head_proj_stats_groups(a.M);
+#define AZG_HPQ(CC)                                                                                          \
+    case CC:                                                                                                 \
+        if (apply) hipLaunchKernelGGL((head_proj_stats_kernel<CC, true, false>), dim3(nwg), dim3(256), 0, st, a); \
+        else hipLaunchKernelGGL((head_proj_stats_kernel<CC, false, false>), dim3(nwg), dim3(256), 0, st, a);      \
+        break;
+    switch (C) {
+        AZG_HPQ(64)
+        AZG_HPQ(128)
+        AZG_HPQ(256)
+        default: return hipErrorInvalidValue;
+    }
+#undef AZG_HPQ
+    return hipGetLastError();
+}
+
+hipError_t launch_head_dgrad(const HeadDgradArgs& a, hipStream_t st, bool fin)
 {
     hipLaunchKernelGGL(head_dgrad_kernel, dim3((a.B + 31) / 32, HD_PT + HD_VT), dim3(256), 0, st, a);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess || !fin) return e;
     hipLaunchKernelGGL(head_bn_bwd_fin_kernel, dim3(1), dim3(64), 0, st, a, head_dgrad_groups(a.B));
     return hipGetLastError();
 }

@@ -333,7 +333,8 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv3x3_wgrad_nat(
     const float* __restrict__ dz, const float* __restrict__ x, float* __restrict__ slab, int M, int S)
 {
     // NWV = 4: 2 x 2 waves of (BT/2) x (BT/2); NWV = 8 (BT = 128): 2 x 4 waves of 64 co x
-    // 32 ci (two accumulators each: four waves per SIMD at two workgroups per CU)
+    // 32 ci (two accumulators each: four waves per SIMD at two workgroups per CU;
+    // measured equal to NWV = 4)
     constexpr int BT = C < 128 ? C : 128, BK = 32, NT = C / BT;
     constexpr int WNW = NWV == 8 ? 4 : 2;           // waves along ci
     constexpr int TA = BT / 64, TB = BT / (32 * WNW); // accumulators along co / ci per wave

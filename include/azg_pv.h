@@ -163,7 +163,8 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *   key 16: train conv weight-grad kernel (3 = natural pixel rows moved into LDS
  *          by LDS-DMA, default; 1 = K-contiguous register staging with 16-B
  *          fragment reads; 2 = the same two chunks ahead; 0 = row staging with 4-B
- *          reads; A/B timing, all bitwise identical);
+ *          reads; 4 = the LDS-DMA kernel with 8 waves per 128x128 tile, C = 128;
+ *          A/B timing, all bitwise identical);
  *   key 17: persistent-tower claim granularity (1 = one M tile with all its N
  *          tiles, run back to back by the claiming workgroup, default: the second
  *          tile's halo rows hit the XCD's L2, +2 % at B = 512 and 4096, measured;
@@ -191,14 +192,30 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *   key 27: train conv weight-grad pixel splits (0 = automatic, default); bitwise
  *          identical only at a fixed value;
  *   key 28: train head chain, bit mask of the fused stages (bit 0 head projections +
- *          BN statistics + finalize, also applying the last block's bn2; bit 1 head BN
- *          apply + FCs + loss + fc data grads per 4 boards; bit 2 head BN-backward +
- *          1x1 backward + the last block's BN-backward partials); 0 = the 18-launch
- *          chain; fp32 sums in another order (within the oracle tolerance);
+ *          BN statistics + finalize by the last workgroup, also applying the last
+ *          block's bn2; bit 4 the same projections with a one-workgroup finalize
+ *          launch; bit 1 head BN apply + FCs + loss + fc data grads per 4 boards; bit 3
+ *          the fc stage as short wide launches: features in the eval row layout ->
+ *          heads_fc -> loss -> LDS-staged masked fc dgrad tiles + head-BN backward
+ *          partials -> one-wave finalize; bit 2 head BN-backward + 1x1 backward + the
+ *          last block's BN-backward partials); default 28 (bits 2, 3, 4); 0 = the
+ *          18-launch chain; fp32 sums in another order (within the oracle tolerance);
  *   key 29: train BN-backward ReLU mask formed from z with the layer's scale and
  *          shift (1, default) or read from the stored activation (0); bitwise identical;
  *   key 30: train weight repack split over the two streams (1, default) or one launch
  *          on the caller's stream (0); bitwise identical;
+ *   key 32: train head weight-grad work (fc weight grads, bias / value_fc2 grads,
+ *          loss means, the 1x1 weight-grad reduction) deferred to the end of the
+ *          tower backward (1, default, with key 28 bit 3) or inside the head chain
+ *          (0); bitwise identical;
+ *   key 33: train stream hand-off events with a device-scope release (1, default)
+ *          or the system-scope default (0); bitwise identical;
+ *   key 34: train backward: one dZ buffer per conv (1, default: no stream waits
+ *          for buffer reuse -- each costs the caller's stream ~6 us, measured) or
+ *          two alternating buffers (0); bitwise identical;
+ *   key 36: train step: the next step's weight packs and eval BN fold right behind
+ *          Adam in azg_pv_train_apply (1, default) or at the start of the next
+ *          azg_pv_train_backward (0); bitwise identical;
  *   key 31: study build only: the 64x64 / 128x64 towers with sc1 dependent loads
  *          and no acquire (two or more workgroups per CU: outside the microarch
  *          guide's measured envelope; the product uses the acquire there and the
