@@ -870,6 +870,16 @@ static hipError_t launch_train_t(const float* in, const float* wp, const float* 
     return launch_train_v<C, EPI, XE, PRO, true, 32, 8>(in, wp, resid, out, M, ex, px, fx, st);
 }
 
+// dgrad of a residual-free layer's conv with that layer's BN backward applied in the
+// staging (PRO_BNBWD, C <= 128: the 256-channel tile body has no room for the prologue)
+template <int C>
+static hipError_t launch_train_bnbwd(const float* in, const float* wp, const float* resid, float* out, int M,
+                                     const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st)
+{
+    if constexpr (C <= 128) return launch_train_t<C, EPI_ADD, XE_BNBWD, PRO_BNBWD>(in, wp, resid, out, M, ex, px, fx, st);
+    return hipErrorInvalidValue;
+}
+
 // Train conv with fused BN partials: (EPI_RAW, XE_STATS) forward, optionally with
 // the input layer's BN applied in the staging (px: PRO_BN / PRO_BN_RES); (EPI_RAW |
 // EPI_ADD, XE_BNBWD) dgrad.  Partials are per TRAIN_BM-row M tile; with fx (cnt set)
@@ -887,6 +897,8 @@ hipError_t launch_conv3x3_train(int C, int epi, int xe, const float* in, const f
             return launch_train_t<CC, EPI_RAW, XE_STATS, PRO_BN>(in, wp, resid, out, M, ex, *px, fx, st); \
         if (epi == EPI_RAW && xe == XE_STATS) return launch_train_t<CC, EPI_RAW, XE_STATS>(in, wp, resid, out, M, ex, p0, fx, st); \
         if (epi == EPI_RAW && xe == XE_BNBWD) return launch_train_t<CC, EPI_RAW, XE_BNBWD>(in, wp, resid, out, M, ex, p0, fx, st); \
+        if (epi == EPI_ADD && xe == XE_BNBWD && px && px->gm)                                      \
+            return launch_train_bnbwd<CC>(in, wp, resid, out, M, ex, *px, fx, st);                 \
         if (epi == EPI_ADD && xe == XE_BNBWD) return launch_train_t<CC, EPI_ADD, XE_BNBWD>(in, wp, resid, out, M, ex, p0, fx, st); \
         return hipErrorInvalidValue;
     switch (C) {
@@ -1054,6 +1066,21 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         if (value >= 0 && value <= 31) azg::g_train_fuse_heads = value;
         return prev;
     }
+    if (key == 41) {  // train: in-kernel split-group combine of the weight-grad slabs (1; slower, measured) or all S slabs to wgrad_reduce (0, default); other sum order
+        const int prev = azg::g_wgrad_comb;
+        if (value == 0 || value == 1) azg::g_wgrad_comb = value;
+        return prev;
+    }
+    if (key == 40) {  // train: residual-free layers' BN backward applied in their conv1 dgrad's staging (1; C <= 128: spills 92 B/lane, slower) or a bn_bwd_apply pass (0, default); bitwise identical
+        const int prev = azg::g_train_fuse_bwd;
+        if (value == 0 || value == 1) azg::g_train_fuse_bwd = value;
+        return prev;
+    }
+    if (key == 39) {  // train: each weight grad's slab reduction after the next conv's weight-grad kernel (1, default) or right behind its own (0); bitwise identical
+        const int prev = azg::g_train_defer_reduce;
+        if (value == 0 || value == 1) azg::g_train_defer_reduce = value;
+        return prev;
+    }
     if (key == 38) {  // train: stem BN statistics from the stem's accumulators (1, default) or a col_stats pass (0)
         const int prev = azg::g_train_stem_stats;
         if (value == 0 || value == 1) azg::g_train_stem_stats = value;
@@ -1079,9 +1106,9 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         if (value == 0 || value == 1) azg::g_train_ev_device = value;
         return prev;
     }
-    if (key == 32) {  // train: head weight-grad work deferred to the end of the tower backward (1, default) or in the head chain (0); bitwise identical
+    if (key == 32) {  // train: head weight-grad work deferred to the end of the tower backward (1, default), on the side stream during the head chain (2) or in the chain (0); bitwise identical
         const int prev = azg::g_train_side_heads;
-        if (value == 0 || value == 1) azg::g_train_side_heads = value;
+        if (value >= 0 && value <= 2) azg::g_train_side_heads = value;
         return prev;
     }
     if (key == 27) {  // train wgrad split-K count (0 automatic; 8..64, multiple of 8); bitwise NOT identical across values

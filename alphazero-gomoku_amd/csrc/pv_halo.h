@@ -60,6 +60,10 @@ constexpr int halo_span(int BM)
     return mx;
 }
 
+// per-channel vectors an operand prologue stages in LDS (PRO, below: 0 none; 1, 2 BN
+// scale / shift; 3 the BN-backward apply's scale, shift, mean, gm, k, iw)
+constexpr int pro_params(int PRO) { return PRO == 3 ? 6 : PRO != 0 ? 2 : 0; }
+
 // LDS: halo rows [HR][32] + two weight chunks [2][BN][32] (register staging), or
 // two halo buffers [2][HRG][32] + [2][BN][32] (LDS-DMA staging, VAR bit 4); the
 // epilogue reuses it as a [BM][ELD] tile.
@@ -70,7 +74,7 @@ constexpr int halo_lds_bytes()
     const int hrg = (halo_span(T::BM) + 7) / 8 * 8;
     const int staging = (VAR & 4) ? (2 * hrg + ((VAR & 2) ? 3 : 2) * BN) * T::BK * 4
                                   : ((halo_span(T::BM) + T::RPP - 1) / T::RPP * T::RPP + 2 * BN) * T::BK * 4 +
-                                        (PRO ? 2 * C * 4 : 0);
+                                        pro_params(PRO) * C * 4;
     const int epilogue = T::BM * (BN + 8) * 4;
     return staging > epilogue ? staging : epilogue;
 }
@@ -227,12 +231,24 @@ __device__ __forceinline__ void bn_fin_combine8(double v0, double v1, double* re
 constexpr int PRO_NONE = 0;
 constexpr int PRO_BN = 1;       // relu(bn(z))
 constexpr int PRO_BN_RES = 2;   // relu(bn(z) + res)
+// PRO_BNBWD (dgrad of a residual-free layer's conv): the staged tensor is the gradient g
+// of the layer's BN + ReLU output, `res` its raw BN input z, and the BatchNorm backward
+// is applied per element exactly as bn_bwd_apply_kernel<C, false, WT, MZ = true>:
+//   dy = fma(z, scale, shift) > 0 ? g : 0;  dz = ((dy - gm) - (z - mean) * k) * iw
+// (padding rows stay 0); the N-tile-0 workgroups write the tile's own rows of dz (the
+// weight gradient's operand)
+constexpr int PRO_BNBWD = 3;
 struct ProX {
-    const float* res;     // PRO_BN_RES: residual input (padded NHWC)
+    const float* res;     // PRO_BN_RES: residual input; PRO_BNBWD: the layer's raw BN input z
     const float* scale;   // [C] BN scale of the input layer (invstd * gamma)
     const float* shift;   // [C] beta - mean * scale
-    float* aout;          // a (padded NHWC): own rows written when n0 == 0
+    float* aout;          // a (dz for PRO_BNBWD, padded NHWC): own rows written when n0 == 0
+    const float* mean = nullptr;   // PRO_BNBWD: [C] batch mean, and the bn_bwd_apply
+    const float* gm = nullptr;     // coefficients gm = S dy / N, k, iw = invstd * gamma
+    const float* kk = nullptr;
+    const float* iw = nullptr;
 };
+
 
 // key of the 16-B slot swizzle of halo row `row` (padded-pixel index): the padded
 // board position v = yy*15 + xx (see halo_tile)
@@ -698,7 +714,7 @@ __device__ __forceinline__ void halo_tile(
 
     float* Ah = smem;                 // [HR][32]
     float* Bs = smem + HR * BK;       // [2][BN][32]
-    float* Ps = smem + (HR + 2 * BN) * BK;   // PRO: [2][C] input-layer BN scale / shift
+    float* Ps = smem + (HR + 2 * BN) * BK;   // PRO: [2][C] input-layer BN scale / shift (+ [4][C] PRO_BNBWD)
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
@@ -730,6 +746,12 @@ __device__ __forceinline__ void halo_tile(
         for (int c = tid; c < C; c += T::NT) {
             Ps[c] = px.scale[c];
             Ps[C + c] = px.shift[c];
+            if constexpr (PRO == PRO_BNBWD) {
+                Ps[2 * C + c] = px.mean[c];
+                Ps[3 * C + c] = px.gm[c];
+                Ps[4 * C + c] = px.kk[c];
+                Ps[5 * C + c] = px.iw[c];
+            }
         }
         __syncthreads();
     }
@@ -739,7 +761,7 @@ __device__ __forceinline__ void halo_tile(
     // the next chunk's MFMAs to land before the ds_write that waits on it (the loops
     // are fully unrolled: the rb1 = rb2 hand-over is a register renaming, not a move)
     f32x4 rh[H_LD], rb1[B_LD], rb2[B_LD];
-    f32x4 rr[PRO == PRO_BN_RES ? H_LD : 1];
+    f32x4 rr[(PRO == PRO_BN_RES || PRO == PRO_BNBWD) ? H_LD : 1];
     // VAR bit 16 (persistent tower at ONE workgroup per CU): halo rows are produced
     // inside the launch by other CUs; every load of them is an sc1 buffer load (L1
     // bypassed) in place of the consumer's acquire -- row 1 of the microarch guide's
@@ -767,7 +789,7 @@ __device__ __forceinline__ void halo_tile(
                                                                                     (VAR & 16) ? 16 : 0));
         else
             rh[i] = *(const f32x4*)(in + hsrc[i] + cg * BK);
-        if constexpr (PRO == PRO_BN_RES) {
+        if constexpr (PRO == PRO_BN_RES || PRO == PRO_BNBWD) {
             if constexpr ((VAR & 32) != 0)
                 rr[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(res_rs, (hsrc[i] + cg * BK) * 4, 0, 0));
             else
@@ -821,11 +843,25 @@ __device__ __forceinline__ void halo_tile(
             const f32x4 s4 = *(const f32x4*)(Ps + cg * BK + sc);
             const f32x4 t4 = *(const f32x4*)(Ps + C + cg * BK + sc);
             f32x4 v = rh[i];
+            if constexpr (PRO == PRO_BNBWD) {   // = bn_bwd_apply_kernel (MZ): v = g, rr = z
+                const f32x4 mu = *(const f32x4*)(Ps + 2 * C + cg * BK + sc);
+                const f32x4 g_ = *(const f32x4*)(Ps + 3 * C + cg * BK + sc);
+                const f32x4 k_ = *(const f32x4*)(Ps + 4 * C + cg * BK + sc);
+                const f32x4 w_ = *(const f32x4*)(Ps + 5 * C + cg * BK + sc);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                float y = fmaf(v[e], s4[e], t4[e]);
-                if constexpr (PRO == PRO_BN_RES) y += rr[i][e];
-                v[e] = (pint >> i) & 1 ? fmaxf(y, 0.f) : 0.f;
+                for (int e = 0; e < 4; ++e) {
+                    const float z = rr[i][e];
+                    const float dy = fmaf(z, s4[e], t4[e]) > 0.f ? v[e] : 0.f;
+                    const float d = ((dy - g_[e]) - (z - mu[e]) * k_[e]) * w_[e];
+                    v[e] = (pint >> i) & 1 ? d : 0.f;
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float y = fmaf(v[e], s4[e], t4[e]);
+                    if constexpr (PRO == PRO_BN_RES) y += rr[i][e];
+                    v[e] = (pint >> i) & 1 ? fmaxf(y, 0.f) : 0.f;
+                }
             }
             rh[i] = v;
             if ((pown >> i) & 1) store4<true>(px.aout, ars, hsrc[i] + cg * BK, v);

@@ -54,6 +54,8 @@ extern int g_train_dz_all;
 extern int g_train_pack_after;
 extern int g_train_side_prio;
 extern int g_train_stem_stats;
+extern int g_train_defer_reduce;
+extern int g_train_fuse_bwd;
 hipError_t launch_stem_stats(int C, const float* x, const float* ws, float* out, int B, float* pa, float* pb,
                              hipStream_t st);
 extern int g_train_maskz;
@@ -62,6 +64,7 @@ extern int g_train_skip;
 extern int g_wgrad_bk;
 extern int g_wgrad_kernel;
 extern int g_wgrad_splits;
+extern int g_wgrad_comb;
 extern int g_train_wt;
 constexpr int kTowerMaxBlocks = 32;
 int conv_batch_bucket(int M);

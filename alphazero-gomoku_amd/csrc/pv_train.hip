@@ -25,7 +25,9 @@
 namespace azg {
 
 hipError_t launch_wgrad(int C, const float* dz, const float* x, float* slab, float* dw, int M, int S,
-                        hipStream_t st);
+                        hipStream_t st, bool reduce = true, unsigned* gcnt = nullptr, float* gslab = nullptr);
+bool wgrad_comb_on(int kernel, int S);
+hipError_t launch_wgrad_reduce(int C, const float* slab, float* dw, int S, hipStream_t st);
 int wgrad_splits(int C, int M);
 constexpr int kMaxWgradSplits = 64;   // wgrad_splits <= slots / tiles <= 56, rounded to 8
 
@@ -48,6 +50,9 @@ struct TrainWS {
     float* hpart = nullptr;                        // [ntile][3][C]
     float* spart = nullptr;                        // [B][27][C]
     float* slab = nullptr;                         // wgrad split-K slabs
+    float* slab2 = nullptr;                        // the second slab buffer (deferred reductions, key 39)
+    float* gslab[2] = {nullptr, nullptr};          // split-group slabs [8][9][C][C] (key 41), alternating
+    unsigned* gcnt = nullptr;                      // split-group arrival counters (key 41)
     int S = 0, rps = 0;
     unsigned* fincnt = nullptr;                    // fused BN finalize: arrival counters per N tile
     // heads
@@ -90,6 +95,8 @@ struct TrainWS {
 
 int g_train_dz_all = 1;     // key 34: 1 one dZ buffer per conv (default); 0 two alternating buffers + reuse waits
 int g_train_pack_after = 1; // key 36: 1 the next step's weight packs right after Adam (same stream, no hand-off); 0 at the step start
+int g_train_fuse_bwd = 0;      // key 40: 1 conv1's BN backward in its dgrad staging (C <= 128); 0 bn_bwd_apply pass
+int g_train_defer_reduce = 1;  // key 39: 1 each weight grad's slab reduction after the next conv's weight-grad kernel
 int g_train_stem_stats = 1;  // key 38: 1 stem BN statistics from the stem's accumulators (default); 0 col_stats pass
 int g_train_side_prio = 0;   // key 37: priority of the weight-grad stream: 0 lowest (default), 1 highest
 int g_train_ev_device = 1;   // key 33: 1 stream hand-off events release at device scope (default); 0 system scope
@@ -936,6 +943,14 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     // split-K for wgrad: ~512 rows per split
     w->S = kMaxWgradSplits;
     A(w->slab, (size_t)w->S * 9 * C * C, false);
+    A(w->slab2, (size_t)w->S * 9 * C * C, false);
+    A(w->gslab[0], (size_t)8 * 9 * C * C, false);
+    A(w->gslab[1], (size_t)8 * 9 * C * C, false);
+    {
+        float* gc = nullptr;
+        A(gc, 9 * 16 * 8, true);   // 9 taps x (C/128)^2 tiles x 8 groups, C <= 512
+        w->gcnt = (unsigned*)gc;
+    }
     A(w->zh, (size_t)cap * 3 * PIX, false);
     A(w->fp, (size_t)cap * 2 * PIX, false);
     A(w->fv, (size_t)cap * PIX, false);
@@ -1135,6 +1150,20 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     float* dzbuf[2] = {w->DZ, w->DZ2};
     const bool dz_all = g_train_dz_all != 0 && !g_wgrad_serial;
     bool side_used = false;
+    // key 39: a weight grad's slab reduction is launched on `side` after the NEXT conv's
+    // weight-grad kernel (two alternating slab buffers), so each weight-grad kernel starts
+    // as soon as its dZ is ready, ahead of the previous reduction's HBM pass
+    const bool defer_red = g_train_defer_reduce != 0 && !g_wgrad_serial;
+    struct PendRed { float* slab; float* dw; int S; };
+    PendRed pend_red{nullptr, nullptr, 0};
+    float* slabs[2] = {w->slab, w->slab2};
+    int slab_i = 0;
+    auto flush_red = [&]() -> int32_t {
+        if (pend_red.slab) AZG_CK(launch_wgrad_reduce(C, pend_red.slab, pend_red.dw, pend_red.S, w->side),
+                                  "train: wgrad reduce");
+        pend_red = PendRed{nullptr, nullptr, 0};
+        return 0;
+    };
     // dZ of backward conv k (2i+1: conv2 of block i, 2i: conv1): its own buffer (key 34)
     // or the alternating slot
     auto dzb = [&](int k, int slot) -> float* { return dz_all ? w->dzs[k] : dzbuf[slot]; };
@@ -1143,7 +1172,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             int pr = prof_begin(h, AZG_PROF_TRAIN_WGRAD, st);
             const int S = wgrad_splits(C, M);
             if (S > w->S) return set_error("train: wgrad splits exceed the slab workspace", hipErrorInvalidValue);
-            AZG_CK(launch_wgrad(C, dz, xin, w->slab, G + h->poff[tensor], M, S, st), "train: wgrad");
+            AZG_CK(launch_wgrad(C, dz, xin, w->slab, G + h->poff[tensor], M, S, st, true, w->gcnt, w->gslab[0]),
+                   "train: wgrad");
             prof_end(h, pr, st);
             return 0;
         }
@@ -1152,7 +1182,16 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         int pr = prof_begin(h, AZG_PROF_TRAIN_WGRAD, w->side);
         const int S = wgrad_splits(C, M);
         if (S > w->S) return set_error("train: wgrad splits exceed the slab workspace", hipErrorInvalidValue);
-        AZG_CK(launch_wgrad(C, dz, xin, w->slab, G + h->poff[tensor], M, S, w->side), "train: wgrad");
+        float* sl = defer_red ? slabs[slab_i] : w->slab;
+        const bool comb = wgrad_comb_on(g_wgrad_kernel, S);
+        float* gsl = w->gslab[defer_red ? slab_i : 0];
+        AZG_CK(launch_wgrad(C, dz, xin, sl, G + h->poff[tensor], M, S, w->side, !defer_red, w->gcnt, gsl),
+               "train: wgrad");
+        if (defer_red) {   // the previous conv's reduction behind this conv's MFMA work
+            if (int32_t r2 = flush_red()) return r2;
+            pend_red = comb ? PendRed{gsl, G + h->poff[tensor], 8} : PendRed{sl, G + h->poff[tensor], S};
+            slab_i ^= 1;
+        }
         prof_end(h, pr, w->side);
         side_used = true;
         if (!dz_all) {
@@ -1299,7 +1338,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     // head weight-grad work only Adam reads waits for the end of the tower backward (key
     // 32): the side stream is the backward's bottleneck (it ends after the caller's),
     // while the caller's stream idles there
-    const bool defer_heads = g_train_side_heads && (fh & 8);
+    const bool defer_heads = g_train_side_heads == 1 && (fh & 8);
+    const bool side_heads = g_train_side_heads == 2 && (fh & 8) && !g_wgrad_serial;   // on `side` during the head chain
     // the fc weight grads, their biases / value_fc2 and the loss means (key 28 bit 3)
     auto fc_wgrads = [&](hipStream_t ws) -> int32_t {
         // weight grads: dWpf = dlogits^T . fp, dWv1 = dhv^T . fv
@@ -1345,8 +1385,14 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         hd.grads = G;
         hd.hinv = w->binv + ho;
         hd.hb = w->hbw;
+        if (side_heads) {   // the fc weight grads only need the loss stage: run them on the idle side stream
+            AZG_CK(hipEventRecord(w->ev_ready[0], st), "train: event record");
+            AZG_CK(hipStreamWaitEvent(w->side, w->ev_ready[0], 0), "train: stream wait");
+            R(fc_wgrads(w->side));
+            side_used = true;
+        }
         AZG_CK(launch_head_dgrad(hd, st, !fold_fin), "train: head_dgrad");
-        if (!defer_heads) R(fc_wgrads(st));   // else after the tower backward
+        if (!defer_heads && !side_heads) R(fc_wgrads(st));   // else after the tower backward / on `side`
     } else if (fh & 2) {
         HeadBoardArgs hb{};
         hb.zh = w->zh;
@@ -1467,7 +1513,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         AZG_CK(hipGetLastError(), "train: heads proj wgrad");
         return 0;
     };
-    if (!defer_heads) R(head_proj_wgrad());
+    if (!defer_heads && !side_heads) R(head_proj_wgrad());
     prof_end(h, pr, st);
     auto snap = [&](int k) -> int32_t {
         if (!w->snap.empty())
@@ -1487,6 +1533,9 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         R(bwd_reduce(w->gX, w->xo[NB - 1], w->z2[NB - 1], h->bn_blk[NB - 1].second));
         bwd_nt = ntile;
     }
+    // key 40: the dZ of each block's conv1 formed in its dgrad's staging (needs dz_all:
+    // the weight grad reads dz1 after the dgrad; the bn1 mask from z1: key 29)
+    const bool fuse_bwd = g_train_fuse_bwd && C <= 128 && dz_all && g_train_maskz && !(g_train_skip & 4);
     bool done_fin = false;   // the previous dgrad launch already finalized the next layer
     for (int i = NB - 1; i >= 0; --i) {
         const float* Xin = i == 0 ? w->a0 : w->xo[i - 1];
@@ -1502,16 +1551,38 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         if (!ffin) R(bwd_fin(h->bn_blk[i].first, ntt));
         R(reuse(1));
         float* dz1 = dzb(2 * i, 1);
-        R(bwd_apply(w->DH, w->hh[i], w->z1[i], h->bn_blk[i].first, dz1, nullptr, true));
-        R(wgrad(1, dz1, Xin, h->t_blk[i].w1));
-        R(conv(EPI_ADD, XE_BNBWD, dz1, w->wdpack + (size_t)(2 * i) * 9 * C * C, w->GR, w->gX, Xin, zin, lin,
-               ffin ? lin : -1));
+        if (fuse_bwd) {
+            // bn1's backward (mask from z1, no residual) applied in this dgrad's staging;
+            // its N-tile-0 workgroups write dz1 for the weight grad, which follows it
+            const int o1 = bd[h->bn_blk[i].first].out_off;
+            ProX px{w->z1[i], w->bscale + o1, w->bshift + o1, dz1, w->bmean + o1, w->bgm + o1, w->bk + o1, w->biw + o1};
+            int pr = prof_begin(h, AZG_PROF_TRAIN_CONV, st, B);
+            const EpiX ex{Xin, zin, w->bmean + bd[lin].out_off, w->part_a, w->part_b};
+            FinX fx{};
+            if (ffin) {
+                fx = fin_args(lin, false);
+                fx.cnt = w->fincnt;
+            }
+            AZG_CK(launch_conv3x3_train(C, EPI_ADD, XE_BNBWD, w->DH, w->wdpack + (size_t)(2 * i) * 9 * C * C, w->GR,
+                                        w->gX, M, ex, st, &px, ffin ? &fx : nullptr),
+                   "train: conv3x3 (fused BN backward)");
+            prof_end(h, pr, st);
+            R(wgrad(1, dz1, Xin, h->t_blk[i].w1));
+        } else {
+            R(bwd_apply(w->DH, w->hh[i], w->z1[i], h->bn_blk[i].first, dz1, nullptr, true));
+            R(wgrad(1, dz1, Xin, h->t_blk[i].w1));
+            R(conv(EPI_ADD, XE_BNBWD, dz1, w->wdpack + (size_t)(2 * i) * 9 * C * C, w->GR, w->gX, Xin, zin, lin,
+                   ffin ? lin : -1));
+        }
         done_fin = ffin;
         bwd_nt = ntt;
         R(snap(NB - i));
     }
+    if (defer_red) R(flush_red());   // the last conv's reduction
     if (defer_heads) {   // the head weight grads (Adam's inputs only)
         R(fc_wgrads(st));
+        R(head_proj_wgrad());
+    } else if (side_heads) {
         R(head_proj_wgrad());
     }
     // ---- stem backward ----

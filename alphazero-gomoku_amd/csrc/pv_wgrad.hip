@@ -328,9 +328,17 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_t(
 // read land on disjoint bank halves.  Rows past the split read padded pixel 0 (the
 // zero halo).  Measured at 6x128, B = 128 (scripts/wgrad_lab.hip): 74.0 vs 89.2 us
 // (hipEvent incl. launch) for the K-contiguous kernel.
-template <int C, bool WT = true, int NWV = 4>
+// COMB (key 41, with WT): the S/8 splits of one pixel-split group (splits g, g + 8, ...:
+// the XCD-aware order puts them on one XCD) combine in-kernel -- every workgroup stores
+// its slab write-through, drains, meets a barrier and counts the tile on the group's
+// agent-scope counter (R1); the workgroup whose add returns the last count runs ONE
+// agent-scope acquire + vmcnt(0), then sums the group's slabs of its tile in split
+// order (plain loads) into the group slab gslab[g] (write-through).  wgrad_reduce then
+// reads 8 group slabs instead of S: 4.7 instead of 33 MB per conv at 6x128, B = 128.
+template <int C, bool WT = true, int NWV = 4, bool COMB = false>
 __global__ __launch_bounds__(64 * NWV, 2) void conv3x3_wgrad_nat(
-    const float* __restrict__ dz, const float* __restrict__ x, float* __restrict__ slab, int M, int S)
+    const float* __restrict__ dz, const float* __restrict__ x, float* __restrict__ slab, int M, int S,
+    unsigned* __restrict__ gcnt = nullptr, float* __restrict__ gslab = nullptr)
 {
     // NWV = 4: 2 x 2 waves of (BT/2) x (BT/2); NWV = 8 (BT = 128): 2 x 4 waves of 64 co x
     // 32 ci (two accumulators each: four waves per SIMD at two workgroups per CU;
@@ -440,6 +448,49 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv3x3_wgrad_nat(
                 const int ci = ci0 + wn * (BT / WNW) + j * 32 + r32;
                 store1<WT>(out, rs, co * C + ci, acc[i][j][r]);
             }
+    if constexpr (COMB) {
+        static_assert(WT, "the group combine reads slabs stored write-through");
+        __shared__ unsigned flag;
+        const int tid_ = threadIdx.x;
+        const int g = xcd, tileid = k % TILES, nmem = S / 8;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid_ == 0) {
+            unsigned* c = gcnt + tileid * 8 + g;
+            const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned last = old == (unsigned)(nmem - 1) ? 1u : 0u;
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-armed
+            }
+            flag = last;
+        }
+        __syncthreads();
+        if (flag) {
+            // this tile's BT x BT region of tap `tap`: float4 runs, the group's slabs in
+            // split order, every load of a run issued before its sum
+            constexpr int NTH = 64 * NWV, F4 = BT * BT / 4 / NTH, MMAX = 8;
+            float* gout = gslab + ((size_t)g * 9 + tap) * C * C;
+            const __amdgpu_buffer_rsrc_t grs = wt_rsrc(gout, (size_t)C * C * sizeof(float));
+            for (int u = 0; u < F4; ++u) {
+                const int e = (tid_ + NTH * u) * 4;
+                const size_t off = (size_t)(co0 + e / BT) * C + ci0 + e % BT;
+                f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+                for (int m0 = 0; m0 < nmem; m0 += MMAX) {
+                    f32x4 v[MMAX];
+#pragma unroll
+                    for (int m = 0; m < MMAX; ++m)
+                        if (m0 + m < nmem)
+                            v[m] = *(const f32x4*)(slab + ((size_t)((m0 + m) * 8 + g) * 9 + tap) * C * C + off);
+#pragma unroll
+                    for (int m = 0; m < MMAX; ++m)
+                        if (m0 + m < nmem) sum += v[m];
+                }
+                store4<true>(gout, grs, (int)off, sum);
+            }
+        }
+    }
 }
 
 // dW (torch layout [co][ci][3][3]) = sum over slabs, fixed order: four interleaved
@@ -469,13 +520,24 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     }
 }
 
+// dW = the S slabs summed in fixed order (wgrad_reduce_kernel)
+hipError_t launch_wgrad_reduce(int C, const float* slab, float* dw, int S, hipStream_t st)
+{
+    const int total = 9 * C * C;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, dw, C, S);
+    return hipGetLastError();
+}
+
 // 3: LDS-DMA natural rows (conv3x3_wgrad_nat, default); 1: K-contiguous register
 // staging; 2: the same two chunks ahead; 0: row staging (A/B; all bitwise identical)
 int g_wgrad_kernel = 3;
 
+bool wgrad_comb_on(int kernel, int S);
+int g_wgrad_comb = 0;   // key 41: 1 in-kernel split-group combine of the LDS-DMA weight grad (slower, measured); 0 off (default)
+
 template <int C, int BK = 32>
 static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, float* dw, int M, int S,
-                                 hipStream_t st)
+                                 hipStream_t st, bool reduce, unsigned* gcnt, float* gslab)
 {
     using T = WgTile<C, BK>;
     if (S % 8) return hipErrorInvalidValue;           // wgrad_splits guarantees S % 8 == 0
@@ -500,11 +562,23 @@ static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, f
             if (g_wgrad_kernel == 4 && (g_train_wt & 4)) {   // 8 waves per 128x128 tile
                 hipLaunchKernelGGL((conv3x3_wgrad_nat<C, true, 8>), grid, dim3(512), lds, st, dz, x, slab, M, S);
                 hipError_t e = hipGetLastError();
-                if (e != hipSuccess) return e;
-                const int total = 9 * C * C;
-                hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, dw, C, S);
-                return hipGetLastError();
+                if (e != hipSuccess || !reduce) return e;
+                return launch_wgrad_reduce(C, slab, dw, S, st);
             }
+        }
+        if (wgrad_comb_on(g_wgrad_kernel, S) && gcnt && gslab) {
+            static bool attr_c = false;
+            if (!attr_c) {
+                hipError_t e = hipFuncSetAttribute((const void*)conv3x3_wgrad_nat<C, true, 4, true>,
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                if (e != hipSuccess) return e;
+                attr_c = true;
+            }
+            hipLaunchKernelGGL((conv3x3_wgrad_nat<C, true, 4, true>), grid, dim3(256), lds, st, dz, x, slab, M, S, gcnt,
+                               gslab);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess || !reduce) return e;
+            return launch_wgrad_reduce(C, gslab, dw, 8, st);
         }
         if (g_train_wt & 4)
             hipLaunchKernelGGL((conv3x3_wgrad_nat<C, true>), grid, dim3(256), lds, st, dz, x, slab, M, S);
@@ -542,11 +616,8 @@ static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, f
         hipLaunchKernelGGL((conv3x3_wgrad_mfma<C, BK>), grid, dim3(256), T::LDS_BYTES, st, dz, x, slab, M, S);
     }
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const int total = 9 * C * C;
-    int nb = (total + 255) / 256;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nb), dim3(256), 0, st, slab, dw, C, S);
-    return hipGetLastError();
+    if (e != hipSuccess || !reduce) return e;
+    return launch_wgrad_reduce(C, slab, dw, S, st);
 }
 
 // Pixel splits: S is a multiple of 8 (the XCD-aware order keeps each split on one
@@ -578,15 +649,22 @@ int wgrad_splits(int C, int M)
 }
 
 // slab must hold S*9*C*C floats, S = wgrad_splits(C, M).
+// the weight grad reduces S / 8 group slabs in-kernel (key 41): the LDS-DMA kernel
+// (key 16 = 3) with write-through slabs
+bool wgrad_comb_on(int kernel, int S)
+{
+    return g_wgrad_comb && kernel == 3 && (g_train_wt & 4) && S % 8 == 0 && g_wgrad_bk == 32;
+}
+
 hipError_t launch_wgrad(int C, const float* dz, const float* x, float* slab, float* dw, int M, int S,
-                        hipStream_t st)
+                        hipStream_t st, bool reduce, unsigned* gcnt, float* gslab)
 {
     switch (C) {
-        case 64: return launch_wgrad_t<64>(dz, x, slab, dw, M, S, st);
+        case 64: return launch_wgrad_t<64>(dz, x, slab, dw, M, S, st, reduce, gcnt, gslab);
         case 128:
-            if (g_wgrad_bk == 16) return launch_wgrad_t<128, 16>(dz, x, slab, dw, M, S, st);
-            return launch_wgrad_t<128>(dz, x, slab, dw, M, S, st);
-        case 256: return launch_wgrad_t<256>(dz, x, slab, dw, M, S, st);
+            if (g_wgrad_bk == 16) return launch_wgrad_t<128, 16>(dz, x, slab, dw, M, S, st, reduce, gcnt, gslab);
+            return launch_wgrad_t<128>(dz, x, slab, dw, M, S, st, reduce, gcnt, gslab);
+        case 256: return launch_wgrad_t<256>(dz, x, slab, dw, M, S, st, reduce, gcnt, gslab);
         default: return hipErrorInvalidValue;
     }
 }

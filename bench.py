@@ -545,9 +545,10 @@ def main():
     ap.add_argument("--sp-games", type=int, default=256)
     ap.add_argument("--sp-sims", type=int, default=400)
     ap.add_argument("--sp-max-moves", type=int, default=225, help="train.py's max_moves (board size squared)")
-    ap.add_argument("--train-steps", type=int, default=20, help="steps of the configs[3] train leg (0: skip)")
+    ap.add_argument("--train-steps", type=int, default=60,
+                    help="steps of the configs[3] train leg (0: skip; 60 steps amortise the first step's enqueue)")
     ap.add_argument("--big-steps", type=int, default=10, help="10x256 forwards (configs[4] net; 0: skip the leg)")
-    ap.add_argument("--big-train-steps", type=int, default=5)
+    ap.add_argument("--big-train-steps", type=int, default=10)
     ap.add_argument("--pente-games", type=int, default=32)
     ap.add_argument("--pente-moves", type=int, default=225,
                     help="max_moves of the configs[4] Pente self-play (225 = every game to its end)")

@@ -1,13 +1,13 @@
 #!/bin/bash
-# Round 3 lease o: head finalizes folded into their consumers (key 28 = 28), side-stream
-# priority (key 37): oracle + bitwise tests, train-step A/B, kernel trace.
+# Round 3 lease p: BN backward of each block's conv1 folded into its dgrad staging
+# (key 40): bitwise key test, oracle gradients, train-step A/B, trace segments.
 set -o pipefail
-O=gpurun_out/r3o
+O=gpurun_out/r3p
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests/test_gpu_train.py -m gpu -v --timeout 200 --timeout-method thread -k "schedule_keys or head_chain" > $O/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_train.py -m gpu -v --timeout 400 --timeout-method thread -k "schedule_keys or gradients_match or two_steps or goldens" > $O/pytest.log 2>&1
 s=$?; echo "pytest rc $s"; grep -E "FAILED|ERROR|passed|failed" $O/pytest.log | tail -8; [ $s -eq 0 ] || exit $s
-timeout -k 10 300 python -u scripts/train_r3_probe.py --ab "39=1,32=1;39=0,32=1;39=1,32=2;39=0,32=2" > $O/probe.log 2>&1
+timeout -k 10 300 python -u scripts/train_r3_probe.py --ab "40=1;40=0" > $O/probe.log 2>&1
 s=$?; tail -1 $O/probe.log; [ $s -eq 0 ] || exit $s
 timeout -k 10 200 rocprofv3 --kernel-trace -f csv -d $O/tr -o run -- python3 scripts/bench_train.py --steps 10 --cpu-steps 0 > $O/tr.log 2>&1
 s=$?; echo "trace rc $s"; [ $s -eq 0 ] || exit $s

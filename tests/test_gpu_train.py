@@ -339,7 +339,7 @@ def test_train_then_predict_uses_new_weights():
 
 
 @pytest.mark.parametrize("key,values", [(18, (0, 1, 2, 4, 7)), (12, (0, 1)), (16, (3, 0, 1, 2, 4)), (23, (1, 0)), (24, (1, 0)),
-                                        (25, (32, 0)), (26, (8, 16)), (29, (1, 0)), (30, (1, 0)), (32, (1, 0)), (33, (1, 0)), (34, (1, 0)), (36, (1, 0)), (37, (0, 1))])
+                                        (25, (32, 0)), (26, (8, 16)), (29, (1, 0)), (30, (1, 0)), (32, (1, 0, 2)), (33, (1, 0)), (34, (1, 0)), (36, (1, 0)), (37, (0, 1)), (39, (1, 0)), (40, (1, 0))])
 def test_train_schedule_keys_bitwise(key, values):
     """Train-step tuning keys change cache policy (18: write-through stores), stream
     schedule (12: weight grads overlapped or serial) or the weight-grad staging (16: LDS-DMA
@@ -359,6 +359,9 @@ def test_train_schedule_keys_bitwise(key, values):
     x = encode_batch(b, p)
     pi, z = synth_targets(128, seed=92)
     prev = lib.azg_pv_set_tuning(key, values[0])
+    # the weight-grad kernels (16) and slab store policies (18) share one reduction only
+    # without the in-kernel split-group combine (41: LDS-DMA kernel, write-through slabs)
+    prev41 = lib.azg_pv_set_tuning(41, 0) if key in (16, 18) else None
     ref = None
     try:
         for v in values:
@@ -375,16 +378,19 @@ def test_train_schedule_keys_bitwise(key, values):
                 assert all(torch.equal(a, c) for a, c in zip(ref, got)), (key, v)
     finally:
         lib.azg_pv_set_tuning(key, prev)
+        if prev41 is not None:
+            lib.azg_pv_set_tuning(41, prev41)
 
 
 
-@pytest.mark.parametrize("key,value", [(27, 16), (38, 0)])
+@pytest.mark.parametrize("key,value", [(27, 16), (38, 0), (41, 1)])
 @pytest.mark.parametrize("tag,blocks,ch,B", [("6x128", 6, 128, 128), ("3x64", 3, 64, 37)])
 def test_train_sum_order_variants_match_oracle(key, value, tag, blocks, ch, B):
     """Train keys that change an fp32 summation order hold the oracle tolerance of
     test_gradients_match_oracle (no bitwise test): the weight-grad split count (27) and
     the stem's BN statistics (38 = 0: a separate col_stats pass over 64-row tiles
-    instead of the stem epilogue's 128-row tiles)."""
+    instead of the stem epilogue's 128-row tiles) and the weight-grad slab reduction
+    (41 = 1: the in-kernel split-group combine instead of all S slabs in wgrad_reduce)."""
     import _native
     lib = _native.load_library()
     prev = lib.azg_pv_set_tuning(key, value)
