@@ -1066,6 +1066,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         if (value >= 0 && value <= 31) azg::g_train_fuse_heads = value;
         return prev;
     }
+    if (key == 42) {  // train: forward conv tiles stored after the BN-partial arrival count (1, default) or before (0); bitwise identical
+        const int prev = azg::g_train_late_store;
+        if (value == 0 || value == 1) azg::g_train_late_store = value;
+        return prev;
+    }
     if (key == 41) {  // train: in-kernel split-group combine of the weight-grad slabs (1; slower, measured) or all S slabs to wgrad_reduce (0, default); other sum order
         const int prev = azg::g_wgrad_comb;
         if (value == 0 || value == 1) azg::g_wgrad_comb = value;

@@ -119,6 +119,8 @@ struct EpiX {
 //     iw = invstd * gamma.
 struct FinX {
     unsigned* cnt = nullptr;     // fused: arrival counter per N tile (0 at launch; reset by the last arriver)
+    int late = 0;                // XE_STATS: store the tile after the arrival count (key 42): the
+                                 // write-through drain of the 32 KB tile leaves the finalize's path
     const float* gamma = nullptr;
     const float* beta = nullptr;                            // FWD
     float *rmean = nullptr, *rvar = nullptr;                // FWD running stats
@@ -324,6 +326,9 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
     // XE partials of this thread's 4 channels over its rows
     f32x4 xa = {0.f, 0.f, 0.f, 0.f}, xb = {0.f, 0.f, 0.f, 0.f}, xmu = {0.f, 0.f, 0.f, 0.f};
     f32x4 vk[XE == XE_STATS ? NPASS : 1];
+    // late store (XE_STATS + fused finalize): the raw tile (kept in vk) is stored after the
+    // partials are published and counted, so the arrival waits only for the partials
+    const bool late = XE == XE_STATS && EPI == EPI_RAW && fx.cnt != nullptr && fx.late != 0;
     if (XE == XE_BNBWD) xmu = *(const f32x4*)(ex.mean + col);
 #pragma unroll
     for (int p = 0; p < NPASS; ++p) {
@@ -369,11 +374,13 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                     xb[e] = fmaf(xz[e] - xmu[e], dy, xb[e]);
                 }
             }
-            if constexpr (SC1) {
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), out_rs, o * 4, 0, 16);
-            } else {
-                *(f32x4*)(out + o) = v;
+            if (!late) {
+                if constexpr (SC1) {
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), out_rs, o * 4, 0, 16);
+                } else {
+                    *(f32x4*)(out + o) = v;
+                }
             }
         }
     }
@@ -451,6 +458,24 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                 *flag = last;
             }
             __syncthreads();
+            if constexpr (XE == XE_STATS) {
+                if (late) {   // the tile (= vk, EPI_RAW) now; it drains while the finalize runs
+#pragma unroll
+                    for (int p = 0; p < NPASS; ++p) {
+                        const int m = m0 + er + p * RPI;
+                        if (m < M) {
+                            const int o = pad_off(m, C) + col;
+                            if constexpr (SC1) {
+                                __builtin_amdgcn_raw_buffer_store_b128(
+                                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, vk[p]), out_rs,
+                                    o * 4, 0, 16);
+                            } else {
+                                *(f32x4*)(out + o) = vk[p];
+                            }
+                        }
+                    }
+                }
+            }
             if (*flag) {
                 // wave w sums tile class w % 8 of channels n0 + lane (coalesced rows of
                 // the [tile][C] partials), the classes combine through LDS in the order

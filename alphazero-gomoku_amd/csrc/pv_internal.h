@@ -56,6 +56,7 @@ extern int g_train_side_prio;
 extern int g_train_stem_stats;
 extern int g_train_defer_reduce;
 extern int g_train_fuse_bwd;
+extern int g_train_late_store;
 hipError_t launch_stem_stats(int C, const float* x, const float* ws, float* out, int B, float* pa, float* pb,
                              hipStream_t st);
 extern int g_train_maskz;

@@ -95,6 +95,7 @@ struct TrainWS {
 
 int g_train_dz_all = 1;     // key 34: 1 one dZ buffer per conv (default); 0 two alternating buffers + reuse waits
 int g_train_pack_after = 1; // key 36: 1 the next step's weight packs right after Adam (same stream, no hand-off); 0 at the step start
+int g_train_late_store = 1;    // key 42: 1 forward conv tiles stored after the BN-partial arrival count; 0 before
 int g_train_fuse_bwd = 0;      // key 40: 1 conv1's BN backward in its dgrad staging (C <= 128); 0 bn_bwd_apply pass
 int g_train_defer_reduce = 1;  // key 39: 1 each weight grad's slab reduction after the next conv's weight-grad kernel
 int g_train_stem_stats = 1;  // key 38: 1 stem BN statistics from the stem's accumulators (default); 0 col_stats pass
@@ -1105,6 +1106,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         if (fin >= 0) {
             fx = fin_args(fin, xe == XE_STATS);
             fx.cnt = w->fincnt;
+            fx.late = xe == XE_STATS ? g_train_late_store : 0;
         }
         AZG_CK(launch_conv3x3_train(C, epi, xe, in, wp, res, out, M, ex, st, nullptr, fin >= 0 ? &fx : nullptr),
                "train: conv3x3");
@@ -1243,6 +1245,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             const ProX px{p.res, w->bscale + o, w->bshift + o, p.out};
             FinX fx = fin_args(fin, true);
             fx.cnt = w->fincnt;
+            fx.late = g_train_late_store;
             AZG_CK(launch_conv3x3_train(C, EPI_RAW, XE_STATS, p.z, wpk, nullptr, out, M, ex, st, &px,
                                         ffin ? &fx : nullptr),
                    "train: conv3x3 (fused BN apply)");
@@ -1562,7 +1565,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             if (ffin) {
                 fx = fin_args(lin, false);
                 fx.cnt = w->fincnt;
-            }
+                }
             AZG_CK(launch_conv3x3_train(C, EPI_ADD, XE_BNBWD, w->DH, w->wdpack + (size_t)(2 * i) * 9 * C * C, w->GR,
                                         w->gX, M, ex, st, &px, ffin ? &fx : nullptr),
                    "train: conv3x3 (fused BN backward)");

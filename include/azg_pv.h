@@ -206,8 +206,8 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          on the caller's stream (0); bitwise identical;
  *   key 32: train head weight-grad work (fc weight grads, bias / value_fc2 grads,
  *          loss means, the 1x1 weight-grad reduction) deferred to the end of the
- *          tower backward (1, default, with key 28 bit 3) or inside the head chain
- *          (0); bitwise identical;
+ *          tower backward (1, default, with key 28 bit 3), on the side stream during
+ *          the head chain (2) or inside the head chain (0); bitwise identical;
  *   key 33: train stream hand-off events with a device-scope release (1, default)
  *          or the system-scope default (0); bitwise identical;
  *   key 34: train backward: one dZ buffer per conv (1, default: no stream waits
@@ -216,6 +216,21 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *   key 36: train step: the next step's weight packs and eval BN fold right behind
  *          Adam in azg_pv_train_apply (1, default) or at the start of the next
  *          azg_pv_train_backward (0); bitwise identical;
+ *   key 37: train weight-grad stream priority: 0 lowest (default), 1 highest;
+ *          bitwise identical;
+ *   key 38: train stem BN statistics from the stem's accumulators (1, default) or
+ *          a separate col_stats pass (0); fp32 sums in another order;
+ *   key 39: train: each conv's weight-grad slab reduction launched after the next
+ *          conv's weight-grad kernel (1, default) or right behind its own (0);
+ *          bitwise identical;
+ *   key 40: train: each block's conv1 BN backward applied in its dgrad's halo
+ *          staging (1; C <= 128, spills, slower) or a bn_bwd_apply pass (0, default);
+ *          bitwise identical;
+ *   key 41: train: in-kernel split-group combine of the weight-grad slabs by the
+ *          last arriver of each group (1; slower) or all slabs to wgrad_reduce (0,
+ *          default); fp32 sums in another order;
+ *   key 42: train forward convs store their tile after the BN-partial arrival count
+ *          (1, default) or before (0); bitwise identical;
  *   key 31: study build only: the 64x64 / 128x64 towers with sc1 dependent loads
  *          and no acquire (two or more workgroups per CU: outside the microarch
  *          guide's measured envelope; the product uses the acquire there and the
