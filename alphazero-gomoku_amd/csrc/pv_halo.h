@@ -61,8 +61,8 @@ constexpr int halo_span(int BM)
 }
 
 // per-channel vectors an operand prologue stages in LDS (PRO, below: 0 none; 1, 2 BN
-// scale / shift; 3 the BN-backward apply's scale, shift, mean, gm, k, iw)
-constexpr int pro_params(int PRO) { return PRO == 3 ? 6 : PRO != 0 ? 2 : 0; }
+// scale / shift; 3, 4 the BN-backward apply's scale, shift, mean, gm, k, iw)
+constexpr int pro_params(int PRO) { return PRO >= 3 ? 6 : PRO != 0 ? 2 : 0; }
 
 // LDS: halo rows [HR][32] + two weight chunks [2][BN][32] (register staging), or
 // two halo buffers [2][HRG][32] + [2][BN][32] (LDS-DMA staging, VAR bit 4); the
@@ -74,7 +74,8 @@ constexpr int halo_lds_bytes()
     const int hrg = (halo_span(T::BM) + 7) / 8 * 8;
     const int staging = (VAR & 4) ? (2 * hrg + ((VAR & 2) ? 3 : 2) * BN) * T::BK * 4
                                   : ((halo_span(T::BM) + T::RPP - 1) / T::RPP * T::RPP + 2 * BN) * T::BK * 4 +
-                                        pro_params(PRO) * C * 4;
+                                        pro_params(PRO) * C * 4 +
+                                        (PRO == 4 ? (halo_span(T::BM) + T::RPP - 1) / T::RPP * T::RPP * T::BK * 4 : 0);
     const int epilogue = T::BM * (BN + 8) * 4;
     return staging > epilogue ? staging : epilogue;
 }
@@ -128,7 +129,10 @@ struct FinX {
     const float* inv_i = nullptr;                           // !FWD: invstd of the layer
     float *ggamma = nullptr, *gbeta = nullptr;              // !FWD: parameter grads
     float *gm_o = nullptr, *k_o = nullptr, *iw_o = nullptr; // !FWD: bn_bwd_apply coefficients
+    float* skp = nullptr;        // stream-K forward (conv3x3_train_sk): [tile][SK_MAXP][NT][16] parts
+    unsigned* skc = nullptr;     // stream-K: arrival counter per tile (0 at launch; reset by the last arriver)
 };
+constexpr int SK_MAXP = 3;       // parts per tile: every part holds >= 18 of a tile's 36 K chunks
 // partial sums of tiles t = j, j+8, ... (the tile class j of 8) for channel c.
 // COH: every load is an agent-scope relaxed atomic load (`global_load_dword sc1`,
 // L1 bypassed) -- the consumer form that may replace an acquire only inside the
@@ -240,6 +244,13 @@ constexpr int PRO_BN_RES = 2;   // relu(bn(z) + res)
 // (padding rows stay 0); the N-tile-0 workgroups write the tile's own rows of dz (the
 // weight gradient's operand)
 constexpr int PRO_BNBWD = 3;
+// PRO_BNBWD_LDS: the same transform, with z staged by LDS-DMA into its own [HR][32]
+// buffer (no registers held across taps) and applied once per channel group as the
+// staged g rows are written to LDS (outside the MFMA taps: no spills)
+constexpr int PRO_BNBWD_LDS = 4;
+#ifndef AZG_PRO_REMAT
+#define AZG_PRO_REMAT 1
+#endif
 struct ProX {
     const float* res;     // PRO_BN_RES: residual input; PRO_BNBWD: the layer's raw BN input z
     const float* scale;   // [C] BN scale of the input layer (invstd * gamma)
@@ -701,14 +712,17 @@ __device__ __forceinline__ void halo_mainloop_glds(const float* __restrict__ in,
 // set): bit 1 skips the weight loads, bit 2 the halo loads, bit 4 the per-chunk
 // barriers, bit 8 replaces LDS fragment reads by register values, bit 16 skips the
 // epilogue stores (kept live by a never-true compare).
+// SK (stream-K part, conv3x3_train_sk): only K chunks [k0, k1) of the tile (chunk j =
+// tap j % 9 of channel group j / 9), accumulated in the same per-group order; the
+// partial accumulator is returned in *sk_acc and no epilogue runs.
 template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1 = false, int ABL = 0, int VAR = 0,
-          int XE = XE_NONE, int PRO = PRO_NONE>
+          int XE = XE_NONE, int PRO = PRO_NONE, bool SK = false>
 __device__ __forceinline__ void halo_tile(
     const float* __restrict__ in, const float* __restrict__ wp,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ resid, float* __restrict__ out, __amdgpu_buffer_rsrc_t out_rs,
     int M, int m0, int n0, float* smem, const EpiX& ex = EpiX{}, const ProX& px = ProX{},
-    const FinX& fx = FinX{})
+    const FinX& fx = FinX{}, int k0 = 0, int k1 = 0, f32x16* sk_acc = nullptr)
 {
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
     if constexpr ((VAR & 4) != 0) {   // LDS-DMA staging
@@ -729,6 +743,7 @@ __device__ __forceinline__ void halo_tile(
     static_assert(H_LD <= 9, "halo loads are spread over the 9 taps");
     static_assert(PRO == PRO_NONE || H_LD <= 8, "the operand prologue of a row runs one tap after its load");
     static_assert(PRO == PRO_NONE || ((VAR == 0 || VAR == 32) && ABL == 0), "operand prologue: register staging only");
+    static_assert(PRO != PRO_BNBWD_LDS || (RPP == 8 * NW_ && T::NT < 1024), "z DMA: one 8-row piece per wave and row block");
     // VAR (A/B studies; the product uses 0, measured fastest): bit 1 = halo rows
     // swizzled on the padded board position (conflict-free fragment reads) and an
     // unpadded epilogue tile; bit 2 = weights staged two chunks ahead; bit 4 = LDS-DMA
@@ -736,10 +751,15 @@ __device__ __forceinline__ void halo_tile(
     constexpr bool VSWZ = (VAR & 1) != 0;
     constexpr bool BPF2 = (VAR & 2) != 0;
     constexpr int NCHK = 9 * CG;
+    static_assert(!SK || (TM == 1 && TN == 1 && !BPF2 && PRO != PRO_BNBWD_LDS && ABL == 0), "stream-K part: one accumulator, register staging");
+    // SK: this part's chunk range and channel groups
+    const int kb = SK ? k0 : 0, ke = SK ? k1 : NCHK;
+    const int cgb = kb / 9, cge = (ke - 1) / 9;
 
     float* Ah = smem;                 // [HR][32]
     float* Bs = smem + HR * BK;       // [2][BN][32]
     float* Ps = smem + (HR + 2 * BN) * BK;   // PRO: [2][C] input-layer BN scale / shift (+ [4][C] PRO_BNBWD)
+    float* Zs = Ps + pro_params(PRO) * C;    // PRO_BNBWD_LDS: [HR][32] z rows (unswizzled, lane-linear DMA)
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
@@ -771,7 +791,7 @@ __device__ __forceinline__ void halo_tile(
         for (int c = tid; c < C; c += T::NT) {
             Ps[c] = px.scale[c];
             Ps[C + c] = px.shift[c];
-            if constexpr (PRO == PRO_BNBWD) {
+            if constexpr (PRO == PRO_BNBWD || PRO == PRO_BNBWD_LDS) {
                 Ps[2 * C + c] = px.mean[c];
                 Ps[3 * C + c] = px.gm[c];
                 Ps[4 * C + c] = px.kk[c];
@@ -809,6 +829,13 @@ __device__ __forceinline__ void halo_tile(
         if constexpr (HPRED) {
             if (hbase + sr + RPP * i > hmax) return;
         }
+        // z row first: in-order vmcnt retirement makes the wait for rh[i] cover it.
+        // Lane l of wave w lands at row 8w + l/8, chunk l%8 of row block i = its own
+        // staged (sr + RPP i, sc) position.
+        // (buffer form: one 32-bit offset VGPR per row, shared with the g load)
+        if constexpr (PRO == PRO_BNBWD_LDS)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(res_rs, (__attribute__((address_space(3))) void*)(Zs + (8 * wid + RPP * i) * BK),
+                                                     16, (hsrc[i] + cg * BK) * 4, 0, 0, 0);
         if constexpr ((VAR & 48) != 0)
             rh[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, (hsrc[i] + cg * BK) * 4, 0,
                                                                                     (VAR & 16) ? 16 : 0));
@@ -863,7 +890,7 @@ __device__ __forceinline__ void halo_tile(
     // per staged row i: applied one tap after its load was issued (the residual row
     // dies there, keeping the PRO_BN_RES register peak low), to all rows of the first
     // group before its store
-    auto pro_row = [&](int cg, int i) {
+    auto pro_row = [&](int cg, int i, bool own = true) {
         if constexpr (PRO != PRO_NONE) {
             const f32x4 s4 = *(const f32x4*)(Ps + cg * BK + sc);
             const f32x4 t4 = *(const f32x4*)(Ps + C + cg * BK + sc);
@@ -889,12 +916,39 @@ __device__ __forceinline__ void halo_tile(
                 }
             }
             rh[i] = v;
-            if ((pown >> i) & 1) store4<true>(px.aout, ars, hsrc[i] + cg * BK, v);
+            if (own && ((pown >> i) & 1)) store4<true>(px.aout, ars, hsrc[i] + cg * BK, v);
         }
     };
-    auto hstore = [&]() {
+    auto hstore = [&](int cg) {
+        if constexpr (PRO == PRO_BNBWD_LDS) {
+            // wait for the last staged row (hence every z DMA before it), then keep the
+            // z reads below that wait
+            asm volatile("" ::"v"(rh[H_LD - 1]));
+            __builtin_amdgcn_sched_barrier(0);
+            const f32x4 s4 = *(const f32x4*)(Ps + cg * BK + sc);
+            const f32x4 t4 = *(const f32x4*)(Ps + C + cg * BK + sc);
+            const f32x4 mu = *(const f32x4*)(Ps + 2 * C + cg * BK + sc);
+            const f32x4 g_ = *(const f32x4*)(Ps + 3 * C + cg * BK + sc);
+            const f32x4 k_ = *(const f32x4*)(Ps + 4 * C + cg * BK + sc);
+            const f32x4 w_ = *(const f32x4*)(Ps + 5 * C + cg * BK + sc);
 #pragma unroll
-        for (int i = 0; i < H_LD; ++i) *(f32x4*)(Ah + (sr + RPP * i) * BK + hwchunk[i]) = rh[i];
+            for (int i = 0; i < H_LD; ++i) {
+                const f32x4 z4 = *(const f32x4*)(Zs + (sr + RPP * i) * BK + sc);
+                f32x4 v = rh[i];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {   // = bn_bwd_apply_kernel (MZ), as PRO_BNBWD
+                    const float z = z4[e];
+                    const float dy = fmaf(z, s4[e], t4[e]) > 0.f ? v[e] : 0.f;
+                    const float d = ((dy - g_[e]) - (z - mu[e]) * k_[e]) * w_[e];
+                    v[e] = (pint >> i) & 1 ? d : 0.f;
+                }
+                *(f32x4*)(Ah + (sr + RPP * i) * BK + hwchunk[i]) = v;
+                if ((pown >> i) & 1) store4<true>(px.aout, ars, hsrc[i] + cg * BK, v);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < H_LD; ++i) *(f32x4*)(Ah + (sr + RPP * i) * BK + hwchunk[i]) = rh[i];
+        }
     };
     auto bstore = [&](const f32x4 (&rb)[B_LD], int buf) {
         float* b = Bs + buf * BN * BK;
@@ -926,22 +980,26 @@ __device__ __forceinline__ void halo_tile(
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
 #pragma unroll
-    for (int i = 0; i < H_LD; ++i) hload(0, i);
+    for (int i = 0; i < H_LD; ++i) hload(cgb, i);
     if (BPF2) {
         bload(rb2, kchunk(0));
         bload(rb1, kchunk(1));
     } else {
-        bload(rb1, kchunk(0));
+        bload(rb1, kchunk(kb));
     }
+    if constexpr (PRO != PRO_BNBWD_LDS) {
+        // a part starting inside a group re-stages it: the part before wrote its own rows
 #pragma unroll
-    for (int i = 0; i < H_LD; ++i) pro_row(0, i);
-    hstore();
+        for (int i = 0; i < H_LD; ++i) pro_row(cgb, i, kb % 9 == 0);
+    }
+    hstore(cgb);
     if (BPF2) bstore(rb2, 0);
-    else bstore(rb1, 0);
+    else bstore(rb1, kb & 1);
     __syncthreads();
 
 #pragma unroll
     for (int cg = 0; cg < CG; ++cg) {
+        if (SK && (cg < cgb || cg > cge)) continue;
         f32x16 at[TM][TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -949,15 +1007,25 @@ __device__ __forceinline__ void halo_tile(
             for (int j = 0; j < TN; ++j)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) at[i][j][r] = 0.f;
-        const bool more = cg + 1 < CG;
+        const bool more = SK ? cg + 1 <= cge : cg + 1 < CG;
+        // PRO (AZG_PRO_REMAT): the fragment row addresses are rebuilt per channel group
+        // (a few VALU ops per tap) instead of 9 x 4 hoisted addresses living across the
+        // unrolled groups -- with the prologue's registers those spilled, and every
+        // reload's vmcnt wait drained the prefetch queue
+        if constexpr (PRO != PRO_NONE && AZG_PRO_REMAT) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(hrow[i]));
+        }
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
             const int j = cg * 9 + tap;            // chunk index
             const int cur = j & 1;
+            // SK: chunks outside [kb, ke) only issue the next group's halo loads / prologue
+            const bool act = !SK || (j >= kb && j < ke);
             if (BPF2) {
                 if (j + 2 < NCHK) bload(rb2, kchunk(j + 2));
             } else {
-                if (j + 1 < NCHK) bload(rb1, kchunk(j + 1));
+                if (act && j + 1 < ke) bload(rb1, kchunk(j + 1));
             }
             if (more && tap < H_LD) hload(cg + 1, tap);
             // keep the next chunk's global loads at the top of the chunk: without this
@@ -973,6 +1041,7 @@ __device__ __forceinline__ void halo_tile(
                 aswz[i] = VSWZ ? ((vpix[i] + vd) >> 1) & 7 : (r >> 1) & 7;
             }
             const float* Bb = Bs + cur * BN * BK;
+            if (act)   // SK: one uniform branch around the tap's MFMA block
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 f32x4 a[TM], b[TN];
@@ -997,17 +1066,17 @@ __device__ __forceinline__ void halo_tile(
                             at[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], at[i][j], 0, 0, 0);
             }
             // the row loaded one tap ago gets its BN / ReLU now (PRO)
-            if (PRO != PRO_NONE && more && tap >= 1 && tap <= H_LD) pro_row(cg + 1, tap - 1);
-            if (j + 1 < NCHK) {
+            if (PRO != PRO_NONE && PRO != PRO_BNBWD_LDS && more && tap >= 1 && tap <= H_LD) pro_row(cg + 1, tap - 1);
+            if (act && j + 1 < ke) {
                 bstore(rb1, cur ^ 1);
                 if (BPF2) {
 #pragma unroll
                     for (int i = 0; i < B_LD; ++i) rb1[i] = rb2[i];
                 }
             }
-            if (!(ABL & 4)) __syncthreads();
+            if (act && !(ABL & 4)) __syncthreads();
             if (tap == 8 && more) {
-                hstore();            // every wave is past its last read of this group's halo
+                hstore(cg + 1);      // every wave is past its last read of this group's halo
                 __syncthreads();
             }
         }
@@ -1017,6 +1086,10 @@ __device__ __forceinline__ void halo_tile(
             for (int j = 0; j < TN; ++j) acc[i][j] += at[i][j];
     }
 
+    if constexpr (SK) {
+        *sk_acc = acc[0][0];
+        return;
+    }
     // the last chunk ended with a barrier: the staging buffers are free
     halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, (VSWZ ? BN : BN + 8), (VAR & 8) != 0, XE,
                   (VAR & 16) ? 2 : (VAR & 32) ? 1 : 0>(
