@@ -247,97 +247,6 @@ __global__ __launch_bounds__(64 * NWT) __attribute__((amdgpu_waves_per_eu(4))) v
                                                           (t % NTN) * T::BN, smem, ex, px, fx);
 }
 
-// Stream-K train conv (key 44; forward XE_STATS convs at C = 128, 8-wave 128x64 tiles):
-// a one-round launch of T tiles on G resident slots leaves every CU holding two tiles
-// or one (450 tiles on 512 slots: the CUs with two bound the launch, measured flat from
-// 394 to 510 tiles).  Here the T x 36 K chunks (tap-major within a channel group, the
-// tile body's order) are cut into G equal contiguous ranges, one per workgroup, so every
-// slot holds 31-32 chunks; a range covers the tail of one tile and the head of the next.
-// Each part of a split tile is published write-through ([tile][part][thread][16]),
-// counted on the tile's agent-scope counter (producer R1: vmcnt(0), barrier, one
-// atomic), and the last arriver runs ONE agent acquire, sums the parts in part order
-// (p0 + p1) + p2 -- the same order whoever arrives last -- and runs the tile's epilogue
-// (tile statistics, store, fused BN finalize) exactly as conv3x3_train.  The sums differ
-// from the one-part tile only in where the K sum is split (fp32 rounding).
-template <int C, int EPI, int XE, bool WT, int PRO>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv3x3_train_sk(
-    const float* __restrict__ in, const float* __restrict__ wp, const float* __restrict__ resid,
-    float* __restrict__ out, int M, EpiX ex, ProX px, FinX fx)
-{
-    using T = typename TrainTile<C, 8>::T;
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int NTN = C / T::BN;
-    constexpr int NCH = T::NCH;
-    const int G = gridDim.x, L = blockIdx.x;
-    // consecutive ranges on one XCD (G % 8 == 0); G = tiles (key 44 = 2): workgroup = tile
-    const int wi = G % 8 ? L : (L & 7) * (G >> 3) + (L >> 3);
-    const int ntiles = ((M + T::BM - 1) / T::BM) * NTN;
-    const long long TT = (long long)ntiles * NCH;
-    const long long g1 = (long long)(wi + 1) * TT / G;
-    auto owner = [&](long long g) { return (int)(((g + 1) * G + TT - 1) / TT - 1); };   // range holding chunk g
-    const __amdgpu_buffer_rsrc_t ors = wt_rsrc(out, padded_bytes(M, C));
-    const __amdgpu_buffer_rsrc_t prs = wt_rsrc(fx.skp, (size_t)ntiles * SK_MAXP * T::NT * 16 * sizeof(float));
-    const int tid = threadIdx.x;
-    for (long long g = (long long)wi * TT / G; g < g1;) {
-        const int t = (int)(g / NCH), kb = (int)(g - (long long)t * NCH);
-        const int ke = (int)min((long long)NCH, kb + (g1 - g));
-        const int m0 = (t / NTN) * T::BM, n0 = (t % NTN) * T::BN;
-        f32x16 acc[1][1];
-        halo_tile<C, T::BN, 4, 1, 8, EPI, WT, 0, 32, XE, PRO, true>(in, wp, nullptr, nullptr, resid, out, ors, M, m0,
-                                                                   n0, smem, ex, px, fx, kb, ke, &acc[0][0]);
-        const int wf = owner((long long)t * NCH);
-        const int np = owner((long long)t * NCH + NCH - 1) - wf + 1, part = wi - wf;
-        bool last = true;
-        if (np > 1) {
-            const int base = ((t * SK_MAXP + part) * T::NT + tid) * 16;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                store4<true>(fx.skp, prs, base + 4 * e,
-                             f32x4{acc[0][0][4 * e], acc[0][0][4 * e + 1], acc[0][0][4 * e + 2], acc[0][0][4 * e + 3]});
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            unsigned* fl = (unsigned*)smem;   // the staging LDS is free (the part ended with a barrier)
-            if (tid == 0) {
-                const unsigned old = __hip_atomic_fetch_add(fx.skc + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned l = old == (unsigned)(np - 1) ? 1u : 0u;
-                if (l) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-                *fl = l;
-            }
-            __syncthreads();
-            last = *fl != 0;
-            __syncthreads();   // every thread has read the flag before the epilogue's LDS writes
-            if (last) {
-                f32x16 sum;
-                for (int q = 0; q < np; ++q) {
-                    f32x16 v = acc[0][0];
-                    if (q != part) {
-                        const float* src = fx.skp + ((t * SK_MAXP + q) * T::NT + tid) * 16;
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            const f32x4 x = *(const f32x4*)(src + 4 * e);
-                            v[4 * e] = x[0];
-                            v[4 * e + 1] = x[1];
-                            v[4 * e + 2] = x[2];
-                            v[4 * e + 3] = x[3];
-                        }
-                    }
-                    sum = q == 0 ? v : sum + v;
-                }
-                acc[0][0] = sum;
-                if (tid == 0) __hip_atomic_store(fx.skc + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        if (last)
-            halo_epilogue<C, T::BN, 4, 1, 8, EPI, WT, 0, T::BN + 8, false, XE, 1>(acc, nullptr, nullptr, resid, out, ors,
-                                                                                 M, m0, n0, smem, ex, fx);
-        g += ke - kb;
-        __syncthreads();   // the next part's staging reuses the LDS
-    }
-}
-
 // Stem conv 3->C (K = 27) on the VALU: 0.2 % of the forward FLOPs.  One
 // workgroup per board; the board's 3 input planes are staged into LDS with a
 // zero halo; each thread owns one output channel (27 weights in registers) and a
@@ -947,62 +856,10 @@ static hipError_t launch_train_v(const float* in, const float* wp, const float* 
     return hipGetLastError();
 }
 
-int g_train_sk = 0;    // key 44: stream-K forward train convs (1; slower, measured), 2 the same kernel with one
-                       // whole tile per workgroup (the predicated loop's cost alone), 0 conv3x3_train (default)
-
-// resident 512-thread slots of the stream-K kernel (two per CU), 0 = not launchable
-static int train_sk_slots()
-{
-    static int slots = -1;
-    if (slots < 0) {
-        int dev = 0, cus = 0;
-        slots = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-            slots = 2 * cus;
-    }
-    return slots;
-}
-
-// the stream-K launch applies when every range holds >= 18 K chunks (<= SK_MAXP parts
-// per tile) and the workspace is given (fx.skp / fx.skc)
-bool train_sk_on(int C, int M, const FinX& fx)
-{
-    if (!g_train_sk || C != 128 || !fx.skp || !fx.skc || !fx.cnt || g_train_tile != 8 || g_train_var != 32) return false;
-    const int G = train_sk_slots();
-    if (G <= 0 || G % 8) return false;
-    using T = TrainTile<128, 8>::T;
-    const long long tiles = (long long)((M + T::BM - 1) / T::BM) * (128 / T::BN);
-    if (tiles * SK_MAXP * T::NT * 16 * 4 >= (1LL << 31)) return false;   // 32-bit part offsets
-    return tiles * T::NCH >= 18LL * G;
-}
-
-template <int C, int EPI, int XE, int PRO>
-static hipError_t launch_train_sk(const float* in, const float* wp, const float* resid, float* out, int M,
-                                  const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st)
-{
-    using T = typename TrainTile<C, 8>::T;
-    constexpr int lds = halo_lds_bytes<C, T::BN, 4, 1, 8, 0, PRO>();
-    static bool attr_done = false;
-    if (!attr_done) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train_sk<C, EPI, XE, true, PRO>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return e;
-        attr_done = true;
-    }
-    const int tiles = ((M + T::BM - 1) / T::BM) * (C / T::BN);
-    hipLaunchKernelGGL((conv3x3_train_sk<C, EPI, XE, true, PRO>), dim3(g_train_sk == 2 ? tiles : train_sk_slots()),
-                       dim3(T::NT), lds, st, in, wp, resid, out, M, ex, px, fx);
-    return hipGetLastError();
-}
-
 template <int C, int EPI, int XE, int PRO = PRO_NONE>
 static hipError_t launch_train_t(const float* in, const float* wp, const float* resid, float* out, int M,
                                  const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st)
 {
-    if constexpr (C == 128 && EPI == EPI_RAW && XE == XE_STATS && PRO != PRO_BNBWD && PRO != PRO_BNBWD_LDS) {
-        if (train_sk_on(C, M, fx)) return launch_train_sk<C, EPI, XE, PRO>(in, wp, resid, out, M, ex, px, fx, st);
-    }
 #ifdef AZG_AB_STUDIES   // plain (write-back) output stores: A/B only
     if (!(g_train_wt & 1)) return launch_train_v<C, EPI, XE, PRO, false, 32, 8>(in, wp, resid, out, M, ex, px, fx, st);
 #endif
@@ -1211,11 +1068,6 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     if (key == 28) {  // train head chain: bit mask of the fused stages (include/azg_pv.h), 0 the 18-launch chain (other sum orders)
         const int prev = azg::g_train_fuse_heads;
         if (value >= 0 && value <= 31) azg::g_train_fuse_heads = value;
-        return prev;
-    }
-    if (key == 44) {  // train: stream-K forward convs (1; C = 128, >= 18 K chunks per slot; slower, measured), 2 its kernel at one tile per workgroup, or conv3x3_train (0, default); 1: fp32 sums split differently
-        const int prev = azg::g_train_sk;
-        if (value >= 0 && value <= 2) azg::g_train_sk = value;
         return prev;
     }
     if (key == 42) {  // train: forward conv tiles stored after the BN-partial arrival count (1, default) or before (0); bitwise identical

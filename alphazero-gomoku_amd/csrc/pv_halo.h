@@ -129,10 +129,7 @@ struct FinX {
     const float* inv_i = nullptr;                           // !FWD: invstd of the layer
     float *ggamma = nullptr, *gbeta = nullptr;              // !FWD: parameter grads
     float *gm_o = nullptr, *k_o = nullptr, *iw_o = nullptr; // !FWD: bn_bwd_apply coefficients
-    float* skp = nullptr;        // stream-K forward (conv3x3_train_sk): [tile][SK_MAXP][NT][16] parts
-    unsigned* skc = nullptr;     // stream-K: arrival counter per tile (0 at launch; reset by the last arriver)
 };
-constexpr int SK_MAXP = 3;       // parts per tile: every part holds >= 18 of a tile's 36 K chunks
 // partial sums of tiles t = j, j+8, ... (the tile class j of 8) for channel c.
 // COH: every load is an agent-scope relaxed atomic load (`global_load_dword sc1`,
 // L1 bypassed) -- the consumer form that may replace an acquire only inside the
@@ -712,17 +709,14 @@ __device__ __forceinline__ void halo_mainloop_glds(const float* __restrict__ in,
 // set): bit 1 skips the weight loads, bit 2 the halo loads, bit 4 the per-chunk
 // barriers, bit 8 replaces LDS fragment reads by register values, bit 16 skips the
 // epilogue stores (kept live by a never-true compare).
-// SK (stream-K part, conv3x3_train_sk): only K chunks [k0, k1) of the tile (chunk j =
-// tap j % 9 of channel group j / 9), accumulated in the same per-group order; the
-// partial accumulator is returned in *sk_acc and no epilogue runs.
 template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1 = false, int ABL = 0, int VAR = 0,
-          int XE = XE_NONE, int PRO = PRO_NONE, bool SK = false>
+          int XE = XE_NONE, int PRO = PRO_NONE>
 __device__ __forceinline__ void halo_tile(
     const float* __restrict__ in, const float* __restrict__ wp,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ resid, float* __restrict__ out, __amdgpu_buffer_rsrc_t out_rs,
     int M, int m0, int n0, float* smem, const EpiX& ex = EpiX{}, const ProX& px = ProX{},
-    const FinX& fx = FinX{}, int k0 = 0, int k1 = 0, f32x16* sk_acc = nullptr)
+    const FinX& fx = FinX{})
 {
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
     if constexpr ((VAR & 4) != 0) {   // LDS-DMA staging
@@ -751,10 +745,6 @@ __device__ __forceinline__ void halo_tile(
     constexpr bool VSWZ = (VAR & 1) != 0;
     constexpr bool BPF2 = (VAR & 2) != 0;
     constexpr int NCHK = 9 * CG;
-    static_assert(!SK || (TM == 1 && TN == 1 && !BPF2 && PRO != PRO_BNBWD_LDS && ABL == 0), "stream-K part: one accumulator, register staging");
-    // SK: this part's chunk range and channel groups
-    const int kb = SK ? k0 : 0, ke = SK ? k1 : NCHK;
-    const int cgb = kb / 9, cge = (ke - 1) / 9;
 
     float* Ah = smem;                 // [HR][32]
     float* Bs = smem + HR * BK;       // [2][BN][32]
@@ -890,7 +880,7 @@ __device__ __forceinline__ void halo_tile(
     // per staged row i: applied one tap after its load was issued (the residual row
     // dies there, keeping the PRO_BN_RES register peak low), to all rows of the first
     // group before its store
-    auto pro_row = [&](int cg, int i, bool own = true) {
+    auto pro_row = [&](int cg, int i) {
         if constexpr (PRO != PRO_NONE) {
             const f32x4 s4 = *(const f32x4*)(Ps + cg * BK + sc);
             const f32x4 t4 = *(const f32x4*)(Ps + C + cg * BK + sc);
@@ -916,7 +906,7 @@ __device__ __forceinline__ void halo_tile(
                 }
             }
             rh[i] = v;
-            if (own && ((pown >> i) & 1)) store4<true>(px.aout, ars, hsrc[i] + cg * BK, v);
+            if ((pown >> i) & 1) store4<true>(px.aout, ars, hsrc[i] + cg * BK, v);
         }
     };
     auto hstore = [&](int cg) {
@@ -980,26 +970,24 @@ __device__ __forceinline__ void halo_tile(
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
 #pragma unroll
-    for (int i = 0; i < H_LD; ++i) hload(cgb, i);
+    for (int i = 0; i < H_LD; ++i) hload(0, i);
     if (BPF2) {
         bload(rb2, kchunk(0));
         bload(rb1, kchunk(1));
     } else {
-        bload(rb1, kchunk(kb));
+        bload(rb1, kchunk(0));
     }
     if constexpr (PRO != PRO_BNBWD_LDS) {
-        // a part starting inside a group re-stages it: the part before wrote its own rows
 #pragma unroll
-        for (int i = 0; i < H_LD; ++i) pro_row(cgb, i, kb % 9 == 0);
+        for (int i = 0; i < H_LD; ++i) pro_row(0, i);
     }
-    hstore(cgb);
+    hstore(0);
     if (BPF2) bstore(rb2, 0);
-    else bstore(rb1, kb & 1);
+    else bstore(rb1, 0);
     __syncthreads();
 
 #pragma unroll
     for (int cg = 0; cg < CG; ++cg) {
-        if (SK && (cg < cgb || cg > cge)) continue;
         f32x16 at[TM][TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -1007,7 +995,7 @@ __device__ __forceinline__ void halo_tile(
             for (int j = 0; j < TN; ++j)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) at[i][j][r] = 0.f;
-        const bool more = SK ? cg + 1 <= cge : cg + 1 < CG;
+        const bool more = cg + 1 < CG;
         // PRO (AZG_PRO_REMAT): the fragment row addresses are rebuilt per channel group
         // (a few VALU ops per tap) instead of 9 x 4 hoisted addresses living across the
         // unrolled groups -- with the prologue's registers those spilled, and every
@@ -1020,12 +1008,10 @@ __device__ __forceinline__ void halo_tile(
         for (int tap = 0; tap < 9; ++tap) {
             const int j = cg * 9 + tap;            // chunk index
             const int cur = j & 1;
-            // SK: chunks outside [kb, ke) only issue the next group's halo loads / prologue
-            const bool act = !SK || (j >= kb && j < ke);
             if (BPF2) {
                 if (j + 2 < NCHK) bload(rb2, kchunk(j + 2));
             } else {
-                if (act && j + 1 < ke) bload(rb1, kchunk(j + 1));
+                if (j + 1 < NCHK) bload(rb1, kchunk(j + 1));
             }
             if (more && tap < H_LD) hload(cg + 1, tap);
             // keep the next chunk's global loads at the top of the chunk: without this
@@ -1041,7 +1027,6 @@ __device__ __forceinline__ void halo_tile(
                 aswz[i] = VSWZ ? ((vpix[i] + vd) >> 1) & 7 : (r >> 1) & 7;
             }
             const float* Bb = Bs + cur * BN * BK;
-            if (act)   // SK: one uniform branch around the tap's MFMA block
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 f32x4 a[TM], b[TN];
@@ -1067,14 +1052,14 @@ __device__ __forceinline__ void halo_tile(
             }
             // the row loaded one tap ago gets its BN / ReLU now (PRO)
             if (PRO != PRO_NONE && PRO != PRO_BNBWD_LDS && more && tap >= 1 && tap <= H_LD) pro_row(cg + 1, tap - 1);
-            if (act && j + 1 < ke) {
+            if (j + 1 < NCHK) {
                 bstore(rb1, cur ^ 1);
                 if (BPF2) {
 #pragma unroll
                     for (int i = 0; i < B_LD; ++i) rb1[i] = rb2[i];
                 }
             }
-            if (act && !(ABL & 4)) __syncthreads();
+            if (!(ABL & 4)) __syncthreads();
             if (tap == 8 && more) {
                 hstore(cg + 1);      // every wave is past its last read of this group's halo
                 __syncthreads();
@@ -1086,10 +1071,6 @@ __device__ __forceinline__ void halo_tile(
             for (int j = 0; j < TN; ++j) acc[i][j] += at[i][j];
     }
 
-    if constexpr (SK) {
-        *sk_acc = acc[0][0];
-        return;
-    }
     // the last chunk ended with a barrier: the staging buffers are free
     halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, (VSWZ ? BN : BN + 8), (VAR & 8) != 0, XE,
                   (VAR & 16) ? 2 : (VAR & 32) ? 1 : 0>(

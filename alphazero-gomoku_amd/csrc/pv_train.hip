@@ -55,8 +55,6 @@ struct TrainWS {
     unsigned* gcnt = nullptr;                      // split-group arrival counters (key 41)
     int S = 0, rps = 0;
     unsigned* fincnt = nullptr;                    // fused BN finalize: arrival counters per N tile
-    float* skp = nullptr;                          // stream-K forward convs: parts [tile][SK_MAXP][512][16]
-    unsigned* skc = nullptr;                       // stream-K: arrival counter per tile (zeroed once)
     // heads
     float *zh = nullptr, *fp = nullptr, *fv = nullptr, *hv = nullptr, *dpre = nullptr;
     float *dlogits = nullptr, *dfp = nullptr, *dfv = nullptr, *dhv = nullptr, *dzh = nullptr, *lossb = nullptr;
@@ -981,10 +979,6 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
         float* fc = nullptr;
         A(fc, 64, true);
         w->fincnt = (unsigned*)fc;
-        const int sk_tiles = C == 128 ? ((M + TRAIN_BM - 1) / TRAIN_BM) * 2 : 1;   // 128x64 train tiles (stream-K: C = 128)
-        A(w->skp, (size_t)sk_tiles * SK_MAXP * 512 * 16, false);
-        A(fc, (size_t)sk_tiles, true);
-        w->skc = (unsigned*)fc;
         float* hc = nullptr;
         A(hc, 16, true);
         w->hcnt = (unsigned*)hc;
@@ -1252,8 +1246,6 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             FinX fx = fin_args(fin, true);
             fx.cnt = w->fincnt;
             fx.late = g_train_late_store;
-            fx.skp = w->skp;   // stream-K when it applies (key 44, pv_conv.hip train_sk_on)
-            fx.skc = w->skc;
             AZG_CK(launch_conv3x3_train(C, EPI_RAW, XE_STATS, p.z, wpk, nullptr, out, M, ex, st, &px,
                                         ffin ? &fx : nullptr),
                    "train: conv3x3 (fused BN apply)");

@@ -232,13 +232,6 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          default); fp32 sums in another order;
  *   key 42: train forward convs store their tile after the BN-partial arrival count
  *          (1, default) or before (0); bitwise identical;
- *   key 44: train forward convs at C = 128 as stream-K ranges (1: the tiles' K
- *          chunks cut into one equal contiguous range per resident slot, split tiles
- *          summed by their last part; applies with keys 23, 24 = 1, 25 = 32, 26 = 8
- *          and >= 18 chunks per slot; fp32 sums split at other K points; slower,
- *          measured), 2 the stream-K kernel with one whole tile per workgroup
- *          (bitwise identical to 0; A/B of its predicated loop), or conv3x3_train
- *          (0, default);
  *   key 31: study build only: the 64x64 / 128x64 towers with sc1 dependent loads
  *          and no acquire (two or more workgroups per CU: outside the microarch
  *          guide's measured envelope; the product uses the acquire there and the

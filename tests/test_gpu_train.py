@@ -339,7 +339,7 @@ def test_train_then_predict_uses_new_weights():
 
 
 @pytest.mark.parametrize("key,values", [(18, (0, 1, 2, 4, 7)), (12, (0, 1)), (16, (3, 0, 1, 2, 4)), (23, (1, 0)), (24, (1, 0)),
-                                        (25, (32, 0)), (26, (8, 16)), (29, (1, 0)), (30, (1, 0)), (32, (1, 0, 2)), (33, (1, 0)), (34, (1, 0)), (36, (1, 0)), (37, (0, 1)), (39, (1, 0)), (40, (1, 0, 2)), (42, (1, 0)), (44, (0, 2))])
+                                        (25, (32, 0)), (26, (8, 16)), (29, (1, 0)), (30, (1, 0)), (32, (1, 0, 2)), (33, (1, 0)), (34, (1, 0)), (36, (1, 0)), (37, (0, 1)), (39, (1, 0)), (40, (1, 0, 2)), (42, (1, 0))])
 def test_train_schedule_keys_bitwise(key, values):
     """Train-step tuning keys change cache policy (18: write-through stores), stream
     schedule (12: weight grads overlapped or serial) or the weight-grad staging (16: LDS-DMA
@@ -362,10 +362,6 @@ def test_train_schedule_keys_bitwise(key, values):
     # the weight-grad kernels (16) and slab store policies (18) share one reduction only
     # without the in-kernel split-group combine (41: LDS-DMA kernel, write-through slabs)
     prev41 = lib.azg_pv_set_tuning(41, 0) if key in (16, 18) else None
-    # the stream-K forward (44) runs only with the fused finalize (24), the staging-fused
-    # BN apply (23), buffer addressing (25) and the 8-wave tile (26): compare those
-    # variants with the one-tile-per-workgroup forward
-    prev44 = lib.azg_pv_set_tuning(44, 0) if key in (23, 24, 25, 26, 44) else None
     ref = None
     try:
         for v in values:
@@ -384,21 +380,17 @@ def test_train_schedule_keys_bitwise(key, values):
         lib.azg_pv_set_tuning(key, prev)
         if prev41 is not None:
             lib.azg_pv_set_tuning(41, prev41)
-        if prev44 is not None:
-            lib.azg_pv_set_tuning(44, prev44)
 
 
 
-@pytest.mark.parametrize("key,value", [(27, 16), (38, 0), (41, 1), (44, 1)])
+@pytest.mark.parametrize("key,value", [(27, 16), (38, 0), (41, 1)])
 @pytest.mark.parametrize("tag,blocks,ch,B", [("6x128", 6, 128, 128), ("3x64", 3, 64, 37)])
 def test_train_sum_order_variants_match_oracle(key, value, tag, blocks, ch, B):
     """Train keys that change an fp32 summation order hold the oracle tolerance of
     test_gradients_match_oracle (no bitwise test): the weight-grad split count (27) and
     the stem's BN statistics (38 = 0: a separate col_stats pass over 64-row tiles
     instead of the stem epilogue's 128-row tiles) and the weight-grad slab reduction
-    (41 = 1: the in-kernel split-group combine instead of all S slabs in wgrad_reduce)
-    and the forward convs' K split (44 = 1: stream-K ranges, whose tiles sum two or
-    three K parts, instead of one tile per workgroup)."""
+    (41 = 1: the in-kernel split-group combine instead of all S slabs in wgrad_reduce)."""
     import _native
     lib = _native.load_library()
     prev = lib.azg_pv_set_tuning(key, value)
