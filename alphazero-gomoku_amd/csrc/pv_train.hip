@@ -28,6 +28,8 @@ hipError_t launch_wgrad(int C, const float* dz, const float* x, float* slab, flo
                         hipStream_t st, bool reduce = true, unsigned* gcnt = nullptr, float* gslab = nullptr);
 bool wgrad_comb_on(int kernel, int S);
 hipError_t launch_wgrad_reduce(int C, const float* slab, float* dw, int S, hipStream_t st);
+hipError_t launch_wgrad_reduce2(int C, const float* slab0, float* dw0, int S0, const float* slab1, float* dw1,
+                                int S1, hipStream_t st);
 int wgrad_splits(int C, int M);
 constexpr int kMaxWgradSplits = 64;   // wgrad_splits <= slots / tiles <= 56, rounded to 8
 
@@ -97,7 +99,8 @@ int g_train_dz_all = 1;     // key 34: 1 one dZ buffer per conv (default); 0 two
 int g_train_pack_after = 1; // key 36: 1 the next step's weight packs right after Adam (same stream, no hand-off); 0 at the step start
 int g_train_late_store = 1;    // key 42: 1 forward conv tiles stored after the BN-partial arrival count; 0 before
 int g_train_fuse_bwd = 0;      // key 40: 1 conv1's BN backward in its dgrad staging (C <= 128); 0 bn_bwd_apply pass
-int g_train_defer_reduce = 1;  // key 39: 1 each weight grad's slab reduction after the next conv's weight-grad kernel
+int g_train_defer_reduce = 2;  // key 39: 1 each weight grad's slab reduction after the next conv's weight-grad kernel;
+                               // 2 the same, the last two convs' reductions in one launch on the caller's stream after the join
 int g_train_stem_stats = 1;  // key 38: 1 stem BN statistics from the stem's accumulators (default); 0 col_stats pass
 int g_train_side_prio = 0;   // key 37: priority of the weight-grad stream: 0 lowest (default), 1 highest
 int g_train_ev_device = 1;   // key 33: 1 stream hand-off events release at device scope (default); 0 system scope
@@ -1156,8 +1159,12 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     // weight-grad kernel (two alternating slab buffers), so each weight-grad kernel starts
     // as soon as its dZ is ready, ahead of the previous reduction's HBM pass
     const bool defer_red = g_train_defer_reduce != 0 && !g_wgrad_serial;
+    // key 39 = 2: the step's last weight grad leaves its own and the previous conv's
+    // reductions pending; both run in one launch on the caller's stream after the join
+    // (idle there, while `side` would run them back to back ahead of the join)
+    const bool tail_red = defer_red && g_train_defer_reduce == 2;
     struct PendRed { float* slab; float* dw; int S; };
-    PendRed pend_red{nullptr, nullptr, 0};
+    PendRed pend_red{nullptr, nullptr, 0}, pend_red2{nullptr, nullptr, 0};
     float* slabs[2] = {w->slab, w->slab2};
     int slab_i = 0;
     auto flush_red = [&]() -> int32_t {
@@ -1169,7 +1176,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     // dZ of backward conv k (2i+1: conv2 of block i, 2i: conv1): its own buffer (key 34)
     // or the alternating slot
     auto dzb = [&](int k, int slot) -> float* { return dz_all ? w->dzs[k] : dzbuf[slot]; };
-    auto wgrad = [&](int slot, const float* dz, const float* xin, int tensor) -> int32_t {
+    auto wgrad = [&](int slot, const float* dz, const float* xin, int tensor, bool last = false) -> int32_t {
         if (g_wgrad_serial) {   // A/B: weight grads on the caller's stream, no overlap
             int pr = prof_begin(h, AZG_PROF_TRAIN_WGRAD, st);
             const int S = wgrad_splits(C, M);
@@ -1190,7 +1197,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         AZG_CK(launch_wgrad(C, dz, xin, sl, G + h->poff[tensor], M, S, w->side, !defer_red, w->gcnt, gsl),
                "train: wgrad");
         if (defer_red) {   // the previous conv's reduction behind this conv's MFMA work
-            if (int32_t r2 = flush_red()) return r2;
+            if (tail_red && last) pend_red2 = pend_red;   // to the caller's stream after the join
+            else if (int32_t r2 = flush_red()) return r2;
             pend_red = comb ? PendRed{gsl, G + h->poff[tensor], 8} : PendRed{sl, G + h->poff[tensor], S};
             slab_i ^= 1;
         }
@@ -1570,10 +1578,10 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
                                         w->gX, M, ex, st, &px, ffin ? &fx : nullptr),
                    "train: conv3x3 (fused BN backward)");
             prof_end(h, pr, st);
-            R(wgrad(1, dz1, Xin, h->t_blk[i].w1));
+            R(wgrad(1, dz1, Xin, h->t_blk[i].w1, i == 0));
         } else {
             R(bwd_apply(w->DH, w->hh[i], w->z1[i], h->bn_blk[i].first, dz1, nullptr, true));
-            R(wgrad(1, dz1, Xin, h->t_blk[i].w1));
+            R(wgrad(1, dz1, Xin, h->t_blk[i].w1, i == 0));
             R(conv(EPI_ADD, XE_BNBWD, dz1, w->wdpack + (size_t)(2 * i) * 9 * C * C, w->GR, w->gX, Xin, zin, lin,
                    ffin ? lin : -1));
         }
@@ -1581,7 +1589,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         bwd_nt = ntt;
         R(snap(NB - i));
     }
-    if (defer_red) R(flush_red());   // the last conv's reduction
+    if (defer_red && !tail_red) R(flush_red());   // the last conv's reduction
     if (defer_heads) {   // the head weight grads (Adam's inputs only)
         R(fc_wgrads(st));
         R(head_proj_wgrad());
@@ -1607,6 +1615,15 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     if (side_used) {             // (and the head weight grads when no conv weight grad follows them)
         AZG_CK(hipEventRecord(w->ev_join, w->side), "train: event record");
         AZG_CK(hipStreamWaitEvent(st, w->ev_join, 0), "train: stream wait");
+    }
+    if (tail_red && pend_red.slab) {   // key 39 = 2: the last two convs' reductions, one launch
+        if (pend_red2.slab)
+            AZG_CK(launch_wgrad_reduce2(C, pend_red2.slab, pend_red2.dw, pend_red2.S, pend_red.slab, pend_red.dw,
+                                        pend_red.S, st),
+                   "train: wgrad reduce (tail)");
+        else
+            AZG_CK(launch_wgrad_reduce(C, pend_red.slab, pend_red.dw, pend_red.S, st), "train: wgrad reduce (tail)");
+        pend_red = pend_red2 = PendRed{nullptr, nullptr, 0};
     }
 #undef R
     return 0;

@@ -496,8 +496,7 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv3x3_wgrad_nat(
 // dW (torch layout [co][ci][3][3]) = sum over slabs, fixed order: four interleaved
 // partial sums (slabs k = 0,1,2,3 mod 4: independent loads in flight) combined as
 // ((p0 + p1) + (p2 + p3)).
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ dw,
-                                                           int C, int S)
+__device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ slab, float* __restrict__ dw, int C, int S)
 {
     const int total = 9 * C * C;
     for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
@@ -519,12 +518,35 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
         dw[(co * C + ci) * 9 + tap] = (p0 + p1) + (p2 + p3);
     }
 }
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ dw,
+                                                           int C, int S)
+{
+    wgrad_reduce_body(slab, dw, C, S);
+}
+// two convs' reductions in one launch (grid.y selects the conv; the same per-element
+// order as wgrad_reduce_kernel, so bitwise identical to two launches)
+__global__ __launch_bounds__(256) void wgrad_reduce2_kernel(const float* __restrict__ slab0, float* __restrict__ dw0,
+                                                            int S0, const float* __restrict__ slab1,
+                                                            float* __restrict__ dw1, int S1, int C)
+{
+    if (blockIdx.y == 0) wgrad_reduce_body(slab0, dw0, C, S0);
+    else wgrad_reduce_body(slab1, dw1, C, S1);
+}
 
 // dW = the S slabs summed in fixed order (wgrad_reduce_kernel)
 hipError_t launch_wgrad_reduce(int C, const float* slab, float* dw, int S, hipStream_t st)
 {
     const int total = 9 * C * C;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, dw, C, S);
+    return hipGetLastError();
+}
+
+hipError_t launch_wgrad_reduce2(int C, const float* slab0, float* dw0, int S0, const float* slab1, float* dw1,
+                                int S1, hipStream_t st)
+{
+    const int total = 9 * C * C;
+    hipLaunchKernelGGL(wgrad_reduce2_kernel, dim3((total + 255) / 256, 2), dim3(256), 0, st, slab0, dw0, S0, slab1,
+                       dw1, S1, C);
     return hipGetLastError();
 }
 
