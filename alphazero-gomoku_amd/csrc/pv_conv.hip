@@ -1085,7 +1085,7 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         if (value >= 0 && value <= 2) azg::g_train_fuse_bwd = value;
         return prev;
     }
-    if (key == 39) {  // train: each weight grad's slab reduction after the next conv's weight-grad kernel (1; 2, default: the last two in one launch on the caller's stream after the join) or right behind its own (0); bitwise identical
+    if (key == 39) {  // train: each weight grad's slab reduction after the next conv's weight-grad kernel (1, default; 2: the last two in one launch on the caller's stream after the join, +0.4 %) or right behind its own (0); bitwise identical
         const int prev = azg::g_train_defer_reduce;
         if (value >= 0 && value <= 2) azg::g_train_defer_reduce = value;
         return prev;

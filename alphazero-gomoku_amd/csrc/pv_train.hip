@@ -99,8 +99,9 @@ int g_train_dz_all = 1;     // key 34: 1 one dZ buffer per conv (default); 0 two
 int g_train_pack_after = 1; // key 36: 1 the next step's weight packs right after Adam (same stream, no hand-off); 0 at the step start
 int g_train_late_store = 1;    // key 42: 1 forward conv tiles stored after the BN-partial arrival count; 0 before
 int g_train_fuse_bwd = 0;      // key 40: 1 conv1's BN backward in its dgrad staging (C <= 128); 0 bn_bwd_apply pass
-int g_train_defer_reduce = 2;  // key 39: 1 each weight grad's slab reduction after the next conv's weight-grad kernel;
-                               // 2 the same, the last two convs' reductions in one launch on the caller's stream after the join
+int g_train_defer_reduce = 1;  // key 39: 1 each weight grad's slab reduction after the next conv's weight-grad kernel;
+                               // 2 the same, the last two convs' reductions in one launch on the caller's stream after
+                               // the join (+0.4 %, measured); 0 each right behind its own weight grad
 int g_train_stem_stats = 1;  // key 38: 1 stem BN statistics from the stem's accumulators (default); 0 col_stats pass
 int g_train_side_prio = 0;   // key 37: priority of the weight-grad stream: 0 lowest (default), 1 highest
 int g_train_ev_device = 1;   // key 33: 1 stream hand-off events release at device scope (default); 0 system scope

@@ -221,9 +221,9 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *   key 38: train stem BN statistics from the stem's accumulators (1, default) or
  *          a separate col_stats pass (0); fp32 sums in another order;
  *   key 39: train: each conv's weight-grad slab reduction launched after the next
- *          conv's weight-grad kernel (1; 2, default: the same, with the step's last
- *          two reductions in one launch on the caller's stream after the join) or
- *          right behind its own (0); bitwise identical;
+ *          conv's weight-grad kernel (1, default; 2: the same, with the step's last
+ *          two reductions in one launch on the caller's stream after the join,
+ *          +0.4 %, measured) or right behind its own (0); bitwise identical;
  *   key 40: train: each block's conv1 BN backward applied in its dgrad's halo
  *          staging (1, z in registers; 2, z by LDS-DMA into its own LDS rows and the
  *          transform at the group's halo store; C <= 128, both slower, measured) or a

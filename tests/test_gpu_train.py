@@ -339,7 +339,7 @@ def test_train_then_predict_uses_new_weights():
 
 
 @pytest.mark.parametrize("key,values", [(18, (0, 1, 2, 4, 7)), (12, (0, 1)), (16, (3, 0, 1, 2, 4)), (23, (1, 0)), (24, (1, 0)),
-                                        (25, (32, 0)), (26, (8, 16)), (29, (1, 0)), (30, (1, 0)), (32, (1, 0, 2)), (33, (1, 0)), (34, (1, 0)), (36, (1, 0)), (37, (0, 1)), (39, (2, 1, 0)), (40, (1, 0, 2)), (42, (1, 0))])
+                                        (25, (32, 0)), (26, (8, 16)), (29, (1, 0)), (30, (1, 0)), (32, (1, 0, 2)), (33, (1, 0)), (34, (1, 0)), (36, (1, 0)), (37, (0, 1)), (39, (1, 0, 2)), (40, (1, 0, 2)), (42, (1, 0))])
 def test_train_schedule_keys_bitwise(key, values):
     """Train-step tuning keys change cache policy (18: write-through stores), stream
     schedule (12: weight grads overlapped or serial) or the weight-grad staging (16: LDS-DMA
