@@ -220,12 +220,11 @@ __global__ __launch_bounds__(64 * NW_, 2) void conv3x3_halo(
 }
 // Train-step conv (forward z = conv(a), dgrad = conv(dZ, flipped W) [+ resid]) with
 // the BatchNorm partial sums fused into the epilogue (pv_halo.h XE_STATS / XE_BNBWD):
-// 128-row M tiles (the partials are per 128-row tile), either 128 x 64 with 8 waves
-// (two workgroups per CU; NWT 8) or 128 x 128 with 16 waves (one workgroup per CU, the
-// halo staged once for all 128 output channels; NWT 16, C = 128).  Same XCD-aware tile
-// order as above.  WT: outputs stored write-through (no dirty L2 lines at the kernel
-// boundary).  PRO (forward only): the input is the previous layer's raw output z and
-// its BN + ReLU (+ residual) is applied in the halo staging (pv_halo.h ProX).
+// 128-row M tiles (the partials are per 128-row tile) x 64 channels, 8 waves, two
+// workgroups per CU.  Same XCD-aware tile order as above.  WT: outputs stored
+// write-through (no dirty L2 lines at the kernel boundary).  PRO (forward only): the
+// input is the previous layer's raw output z and its BN + ReLU (+ residual) is applied
+// in the halo staging (pv_halo.h ProX).
 template <int C, int NWT>
 struct TrainTile {
     static constexpr int BN = NWT >= 16 ? 128 : 64;
@@ -831,57 +830,25 @@ hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, cons
     return launch_conv3x3_shape(shape, C, epi, in, wp, scale, shift, resid, out, M, st);
 }
 
-int g_train_wt = 7;   // key 18 bits: 1 train conv outputs, 2 BN apply outputs, 4 wgrad slabs write-through
-
-int g_train_var = 32;  // key 25: halo_tile VAR of the train convs (32 buffer-resource addressing, default; 0 64-bit pointers)
-
-int g_train_tile = 8;  // key 26: train conv tile (8: 128x64 / 8 waves; 16: 128x128 / 16 waves, C = 128)
-
-template <int C, int EPI, int XE, int PRO, bool WT, int VAR, int NWT>
-static hipError_t launch_train_v(const float* in, const float* wp, const float* resid, float* out, int M,
+// Train convs: 128 x 64 tiles, 8 waves (two workgroups per CU), buffer-resource operand
+// addressing (halo_tile VAR 32), outputs stored write-through.
+template <int C, int EPI, int XE, int PRO = PRO_NONE>
+static hipError_t launch_train_t(const float* in, const float* wp, const float* resid, float* out, int M,
                                  const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st)
 {
-    using T = typename TrainTile<C, NWT>::T;
-    constexpr int lds = halo_lds_bytes<C, T::BN, 4, 1, NWT, 0, PRO>();
+    using T = typename TrainTile<C, 8>::T;
+    constexpr int lds = halo_lds_bytes<C, T::BN, 4, 1, 8, 0, PRO>();
     static bool attr_done = false;
     if (!attr_done) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, WT, PRO, VAR, NWT>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, true, PRO, 32, 8>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
         attr_done = true;
     }
     dim3 grid(((M + T::BM - 1) / T::BM) * (C / T::BN));
-    hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, WT, PRO, VAR, NWT>), grid, dim3(T::NT), lds, st, in, wp, resid,
+    hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, true, PRO, 32, 8>), grid, dim3(T::NT), lds, st, in, wp, resid,
                        out, M, ex, px, fx);
     return hipGetLastError();
-}
-
-template <int C, int EPI, int XE, int PRO = PRO_NONE>
-static hipError_t launch_train_t(const float* in, const float* wp, const float* resid, float* out, int M,
-                                 const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st)
-{
-#ifdef AZG_AB_STUDIES   // plain (write-back) output stores: A/B only
-    if (!(g_train_wt & 1)) return launch_train_v<C, EPI, XE, PRO, false, 32, 8>(in, wp, resid, out, M, ex, px, fx, st);
-#endif
-    if constexpr (C == 128) {
-        if (g_train_tile == 16) return launch_train_v<C, EPI, XE, PRO, true, 32, 16>(in, wp, resid, out, M, ex, px, fx, st);
-    }
-    if (g_train_var == 0) return launch_train_v<C, EPI, XE, PRO, true, 0, 8>(in, wp, resid, out, M, ex, px, fx, st);
-    return launch_train_v<C, EPI, XE, PRO, true, 32, 8>(in, wp, resid, out, M, ex, px, fx, st);
-}
-
-// dgrad of a residual-free layer's conv with that layer's BN backward applied in the
-// staging (PRO_BNBWD, C <= 128: the 256-channel tile body has no room for the prologue)
-template <int C>
-static hipError_t launch_train_bnbwd(const float* in, const float* wp, const float* resid, float* out, int M,
-                                     const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st)
-{
-    if constexpr (C <= 128) {
-        if (g_train_fuse_bwd == 2)   // 8-wave tile only (one 8-row z piece per wave)
-            return launch_train_v<C, EPI_ADD, XE_BNBWD, PRO_BNBWD_LDS, true, 32, 8>(in, wp, resid, out, M, ex, px, fx, st);
-        return launch_train_t<C, EPI_ADD, XE_BNBWD, PRO_BNBWD>(in, wp, resid, out, M, ex, px, fx, st);
-    }
-    return hipErrorInvalidValue;
 }
 
 // Train conv with fused BN partials: (EPI_RAW, XE_STATS) forward, optionally with
@@ -901,8 +868,6 @@ hipError_t launch_conv3x3_train(int C, int epi, int xe, const float* in, const f
             return launch_train_t<CC, EPI_RAW, XE_STATS, PRO_BN>(in, wp, resid, out, M, ex, *px, fx, st); \
         if (epi == EPI_RAW && xe == XE_STATS) return launch_train_t<CC, EPI_RAW, XE_STATS>(in, wp, resid, out, M, ex, p0, fx, st); \
         if (epi == EPI_RAW && xe == XE_BNBWD) return launch_train_t<CC, EPI_RAW, XE_BNBWD>(in, wp, resid, out, M, ex, p0, fx, st); \
-        if (epi == EPI_ADD && xe == XE_BNBWD && px && px->gm)                                      \
-            return launch_train_bnbwd<CC>(in, wp, resid, out, M, ex, *px, fx, st);                 \
         if (epi == EPI_ADD && xe == XE_BNBWD) return launch_train_t<CC, EPI_ADD, XE_BNBWD>(in, wp, resid, out, M, ex, p0, fx, st); \
         return hipErrorInvalidValue;
     switch (C) {
@@ -1028,13 +993,6 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         azg::g_tower_group = value ? 1 : 0;
         return prev;
     }
-    if (key == 19) {  // study build only: skip BN kernels of the train step (bits 1 apply, 2 finalize, 4 bwd apply, 8 bwd finalize; results invalid)
-        const int prev = azg::g_train_skip;
-#ifdef AZG_AB_STUDIES
-        azg::g_train_skip = value;
-#endif
-        return prev;
-    }
     if (key == 22) {  // per-layer 128x64 conv tile-body variant (1 default; 0, 4, 5 A/B, bitwise identical)
         const int prev = azg::g_conv_var;
         if (value == 0 || value == 1 || value == 4 || value == 5) azg::g_conv_var = value;
@@ -1045,79 +1003,14 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         azg::g_conv_tail_split = value ? 1 : 0;
         return prev;
     }
-    if (key == 24) {  // train: BN finalize fused into the producing conv's last workgroup (1, default) or separate (0)
+    if (key == 43) {  // train: tower backward as one persistent launch (1, default) or the two-stream schedule (0); bitwise identical
+        const int prev = azg::g_train_bwd_tower;
+        if (value == 0 || value == 1) azg::g_train_bwd_tower = value;
+        return prev;
+    }
+    if (key == 24) {  // train: BN finalize fused into the producing conv's last workgroup (1, default) or separate (0; two-stream backward); bitwise identical
         const int prev = azg::g_train_fuse_fin;
         if (value == 0 || value == 1) azg::g_train_fuse_fin = value;
-        return prev;
-    }
-    if (key == 25) {  // train convs: halo_tile VAR (32 buffer-resource addressing, default; 0 64-bit pointers); bitwise identical
-        const int prev = azg::g_train_var;
-        if (value == 0 || value == 32) azg::g_train_var = value;
-        return prev;
-    }
-    if (key == 30) {  // train: split repack at the start of a step (1, default) or one launch on the stream (0); bitwise identical
-        const int prev = azg::g_train_split_pack;
-        if (value == 0 || value == 1) azg::g_train_split_pack = value;
-        return prev;
-    }
-    if (key == 29) {  // train: BN-backward apply of residual-free layers masks from z (1, default) or reads act (0); bitwise identical
-        const int prev = azg::g_train_maskz;
-        if (value == 0 || value == 1) azg::g_train_maskz = value;
-        return prev;
-    }
-    if (key == 28) {  // train head chain: bit mask of the fused stages (include/azg_pv.h), 0 the 18-launch chain (other sum orders)
-        const int prev = azg::g_train_fuse_heads;
-        if (value >= 0 && value <= 31) azg::g_train_fuse_heads = value;
-        return prev;
-    }
-    if (key == 42) {  // train: forward conv tiles stored after the BN-partial arrival count (1, default) or before (0); bitwise identical
-        const int prev = azg::g_train_late_store;
-        if (value == 0 || value == 1) azg::g_train_late_store = value;
-        return prev;
-    }
-    if (key == 41) {  // train: in-kernel split-group combine of the weight-grad slabs (1; slower, measured) or all S slabs to wgrad_reduce (0, default); other sum order
-        const int prev = azg::g_wgrad_comb;
-        if (value == 0 || value == 1) azg::g_wgrad_comb = value;
-        return prev;
-    }
-    if (key == 40) {  // train: residual-free layers' BN backward applied in their conv1 dgrad's staging (1 register staging, 2 z by LDS-DMA into its own LDS rows; C <= 128; both slower, measured) or a bn_bwd_apply pass (0, default); bitwise identical
-        const int prev = azg::g_train_fuse_bwd;
-        if (value >= 0 && value <= 2) azg::g_train_fuse_bwd = value;
-        return prev;
-    }
-    if (key == 39) {  // train: each weight grad's slab reduction after the next conv's weight-grad kernel (1, default; 2: the last two in one launch on the caller's stream after the join, +0.4 %) or right behind its own (0); bitwise identical
-        const int prev = azg::g_train_defer_reduce;
-        if (value >= 0 && value <= 2) azg::g_train_defer_reduce = value;
-        return prev;
-    }
-    if (key == 38) {  // train: stem BN statistics from the stem's accumulators (1, default) or a col_stats pass (0)
-        const int prev = azg::g_train_stem_stats;
-        if (value == 0 || value == 1) azg::g_train_stem_stats = value;
-        return prev;
-    }
-    if (key == 37) {  // train: weight-grad stream priority, 0 lowest (default) or 1 highest; bitwise identical
-        const int prev = azg::g_train_side_prio;
-        if (value == 0 || value == 1) azg::g_train_side_prio = value;
-        return prev;
-    }
-    if (key == 36) {  // train: next step's weight packs right after Adam (1, default) or at the step start (0); bitwise identical
-        const int prev = azg::g_train_pack_after;
-        if (value == 0 || value == 1) azg::g_train_pack_after = value;
-        return prev;
-    }
-    if (key == 34) {  // train: one dZ buffer per backward conv (1, default) or two alternating + reuse waits (0); bitwise identical
-        const int prev = azg::g_train_dz_all;
-        if (value == 0 || value == 1) azg::g_train_dz_all = value;
-        return prev;
-    }
-    if (key == 33) {  // train: stream hand-off events with a device-scope release (1, default) or system scope (0); bitwise identical
-        const int prev = azg::g_train_ev_device;
-        if (value == 0 || value == 1) azg::g_train_ev_device = value;
-        return prev;
-    }
-    if (key == 32) {  // train: head weight-grad work deferred to the end of the tower backward (1, default), on the side stream during the head chain (2) or in the chain (0); bitwise identical
-        const int prev = azg::g_train_side_heads;
-        if (value >= 0 && value <= 2) azg::g_train_side_heads = value;
         return prev;
     }
     if (key == 27) {  // train wgrad split-K count (0 automatic; 8..64, multiple of 8); bitwise NOT identical across values
@@ -1125,34 +1018,9 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         if (value == 0 || (value >= 8 && value <= 64 && value % 8 == 0)) azg::g_wgrad_splits = value;
         return prev;
     }
-    if (key == 26) {  // train conv tile: 8 (128x64, 8 waves, default) or 16 (128x128, 16 waves, C = 128); bitwise identical
-        const int prev = azg::g_train_tile;
-        if (value == 8 || value == 16) azg::g_train_tile = value;
-        return prev;
-    }
-    if (key == 23) {  // train: BN applies folded into the next conv's halo staging (1, default) or separate (0)
+    if (key == 23) {  // train: BN applies folded into the next conv's halo staging (1, default) or separate passes (0); bitwise identical
         const int prev = azg::g_train_fuse_apply;
         if (value == 0 || value == 1) azg::g_train_fuse_apply = value;
-        return prev;
-    }
-    if (key == 18) {  // train: write-through outputs (bits: 1 convs, 2 BN apply, 4 wgrad slabs)
-        const int prev = azg::g_train_wt;
-        if (value >= 0 && value <= 7) azg::g_train_wt = value;
-        return prev;
-    }
-    if (key == 16) {  // train: wgrad kernel (3 LDS-DMA natural rows, default; 1 K-contiguous, 2 same 2 ahead, 0 row staging; bitwise identical)
-        const int prev = azg::g_wgrad_kernel;
-        if (value >= 0 && value <= 4) azg::g_wgrad_kernel = value;
-        return prev;
-    }
-    if (key == 13) {  // train: wgrad K chunk (32 default, 16 A/B)
-        const int prev = azg::g_wgrad_bk;
-        if (value == 16 || value == 32) azg::g_wgrad_bk = value;
-        return prev;
-    }
-    if (key == 12) {  // train: conv weight grads on the caller's stream (1) or overlapped (0)
-        const int prev = azg::g_wgrad_serial;
-        azg::g_wgrad_serial = value ? 1 : 0;
         return prev;
     }
     if (key == 11) {  // stem ablation mask (timing studies only)

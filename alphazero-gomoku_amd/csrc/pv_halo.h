@@ -61,8 +61,8 @@ constexpr int halo_span(int BM)
 }
 
 // per-channel vectors an operand prologue stages in LDS (PRO, below: 0 none; 1, 2 BN
-// scale / shift; 3, 4 the BN-backward apply's scale, shift, mean, gm, k, iw)
-constexpr int pro_params(int PRO) { return PRO >= 3 ? 6 : PRO != 0 ? 2 : 0; }
+// scale / shift)
+constexpr int pro_params(int PRO) { return PRO != 0 ? 2 : 0; }
 
 // LDS: halo rows [HR][32] + two weight chunks [2][BN][32] (register staging), or
 // two halo buffers [2][HRG][32] + [2][BN][32] (LDS-DMA staging, VAR bit 4); the
@@ -74,8 +74,7 @@ constexpr int halo_lds_bytes()
     const int hrg = (halo_span(T::BM) + 7) / 8 * 8;
     const int staging = (VAR & 4) ? (2 * hrg + ((VAR & 2) ? 3 : 2) * BN) * T::BK * 4
                                   : ((halo_span(T::BM) + T::RPP - 1) / T::RPP * T::RPP + 2 * BN) * T::BK * 4 +
-                                        pro_params(PRO) * C * 4 +
-                                        (PRO == 4 ? (halo_span(T::BM) + T::RPP - 1) / T::RPP * T::RPP * T::BK * 4 : 0);
+                                        pro_params(PRO) * C * 4;
     const int epilogue = T::BM * (BN + 8) * 4;
     return staging > epilogue ? staging : epilogue;
 }
@@ -83,6 +82,10 @@ constexpr int halo_lds_bytes()
 // Tower epilogue: BN scale/shift, residual added when `resid` is non-null, ReLU
 // (EPI_BN_RELU / EPI_BN_RES_RELU chosen at run time, same arithmetic).
 constexpr int EPI_BN_OPTRES_RELU = 4;
+// Dgrad epilogue with the residual gradient added when `resid` is non-null (EPI_ADD /
+// EPI_RAW chosen at run time, same arithmetic): one tile body for both dgrads of a
+// residual block in the persistent train backward (pv_bwd_tower.hip).
+constexpr int EPI_OPTADD = 5;
 
 // Train-step epilogue extras (template XE of halo_tile / halo_epilogue), computed
 // from the tile while it is on chip so no separate pass re-reads the conv output:
@@ -119,9 +122,11 @@ struct EpiX {
 //     bn_bwd_apply coefficients gm = S dy / N, k = S(z-mean)dy invstd^2 / N,
 //     iw = invstd * gamma.
 struct FinX {
-    unsigned* cnt = nullptr;     // fused: arrival counter per N tile (0 at launch; reset by the last arriver)
-    int late = 0;                // XE_STATS: store the tile after the arrival count (key 42): the
+    unsigned* cnt = nullptr;     // fused: arrival counter per N tile (0 at launch; reset by the last arriver).
+                                 // XE_STATS: the tile is stored after the arrival count, so the
                                  // write-through drain of the 32 KB tile leaves the finalize's path
+    unsigned* done = nullptr;    // in-launch consumers (pv_bwd_tower.hip): the results are stored
+                                 // write-through, drained, and each finalizing workgroup then adds 1
     const float* gamma = nullptr;
     const float* beta = nullptr;                            // FWD
     float *rmean = nullptr, *rvar = nullptr;                // FWD running stats
@@ -175,6 +180,13 @@ __device__ __forceinline__ void bn_fin_accum(const float* __restrict__ pa, const
 }
 // combine the 8 tile classes in the fixed order ((0+4)+(2+6))+((1+5)+(3+7)) and write
 // channel c's results
+// publish one result: write-through (agent-scope relaxed store = global_store sc1) when
+// a consumer of the same launch reads it (f.done), plain otherwise
+__device__ __forceinline__ void fin_put(float* p, float v, bool wt)
+{
+    if (wt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
 template <bool FWD>
 __device__ __forceinline__ void bn_fin_out(double v0, double v1, int M, int c, const FinX& f)
 {
@@ -195,11 +207,12 @@ __device__ __forceinline__ void bn_fin_out(double v0, double v1, int M, int c, c
         f.rvar[c] = (float)((double)BN_MOMENTUM * unb + (1.0 - (double)BN_MOMENTUM) * (double)f.rvar[c]);
     } else {
         const double inv = (double)f.inv_i[c];
-        f.ggamma[c] = (float)(v1 * inv);
-        f.gbeta[c] = (float)v0;
-        f.gm_o[c] = (float)(v0 / (double)M);
-        f.k_o[c] = (float)(v1 * inv * inv / (double)M);
-        f.iw_o[c] = (float)inv * f.gamma[c];
+        const bool wt = f.done != nullptr;
+        fin_put(f.ggamma + c, (float)(v1 * inv), wt);
+        fin_put(f.gbeta + c, (float)v0, wt);
+        fin_put(f.gm_o + c, (float)(v0 / (double)M), wt);
+        fin_put(f.k_o + c, (float)(v1 * inv * inv / (double)M), wt);
+        fin_put(f.iw_o + c, (float)inv * f.gamma[c], wt);
     }
 }
 // 8 waves x 64 lanes: wave w holds tile class w of channel c (lane); the classes are
@@ -234,29 +247,14 @@ __device__ __forceinline__ void bn_fin_combine8(double v0, double v1, double* re
 constexpr int PRO_NONE = 0;
 constexpr int PRO_BN = 1;       // relu(bn(z))
 constexpr int PRO_BN_RES = 2;   // relu(bn(z) + res)
-// PRO_BNBWD (dgrad of a residual-free layer's conv): the staged tensor is the gradient g
-// of the layer's BN + ReLU output, `res` its raw BN input z, and the BatchNorm backward
-// is applied per element exactly as bn_bwd_apply_kernel<C, false, WT, MZ = true>:
-//   dy = fma(z, scale, shift) > 0 ? g : 0;  dz = ((dy - gm) - (z - mean) * k) * iw
-// (padding rows stay 0); the N-tile-0 workgroups write the tile's own rows of dz (the
-// weight gradient's operand)
-constexpr int PRO_BNBWD = 3;
-// PRO_BNBWD_LDS: the same transform, with z staged by LDS-DMA into its own [HR][32]
-// buffer (no registers held across taps) and applied once per channel group as the
-// staged g rows are written to LDS (outside the MFMA taps: no spills)
-constexpr int PRO_BNBWD_LDS = 4;
 #ifndef AZG_PRO_REMAT
 #define AZG_PRO_REMAT 1
 #endif
 struct ProX {
-    const float* res;     // PRO_BN_RES: residual input; PRO_BNBWD: the layer's raw BN input z
+    const float* res;     // PRO_BN_RES: residual input
     const float* scale;   // [C] BN scale of the input layer (invstd * gamma)
     const float* shift;   // [C] beta - mean * scale
-    float* aout;          // a (dz for PRO_BNBWD, padded NHWC): own rows written when n0 == 0
-    const float* mean = nullptr;   // PRO_BNBWD: [C] batch mean, and the bn_bwd_apply
-    const float* gm = nullptr;     // coefficients gm = S dy / N, k, iw = invstd * gamma
-    const float* kk = nullptr;
-    const float* iw = nullptr;
+    float* aout;          // a (padded NHWC): own rows written when n0 == 0
 };
 
 
@@ -300,7 +298,8 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
     const int ec = (tid % CPR) * 4;
     const int er = tid / CPR;
     const int col = n0 + ec;
-    const bool has_res = EPI == EPI_BN_RES_RELU || EPI == EPI_ADD || (EPI == EPI_BN_OPTRES_RELU && resid);
+    const bool has_res = EPI == EPI_BN_RES_RELU || EPI == EPI_ADD ||
+                         ((EPI == EPI_BN_OPTRES_RELU || EPI == EPI_OPTADD) && resid);
     // EARLY: the residual / scale / shift loads are issued before the accumulator
     // tile goes through LDS, so their latency overlaps the ds_write + barrier
     f32x4 rve[EARLY ? NPASS : 1];
@@ -336,7 +335,7 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
     f32x4 vk[XE == XE_STATS ? NPASS : 1];
     // late store (XE_STATS + fused finalize): the raw tile (kept in vk) is stored after the
     // partials are published and counted, so the arrival waits only for the partials
-    const bool late = XE == XE_STATS && EPI == EPI_RAW && fx.cnt != nullptr && fx.late != 0;
+    const bool late = XE == XE_STATS && EPI == EPI_RAW && fx.cnt != nullptr;
     if (XE == XE_BNBWD) xmu = *(const f32x4*)(ex.mean + col);
 #pragma unroll
     for (int p = 0; p < NPASS; ++p) {
@@ -370,6 +369,8 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                     x = has_res ? fmaxf(x * s4[e] + t4[e] + rv[e], 0.f) : fmaxf(x * s4[e] + t4[e], 0.f);
                 } else if (EPI == EPI_ADD) {
                     x = x + rv[e];
+                } else if (EPI == EPI_OPTADD) {
+                    if (has_res) x = x + rv[e];
                 }
                 v[e] = x;
             }
@@ -498,6 +499,13 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                 bn_fin_accum<XE == XE_STATS, false>(ex.pa, ex.pb, C, ntm, BM, M, ch, wv, v0, v1);
                 bn_fin_combine8<XE == XE_STATS>(v0, v1, red, M, ch, true, fx);
                 if (tid == 0) __hip_atomic_store(fx.cnt + n0 / BN, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (fx.done) {
+                    // R1 producer: the results were stored write-through; every storing wave
+                    // drains, a barrier, then one agent-scope add (consumers poll + acquire)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
+                    if (tid == 0) __hip_atomic_fetch_add(fx.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
         }
     }
@@ -737,7 +745,6 @@ __device__ __forceinline__ void halo_tile(
     static_assert(H_LD <= 9, "halo loads are spread over the 9 taps");
     static_assert(PRO == PRO_NONE || H_LD <= 8, "the operand prologue of a row runs one tap after its load");
     static_assert(PRO == PRO_NONE || ((VAR == 0 || VAR == 32) && ABL == 0), "operand prologue: register staging only");
-    static_assert(PRO != PRO_BNBWD_LDS || (RPP == 8 * NW_ && T::NT < 1024), "z DMA: one 8-row piece per wave and row block");
     // VAR (A/B studies; the product uses 0, measured fastest): bit 1 = halo rows
     // swizzled on the padded board position (conflict-free fragment reads) and an
     // unpadded epilogue tile; bit 2 = weights staged two chunks ahead; bit 4 = LDS-DMA
@@ -748,8 +755,7 @@ __device__ __forceinline__ void halo_tile(
 
     float* Ah = smem;                 // [HR][32]
     float* Bs = smem + HR * BK;       // [2][BN][32]
-    float* Ps = smem + (HR + 2 * BN) * BK;   // PRO: [2][C] input-layer BN scale / shift (+ [4][C] PRO_BNBWD)
-    float* Zs = Ps + pro_params(PRO) * C;    // PRO_BNBWD_LDS: [HR][32] z rows (unswizzled, lane-linear DMA)
+    float* Ps = smem + (HR + 2 * BN) * BK;   // PRO: [2][C] input-layer BN scale / shift
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
@@ -781,12 +787,6 @@ __device__ __forceinline__ void halo_tile(
         for (int c = tid; c < C; c += T::NT) {
             Ps[c] = px.scale[c];
             Ps[C + c] = px.shift[c];
-            if constexpr (PRO == PRO_BNBWD || PRO == PRO_BNBWD_LDS) {
-                Ps[2 * C + c] = px.mean[c];
-                Ps[3 * C + c] = px.gm[c];
-                Ps[4 * C + c] = px.kk[c];
-                Ps[5 * C + c] = px.iw[c];
-            }
         }
         __syncthreads();
     }
@@ -796,7 +796,7 @@ __device__ __forceinline__ void halo_tile(
     // the next chunk's MFMAs to land before the ds_write that waits on it (the loops
     // are fully unrolled: the rb1 = rb2 hand-over is a register renaming, not a move)
     f32x4 rh[H_LD], rb1[B_LD], rb2[B_LD];
-    f32x4 rr[(PRO == PRO_BN_RES || PRO == PRO_BNBWD) ? H_LD : 1];
+    f32x4 rr[PRO == PRO_BN_RES ? H_LD : 1];
     // VAR bit 16 (persistent tower at ONE workgroup per CU): halo rows are produced
     // inside the launch by other CUs; every load of them is an sc1 buffer load (L1
     // bypassed) in place of the consumer's acquire -- row 1 of the microarch guide's
@@ -819,19 +819,12 @@ __device__ __forceinline__ void halo_tile(
         if constexpr (HPRED) {
             if (hbase + sr + RPP * i > hmax) return;
         }
-        // z row first: in-order vmcnt retirement makes the wait for rh[i] cover it.
-        // Lane l of wave w lands at row 8w + l/8, chunk l%8 of row block i = its own
-        // staged (sr + RPP i, sc) position.
-        // (buffer form: one 32-bit offset VGPR per row, shared with the g load)
-        if constexpr (PRO == PRO_BNBWD_LDS)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(res_rs, (__attribute__((address_space(3))) void*)(Zs + (8 * wid + RPP * i) * BK),
-                                                     16, (hsrc[i] + cg * BK) * 4, 0, 0, 0);
         if constexpr ((VAR & 48) != 0)
             rh[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, (hsrc[i] + cg * BK) * 4, 0,
                                                                                     (VAR & 16) ? 16 : 0));
         else
             rh[i] = *(const f32x4*)(in + hsrc[i] + cg * BK);
-        if constexpr (PRO == PRO_BN_RES || PRO == PRO_BNBWD) {
+        if constexpr (PRO == PRO_BN_RES) {
             if constexpr ((VAR & 32) != 0)
                 rr[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(res_rs, (hsrc[i] + cg * BK) * 4, 0, 0));
             else
@@ -885,60 +878,19 @@ __device__ __forceinline__ void halo_tile(
             const f32x4 s4 = *(const f32x4*)(Ps + cg * BK + sc);
             const f32x4 t4 = *(const f32x4*)(Ps + C + cg * BK + sc);
             f32x4 v = rh[i];
-            if constexpr (PRO == PRO_BNBWD) {   // = bn_bwd_apply_kernel (MZ): v = g, rr = z
-                const f32x4 mu = *(const f32x4*)(Ps + 2 * C + cg * BK + sc);
-                const f32x4 g_ = *(const f32x4*)(Ps + 3 * C + cg * BK + sc);
-                const f32x4 k_ = *(const f32x4*)(Ps + 4 * C + cg * BK + sc);
-                const f32x4 w_ = *(const f32x4*)(Ps + 5 * C + cg * BK + sc);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float z = rr[i][e];
-                    const float dy = fmaf(z, s4[e], t4[e]) > 0.f ? v[e] : 0.f;
-                    const float d = ((dy - g_[e]) - (z - mu[e]) * k_[e]) * w_[e];
-                    v[e] = (pint >> i) & 1 ? d : 0.f;
-                }
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    float y = fmaf(v[e], s4[e], t4[e]);
-                    if constexpr (PRO == PRO_BN_RES) y += rr[i][e];
-                    v[e] = (pint >> i) & 1 ? fmaxf(y, 0.f) : 0.f;
-                }
+            for (int e = 0; e < 4; ++e) {
+                float y = fmaf(v[e], s4[e], t4[e]);
+                if constexpr (PRO == PRO_BN_RES) y += rr[i][e];
+                v[e] = (pint >> i) & 1 ? fmaxf(y, 0.f) : 0.f;
             }
             rh[i] = v;
             if ((pown >> i) & 1) store4<true>(px.aout, ars, hsrc[i] + cg * BK, v);
         }
     };
     auto hstore = [&](int cg) {
-        if constexpr (PRO == PRO_BNBWD_LDS) {
-            // wait for the last staged row (hence every z DMA before it), then keep the
-            // z reads below that wait
-            asm volatile("" ::"v"(rh[H_LD - 1]));
-            __builtin_amdgcn_sched_barrier(0);
-            const f32x4 s4 = *(const f32x4*)(Ps + cg * BK + sc);
-            const f32x4 t4 = *(const f32x4*)(Ps + C + cg * BK + sc);
-            const f32x4 mu = *(const f32x4*)(Ps + 2 * C + cg * BK + sc);
-            const f32x4 g_ = *(const f32x4*)(Ps + 3 * C + cg * BK + sc);
-            const f32x4 k_ = *(const f32x4*)(Ps + 4 * C + cg * BK + sc);
-            const f32x4 w_ = *(const f32x4*)(Ps + 5 * C + cg * BK + sc);
 #pragma unroll
-            for (int i = 0; i < H_LD; ++i) {
-                const f32x4 z4 = *(const f32x4*)(Zs + (sr + RPP * i) * BK + sc);
-                f32x4 v = rh[i];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {   // = bn_bwd_apply_kernel (MZ), as PRO_BNBWD
-                    const float z = z4[e];
-                    const float dy = fmaf(z, s4[e], t4[e]) > 0.f ? v[e] : 0.f;
-                    const float d = ((dy - g_[e]) - (z - mu[e]) * k_[e]) * w_[e];
-                    v[e] = (pint >> i) & 1 ? d : 0.f;
-                }
-                *(f32x4*)(Ah + (sr + RPP * i) * BK + hwchunk[i]) = v;
-                if ((pown >> i) & 1) store4<true>(px.aout, ars, hsrc[i] + cg * BK, v);
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < H_LD; ++i) *(f32x4*)(Ah + (sr + RPP * i) * BK + hwchunk[i]) = rh[i];
-        }
+        for (int i = 0; i < H_LD; ++i) *(f32x4*)(Ah + (sr + RPP * i) * BK + hwchunk[i]) = rh[i];
     };
     auto bstore = [&](const f32x4 (&rb)[B_LD], int buf) {
         float* b = Bs + buf * BN * BK;
@@ -977,10 +929,8 @@ __device__ __forceinline__ void halo_tile(
     } else {
         bload(rb1, kchunk(0));
     }
-    if constexpr (PRO != PRO_BNBWD_LDS) {
 #pragma unroll
-        for (int i = 0; i < H_LD; ++i) pro_row(0, i);
-    }
+    for (int i = 0; i < H_LD; ++i) pro_row(0, i);
     hstore(0);
     if (BPF2) bstore(rb2, 0);
     else bstore(rb1, 0);
@@ -1051,7 +1001,7 @@ __device__ __forceinline__ void halo_tile(
                             at[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], at[i][j], 0, 0, 0);
             }
             // the row loaded one tap ago gets its BN / ReLU now (PRO)
-            if (PRO != PRO_NONE && PRO != PRO_BNBWD_LDS && more && tap >= 1 && tap <= H_LD) pro_row(cg + 1, tap - 1);
+            if (PRO != PRO_NONE && more && tap >= 1 && tap <= H_LD) pro_row(cg + 1, tap - 1);
             if (j + 1 < NCHK) {
                 bstore(rb1, cur ^ 1);
                 if (BPF2) {

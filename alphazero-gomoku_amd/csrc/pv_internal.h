@@ -44,29 +44,12 @@ extern int g_tower_mode;
 extern int g_tower_shape;
 extern int g_tower_ablation;
 extern int g_tower_var;
-extern int g_wgrad_serial;
 extern int g_train_fuse_apply;
 extern int g_train_fuse_fin;
-extern int g_train_fuse_heads;
-extern int g_train_side_heads;
-extern int g_train_ev_device;
-extern int g_train_dz_all;
-extern int g_train_pack_after;
-extern int g_train_side_prio;
-extern int g_train_stem_stats;
-extern int g_train_defer_reduce;
-extern int g_train_fuse_bwd;
-extern int g_train_late_store;
+extern int g_train_bwd_tower;
+extern int g_wgrad_splits;
 hipError_t launch_stem_stats(int C, const float* x, const float* ws, float* out, int B, float* pa, float* pb,
                              hipStream_t st);
-extern int g_train_maskz;
-extern int g_train_split_pack;
-extern int g_train_skip;
-extern int g_wgrad_bk;
-extern int g_wgrad_kernel;
-extern int g_wgrad_splits;
-extern int g_wgrad_comb;
-extern int g_train_wt;
 constexpr int kTowerMaxBlocks = 32;
 int conv_batch_bucket(int M);
 size_t tower_sync_bytes(int nlayers, int M);

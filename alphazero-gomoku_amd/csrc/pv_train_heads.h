@@ -15,7 +15,6 @@ struct HeadStatsArgs {
     const float* wvc;      // value_conv.weight [C]
     float* zh;             // [B][3][225]
     double* part;          // [nwg][6]
-    unsigned* cnt;
     int M;
     // finalize (reference BatchNorm2d train-mode forward of policy_bn / value_bn)
     const BnDesc* desc;
@@ -25,36 +24,6 @@ struct HeadStatsArgs {
     float *bmean, *binv, *bscale, *bshift;
     int64_t* nbt;
     int nbn;
-};
-
-struct HeadBoardArgs {
-    const float* zh;       // [B][3][225]
-    const float* hmean;    // head BN mean / scale / shift / invstd (policy ch 0, 1, value)
-    const float* hscale;
-    const float* hshift;
-    const float* hinv;
-    const float* wfc;      // packed policy_fc + value_fc1 rows [289][456] (pv_pack.hip), zero-padded
-    const float* wpf;      // policy_fc.weight [225][450], bias [225]
-    const float* bpf;
-    const float* wv1;      // value_fc1.weight [64][225], bias [64]
-    const float* bv1;
-    const float* wv2;      // value_fc2.weight [64], bias [1]
-    const float* bv2;
-    const float* pis;      // [B][225]
-    const float* zs;       // [B]
-    float *fp, *fv, *hv, *dlogits, *dhv, *dfp, *dfv;
-    double* pd;            // [nwg][HB_PD]
-    float* pf;             // [nwg][HB_PF]
-    unsigned* cnt;
-    int B;
-    // finalize
-    const BnDesc* desc;
-    int pol_layer, val_layer;
-    const float* params;
-    float* grads;
-    float* hb;             // [3][3] head-BN backward coefficients (S dy / N, k, invstd*gamma)
-    float *g_pfb, *g_v1b, *g_v2w, *g_v2b;
-    float* losses;
 };
 
 struct HeadDgradArgs {
@@ -69,13 +38,12 @@ struct HeadDgradArgs {
     float *dfp, *dfv;      // masked fc data gradients
     double* part;          // [groups][6] head-BN backward sums per workgroup
     int B;
-    // finalize (head_bn_bwd_fin_kernel)
+    // finalize (head_bwd_fin_wave, run by every heads_bwd_fused_kernel workgroup)
     const BnDesc* desc;
     int pol_layer, val_layer;
     const float* params;
     float* grads;
     const float* hinv;     // head BN invstd (3)
-    float* hb;             // [3][3] head-BN backward coefficients
 };
 
 struct HeadBwdArgs {
@@ -84,7 +52,6 @@ struct HeadBwdArgs {
     const float* dfp;      // [B][450]
     const float* dfv;      // [B][225]
     const float* hmean;    // head BN mean (3)
-    const float* hb;       // [3][3] head-BN backward coefficients
     const float* wpc;      // policy_conv.weight [2][C]
     const float* wvc;      // value_conv.weight [C]
     float* gx;             // gradient of the tower output (padded NHWC)
@@ -95,29 +62,20 @@ struct HeadBwdArgs {
     float* pa;             // [tile][C]: S dy
     float* pb;             // [tile][C]: S (z - mean) dy
     int M;
-    // key 28 bit 4: the head-BN backward finalize folded in (every workgroup reduces
-    // head_dgrad_kernel's partials itself; null: read hb)
+    // the head-BN backward finalize, run by every workgroup from head_dgrad_kernel's
+    // dg_nwg partials
     HeadDgradArgs dg;
-    int dg_nwg;            // 0: read hb
+    int dg_nwg;
 };
 
-// key 28 bit 3: the fc stage as short, wide launches (pv_train_heads.hip)
 int head_dgrad_groups(int B);
-hipError_t launch_head_dgrad(const HeadDgradArgs& a, hipStream_t st, bool fin);
-hipError_t launch_head_bn_apply_feat(const float* zh, const float* hscale, const float* hshift, float* fp, float* fv,
-                                     float* feat, int B, hipStream_t st, const HeadStatsArgs* fin);
+int head_proj_stats_groups(int M);
+hipError_t launch_head_proj_partials(int C, bool apply, const HeadStatsArgs& a, hipStream_t st);
+hipError_t launch_head_bn_apply_feat(float* fp, float* fv, float* feat, int B, const HeadStatsArgs& fin,
+                                     hipStream_t st);
+hipError_t launch_head_dgrad(const HeadDgradArgs& a, hipStream_t st);
 hipError_t launch_head_fc_wgrad(const float* dlogits, const float* fp, const float* dhv, const float* fv, float* gpf,
                                 float* gv1, int B, hipStream_t st);
-hipError_t launch_head_proj_partials(int C, bool apply, const HeadStatsArgs& a, hipStream_t st);
-// key 28 bit 4: head_proj_stats_kernel's partials finalized by a one-workgroup kernel
-hipError_t launch_head_proj_split(int C, bool apply, const HeadStatsArgs& a, hipStream_t st);
-
-int head_proj_stats_groups(int M);
-int head_board_groups(int B);
-int head_board_pd();
-int head_board_pf();
-hipError_t launch_head_proj_stats(int C, bool apply, const HeadStatsArgs& a, hipStream_t st);
-hipError_t launch_head_board(const HeadBoardArgs& a, hipStream_t st);
 hipError_t launch_heads_bwd_fused(int C, bool bnx, const HeadBwdArgs& a, hipStream_t st);
 
 }  // namespace azg

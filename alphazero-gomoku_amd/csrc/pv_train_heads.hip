@@ -1,88 +1,39 @@
 // Train-step head chain (reference network.py:101-115 forward in train mode, the
-// loss of network.py:216-221 and its backward down to the tower output), as three
-// launches on the critical path instead of eighteen:
+// loss of network.py:216-221 and its backward down to the tower output), as short,
+// wide launches (the chain is latency-bound: every launch here is 6-16 us):
 //
 //   head_proj_stats_kernel  the last block's BN2 + residual + ReLU (the tower output
 //       a = relu(z*s + t + x), written for the backward) fused with the three 1x1
-//       head projections (policy_conv C->2, value_conv C->1: zh[b][3][225]) and the
-//       head BatchNorms' batch statistics: per-workgroup fp64 sums, finalized by the
-//       last workgroup to arrive (mean / invstd / folded scale+shift, running stats,
-//       every BN layer's num_batches_tracked += 1);
-//   head_board_kernel  one wave per board, four boards per workgroup: head BN + ReLU
-//       (fp [450], fv [225]), policy_fc / value_fc1 forward (fp32 VALU dot products,
-//       weights streamed from L2), log_softmax + KLDiv(batchmean) + MSE and their
-//       gradients, the masked fc data gradients dfp / dfv, and per-workgroup partials
-//       of the head-BN backward sums, the fc bias grads, value_fc2 grads and the loss
-//       means -- finalized by the last workgroup (head-BN dgamma / dbeta and the
-//       backward-apply coefficients, bias grads, losses);
-//   heads_bwd_fused_kernel  the head-BN backward apply computed per pixel on the fly,
-//       the projections' data gradient gX = sum_ch dzh * Wh and weight-grad partials,
-//       and the BatchNorm-backward partial sums of the last block's bn2 (dy = gX * (a
-//       > 0), S dy, S (z - mean) dy per 128-row tile) for the next finalize.
+//       head projections (policy_conv C->2, value_conv C->1: zh[b][3][225]) and
+//       per-workgroup fp64 partials of the head BatchNorms' batch statistics;
+//   head_bn_apply_feat_kernel  every workgroup finalizes the head statistics from those
+//       partials in one fixed order (workgroup 0 publishes mean / invstd / scale / shift,
+//       the running stats and every BN layer's num_batches_tracked += 1), then head BN +
+//       ReLU into fp / fv and the eval forward's padded feature rows for heads_fc;
+//   heads_fc (pv_heads.hip) + heads_loss_kernel (pv_train.hip): the fc forward, log_softmax
+//       + KLDiv(batchmean) + MSE and their gradients;
+//   head_dgrad_kernel  the masked fc data gradients dfp / dfv (fp32 MFMA) with per-
+//       workgroup head-BN backward partials;
+//   heads_bwd_fused_kernel  every workgroup finalizes the head-BN backward from those
+//       partials (workgroup 0 publishes dgamma / dbeta), applies it per pixel on the fly,
+//       and writes the projections' data gradient gX = sum_ch dzh * Wh, their weight-grad
+//       partials, and the BatchNorm-backward partial sums of the last block's bn2 (dy =
+//       gX * (a > 0), S dy, S (z - mean) dy per 128-row tile) for the tower backward.
 //
-// The fc weight gradients (dW = dlogits^T fp, dW1 = dhv^T fv) are a separate small
-// GEMM off the critical path.  Hand-offs to the last-arriving workgroups follow the
-// microarch guide's R1 producer + consumer acquire (valid at any occupancy):
-// write-through stores, s_waitcnt vmcnt(0), barrier, one relaxed agent-scope atomic
-// per workgroup; the workgroup whose add returns n - 1 runs an agent acquire before
-// its plain loads.
+// The fc weight gradients (dW = dlogits^T fp, dW1 = dhv^T fv, head_fc_wgrad_kernel) run
+// at the end of the step, off the critical path.
 #include "pv_train_heads.h"
 
 #include <type_traits>
 
-#ifdef AZG_HB_TIMING   // ad-hoc phase timing (wall clock, 100 MHz), never in the product
-#define HBT_DECL unsigned long long hbt_[8] = {0, 0, 0, 0, 0, 0, 0, 0}
-#define HBT(i) do { if (threadIdx.x == 0) hbt_[i] = wall_clock64(); } while (0)
-#define HBT_MID(n) do { if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1)) \
-    printf("HBT %s blk %d mid %llu | %llu %llu %llu %llu %llu %llu %llu\n", n, (int)blockIdx.x, hbt_[0], \
-           hbt_[1] - hbt_[0], hbt_[2] - hbt_[0], hbt_[3] - hbt_[0], hbt_[4] - hbt_[0], hbt_[5] - hbt_[0], \
-           hbt_[6] - hbt_[0], hbt_[7] - hbt_[0]); } while (0)
-#define HBT_END(n) do { if (threadIdx.x == 0) printf("HBT %s last %d start %llu end %llu\n", n, \
-    (int)blockIdx.x, hbt_[0], wall_clock64() - hbt_[0]); } while (0)
-#else
-#define HBT_DECL
-#define HBT(i)
-#define HBT_MID(n)
-#define HBT_END(n)
-#endif
 namespace azg {
 
 constexpr int HP_ROWS = 64;     // pixels per workgroup of head_proj_stats_kernel
-constexpr int HB_BOARDS = 4;    // boards per workgroup of head_board_kernel (one wave each)
-// per-workgroup partials of head_board_kernel: doubles [6 head-BN sums | 2 losses],
-// floats [225 policy bias | 64 value_fc1 bias | 64 value_fc2 weight | 1 value_fc2 bias]
-constexpr int HB_PD = 8;
-constexpr int HB_PF = ACTIONS + 2 * VHID + 1;
-
-// relaxed agent-scope arrival count, the last workgroup learns it is last (R1 + acquire)
-__device__ __forceinline__ bool last_arrival(unsigned* cnt, unsigned n, unsigned* flag)
-{
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned last = old == n - 1 ? 1u : 0u;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-armed for the next step
-        }
-        *flag = last;
-    }
-    __syncthreads();
-    return *flag != 0;
-}
-
 __device__ __forceinline__ void st_wt_d(double* p, double v)
 {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v),
                                           wt_rsrc(p, 8), 0, 0, 16);
 }
-__device__ __forceinline__ void st_wt_f(float* p, float v)
-{
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), wt_rsrc(p, 4), 0, 0, 16);
-}
-
 __device__ __forceinline__ double wsum_d(double v)
 {
 #pragma unroll
@@ -158,10 +109,8 @@ __device__ __forceinline__ void head_stats_fin(const HeadStatsArgs& a, int nwg, 
     if (write && a.nbt)
         for (int i = threadIdx.x; i < a.nbn; i += 256) a.nbt[i] += 1;
 }
-
-// LAST: the last-arriving workgroup finalizes (key 28 bit 0); otherwise the partials
-// are left to head_proj_fin_kernel (key 28 bit 4)
-template <int C, bool APPLY, bool LAST = true>
+// partials only: every workgroup of head_bn_apply_feat_kernel finalizes them
+template <int C, bool APPLY>
 __global__ __launch_bounds__(256) void head_proj_stats_kernel(const HeadStatsArgs a)
 {
     // C/4 consecutive threads own one pixel (4 channels each: 16-B runs, every wave
@@ -170,7 +119,6 @@ __global__ __launch_bounds__(256) void head_proj_stats_kernel(const HeadStatsArg
     constexpr int TPP = C / 4, PPP = 256 / TPP, NP = HP_ROWS / PPP;
     static_assert(TPP <= 64 && 64 % TPP == 0 && HP_ROWS % PPP == 0, "pixel layout");
     __shared__ double red[4][6];
-    __shared__ unsigned flag;
     const int tid = threadIdx.x;
     const int c = (tid % TPP) * 4, pp = tid / TPP;
     const f32x4 w0 = *(const f32x4*)(a.wpc + c), w1 = *(const f32x4*)(a.wpc + C + c), w2 = *(const f32x4*)(a.wvc + c);
@@ -179,7 +127,6 @@ __global__ __launch_bounds__(256) void head_proj_stats_kernel(const HeadStatsArg
         s4 = *(const f32x4*)(a.scale + c);
         t4 = *(const f32x4*)(a.shift + c);
     }
-    HBT_DECL; HBT(0);
     const int mb = blockIdx.x * HP_ROWS;
     f32x4 zv[NP], rv[APPLY ? NP : 1];
 #pragma unroll
@@ -239,411 +186,9 @@ __global__ __launch_bounds__(256) void head_proj_stats_kernel(const HeadStatsArg
 #pragma unroll
         for (int k = 0; k < 6; ++k) red[wid][k] = v[k];
     __syncthreads();
-    HBT(1);
     if (threadIdx.x < 6)
         st_wt_d(a.part + (size_t)blockIdx.x * 6 + threadIdx.x,
                 (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]));
-    HBT(7); HBT_MID("proj");
-    if constexpr (!LAST) return;
-    if (!last_arrival(a.cnt, gridDim.x, &flag)) return;
-    head_stats_fin(a, gridDim.x, red);
-    HBT_END("proj");
-}
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void head_board_kernel(const HeadBoardArgs a)
-{
-    constexpr int FK = 512;   // feature row: policy 450 (zero pads to 512) | value 225 (zero pads to 512)
-    __shared__ __attribute__((aligned(16))) float fb[HB_BOARDS][2][FK];
-    __shared__ float lgs[HB_BOARDS][ACTIONS];
-    __shared__ float dls[HB_BOARDS][ACTIONS];
-    __shared__ float hps[HB_BOARDS][VHID];
-    __shared__ float dhs[HB_BOARDS][VHID];
-    __shared__ float hvs[HB_BOARDS][VHID];
-    __shared__ float dps[HB_BOARDS];
-    __shared__ double lss[HB_BOARDS][2];
-    __shared__ double red[4][6];
-    __shared__ unsigned flag;
-    constexpr int KC = 64, LDW = KC + 4;                         // fc weight chunk [289][64 + 4]
-    __shared__ __attribute__((aligned(16))) float lwbuf[FC_OUT * LDW];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int b0 = blockIdx.x * HB_BOARDS;
-    HBT_DECL; HBT(0);
-    const int nb = min(HB_BOARDS, a.B - b0);
-    // head BN + ReLU (= head_bn_apply_kernel); feature pads and absent boards are 0.
-    // Every zh load of the thread first (the feature stores may alias them)
-    constexpr int NA = (HB_BOARDS * 2 * FK) / 256;   // 16 items per thread
-    {
-        const float hs0 = a.hscale[0], hs1 = a.hscale[1], hs2 = a.hscale[2];
-        const float ht0 = a.hshift[0], ht1 = a.hshift[1], ht2 = a.hshift[2];
-        float zv[NA];
-#pragma unroll
-        for (int u = 0; u < NA; ++u) {
-            const int i = tid + 256 * u;
-            const int bb = i / (2 * FK), pol = ((i / FK) & 1) == 0, kk = i & (FK - 1);
-            const bool in = bb < nb && kk < (pol ? 2 * PIX : PIX);
-            zv[u] = in ? a.zh[(size_t)(b0 + bb) * 3 * PIX + (pol ? kk : 2 * PIX + kk)] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < NA; ++u) {
-            const int i = tid + 256 * u;
-            const int bb = i / (2 * FK), pol = ((i / FK) & 1) == 0, kk = i & (FK - 1);
-            const bool in = bb < nb && kk < (pol ? 2 * PIX : PIX);
-            const int ch = pol ? (kk < PIX ? 0 : 1) : 2;
-            const float sc = ch == 0 ? hs0 : ch == 1 ? hs1 : hs2, sh = ch == 0 ? ht0 : ch == 1 ? ht1 : ht2;
-            const float y = in ? fmaxf(zv[u] * sc + sh, 0.f) : 0.f;
-            fb[bb][pol ? 0 : 1][kk] = y;
-            zv[u] = y;
-        }
-#pragma unroll
-        for (int u = 0; u < NA; ++u) {
-            const int i = tid + 256 * u;
-            const int bb = i / (2 * FK), pol = ((i / FK) & 1) == 0, kk = i & (FK - 1);
-            if (bb < nb && kk < (pol ? 2 * PIX : PIX)) {
-                if (pol) a.fp[(size_t)(b0 + bb) * 2 * PIX + kk] = zv[u];
-                else a.fv[(size_t)(b0 + bb) * PIX + kk] = zv[u];
-            }
-        }
-    }
-    HBT(1);
-    // policy_fc / value_fc1 forward on the packed rows wfc[289][456] (16-B aligned, zero
-    // pads), staged through LDS in K chunks of 64: every thread issues its share of a
-    // chunk's 289 x 64 floats (19 float4, coalesced 256-B row pieces) at once, the next
-    // chunk's loads are issued before the current chunk's FMAs.  Thread t owns output row
-    // t (wave 0 also row t + 256); the features are LDS broadcasts, the K loop is fully
-    // unrolled (the last chunk's columns past 456 are zero weights and zero features)
-    {
-        constexpr int NCH = (FC_KP + KC - 1) / KC;            // 8 chunks
-        constexpr int NV4 = (FC_OUT * KC / 4 + 255) / 256;    // float4 loads per thread per chunk (19)
-        float* wl = lwbuf;
-        f32x4 wv[NV4];
-        auto load = [&](int c) {
-            const int k0 = c * KC;
-#pragma unroll
-            for (int u = 0; u < NV4; ++u) {
-                const int e = tid + 256 * u;                  // float4 index in the chunk
-                const int r = e / (KC / 4), q = e - r * (KC / 4);
-                wv[u] = (r < FC_OUT && k0 + 4 * q < FC_KP)
-                            ? *(const f32x4*)(a.wfc + (size_t)r * FC_KP + k0 + 4 * q)
-                            : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-        };
-        float s0[HB_BOARDS] = {0.f, 0.f, 0.f, 0.f}, s1[HB_BOARDS] = {0.f, 0.f, 0.f, 0.f};
-        const int j0 = tid, j1 = tid + 256;                   // j1 < 289 only in wave 0
-        const float* f0 = &fb[0][j0 < ACTIONS ? 0 : 1][0];    // policy rows: policy features
-        const float* f1 = &fb[0][1][0];
-        const float* w0p = wl + j0 * LDW;
-        const float* w1p = wl + min(j1, FC_OUT - 1) * LDW;
-        load(0);
-        for (int c = 0; c < NCH; ++c) {
-#pragma unroll
-            for (int u = 0; u < NV4; ++u) {
-                const int e = tid + 256 * u;
-                const int r = e / (KC / 4), q = e - r * (KC / 4);
-                if (r < FC_OUT) *(f32x4*)(wl + r * LDW + 4 * q) = wv[u];
-            }
-            __syncthreads();
-            if (c + 1 < NCH) load(c + 1);
-            const int k0 = c * KC;
-            if (wid == 0) {
-#pragma unroll
-                for (int k = 0; k < KC; k += 4) {
-                    const f32x4 w0 = *(const f32x4*)(w0p + k), w1 = *(const f32x4*)(w1p + k);
-#pragma unroll
-                    for (int bb = 0; bb < HB_BOARDS; ++bb) {
-                        const f32x4 x0 = *(const f32x4*)(f0 + bb * 2 * FK + k0 + k);
-                        const f32x4 x1 = *(const f32x4*)(f1 + bb * 2 * FK + k0 + k);
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            s0[bb] = fmaf(x0[e], w0[e], s0[bb]);
-                            s1[bb] = fmaf(x1[e], w1[e], s1[bb]);
-                        }
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < KC; k += 4) {
-                    const f32x4 w0 = *(const f32x4*)(w0p + k);
-#pragma unroll
-                    for (int bb = 0; bb < HB_BOARDS; ++bb) {
-                        const f32x4 x0 = *(const f32x4*)(f0 + bb * 2 * FK + k0 + k);
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) s0[bb] = fmaf(x0[e], w0[e], s0[bb]);
-                    }
-                }
-            }
-            __syncthreads();
-        }
-#pragma unroll
-        for (int bb = 0; bb < HB_BOARDS; ++bb) {
-            if (j0 < ACTIONS) lgs[bb][j0] = s0[bb];
-            else hps[bb][j0 - ACTIONS] = s0[bb];
-            if (j1 < FC_OUT) hps[bb][j1 - ACTIONS] = s1[bb];
-        }
-    }
-    __syncthreads();
-    HBT(2);
-    // loss and output gradients, one wave per board (= heads_loss_kernel)
-    {
-        const int bb = wid, b = b0 + bb;
-        const bool ok = bb < nb;
-        float lg[4];
-        float mx = -INFINITY;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int j = lane + 64 * t;
-            lg[t] = j < ACTIONS ? lgs[bb][j] + a.bpf[j] : -INFINITY;
-            mx = fmaxf(mx, lg[t]);
-        }
-        mx = wave_max(mx);
-        float se = 0.f;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-            if (lane + 64 * t < ACTIONS) se += expf(lg[t] - mx);
-        se = wave_sum(se);
-        const float lse = logf(se);
-        float kl = 0.f, st = 0.f, tv[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int j = lane + 64 * t;
-            tv[t] = (ok && j < ACTIONS) ? a.pis[(size_t)b * ACTIONS + j] : 0.f;
-            if (j < ACTIONS) {
-                const float lp = (lg[t] - mx) - lse;
-                if (tv[t] > 0.f) kl += tv[t] * (logf(tv[t]) - lp);
-                st += tv[t];
-            }
-        }
-        kl = wave_sum(kl);
-        st = wave_sum(st);
-        const float invB = 1.f / (float)a.B;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int j = lane + 64 * t;
-            if (j < ACTIONS) {
-                const float lp = (lg[t] - mx) - lse;
-                const float dl = ok ? (expf(lp) * st - tv[t]) * invB : 0.f;
-                dls[bb][j] = dl;
-                if (ok) a.dlogits[(size_t)b * ACTIONS + j] = dl;
-            }
-        }
-        const float hid = fmaxf(hps[bb][lane] + a.bv1[lane], 0.f);
-        const float pre = wave_sum(a.wv2[lane] * hid) + a.bv2[0];
-        const float v = tanhf(pre);
-        const float z = ok ? a.zs[b] : 0.f;
-        const float dv = 2.f * (v - z) / (float)a.B;
-        const float dp = ok ? dv * (1.f - v * v) : 0.f;
-        const float dh = hid > 0.f ? dp * a.wv2[lane] : 0.f;
-        hvs[bb][lane] = ok ? hid : 0.f;
-        dhs[bb][lane] = dh;
-        if (ok) {
-            a.hv[(size_t)b * VHID + lane] = hid;
-            a.dhv[(size_t)b * VHID + lane] = dh;
-        }
-        if (lane == 0) {
-            dps[bb] = dp;
-            lss[bb][0] = ok ? (double)kl : 0.0;
-            lss[bb][1] = ok ? (double)((v - z) * (v - z)) : 0.0;
-        }
-    }
-    __syncthreads();
-    HBT(3);
-    // fc data gradients with the ReLU masks (= small_gemm dgrad) on the packed rows:
-    // thread t owns the float4 column group cg = t & 127 (< 114) of wfc and the row half
-    // h = t >> 7: policy rows [113 h, 113 h + 113) (-> policy features 4 cg .. 4 cg + 3)
-    // and, for cg < 57, value rows [32 h, 32 h + 32) (-> value features 4 cg ..).  Rows in
-    // batches of 16 float4 loads, the next batch issued before the current one's FMAs;
-    // the two halves are added in LDS (half 0 + half 1)
-    double hs[6] = {0, 0, 0, 0, 0, 0};   // (S dy, S (z - mean) dy) for ch 0, 1, 2
-    {
-        constexpr int NCG = FC_KP / 4, NCV = (PIX + 3) / 4;     // 114 policy, 57 value column groups
-        constexpr int PH = (ACTIONS + 1) / 2, VH = VHID / 2;     // 113 / 32 rows per half
-        constexpr int RB = 16;
-        const int cg = tid & 127, h = tid >> 7;
-        const bool act = cg < NCG, vact = cg < NCV;
-        const int pr0 = h * PH, pr1 = min(ACTIONS, pr0 + PH);    // policy rows of this half
-        const int np = pr1 - pr0;                                // 113 or 112
-        const int nrows = np + (vact ? VH : 0);                  // this thread's rows: policy then value
-        f32x4 ap[HB_BOARDS], av[HB_BOARDS];
-#pragma unroll
-        for (int bb = 0; bb < HB_BOARDS; ++bb) {
-            ap[bb] = f32x4{0.f, 0.f, 0.f, 0.f};
-            av[bb] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        // row r of this thread: r < np -> wfc row pr0 + r (policy, d = dls), else value
-        // row ACTIONS + 32 h + (r - np) (d = dhs)
-        auto wrow = [&](int r) {
-            return r < np ? pr0 + r : ACTIONS + VH * h + (r - np);
-        };
-        f32x4 wa[RB], wb[RB];
-#define HB_LD(W, R0)                                                                                    \
-    _Pragma("unroll") for (int u = 0; u < RB; ++u) {                                                    \
-        const int r = (R0) + u;                                                                         \
-        W[u] = (act && r < nrows) ? *(const f32x4*)(a.wfc + (size_t)wrow(r) * FC_KP + 4 * cg)           \
-                                  : f32x4{0.f, 0.f, 0.f, 0.f};                                          \
-    }
-#define HB_USE(W, R0)                                                                                   \
-    _Pragma("unroll") for (int u = 0; u < RB; ++u) {                                                    \
-        const int r = (R0) + u;                                                                         \
-        if (r < np) {                                                                                   \
-            const int j = pr0 + r;                                                                      \
-            _Pragma("unroll") for (int bb = 0; bb < HB_BOARDS; ++bb) {                                  \
-                const float d = dls[bb][j];                                                             \
-                _Pragma("unroll") for (int e = 0; e < 4; ++e) ap[bb][e] = fmaf(d, W[u][e], ap[bb][e]);  \
-            }                                                                                           \
-        } else if (r < nrows) {                                                                         \
-            const int jv = VH * h + (r - np);                                                           \
-            _Pragma("unroll") for (int bb = 0; bb < HB_BOARDS; ++bb) {                                  \
-                const float d = dhs[bb][jv];                                                            \
-                _Pragma("unroll") for (int e = 0; e < 4; ++e) av[bb][e] = fmaf(d, W[u][e], av[bb][e]);  \
-            }                                                                                           \
-        }                                                                                               \
-    }
-        constexpr int MAXR = PH + VH;                            // 145 rows at most
-        HB_LD(wa, 0)
-        for (int r0 = 0; r0 < MAXR; r0 += 2 * RB) {
-            HB_LD(wb, r0 + RB)
-            HB_USE(wa, r0)
-            if (r0 + 2 * RB < MAXR) {
-                HB_LD(wa, r0 + 2 * RB)
-            }
-            HB_USE(wb, r0 + RB)
-        }
-#undef HB_LD
-#undef HB_USE
-        // halves: half 1 parks its sums in the (free) weight-chunk LDS, half 0 adds them
-        f32x4* park = (f32x4*)lwbuf;                             // [2][HB_BOARDS][128]
-        if (h == 1)
-#pragma unroll
-            for (int bb = 0; bb < HB_BOARDS; ++bb) {
-                park[(0 * HB_BOARDS + bb) * 128 + cg] = ap[bb];
-                park[(1 * HB_BOARDS + bb) * 128 + cg] = av[bb];
-            }
-        __syncthreads();
-        if (h == 0 && act) {
-#pragma unroll
-            for (int bb = 0; bb < HB_BOARDS; ++bb) {
-                const f32x4 p1 = park[(0 * HB_BOARDS + bb) * 128 + cg], v1 = park[(1 * HB_BOARDS + bb) * 128 + cg];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    ap[bb][e] += p1[e];
-                    av[bb][e] += v1[e];
-                }
-            }
-            // masks, stores and the head BN-backward sums: policy features k = 4 cg + e
-            // (k < 450: channel k / 225), value features k = 4 cg + e (k < 225: channel 2)
-            float zp[HB_BOARDS][4], zq[HB_BOARDS][4];
-#pragma unroll
-            for (int bb = 0; bb < HB_BOARDS; ++bb)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int k = 4 * cg + e;
-                    const bool ok = bb < nb;
-                    zp[bb][e] = ok && k < 2 * PIX ? a.zh[(size_t)(b0 + bb) * 3 * PIX + k] : 0.f;
-                    zq[bb][e] = ok && vact && k < PIX ? a.zh[(size_t)(b0 + bb) * 3 * PIX + 2 * PIX + k] : 0.f;
-                }
-            const double mu0 = (double)a.hmean[0], mu1 = (double)a.hmean[1], mu2 = (double)a.hmean[2];
-#pragma unroll
-            for (int bb = 0; bb < HB_BOARDS; ++bb) {
-                if (bb >= nb) continue;
-                const int b = b0 + bb;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int k = 4 * cg + e;
-                    if (k < 2 * PIX) {
-                        const float d = fb[bb][0][k] > 0.f ? ap[bb][e] : 0.f;
-                        a.dfp[(size_t)b * 2 * PIX + k] = d;
-                        if (k < PIX) {
-                            hs[0] += (double)d;
-                            hs[1] += ((double)zp[bb][e] - mu0) * (double)d;
-                        } else {
-                            hs[2] += (double)d;
-                            hs[3] += ((double)zp[bb][e] - mu1) * (double)d;
-                        }
-                    }
-                    if (vact && k < PIX) {
-                        const float d = fb[bb][1][k] > 0.f ? av[bb][e] : 0.f;
-                        a.dfv[(size_t)b * PIX + k] = d;
-                        hs[4] += (double)d;
-                        hs[5] += ((double)zq[bb][e] - mu2) * (double)d;
-                    }
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < 6; ++k) hs[k] = wsum_d(hs[k]);
-    if (lane == 0)
-#pragma unroll
-        for (int k = 0; k < 6; ++k) red[wid][k] = hs[k];
-    __syncthreads();
-    HBT(6);
-    double* pd = a.pd + (size_t)blockIdx.x * HB_PD;
-    float* pf = a.pf + (size_t)blockIdx.x * HB_PF;
-    if (tid < 6) st_wt_d(pd + tid, (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]));
-    if (tid == 6) st_wt_d(pd + 6, (lss[0][0] + lss[1][0]) + (lss[2][0] + lss[3][0]));
-    if (tid == 7) st_wt_d(pd + 7, (lss[0][1] + lss[1][1]) + (lss[2][1] + lss[3][1]));
-    for (int o = tid; o < HB_PF; o += 256) {   // bias / value_fc2 partials over this group's boards
-        float s = 0.f;
-#pragma unroll
-        for (int bb = 0; bb < HB_BOARDS; ++bb) {
-            if (o < ACTIONS) s += dls[bb][o];
-            else if (o < ACTIONS + VHID) s += dhs[bb][o - ACTIONS];
-            else if (o < ACTIONS + 2 * VHID) s = fmaf(dps[bb], hvs[bb][o - ACTIONS - VHID], s);
-            else s += dps[bb];
-        }
-        st_wt_f(pf + o, s);
-    }
-    HBT(7); HBT_MID("board");
-    if (!last_arrival(a.cnt, gridDim.x, &flag)) return;
-    // finalize over workgroups in order; every load of a group issued before its sums
-    const int nwg = gridDim.x;
-    if (wid == 0) {
-        double s[HB_PD];
-#pragma unroll
-        for (int k = 0; k < HB_PD; ++k) s[k] = 0.0;
-        for (int g = lane; g < nwg; g += 64)
-#pragma unroll
-            for (int k = 0; k < HB_PD; ++k) s[k] += a.pd[(size_t)g * HB_PD + k];
-#pragma unroll
-        for (int k = 0; k < HB_PD; ++k) s[k] = wsum_d(s[k]);
-        if (lane < 3) {   // = head_bn_bwd_finalize_kernel
-            const int ch = lane;
-            const BnDesc d = a.desc[ch < 2 ? a.pol_layer : a.val_layer];
-            const int c = ch < 2 ? ch : 0;
-            const double N = (double)a.B * PIX;
-            const double sd = ch == 0 ? s[0] : ch == 1 ? s[2] : s[4];
-            const double qd = ch == 0 ? s[1] : ch == 1 ? s[3] : s[5];
-            const float inv = a.hinv[ch];
-            const double invd = (double)inv;
-            a.grads[d.gamma_off + c] = (float)(qd * invd);
-            a.grads[d.beta_off + c] = (float)sd;
-            a.hb[ch * 3 + 0] = (float)(sd / N);
-            a.hb[ch * 3 + 1] = (float)(qd * invd * invd / N);
-            a.hb[ch * 3 + 2] = inv * a.params[d.gamma_off + c];
-        }
-        if (lane == 0) {   // = heads_small_grads_kernel's loss means
-            const float plf = (float)(s[6] / (double)a.B), vlf = (float)(s[7] / (double)a.B);
-            a.losses[0] = plf;
-            a.losses[1] = vlf;
-            a.losses[2] = plf + vlf;
-        }
-    }
-    constexpr int UG = 8;
-    for (int o = tid; o < HB_PF; o += 256) {
-        float s = 0.f;
-        for (int g0 = 0; g0 < nwg; g0 += UG) {
-            float v[UG];
-#pragma unroll
-            for (int u = 0; u < UG; ++u) v[u] = g0 + u < nwg ? a.pf[(size_t)(g0 + u) * HB_PF + o] : 0.f;
-#pragma unroll
-            for (int u = 0; u < UG; ++u)
-                if (g0 + u < nwg) s += v[u];
-        }
-        if (o < ACTIONS) a.g_pfb[o] = s;
-        else if (o < ACTIONS + VHID) a.g_v1b[o - ACTIONS] = s;
-        else if (o < ACTIONS + 2 * VHID) a.g_v2w[o - ACTIONS - VHID] = s;
-        else a.g_v2b[0] = s;
-    }
-    HBT_END("board");
 }
 
 // = head_bn_bwd_apply_kernel (dzh on the fly) + heads_bwd_proj_kernel, and the last
@@ -664,16 +209,13 @@ __global__ __launch_bounds__(256) void heads_bwd_fused_kernel(const HeadBwdArgs 
     const f32x4 w0 = *(const f32x4*)(a.wpc + c), w1 = *(const f32x4*)(a.wpc + C + c), w2 = *(const f32x4*)(a.wvc + c);
     f32x4 mu2 = {0.f, 0.f, 0.f, 0.f};
     if (BNX) mu2 = *(const f32x4*)(a.mean2 + c);
-    // head-BN backward coefficients: from head_bn_bwd_fin_kernel (a.dg_nwg == 0) or
-    // finalized here by every workgroup from head_dgrad_kernel's partials (workgroup 0
-    // publishes the BN grads): the same wave reduction, bitwise equal
+    // head-BN backward coefficients, finalized here by every workgroup from
+    // head_dgrad_kernel's partials (one wave, fixed order; workgroup 0 publishes dgamma /
+    // dbeta): the same values in every workgroup, bitwise
     __shared__ float shk[9];
-    const float* hbp = a.hb;
-    if (a.dg_nwg) {
-        if (threadIdx.x < 64) head_bwd_fin_wave(a.dg, a.dg_nwg, shk, blockIdx.x == 0);
-        __syncthreads();
-        hbp = shk;
-    }
+    if (threadIdx.x < 64) head_bwd_fin_wave(a.dg, a.dg_nwg, shk, blockIdx.x == 0);
+    __syncthreads();
+    const float* hbp = shk;
     float hm[3], hk[3][3];
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
@@ -739,37 +281,23 @@ __global__ __launch_bounds__(256) void heads_bwd_fused_kernel(const HeadBwdArgs 
     }
 }
 
-// ---- key 28 bits 3 / 4: short, wide launches for the latency-bound head chain -----
-
-__global__ __launch_bounds__(256) void head_proj_fin_kernel(const HeadStatsArgs a, int nwg)
-{
-    __shared__ double red[4][6];
-    head_stats_fin(a, nwg, red);
-}
-
-// = head_bn_apply_kernel, also writing the features in the eval forward's padded row
+// head BN + ReLU (fp, fv), also writing the features in the eval forward's padded row
 // layout feat[b][FC_FS] (policy 450 -> FC_KP, value 225 at FC_KP; the zero pads are set
 // at allocation) so the fc forward runs on heads_fc's 16-B operand loads
-// FIN (key 28 bit 4): the head BN statistics are finalized by every workgroup from
-// head_proj_stats_kernel's nwg partials (the same fixed-order reduction as
-// head_proj_fin_kernel, which this replaces: bitwise equal coefficients); workgroup 0
-// publishes them with the running stats
-template <bool FIN>
+// The head BN statistics are finalized by every workgroup from head_proj_stats_kernel's
+// nwg partials (one fixed-order reduction: the same coefficients in every workgroup);
+// workgroup 0 publishes them with the running stats
 __global__ __launch_bounds__(256) void head_bn_apply_feat_kernel(const float* __restrict__ zh,
-                                                                 const float* __restrict__ hscale,
-                                                                 const float* __restrict__ hshift,
                                                                  float* __restrict__ fp, float* __restrict__ fv,
                                                                  float* __restrict__ feat, int B,
                                                                  const HeadStatsArgs fa, int nwg)
 {
     __shared__ double red[4][6];
     __shared__ float coef[6];
-    if (FIN) {
-        head_stats_fin(fa, nwg, red, coef, blockIdx.x == 0);
-        __syncthreads();
-        hscale = coef;
-        hshift = coef + 3;
-    }
+    head_stats_fin(fa, nwg, red, coef, blockIdx.x == 0);
+    __syncthreads();
+    const float* hscale = coef;
+    const float* hshift = coef + 3;
     const int total = B * 3 * PIX;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
         const int b = i / (3 * PIX), k = i - b * 3 * PIX;
@@ -879,10 +407,9 @@ __global__ __launch_bounds__(256) void head_dgrad_kernel(const HeadDgradArgs a)
     if (lane < 6) a.part[(size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 6 + lane] = hs[lane];
 }
 
-// = head_bn_bwd_finalize_kernel over head_dgrad_kernel's per-workgroup partials (one
-// wave: lane g sums workgroups g, g + 64, ..., then a fixed xor tree)
-// one wave: lane g sums workgroups g, g + 64, ..., then a fixed xor tree; hk (optional):
-// the [3][3] coefficients for the caller's own use; write: publish grads and hb
+// head-BN backward finalize over head_dgrad_kernel's per-workgroup partials, one
+// wave: lane g sums workgroups g, g + 64, ..., then a fixed xor tree; hk (optional):
+// the [3][3] coefficients (S dy / N, k, invstd * gamma) for the caller's own use; write: publish dgamma / dbeta
 __device__ __forceinline__ void head_bwd_fin_wave(const HeadDgradArgs& a, int nwg, float* hk, bool write)
 {
     const int lane = threadIdx.x & 63;
@@ -909,16 +436,8 @@ __device__ __forceinline__ void head_bwd_fin_wave(const HeadDgradArgs& a, int nw
         if (write) {
             a.grads[d.gamma_off + c] = (float)(qd * invd);
             a.grads[d.beta_off + c] = (float)sd;
-            a.hb[ch * 3 + 0] = k0;
-            a.hb[ch * 3 + 1] = k1;
-            a.hb[ch * 3 + 2] = k2;
         }
     }
-}
-
-__global__ __launch_bounds__(64) void head_bn_bwd_fin_kernel(const HeadDgradArgs a, int nwg)
-{
-    head_bwd_fin_wave(a, nwg, nullptr, true);
 }
 
 // fc weight gradients dWpf[j][k] = S_b dlogits[b][j] fp[b][k] (225 x 450) and dWv1[u][k]
@@ -993,51 +512,26 @@ hipError_t launch_head_fc_wgrad(const float* dlogits, const float* fp, const flo
 
 int head_dgrad_groups(int B) { return ((B + 31) / 32) * (HD_PT + HD_VT); }
 
-hipError_t launch_head_proj_split(int C, bool apply, const HeadStatsArgs& a, hipStream_t st)
-{
-    const int nwg = head_proj_stats_groups(a.M);
-#define AZG_HPP(CC)                                                                                          \
-    case CC:                                                                                                 \
-        if (apply) hipLaunchKernelGGL((head_proj_stats_kernel<CC, true, false>), dim3(nwg), dim3(256), 0, st, a); \
-        else hipLaunchKernelGGL((head_proj_stats_kernel<CC, false, false>), dim3(nwg), dim3(256), 0, st, a);      \
-        break;
-    switch (C) {
-        AZG_HPP(64)
-        AZG_HPP(128)
-        AZG_HPP(256)
-        default: return hipErrorInvalidValue;
-    }
-#undef AZG_HPP
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(head_proj_fin_kernel, dim3(1), dim3(256), 0, st, a, nwg);
-    return hipGetLastError();
-}
-
-hipError_t launch_head_bn_apply_feat(const float* zh, const float* hscale, const float* hshift, float* fp, float* fv,
-                                     float* feat, int B, hipStream_t st, const HeadStatsArgs* fin)
+hipError_t launch_head_bn_apply_feat(float* fp, float* fv, float* feat, int B, const HeadStatsArgs& fin,
+                                     hipStream_t st)
 {
     const int total = B * 3 * PIX;
     int nb = (total + 255) / 256;
     nb = nb > 8192 ? 8192 : nb;
-    if (fin)
-        hipLaunchKernelGGL(head_bn_apply_feat_kernel<true>, dim3(nb), dim3(256), 0, st, zh, hscale, hshift, fp, fv,
-                           feat, B, *fin, head_proj_stats_groups(fin->M));
-    else
-        hipLaunchKernelGGL(head_bn_apply_feat_kernel<false>, dim3(nb), dim3(256), 0, st, zh, hscale, hshift, fp, fv,
-                           feat, B, HeadStatsArgs{}, 0);
+    hipLaunchKernelGGL(head_bn_apply_feat_kernel, dim3(nb), dim3(256), 0, st, fin.zh, fp, fv, feat, B, fin,
+                       head_proj_stats_groups(fin.M));
     return hipGetLastError();
 }
 
-// the projections + statistics partials alone (key 28 bit 4 with the finalize folded
-// into the feature kernel)
+// the projections + statistics partials (finalized by every workgroup of
+// head_bn_apply_feat_kernel)
 hipError_t launch_head_proj_partials(int C, bool apply, const HeadStatsArgs& a, hipStream_t st)
 {
     const int nwg = head_proj_stats_groups(a.M);
 #define AZG_HPQ(CC)                                                                                          \
     case CC:                                                                                                 \
-        if (apply) hipLaunchKernelGGL((head_proj_stats_kernel<CC, true, false>), dim3(nwg), dim3(256), 0, st, a); \
-        else hipLaunchKernelGGL((head_proj_stats_kernel<CC, false, false>), dim3(nwg), dim3(256), 0, st, a);      \
+        if (apply) hipLaunchKernelGGL((head_proj_stats_kernel<CC, true>), dim3(nwg), dim3(256), 0, st, a);  \
+        else hipLaunchKernelGGL((head_proj_stats_kernel<CC, false>), dim3(nwg), dim3(256), 0, st, a);       \
         break;
     switch (C) {
         AZG_HPQ(64)
@@ -1049,42 +543,13 @@ hipError_t launch_head_proj_partials(int C, bool apply, const HeadStatsArgs& a, 
     return hipGetLastError();
 }
 
-hipError_t launch_head_dgrad(const HeadDgradArgs& a, hipStream_t st, bool fin)
+hipError_t launch_head_dgrad(const HeadDgradArgs& a, hipStream_t st)
 {
     hipLaunchKernelGGL(head_dgrad_kernel, dim3((a.B + 31) / 32, HD_PT + HD_VT), dim3(256), 0, st, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || !fin) return e;
-    hipLaunchKernelGGL(head_bn_bwd_fin_kernel, dim3(1), dim3(64), 0, st, a, head_dgrad_groups(a.B));
     return hipGetLastError();
-}
-
-hipError_t launch_head_proj_stats(int C, bool apply, const HeadStatsArgs& a, hipStream_t st)
-{
-    dim3 grid((a.M + HP_ROWS - 1) / HP_ROWS);
-#define AZG_HPS(CC)                                                                                     \
-    case CC:                                                                                            \
-        if (apply) hipLaunchKernelGGL((head_proj_stats_kernel<CC, true>), grid, dim3(256), 0, st, a);  \
-        else hipLaunchKernelGGL((head_proj_stats_kernel<CC, false>), grid, dim3(256), 0, st, a);       \
-        return hipGetLastError();
-    switch (C) {
-        AZG_HPS(64)
-        AZG_HPS(128)
-        AZG_HPS(256)
-        default: return hipErrorInvalidValue;
-    }
-#undef AZG_HPS
 }
 
 int head_proj_stats_groups(int M) { return (M + HP_ROWS - 1) / HP_ROWS; }
-int head_board_groups(int B) { return (B + HB_BOARDS - 1) / HB_BOARDS; }
-int head_board_pd() { return HB_PD; }
-int head_board_pf() { return HB_PF; }
-
-hipError_t launch_head_board(const HeadBoardArgs& a, hipStream_t st)
-{
-    hipLaunchKernelGGL(head_board_kernel, dim3(head_board_groups(a.B)), dim3(256), 0, st, a);
-    return hipGetLastError();
-}
 
 hipError_t launch_heads_bwd_fused(int C, bool bnx, const HeadBwdArgs& a, hipStream_t st)
 {

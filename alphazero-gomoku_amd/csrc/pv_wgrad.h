@@ -1,0 +1,206 @@
+// Weight-gradient tile of the 3x3 convolution and its slab reduction, shared by the
+// stand-alone launches (pv_wgrad.hip) and the persistent train backward
+// (pv_bwd_tower.hip), so both compute the same K order bit for bit.
+//   dW[co][ci][tap] = sum_m dz[m][co] * X[m + off(tap)][ci]   (autograd of network.py:12,14)
+#pragma once
+#include "pv_common.h"
+
+namespace azg {
+
+// Split s covers the whole 32-pixel chunks [s*NCH/S, (s+1)*NCH/S) of the batch
+// (NCH = ceil(M/32)).  Rows past M load zeros.
+__device__ __forceinline__ void wgrad_split_rows(int split, int S, int M, int& mbeg, int& mend)
+{
+    const int nch = (M + 31) / 32;
+    mbeg = (int)((int64_t)split * nch / S) * 32;
+    mend = min(M, (int)((int64_t)(split + 1) * nch / S) * 32);
+}
+
+// Geometry of the LDS-DMA weight-grad tile: BT x BT outputs (co x ci) of one tap, K =
+// the pixels of one split in chunks of 32.  NWV = 4: 2 x 2 waves of (BT/2)^2; NWV = 8
+// (BT = 128): 2 x 4 waves of 64 co x 32 ci.  Both give every output the same chain.
+template <int C>
+struct WgNat {
+    static constexpr int BT = C < 128 ? C : 128;
+    static constexpr int NT = C / BT;               // tiles per edge
+    static constexpr int TILES = 9 * NT * NT;       // tiles per pixel split
+    static constexpr int LDS_BYTES = 2 * 2 * 32 * BT * 4;
+    static constexpr int NWV = BT >= 128 ? 8 : 4;   // waves of an 8-wave workgroup that work
+};
+
+// One weight-grad tile (split, tap, co0, ci0) with NATURAL operand rows in LDS filled
+// by LDS-DMA: each wave-instruction global_load_lds_dwordx4 moves 1 KiB = 256/BT pixel
+// rows of BT channels straight into LDS (no staging VGPRs, no ds_write), issued one chunk
+// ahead.  MFMA step s reads, per operand, one ds_read_b32 per lane: lanes 0-31 pixel s,
+// lanes 32-63 pixel s + 16, 32 consecutive channels.  16-B chunk j of LDS row p holds
+// global chunk j ^ 8*((p >> 4) & 1) (swizzle on each lane's source address,
+// cdna_hip_programming.md §5.4): the two half-waves of a fragment read land on disjoint
+// bank halves.  Rows past the split read padded pixel 0 (the zero halo).
+// Waves wid >= NWV of a larger workgroup only join the barriers.  The caller guarantees
+// every wave is past its last read of `smem` (barrier) before the call; the call ends
+// with the slab stores issued (not drained).
+template <int C, bool WT, int NWV>
+__device__ __forceinline__ void wgrad_nat_tile(const float* __restrict__ dz, const float* __restrict__ x,
+                                               float* __restrict__ slab, int M, int S, int split, int tap,
+                                               int co0, int ci0, float* smem)
+{
+    constexpr int BT = C < 128 ? C : 128, BK = 32;
+    constexpr int WNW = NWV == 8 ? 4 : 2;           // waves along ci
+    constexpr int TA = BT / 64, TB = BT / (32 * WNW); // accumulators along co / ci per wave
+    constexpr int RPI = 256 / BT;      // pixel rows per wave-instruction (1 KiB)
+    constexpr int CPR = BT / 4;        // 16-B chunks per row
+    constexpr int IPW = BK / RPI / NWV;  // instructions per wave per operand per chunk
+    static_assert(IPW >= 1 && CPR >= 16 && TB >= 1, "tile");
+    float* As = smem;                  // [2][BK][BT]  dz rows (co)
+    float* Bs = smem + 2 * BK * BT;    // [2][BK][BT]  x rows (ci, tap-shifted)
+
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const bool active = wid < NWV;
+    const int wm = wid / WNW, wn = wid % WNW;
+    const int ky = tap / 3, kx = tap - ky * 3;
+    const int toff = ((ky - 1) * PADW + (kx - 1)) * C;
+    int mbeg, mend;
+    wgrad_split_rows(split, S, M, mbeg, mend);
+    const int nch = (mend - mbeg + BK - 1) / BK;
+
+    auto glds = [](const float* src, float* dst) {
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    };
+    const int ri = lane / CPR, jl = lane % CPR;
+    auto issue = [&](int kc, int buf) {
+        if (!active) return;
+#pragma unroll
+        for (int i = 0; i < IPW; ++i) {
+            const int r0 = (wid * IPW + i) * RPI;       // first LDS row of this instruction
+            const int p = r0 + ri;
+            const int m = mbeg + kc * BK + p;
+            const int j = jl ^ (((p >> 4) & 1) << 3);
+            const int po = m < mend ? pad_off(m, C) : 0;
+            const int px = m < mend ? po + toff : 0;
+            glds(dz + po + co0 + 4 * j, As + buf * BK * BT + r0 * BT);
+            glds(x + px + ci0 + 4 * j, Bs + buf * BK * BT + r0 * BT);
+        }
+    };
+    const int r32 = lane & 31, h = lane >> 5;
+    int aoff[TA], boff[TB];
+#pragma unroll
+    for (int i = 0; i < TA; ++i) {
+        const int ca = wm * (BT / 2) + i * 32 + r32;
+        aoff[i] = 16 * h * BT + (((ca >> 2) ^ (h << 3)) << 2) + (ca & 3);
+    }
+#pragma unroll
+    for (int j = 0; j < TB; ++j) {
+        const int cb = wn * (BT / WNW) + j * 32 + r32;
+        boff[j] = 16 * h * BT + (((cb >> 2) ^ (h << 3)) << 2) + (cb & 3);
+    }
+
+    f32x16 acc[TA][TB];
+#pragma unroll
+    for (int i = 0; i < TA; ++i)
+#pragma unroll
+        for (int j = 0; j < TB; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    if (nch > 0) issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kc = 0; kc < nch; ++kc) {
+        const int cur = kc & 1;
+        // the other buffer's last reads ended at the previous chunk's barrier
+        if (kc + 1 < nch) issue(kc + 1, cur ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (active) {
+            const float* Ab = As + cur * BK * BT;
+            const float* Bb = Bs + cur * BK * BT;
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                float a[TA], b[TB];
+#pragma unroll
+                for (int i = 0; i < TA; ++i) a[i] = Ab[s * BT + aoff[i]];
+#pragma unroll
+                for (int j = 0; j < TB; ++j) b[j] = Bb[s * BT + boff[j]];
+#pragma unroll
+                for (int i = 0; i < TA; ++i)
+#pragma unroll
+                    for (int j = 0; j < TB; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of chunk kc+1 retired
+        __syncthreads();
+    }
+
+    if (active) {
+        float* out = slab + ((size_t)split * 9 + tap) * C * C;
+        const __amdgpu_buffer_rsrc_t rs = wt_rsrc(out, (size_t)C * C * sizeof(float));
+#pragma unroll
+        for (int i = 0; i < TA; ++i)
+#pragma unroll
+            for (int j = 0; j < TB; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int co = co0 + wm * (BT / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const int ci = ci0 + wn * (BT / WNW) + j * 32 + r32;
+                    store1<WT>(out, rs, co * C + ci, acc[i][j][r]);
+                }
+    }
+}
+
+// dW (torch layout [co][ci][3][3]) element idx of the slab layout [tap][co][ci] = the S
+// slabs summed in a fixed order: four interleaved partial sums (slabs k = 0,1,2,3 mod 4)
+// combined as ((p0 + p1) + (p2 + p3)).  NV consecutive-by-`stride` elements per call,
+// every slab's loads of them issued together (the per-element order is unchanged).
+template <int NV>
+__device__ __forceinline__ void wgrad_reduce_elems(const float* __restrict__ slab, float* __restrict__ dw, int C,
+                                                   int S, int idx0, int stride)
+{
+    const int total = 9 * C * C;
+    float p0[NV], p1[NV], p2[NV], p3[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) p0[v] = p1[v] = p2[v] = p3[v] = 0.f;
+    int k = 0;
+    for (; k + 4 <= S; k += 4) {
+        float a[NV], b[NV], c[NV], d[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const int idx = min(idx0 + v * stride, total - 1);
+            a[v] = slab[(size_t)k * total + idx];
+            b[v] = slab[(size_t)(k + 1) * total + idx];
+            c[v] = slab[(size_t)(k + 2) * total + idx];
+            d[v] = slab[(size_t)(k + 3) * total + idx];
+        }
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            p0[v] += a[v];
+            p1[v] += b[v];
+            p2[v] += c[v];
+            p3[v] += d[v];
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int idx = idx0 + v * stride;
+        if (idx >= total) continue;
+        if (k < S) p0[v] += slab[(size_t)k * total + idx];
+        if (k + 1 < S) p1[v] += slab[(size_t)(k + 1) * total + idx];
+        if (k + 2 < S) p2[v] += slab[(size_t)(k + 2) * total + idx];
+        const int tap = idx / (C * C);
+        const int rem = idx - tap * C * C;
+        const int co = rem / C, ci = rem - co * C;
+        dw[(co * C + ci) * 9 + tap] = (p0[v] + p1[v]) + (p2[v] + p3[v]);
+    }
+}
+
+// BatchNorm backward apply of one element (bn_bwd_apply_kernel, network.py:12-25
+// autograd): dy = g * (act > 0); dz = ((dy - gm) - (z - mean) * k) * iw.
+__device__ __forceinline__ float bnbwd_elem(float g, float av, float z, float mu, float gm, float k, float iw,
+                                            float& dy)
+{
+    dy = av > 0.f ? g : 0.f;
+    return ((dy - gm) - (z - mu) * k) * iw;
+}
+
+}  // namespace azg

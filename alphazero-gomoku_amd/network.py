@@ -328,6 +328,9 @@ class PyTorchModel:
         if return_tensor:
             return mean
         vals = (mean.double() if epochs == 1 else acc / float(epochs)).tolist()
+        # the persistent train backward shares the tower's sticky status word (a timed-out
+        # dependency wait): raise after the host sync above
+        eng.check_status()
         return {"policy_loss": vals[0], "value_loss": vals[1], "total_loss": vals[2]}
 
     train_step = train_batch

@@ -166,22 +166,6 @@ def test_gradients_match_oracle(tag, blocks, ch, B):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("fuse", [0, 1, 2, 4, 7, 8, 12, 16, 20, 28])
-@pytest.mark.parametrize("tag,blocks,ch,B", [("3x64", 3, 64, 37), ("6x128", 6, 128, 128)])
-def test_head_chain_variants_match_oracle(fuse, tag, blocks, ch, B):
-    """Every fused head stage (key 28 bits: projections + statistics, per-board FCs +
-    loss, head BN-backward + 1x1 backward) and the 18-launch chain hold the oracle
-    tolerance of test_gradients_match_oracle, at a ragged batch (37: a partial 4-board
-    group) and at the bench's train shape."""
-    import _native
-    lib = _native.load_library()
-    prev = lib.azg_pv_set_tuning(28, fuse)
-    try:
-        test_gradients_match_oracle(tag, blocks, ch, B)
-    finally:
-        lib.azg_pv_set_tuning(28, prev)
-
-
 def fp32_masks(st, blocks, ch, x):
     """The fp32 CPU oracle's own ReLU masks (train-mode forward), NCHW / [B, n]."""
     net = RefModel(blocks, ch).net
@@ -338,59 +322,99 @@ def test_train_then_predict_uses_new_weights():
     np.testing.assert_allclose(v1, rv, atol=1e-5)
 
 
-@pytest.mark.parametrize("key,values", [(18, (0, 1, 2, 4, 7)), (12, (0, 1)), (16, (3, 0, 1, 2, 4)), (23, (1, 0)), (24, (1, 0)),
-                                        (25, (32, 0)), (26, (8, 16)), (29, (1, 0)), (30, (1, 0)), (32, (1, 0, 2)), (33, (1, 0)), (34, (1, 0)), (36, (1, 0)), (37, (0, 1)), (39, (1, 0, 2)), (40, (1, 0, 2)), (42, (1, 0))])
+def train_state_after(x, pi, z, blocks, ch, steps=2, seed=3):
+    """params, BN buffers, grads and Adam moments after `steps` train steps."""
+    m = make_model(blocks, ch, seed=seed)
+    for _ in range(steps):
+        m.train_batch(x, pi, z)
+    got = [t.detach().cpu().clone() for t in m.net.state_dict().values()]
+    got += [m.engine.flat_grads.cpu().clone(), m.optimizer.flat_exp_avg.cpu().clone(),
+            m.optimizer.flat_exp_avg_sq.cpu().clone()]
+    return got
+
+
+@pytest.mark.parametrize("key,values", [(43, (1, 0)), (23, (1, 0)), (24, (1, 0))])
 def test_train_schedule_keys_bitwise(key, values):
-    """Train-step tuning keys change cache policy (18: write-through stores), stream
-    schedule (12: weight grads overlapped or serial) or the weight-grad staging (16: LDS-DMA
-    natural rows, register K-contiguous, two chunks ahead, row staging) or where the forward
-    BN applies run (23: folded into the next conv's halo staging, or separate passes) and
-    the BN finalizes (24: by the producing conv's last workgroup, or separate kernels)
-    or the train convs' operand addressing (25: buffer resources or 64-bit pointers) or
-    tile (26: 128x64 with 8 waves, or 128x128 with 16 waves at one workgroup per CU) or
-    the BN-backward apply's ReLU mask (29: formed from z with the layer's scale / shift,
-    or read from the stored activation) or the step's weight repack (30: split across
-    the two streams, or one launch):
-    two steps from one state must give bitwise-identical params, grads, BN buffers
-    and Adam moments under every value."""
+    """The train step's product tuning keys change only the schedule: the tower
+    backward as one persistent launch or the two-stream schedule (43), where the forward
+    BN applies run (23: folded into the next conv's halo staging, or separate passes)
+    and the BN finalizes (24: by the producing conv's last workgroup, or separate
+    kernels; 0 also selects the two-stream backward): two steps from one state must
+    give bitwise-identical params, grads, BN buffers and Adam moments under every value."""
     import _native
     lib = _native.load_library()
     b, p = synth_positions(128, seed=91)
     x = encode_batch(b, p)
     pi, z = synth_targets(128, seed=92)
     prev = lib.azg_pv_set_tuning(key, values[0])
-    # the weight-grad kernels (16) and slab store policies (18) share one reduction only
-    # without the in-kernel split-group combine (41: LDS-DMA kernel, write-through slabs)
-    prev41 = lib.azg_pv_set_tuning(41, 0) if key in (16, 18) else None
     ref = None
     try:
         for v in values:
             lib.azg_pv_set_tuning(key, v)
-            m = make_model(2, 128, seed=3)
-            for _ in range(2):
-                m.train_batch(x, pi, z)
-            got = [t.detach().cpu().clone() for t in m.net.state_dict().values()]
-            got += [m.engine.flat_grads.cpu().clone(), m.optimizer.flat_exp_avg.cpu().clone(),
-                    m.optimizer.flat_exp_avg_sq.cpu().clone()]
+            got = train_state_after(x, pi, z, 2, 128)
             if ref is None:
                 ref = got
             else:
                 assert all(torch.equal(a, c) for a, c in zip(ref, got)), (key, v)
     finally:
         lib.azg_pv_set_tuning(key, prev)
-        if prev41 is not None:
-            lib.azg_pv_set_tuning(41, prev41)
 
 
+@pytest.mark.parametrize("blocks,ch,B", [(6, 128, 128), (3, 64, 37), (2, 256, 16), (1, 128, 2), (4, 128, 300)])
+def test_bwd_tower_bitwise_vs_two_stream(blocks, ch, B):
+    """The persistent train backward (pv_bwd_tower.hip, key 43 = 1) is bitwise equal to
+    the two-stream schedule of stand-alone kernels (key 43 = 0) over three steps: the
+    configs[3] shape, a ragged batch (37: a partial 128-row tile), C = 256 (four dgrad N
+    tiles, 36 weight-grad tiles per split), one block at the smallest batch, and a batch
+    above the workspace's first capacity (300: re-allocation, new descriptors)."""
+    import _native
+    lib = _native.load_library()
+    b, p = synth_positions(B, seed=93 + B)
+    x = encode_batch(b, p)
+    pi, z = synth_targets(B, seed=94 + B)
+    prev = lib.azg_pv_set_tuning(43, 1)
+    try:
+        got = train_state_after(x, pi, z, blocks, ch, steps=3)
+        lib.azg_pv_set_tuning(43, 0)
+        ref = train_state_after(x, pi, z, blocks, ch, steps=3)
+    finally:
+        lib.azg_pv_set_tuning(43, prev)
+    bad = [i for i, (a, c) in enumerate(zip(ref, got)) if not torch.equal(a, c)]
+    assert not bad, bad
 
-@pytest.mark.parametrize("key,value", [(27, 16), (38, 0), (41, 1)])
+
+def test_bwd_tower_timeout_raises_and_drains():
+    """A dependency wait of the persistent train backward that times out (tuning key 14
+    = 0 makes every poll time out) sets the sticky status: train_batch raises, the
+    launch still drains (the next steps run), and after clear_status a fresh model
+    trains to the same state as without the fault."""
+    import _native
+    lib = _native.load_library()
+    b, p = synth_positions(64, seed=95)
+    x = encode_batch(b, p)
+    pi, z = synth_targets(64, seed=96)
+    ref = train_state_after(x, pi, z, 2, 64, steps=1)
+    m = make_model(2, 64, seed=3)
+    try:
+        lib.azg_pv_set_tuning(14, 0)
+        with pytest.raises(RuntimeError, match="timed out"):
+            m.train_batch(x, pi, z)
+        lib.azg_pv_set_tuning(14, -1)
+        with pytest.raises(RuntimeError, match="timed out"):   # sticky
+            m.train_batch(x, pi, z)
+    finally:
+        lib.azg_pv_set_tuning(14, -1)
+        m.engine.clear_status()
+    got = train_state_after(x, pi, z, 2, 64, steps=1)
+    assert all(torch.equal(a, c) for a, c in zip(ref, got))
+
+
+@pytest.mark.parametrize("key,value", [(27, 16), (27, 64)])
 @pytest.mark.parametrize("tag,blocks,ch,B", [("6x128", 6, 128, 128), ("3x64", 3, 64, 37)])
 def test_train_sum_order_variants_match_oracle(key, value, tag, blocks, ch, B):
-    """Train keys that change an fp32 summation order hold the oracle tolerance of
-    test_gradients_match_oracle (no bitwise test): the weight-grad split count (27) and
-    the stem's BN statistics (38 = 0: a separate col_stats pass over 64-row tiles
-    instead of the stem epilogue's 128-row tiles) and the weight-grad slab reduction
-    (41 = 1: the in-kernel split-group combine instead of all S slabs in wgrad_reduce)."""
+    """The weight-grad split count (key 27) changes an fp32 summation order: it holds
+    the oracle tolerance of test_gradients_match_oracle (no bitwise test); 64 splits also
+    exercise the persistent backward's largest slab."""
     import _native
     lib = _native.load_library()
     prev = lib.azg_pv_set_tuning(key, value)
