@@ -48,7 +48,10 @@ inline unsigned* bwd_fin_word(unsigned* sync, int p) { return sync + kBwdSyncHea
 
 // desc: device array of nconv BwdConv; sync: bwd_sync_words(nconv) words, zero at the
 // first launch (every launch leaves them zero)
+// trace (timing studies, AZG_BWD_TRACE): bwd_tower_items() x 5 u64 {claim, workgroup,
+// start, dependencies met, end} (wall_clock64, 100 MHz), or null
+int bwd_tower_items(int C, int nconv, int M, int S);
 hipError_t launch_bwd_tower(int C, const BwdConv* desc, int nconv, int M, int S, unsigned* sync, unsigned* status,
-                            hipStream_t st);
+                            hipStream_t st, unsigned long long* trace = nullptr);
 
 }  // namespace azg

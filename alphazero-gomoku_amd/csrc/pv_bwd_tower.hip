@@ -63,6 +63,7 @@ struct BwdArgs {
     unsigned* sync;
     unsigned* status;
     unsigned spin_limit;
+    unsigned long long* trace;   // timing studies (AZG_BWD_TRACE): per item {claim, slot, t0, t1, t2}, or null
 };
 
 // poll *c >= target (one lane); false on timeout (error word + sticky status set)
@@ -175,6 +176,8 @@ __global__ __launch_bounds__(kBwdThreads) __attribute__((amdgpu_waves_per_eu(4))
             kind = 3, idx = off - G0, rq = p - 1;
         }
         __syncthreads();   // every wave has read s_claim and is done with the previous item's LDS
+        unsigned long long t0 = 0, t1 = 0;
+        if (a.trace && tid == 0) t0 = wall_clock64();
         if (tid == 0) {
             // the next claim now: its latency overlaps this item
             s_claim[0] = (int)__hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -194,6 +197,7 @@ __global__ __launch_bounds__(kBwdThreads) __attribute__((amdgpu_waves_per_eu(4))
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
+            if (a.trace) t1 = wall_clock64();
         }
         __syncthreads();
         if (kind == 0) {
@@ -221,6 +225,14 @@ __global__ __launch_bounds__(kBwdThreads) __attribute__((amdgpu_waves_per_eu(4))
             const BwdConv& cv = a.conv[rq];
             wgrad_reduce_elems<kBwdRed / kBwdThreads>(cv.slab, cv.dw, C, a.S, idx * kBwdRed + tid, kBwdThreads);
             bwd_publish(cnt + 4 * rq + 2);
+        }
+        if (a.trace && tid == 0) {
+            unsigned long long* tr = a.trace + (size_t)w * 5;
+            tr[0] = (unsigned long long)w;
+            tr[1] = blockIdx.x;
+            tr[2] = t0;
+            tr[3] = t1;
+            tr[4] = wall_clock64();
         }
         w = __builtin_amdgcn_readfirstlane(s_claim[0]);
     }
@@ -254,11 +266,18 @@ static hipError_t launch_bwd_tower_t(const BwdArgs& a, hipStream_t st)
     return hipGetLastError();
 }
 
+int bwd_tower_items(int C, int nconv, int M, int S)
+{
+    const int ntt = (M + TRAIN_BM - 1) / TRAIN_BM, nt = C < 128 ? 1 : C / 128;
+    const int G0 = ntt + ntt * (C / 64) + 9 * nt * nt * S, nR = (9 * C * C + kBwdRed - 1) / kBwdRed;
+    return G0 + (nconv - 1) * (G0 + nR) + nR;
+}
+
 hipError_t launch_bwd_tower(int C, const BwdConv* desc, int nconv, int M, int S, unsigned* sync, unsigned* status,
-                            hipStream_t st)
+                            hipStream_t st, unsigned long long* trace)
 {
     if (nconv < 1 || S < 1 || M < 1) return hipErrorInvalidValue;
-    BwdArgs a{desc, nconv, M, S, sync, status, g_tower_spin_limit};
+    BwdArgs a{desc, nconv, M, S, sync, status, g_tower_spin_limit, trace};
     switch (C) {
         case 64: return launch_bwd_tower_t<64>(a, st);
         case 128: return launch_bwd_tower_t<128>(a, st);

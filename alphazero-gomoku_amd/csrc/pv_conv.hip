@@ -1003,9 +1003,16 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         azg::g_conv_tail_split = value ? 1 : 0;
         return prev;
     }
-    if (key == 43) {  // train: tower backward as one persistent launch (1, default) or the two-stream schedule (0); bitwise identical
+    if (key == 43) {  // study build: tower backward as one persistent launch (1; slower, measured) or the two-stream schedule (0, product); bitwise identical
         const int prev = azg::g_train_bwd_tower;
+#ifdef AZG_AB_STUDIES
         if (value == 0 || value == 1) azg::g_train_bwd_tower = value;
+#endif
+        return prev;
+    }
+    if (key == 44) {  // train: workgroup cap of the BN apply / BN-backward apply passes (0 = one float4 per thread); bitwise identical
+        const int prev = azg::g_train_apply_grid;
+        if (value >= 0) azg::g_train_apply_grid = value;
         return prev;
     }
     if (key == 24) {  // train: BN finalize fused into the producing conv's last workgroup (1, default) or separate (0; two-stream backward); bitwise identical

@@ -47,6 +47,7 @@ extern int g_tower_var;
 extern int g_train_fuse_apply;
 extern int g_train_fuse_fin;
 extern int g_train_bwd_tower;
+extern int g_train_apply_grid;
 extern int g_wgrad_splits;
 hipError_t launch_stem_stats(int C, const float* x, const float* ws, float* out, int B, float* pa, float* pb,
                              hipStream_t st);

@@ -18,18 +18,21 @@
 // Schedule of one step (train_backward_t): stem (+ BN statistics from its accumulators)
 // -> 12 x conv3x3_train (each applies the previous BN + ReLU (+ residual) in its halo
 // staging and finalizes its own BN in its last workgroup) -> the head chain
-// (pv_train_heads.hip) -> the tower backward as ONE persistent launch (pv_bwd_tower.hip,
-// tuning key 43 = 1; key 43 = 0 keeps the round-3 two-stream schedule as the bitwise
-// reference) -> head weight grads, stem backward; train_apply: clip + Adam + the next
-// step's weight packs.
+// (pv_train_heads.hip) -> the tower backward on two streams (dgrads on the caller's,
+// weight grads on a low-priority side stream) -> head weight grads, stem backward;
+// train_apply: clip + Adam + the next step's weight packs.  (The study build also has
+// the tower backward as ONE persistent launch, pv_bwd_tower.hip, key 43: bitwise equal,
+// measured slower.)
 #include "pv_internal.h"
 #include "pv_halo.h"
 #include "pv_train_heads.h"
 #include "pv_bwd_tower.h"
 #include "pv_wgrad.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -46,7 +49,9 @@ constexpr int HROWS = 128;   // rows per tile of the head-projection backward pa
 
 int g_train_fuse_apply = 1;   // key 23: 1 BN applies folded into the next conv's staging; 0 separate passes
 int g_train_fuse_fin = 1;     // key 24: 1 BN finalize by the last workgroup of the producing conv; 0 separate kernels
-int g_train_bwd_tower = 1;    // key 43: 1 the tower backward as one persistent launch; 0 the two-stream schedule
+int g_train_apply_grid = 0;   // key 44: workgroup cap of the BN apply / BN-backward apply passes (0: one float4 per thread)
+int g_train_bwd_tower = 0;    // key 43 (study build): 1 the tower backward as one persistent launch (slower,
+                              // measured); 0 the two-stream schedule (product)
 
 struct TrainWS {
     int cap = 0;
@@ -64,7 +69,8 @@ struct TrainWS {
     float *part_a = nullptr, *part_b = nullptr;   // [ntile][C]
     float* hpart = nullptr;                        // [ntile][3][C]
     float* spart = nullptr;                        // [B][27][C]
-    float* slab[3] = {nullptr, nullptr, nullptr};  // weight-grad split-K slabs (rotating)
+    float* slab[3] = {nullptr, nullptr, nullptr};  // weight-grad split-K slabs (two alternate; study build: three rotate)
+    int slab_S = 0;                                // splits one slab holds
     unsigned* fincnt = nullptr;   // fused BN finalize arrival counters: [0..3] forward / two-stream, 4 per conv after
     // heads
     float *zh = nullptr, *fp = nullptr, *fv = nullptr, *hv = nullptr, *dpre = nullptr;
@@ -73,6 +79,7 @@ struct TrainWS {
     double* hdp = nullptr;       // head_dgrad_kernel partials [groups][6]
     float* feat = nullptr;       // [B][FC_FS] head features, eval row layout (zero pads)
     float* pre = nullptr;        // [B][FC_OUT] fc pre-activations (logits | value hidden)
+    float* hbw = nullptr;        // [3][3] head-BN backward coefficients (batches above kHeadFoldMaxB)
     // optimizer
     double* npart = nullptr;     // grad sq-sum partials
     float* scal = nullptr;       // [0] total norm, [1] clip coef
@@ -80,6 +87,10 @@ struct TrainWS {
     unsigned* bsync = nullptr;
     BwdConv* bdesc = nullptr;
     std::vector<BwdConv> bdesc_host;   // what bdesc holds
+    // timing studies (AZG_BWD_TRACE=<file>): the last persistent launch's per-item trace,
+    // host-mapped, written to <file> with its geometry when the workspace is freed
+    unsigned long long* trace = nullptr;
+    int trace_hdr[4] = {0, 0, 0, 0};   // C, nconv, M, S of the last traced launch
     // two-stream backward (key 43 = 0): weight grads on `side`
     hipStream_t side = nullptr;
     hipEvent_t ev_ready = nullptr, ev_join = nullptr;
@@ -113,6 +124,21 @@ void free_train_workspace(azg_pv* h)
     if (w->ev_ready) (void)hipEventDestroy(w->ev_ready);
     if (w->ev_join) (void)hipEventDestroy(w->ev_join);
     if (w->side) (void)hipStreamDestroy(w->side);
+#ifdef AZG_AB_STUDIES
+    if (w->trace) {
+        (void)hipDeviceSynchronize();
+        if (const char* path = getenv("AZG_BWD_TRACE")) {
+            if (FILE* f = fopen(path, "wb")) {
+                const int* g = w->trace_hdr;
+                const size_t n = g[0] ? (size_t)bwd_tower_items(g[0], g[1], g[2], g[3]) : 0;
+                fwrite(g, sizeof(int), 4, f);
+                fwrite(w->trace, sizeof(unsigned long long), n * 5, f);
+                fclose(f);
+            }
+        }
+        (void)hipHostFree(w->trace);
+    }
+#endif
     delete w;
     h->train = nullptr;
 }
@@ -607,7 +633,14 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     A(w->part_b, (size_t)ntile * C, false);
     A(w->hpart, (size_t)((M + HROWS - 1) / HROWS) * 3 * C, false);
     A(w->spart, (size_t)cap * STEM_WG_CHUNKS * 27 * C, false);
-    for (int k = 0; k < 3; ++k) A(w->slab[k], (size_t)kMaxWgradSplits * 9 * C * C, false);
+    // slabs for the automatic split count at this capacity (or the key-27 override)
+    w->slab_S = std::max(wgrad_splits(C, M), std::min(g_wgrad_splits, kMaxWgradSplits));
+#ifdef AZG_AB_STUDIES
+    const int nslab = 3;
+#else
+    const int nslab = 2;
+#endif
+    for (int k = 0; k < nslab; ++k) A(w->slab[k], (size_t)w->slab_S * 9 * C * C, false);
     A(w->zh, (size_t)cap * 3 * PIX, false);
     A(w->fp, (size_t)cap * 2 * PIX, false);
     A(w->fv, (size_t)cap * PIX, false);
@@ -630,10 +663,18 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     w->hdp = (double*)t;
     A(w->feat, (size_t)cap * FC_FS, true);
     A(w->pre, (size_t)cap * FC_OUT, false);
+    A(w->hbw, 16, false);
+#ifdef AZG_AB_STUDIES
     A(t, bwd_sync_words(2 * NB), true);
     w->bsync = (unsigned*)t;
     A(t, (sizeof(BwdConv) * (2 * NB > 0 ? 2 * NB : 1) + 3) / 4, false);
     w->bdesc = (BwdConv*)t;
+    if (getenv("AZG_BWD_TRACE") && NB > 0) {
+        const size_t n = (size_t)bwd_tower_items(C, 2 * NB, M, kMaxWgradSplits) * 5;
+        hipError_t e = hipHostMalloc((void**)&w->trace, n * sizeof(unsigned long long), hipHostMallocMapped);
+        if (e != hipSuccess) return set_error("train workspace: trace buffer", e);
+    }
+#endif
     if (getenv("AZG_DEBUG_SNAP")) {
         w->snap.assign(NB + 1, nullptr);
         for (int i = 0; i <= NB; ++i) A(w->snap[i], act, true);
@@ -662,7 +703,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     float* G = h->grads;
     const BnDesc* bd = h->bn_desc.data();
     const BnDesc* bdd = (const BnDesc*)h->bn_desc_dev;
-    const int gM = grid_for((int64_t)M * C / 4);
+    const int gM = g_train_apply_grid > 0 ? std::min(grid_for((int64_t)M * C / 4), g_train_apply_grid)
+                                          : grid_for((int64_t)M * C / 4);
     const int ntt = (M + TRAIN_BM - 1) / TRAIN_BM;   // M tiles of conv3x3_train (partials per tile)
     const size_t CC9 = (size_t)9 * C * C;
     // the conv3x3_train launch that produces a layer's partials also finalizes it (key
@@ -879,6 +921,11 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         hd.grads = G;
         hd.hinv = w->binv + ho;
         AZG_CK(launch_head_dgrad(hd, st), "train: head_dgrad");
+        const bool fold_hb = B <= kHeadFoldMaxB;
+        if (!fold_hb) {   // one wave finalizes; heads_bwd_fused reads the coefficients
+            hd.hb = w->hbw;
+            AZG_CK(launch_head_bwd_fin(hd, st), "train: head_bwd_fin");
+        }
         HeadBwdArgs hw{};
         hw.act = X;
         hw.zh = w->zh;
@@ -897,7 +944,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         }
         hw.M = M;
         hw.dg = hd;
-        hw.dg_nwg = head_dgrad_groups(B);
+        hw.dg_nwg = fold_hb ? head_dgrad_groups(B) : 0;
         AZG_CK(launch_heads_bwd_fused(C, NB > 0, hw, st), "train: heads_bwd_fused");
         prof_end(h, pr, st);
     }
@@ -910,11 +957,12 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     bool done_fin = false;   // the stem's BN backward is finalized (by the last dgrad)
     bool side_used = false;
     if (NB > 0) R(bwd_fin(h->bn_blk[NB - 1].second, hntile));
+#ifdef AZG_AB_STUDIES
     if (NB > 0 && g_train_bwd_tower && ffin) {
         // ---- one persistent launch (pv_bwd_tower.hip) ----
         const int nconv = 2 * NB;
         const int S = wgrad_splits(C, M);
-        if (S > kMaxWgradSplits) return set_error("train: wgrad splits exceed the slab workspace", hipErrorInvalidValue);
+        if (S > w->slab_S) return set_error("train: wgrad splits exceed the slab workspace (key 27 above the allocation)", hipErrorInvalidValue);
         std::vector<BwdConv> ds(nconv);
         for (int i = NB - 1; i >= 0; --i) {
             const int p2 = 2 * (NB - 1 - i), p1 = p2 + 1;
@@ -974,16 +1022,23 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             w->bdesc_host = ds;
         }
         int pr = prof_begin(h, AZG_PROF_TRAIN_CONV, st, B);
-        AZG_CK(launch_bwd_tower(C, w->bdesc, nconv, M, S, w->bsync, h->status_dev, st), "train: bwd tower");
+        unsigned long long* tr = nullptr;
+        if (w->trace) {
+            AZG_CK(hipHostGetDevicePointer((void**)&tr, w->trace, 0), "train: trace buffer");
+            w->trace_hdr[0] = C, w->trace_hdr[1] = nconv, w->trace_hdr[2] = M, w->trace_hdr[3] = S;
+        }
+        AZG_CK(launch_bwd_tower(C, w->bdesc, nconv, M, S, w->bsync, h->status_dev, st, tr), "train: bwd tower");
         prof_end(h, pr, st);
         done_fin = true;
-    } else if (NB > 0) {
+    } else
+#endif
+    if (NB > 0) {
         // ---- the two-stream schedule (key 43 = 0): dgrads on the caller's stream, the
         // weight grads on `side` (one event hand-off per conv), each slab reduction
         // deferred behind the next conv's weight-grad kernel ----
         AZG_CK(make_side_stream(w), "train: side stream");
         const int S = wgrad_splits(C, M);
-        if (S > kMaxWgradSplits) return set_error("train: wgrad splits exceed the slab workspace", hipErrorInvalidValue);
+        if (S > w->slab_S) return set_error("train: wgrad splits exceed the slab workspace (key 27 above the allocation)", hipErrorInvalidValue);
         struct PendRed { float* slab; float* dw; } pend{nullptr, nullptr};
         int slab_i = 0;
         auto wgrad = [&](const float* dz, const float* xin, int tensor) -> int32_t {
@@ -1063,6 +1118,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
 int32_t train_backward(azg_pv* h, const float* x, const float* pis, const float* zs, int B, float* losses,
                        hipStream_t st)
 {
+    // a split-count override (key 27) above what the slabs were sized for: re-allocate
+    if (TrainWS* w0 = ws_of(h); w0 && wgrad_splits(h->C, B * PIX) > w0->slab_S) free_train_workspace(h);
     if (int32_t r = ensure_train_ws(h, B, st)) return r;
     TrainWS* w = ws_of(h);
     // the packs are refreshed right after every Adam step (train_apply); a parameter

@@ -44,6 +44,7 @@ struct HeadDgradArgs {
     const float* params;
     float* grads;
     const float* hinv;     // head BN invstd (3)
+    float* hb;             // large batches: the [3][3] coefficients, written by head_bn_bwd_fin_kernel
 };
 
 struct HeadBwdArgs {
@@ -63,10 +64,12 @@ struct HeadBwdArgs {
     float* pb;             // [tile][C]: S (z - mean) dy
     int M;
     // the head-BN backward finalize, run by every workgroup from head_dgrad_kernel's
-    // dg_nwg partials
+    // dg_nwg partials; dg_nwg = 0 (batches above kHeadFoldMaxB, where every workgroup
+    // re-reducing all partials would grow as B^2): read dg.hb, written by one wave before
     HeadDgradArgs dg;
     int dg_nwg;
 };
+constexpr int kHeadFoldMaxB = 512;
 
 int head_dgrad_groups(int B);
 int head_proj_stats_groups(int M);
@@ -74,6 +77,8 @@ hipError_t launch_head_proj_partials(int C, bool apply, const HeadStatsArgs& a, 
 hipError_t launch_head_bn_apply_feat(float* fp, float* fv, float* feat, int B, const HeadStatsArgs& fin,
                                      hipStream_t st);
 hipError_t launch_head_dgrad(const HeadDgradArgs& a, hipStream_t st);
+// one wave: the head-BN backward finalize into a.hb (B > kHeadFoldMaxB)
+hipError_t launch_head_bwd_fin(const HeadDgradArgs& a, hipStream_t st);
 hipError_t launch_head_fc_wgrad(const float* dlogits, const float* fp, const float* dhv, const float* fv, float* gpf,
                                 float* gv1, int B, hipStream_t st);
 hipError_t launch_heads_bwd_fused(int C, bool bnx, const HeadBwdArgs& a, hipStream_t st);

@@ -213,9 +213,12 @@ __global__ __launch_bounds__(256) void heads_bwd_fused_kernel(const HeadBwdArgs 
     // head_dgrad_kernel's partials (one wave, fixed order; workgroup 0 publishes dgamma /
     // dbeta): the same values in every workgroup, bitwise
     __shared__ float shk[9];
-    if (threadIdx.x < 64) head_bwd_fin_wave(a.dg, a.dg_nwg, shk, blockIdx.x == 0);
-    __syncthreads();
-    const float* hbp = shk;
+    const float* hbp = a.dg.hb;
+    if (a.dg_nwg) {
+        if (threadIdx.x < 64) head_bwd_fin_wave(a.dg, a.dg_nwg, shk, blockIdx.x == 0);
+        __syncthreads();
+        hbp = shk;
+    }
     float hm[3], hk[3][3];
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
@@ -436,6 +439,11 @@ __device__ __forceinline__ void head_bwd_fin_wave(const HeadDgradArgs& a, int nw
         if (write) {
             a.grads[d.gamma_off + c] = (float)(qd * invd);
             a.grads[d.beta_off + c] = (float)sd;
+            if (a.hb) {
+                a.hb[ch * 3 + 0] = k0;
+                a.hb[ch * 3 + 1] = k1;
+                a.hb[ch * 3 + 2] = k2;
+            }
         }
     }
 }
@@ -515,9 +523,11 @@ int head_dgrad_groups(int B) { return ((B + 31) / 32) * (HD_PT + HD_VT); }
 hipError_t launch_head_bn_apply_feat(float* fp, float* fv, float* feat, int B, const HeadStatsArgs& fin,
                                      hipStream_t st)
 {
+    // grid-stride: every workgroup reduces all M/64 statistics partials first, so the
+    // grid is capped (256 workgroups: the reduction traffic stays linear in B)
     const int total = B * 3 * PIX;
     int nb = (total + 255) / 256;
-    nb = nb > 8192 ? 8192 : nb;
+    nb = nb > 256 ? 256 : nb;
     hipLaunchKernelGGL(head_bn_apply_feat_kernel, dim3(nb), dim3(256), 0, st, fin.zh, fp, fv, feat, B, fin,
                        head_proj_stats_groups(fin.M));
     return hipGetLastError();
@@ -540,6 +550,17 @@ hipError_t launch_head_proj_partials(int C, bool apply, const HeadStatsArgs& a, 
         default: return hipErrorInvalidValue;
     }
 #undef AZG_HPQ
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(64) void head_bn_bwd_fin_kernel(const HeadDgradArgs a, int nwg)
+{
+    head_bwd_fin_wave(a, nwg, nullptr, true);
+}
+
+hipError_t launch_head_bwd_fin(const HeadDgradArgs& a, hipStream_t st)
+{
+    hipLaunchKernelGGL(head_bn_bwd_fin_kernel, dim3(1), dim3(64), 0, st, a, head_dgrad_groups(a.B));
     return hipGetLastError();
 }
 

@@ -380,6 +380,29 @@ def selfplay_run(model, game_class, G, S, max_moves, seeds, profile=True):
     return sp, dt, prof, boards, results
 
 
+PRETRAIN_STEPS = 20
+
+
+def pretrain(model, dev, steps=PRETRAIN_STEPS, batch=128):
+    """SURVEY.md §8(d) / §7 synthetic setup: the benchmarked weights are the seeded
+    init (torch.manual_seed(0)) + 20 train_batch steps (network.py:199-235) on synthetic
+    data -- legal boards (synth_encoded, seed = step), pi ~ normalised U[0,1)^225,
+    z in {-1, 0, 1} (np.random.default_rng(0)), batch 128 (train.py's batch_size).
+    Fresh Kaiming init is not what a self-play generation runs on (its logits
+    reach +-48); ~0.06 s of GPU time, outside every timed region."""
+    from synth import synth_encoded
+    rng = np.random.default_rng(0)
+    for s in range(steps):
+        x = torch.from_numpy(synth_encoded(batch, seed=s)).to(dev)
+        pi = rng.random((batch, 225)).astype(np.float32)
+        pi /= pi.sum(1, keepdims=True)
+        z = rng.integers(-1, 2, (batch, 1)).astype(np.float32)
+        model.train_batch_device(x, torch.from_numpy(pi).to(dev), torch.from_numpy(z).to(dev), return_tensor=True)
+    torch.cuda.synchronize()
+    model.engine.check_status()
+    model.net.eval()
+
+
 def selfplay_leg(model, args, rank, world, dist, dev, local):
     """configs[2] headline: G games x S sims/move per rank, every game to its end."""
     from games.gomoku import Gomoku
@@ -553,6 +576,8 @@ def main():
     ap.add_argument("--pente-moves", type=int, default=225,
                     help="max_moves of the configs[4] Pente self-play (225 = every game to its end)")
     ap.add_argument("--skip-forward", action="store_true", help="profiling runs: no configs[1] sub-leg")
+    ap.add_argument("--pretrain-steps", type=int, default=PRETRAIN_STEPS,
+                    help="seeded train_batch steps on synthetic data before the legs (SURVEY §8(d); 0: raw init)")
     ap.add_argument("--tune", action="append", default=[], help="KEY=VALUE tuning key (A/B and profiling runs)")
     args = ap.parse_args()
     if args.tune:
@@ -570,6 +595,8 @@ def main():
 
     torch.manual_seed(0)
     model = PyTorchModel(board_size=15, device=str(dev), n_res_blocks=BLOCKS, channels=CHANNELS)
+    if args.pretrain_steps > 0:
+        pretrain(model, dev, args.pretrain_steps)
 
     fwd = sp = None
     if not args.skip_forward:
@@ -615,7 +642,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (self-play from the empty board; seeded Kaiming-init 6x128 weights, no checkpoint)",
+        "data": (f"synthetic (self-play from the empty board; 6x128 weights = seeded init + {args.pretrain_steps} "
+                 f"train_batch steps on synthetic boards / pi / z, SURVEY §8(d); no checkpoint)"),
         "config": {"workload": f"configs[2]: {args.sp_games} concurrent self-play games/GPU x {args.sp_sims} "
                                f"sims/move, 15x15 Gomoku, 6-block/128-filter ResNet, every game played to its end "
                                f"(train.py:360-412); value = NN-evaluated leaf boards / wall time of the whole "

@@ -78,8 +78,12 @@ int32_t azg_pv_bind(azg_pv* h, float* params, float* grads, float* bn_stats);
 int32_t azg_pv_bind_counters(azg_pv* h, int64_t* num_batches_tracked);
 int32_t azg_pv_num_bn_layers(const azg_pv* h);
 
-/* Parameters or BN stats changed outside the library (load_state_dict, copy_):
- * re-derive packed weights / folded BN before the next forward. */
+/* Parameters or BN stats changed outside the library (load_state_dict, copy_, a
+ * write through the bound pointers, a collective that rewrites them): re-derive
+ * packed weights / folded BN before the next forward AND the next train step.
+ * azg_pv_train_apply refreshes the packs itself; between two train steps the
+ * library trusts them unless this is called (the Python engine calls it whenever a
+ * parameter tensor's version counter moved). */
 int32_t azg_pv_mark_dirty(azg_pv* h);
 
 /* Eval-mode forward (BN running stats).  x: [batch,3,15,15] NCHW fp32.
@@ -157,22 +161,10 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          bitwise identical to 0);
  *   key 9: stem kernel (1 = fp32 MFMA, default; 0 = VALU reference, bitwise equal);
  *   key 11: stem ablation mask (timing only, results invalid while set);
- *   key 12: train step conv weight grads (0 = overlapped on a side stream, default;
- *          1 = on the caller's stream);
- *   key 13: train wgrad K chunk in pixels (32 default; 16 for A/B timing, C=128);
- *   key 16: train conv weight-grad kernel (3 = natural pixel rows moved into LDS
- *          by LDS-DMA, default; 1 = K-contiguous register staging with 16-B
- *          fragment reads; 2 = the same two chunks ahead; 0 = row staging with 4-B
- *          reads; 4 = the LDS-DMA kernel with 8 waves per 128x128 tile, C = 128;
- *          A/B timing, all bitwise identical);
  *   key 17: persistent-tower claim granularity (1 = one M tile with all its N
  *          tiles, run back to back by the claiming workgroup, default: the second
  *          tile's halo rows hit the XCD's L2, +2 % at B = 512 and 4096, measured;
  *          0 = one 128x64 tile per claim); bitwise identical results;
- *   key 18: train write-through stores (bits: 1 conv outputs -- study build only,
- *          2 BN-apply outputs, 4 weight-grad slabs; default 7): no dirty L2 lines at
- *          the kernel boundaries; bitwise identical;
- *   key 19: study build only: skip train BN kernels (timing, results invalid);
  *   key 21: per-layer 128x64 conv: the last partial round of workgroups runs as a
  *          second launch of 64x64 tiles (1, default) or not (0); bitwise identical;
  *   key 22: per-layer 128x64 conv tile body (1 = halo rows keyed on the board
@@ -185,54 +177,13 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *   key 24: train BN finalize run by the last workgroup of the conv producing the
  *          layer's partials (1, default) or by separate finalize kernels (0); one
  *          shared fp64 reduction order, bitwise identical;
- *   key 25: train convs: operand addressing through buffer resources (32,
- *          default) or 64-bit pointers (0); bitwise identical;
- *   key 26: train conv tile (8: 128x64 with 8 waves, default; 16: 128x128 with 16
- *          waves, one workgroup per CU); bitwise identical;
- *   key 27: train conv weight-grad pixel splits (0 = automatic, default); bitwise
- *          identical only at a fixed value;
- *   key 28: train head chain, bit mask of the fused stages (bit 0 head projections +
- *          BN statistics + finalize by the last workgroup, also applying the last
- *          block's bn2; bit 4 the same projections with a one-workgroup finalize
- *          launch; bit 1 head BN apply + FCs + loss + fc data grads per 4 boards; bit 3
- *          the fc stage as short wide launches: features in the eval row layout ->
- *          heads_fc -> loss -> LDS-staged masked fc dgrad tiles + head-BN backward
- *          partials -> one-wave finalize; bit 2 head BN-backward + 1x1 backward + the
- *          last block's BN-backward partials); default 28 (bits 2, 3, 4); 0 = the
- *          18-launch chain; fp32 sums in another order (within the oracle tolerance);
- *   key 29: train BN-backward ReLU mask formed from z with the layer's scale and
- *          shift (1, default) or read from the stored activation (0); bitwise identical;
- *   key 30: train weight repack split over the two streams (1, default) or one launch
- *          on the caller's stream (0); bitwise identical;
- *   key 32: train head weight-grad work (fc weight grads, bias / value_fc2 grads,
- *          loss means, the 1x1 weight-grad reduction) deferred to the end of the
- *          tower backward (1, default, with key 28 bit 3), on the side stream during
- *          the head chain (2) or inside the head chain (0); bitwise identical;
- *   key 33: train stream hand-off events with a device-scope release (1, default)
- *          or the system-scope default (0); bitwise identical;
- *   key 34: train backward: one dZ buffer per conv (1, default: no stream waits
- *          for buffer reuse -- each costs the caller's stream ~6 us, measured) or
- *          two alternating buffers (0); bitwise identical;
- *   key 36: train step: the next step's weight packs and eval BN fold right behind
- *          Adam in azg_pv_train_apply (1, default) or at the start of the next
- *          azg_pv_train_backward (0); bitwise identical;
- *   key 37: train weight-grad stream priority: 0 lowest (default), 1 highest;
- *          bitwise identical;
- *   key 38: train stem BN statistics from the stem's accumulators (1, default) or
- *          a separate col_stats pass (0); fp32 sums in another order;
- *   key 39: train: each conv's weight-grad slab reduction launched after the next
- *          conv's weight-grad kernel (1, default; 2: the same, with the step's last
- *          two reductions in one launch on the caller's stream after the join,
- *          +0.4 %, measured) or right behind its own (0); bitwise identical;
- *   key 40: train: each block's conv1 BN backward applied in its dgrad's halo
- *          staging (1, z in registers; 2, z by LDS-DMA into its own LDS rows and the
- *          transform at the group's halo store; C <= 128, both slower, measured) or a
- *          bn_bwd_apply pass (0, default); bitwise identical;
- *   key 41: train: in-kernel split-group combine of the weight-grad slabs by the
- *          last arriver of each group (1; slower) or all slabs to wgrad_reduce (0,
- *          default); fp32 sums in another order;
- *   key 42: train forward convs store their tile after the BN-partial arrival count
- *          (1, default) or before (0); bitwise identical;
+ *   key 27: train conv weight-grad pixel splits (0 = automatic, default; 8..64, a
+ *          multiple of 8); bitwise identical only at a fixed value;
+ *   key 43: study build only: the train step's tower backward as ONE persistent
+ *          launch (pv_bwd_tower.hip, 1) or the product's two-stream schedule (0);
+ *          bitwise identical, measured slower; returns 0 in the product library;
+ *   key 44: train BN apply / BN-backward apply passes: workgroup cap of their
+ *          grid-stride launch (0 = one float4 per thread, default); bitwise identical;
  *   key 31: study build only: the 64x64 / 128x64 towers with sc1 dependent loads
  *          and no acquire (two or more workgroups per CU: outside the microarch
  *          guide's measured envelope; the product uses the acquire there and the

@@ -71,7 +71,7 @@ def compare(a, b):
             bad += 1
             continue
         x, y = A[k], Bz[k]
-        same = x.shape == y.shape and np.array_equal(x.view(np.uint8), y.view(np.uint8))
+        same = x.shape == y.shape and np.array_equal(np.atleast_1d(x).view(np.uint8), np.atleast_1d(y).view(np.uint8))
         if not same:
             d = np.abs(x.astype(np.float64) - y.astype(np.float64)).max() if x.shape == y.shape else -1
             print(f"DIFF {k}: max|d| {d:.3e}, {np.count_nonzero(x != y)} of {x.size}")

@@ -150,3 +150,31 @@ def test_collectives_see_device_tensors_under_rccl(monkeypatch):
     assert D.allreduce_min_int(5, "cpu") == 5
     assert len(seen) >= 8
     assert all(dev == "cuda" for _, dev, _, _ in seen), seen
+
+
+def test_bench_collectives_see_device_tensors_under_rccl(monkeypatch):
+    """bench.py's own collectives: under a backend reported as "nccl"
+    (RCCL), reduce_ hands a HIP tensor to all_reduce (sum and max) and barrier_sync
+    passes the rank's device to dist.barrier; both return the right values."""
+    import importlib
+    import torch.distributed as dist
+    bench = importlib.import_module("bench")
+    seen = []
+
+    def all_reduce(t, op=None, **k):
+        seen.append(("all_reduce", t.device.type, t.dtype, op))
+        t.mul_(2)                      # a 2-rank sum of equal contributions
+
+    def barrier(*a, **k):
+        seen.append(("barrier", k.get("device_ids")))
+
+    monkeypatch.setattr(dist, "get_backend", lambda *a, **k: "nccl")
+    monkeypatch.setattr(dist, "all_reduce", all_reduce)
+    monkeypatch.setattr(dist, "barrier", barrier)
+    dev = torch.device("cuda", 0)
+    assert bench.reduce_(dist, dev, [1.5, 2.0]) == [3.0, 4.0]
+    assert bench.reduce_(dist, dev, [7.0], op="max") == [14.0]
+    bench.barrier_sync(dist, 0)
+    assert [s[:3] for s in seen[:2]] == [("all_reduce", "cuda", torch.float64)] * 2
+    assert seen[0][3] == dist.ReduceOp.SUM and seen[1][3] == dist.ReduceOp.MAX
+    assert seen[2] == ("barrier", [0])
