@@ -63,11 +63,17 @@ struct TowerArgs {
                          // N tile's halo rows are hits in that XCD's L2)
     int abl;             // timing studies only (0 in the product; results not valid otherwise):
                          // bit 1 skips the dependency wait + acquire, bit 2 the publish drain
+    unsigned* xq;        // non-null: eight claim queues, one per workgroup group blockIdx % 8 (the
+                         // workgroups of a group share an XCD -- observed placement, speed only):
+                         // queue q holds the M tiles [q*mtiles/8, (q+1)*mtiles/8) of every layer,
+                         // layer-major; its counter is sync[0] for q = 0, xq[q - 1] otherwise.  A
+                         // drained queue's workgroups steal from the next queues.
 };
 
 constexpr unsigned kSpinLimit = 1u << 22;    // x s_sleep(2): seconds, far above any tile time
 unsigned g_tower_spin_limit = kSpinLimit;    // tuning key 14 (tests: 0 forces the timeout path)
-int g_tower_group = 1;                       // tuning key 17: 1 (default) = claim an M tile with all its N tiles
+int g_tower_group = 1;                       // tuning key 17: 1 (default) = claim an M tile with all its N tiles;
+                                             // 2 = one N tile per claim from eight per-XCD-group queues
 #ifdef AZG_AB_STUDIES
 int g_tower_coh = 0;   // study key 31: sc1 dependent loads with 64x64 / 128x64 tiles (OUTSIDE the guide's envelope)
 #endif
@@ -87,7 +93,9 @@ constexpr int tower_lds_bytes()
     return NW >= 16 && need <= 82 * 1024 ? 82 * 1024 : need;
 }
 
-template <int C, int BN_, int WM_, int TM_, int NW_, int VAR = 0>
+// HABL (study build, timing / traffic ablations only: results invalid): halo_tile's ABL
+// bits -- 1 skips the weight loads, 2 the halo loads
+template <int C, int BN_, int WM_, int TM_, int NW_, int VAR = 0, int HABL = 0>
 __global__ __launch_bounds__(64 * NW_, (tower_min_waves<BN_, NW_>())) void conv_tower(const TowerArgs a)
 {
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
@@ -100,18 +108,40 @@ __global__ __launch_bounds__(64 * NW_, (tower_min_waves<BN_, NW_>())) void conv_
     const int tid = threadIdx.x;
     const int mtiles = (a.M + T::BM - 1) / T::BM;
     const int grp = a.group;                     // N tiles per claim (1 or NTN)
-    const int tpl = mtiles * (NTN / grp);        // claims per layer
-    const int total = tpl * a.nlayers;
-    unsigned* work = a.sync;
     unsigned* err = a.sync + 1;
     unsigned* cnt = a.sync + 4;
+    // claim queue q: its first M tile, M tiles, claims per layer and in all, counter
+    const bool xq = a.xq != nullptr;
+    int q = xq ? (int)(blockIdx.x & 7) : 0, qtried = 1;
+    int qm0 = 0, tpl = 0, total = 0;
+    unsigned* work = a.sync;
+    auto set_queue = [&](int qq) {
+        qm0 = xq ? qq * mtiles / 8 : 0;
+        const int qn = xq ? (qq + 1) * mtiles / 8 - qm0 : mtiles;
+        tpl = qn * (NTN / grp);
+        total = tpl * a.nlayers;
+        work = (xq && qq > 0) ? a.xq + qq - 1 : a.sync;
+    };
+    set_queue(q);
 
     if (tid == 0) s_claim[0] = (int)__hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     int w = s_claim[0];
-    while (w < total) {
+    while (true) {
+        if (w >= total) {
+            // this queue is drained: steal from the next one (every queue once)
+            if (!xq || qtried == 8) break;
+            q = (q + 1) & 7;
+            ++qtried;
+            set_queue(q);
+            __syncthreads();                      // every wave has read s_claim
+            if (tid == 0) s_claim[0] = (int)__hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            w = s_claim[0];
+            continue;
+        }
         const int l = w / tpl, t = w - l * tpl;
-        const int mt = t / (NTN / grp), nt0 = (t - mt * (NTN / grp)) * grp;
+        const int mt = qm0 + t / (NTN / grp), nt0 = (t % (NTN / grp)) * grp;
         __syncthreads();                          // every wave has read s_claim
         if (tid == 0) {
             // next claim now: its latency overlaps this tile (read after the tile)
@@ -146,7 +176,7 @@ __global__ __launch_bounds__(64 * NW_, (tower_min_waves<BN_, NW_>())) void conv_
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Ly.out, (short)0, a.act_bytes, 0x00020000);
         for (int nt = nt0; nt < nt0 + grp; ++nt) {
             if (nt > nt0) __syncthreads();        // the previous tile's epilogue is done with LDS
-            halo_tile<C, BN_, WM_, TM_, NW_, EPI_BN_OPTRES_RELU, true, 0, VAR>(Ly.in, Ly.wp, Ly.scale, Ly.shift, Ly.resid,
+            halo_tile<C, BN_, WM_, TM_, NW_, EPI_BN_OPTRES_RELU, true, HABL, VAR>(Ly.in, Ly.wp, Ly.scale, Ly.shift, Ly.resid,
                                                                       Ly.out, rs, a.M, mt * T::BM, nt * T::BN, smem);
         }
         if (!(a.abl & 2)) {
@@ -159,17 +189,17 @@ __global__ __launch_bounds__(64 * NW_, (tower_min_waves<BN_, NW_>())) void conv_
     }
 }
 
-template <int C, int BN, int WM, int TM, int NW, int VAR = 0>
+template <int C, int BN, int WM, int TM, int NW, int VAR = 0, int HABL = 0>
 static hipError_t launch_tower_t(const TowerArgs& a, hipStream_t st, int* grid_out)
 {
     constexpr int lds = tower_lds_bytes<C, BN, WM, TM, NW, VAR>();
     static int grid = 0;
     if (grid == 0) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv_tower<C, BN, WM, TM, NW, VAR>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv_tower<C, BN, WM, TM, NW, VAR, HABL>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
         int per_cu = 0, dev = 0, cus = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)conv_tower<C, BN, WM, TM, NW, VAR>,
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)conv_tower<C, BN, WM, TM, NW, VAR, HABL>,
                                                          64 * NW, lds);
         if (e != hipSuccess) return e;
         if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
@@ -185,7 +215,7 @@ static hipError_t launch_tower_t(const TowerArgs& a, hipStream_t st, int* grid_o
         grid = max(1, per_cu) * cus;
     }
     if (grid_out) *grid_out = grid;
-    hipLaunchKernelGGL((conv_tower<C, BN, WM, TM, NW, VAR>), dim3(grid), dim3(64 * NW), lds, st, a);
+    hipLaunchKernelGGL((conv_tower<C, BN, WM, TM, NW, VAR, HABL>), dim3(grid), dim3(64 * NW), lds, st, a);
     return hipGetLastError();
 }
 
@@ -194,10 +224,16 @@ int g_tower_var = 0;     // halo_tile VAR of the 128x64 C=128 tower (0 = product
 int g_tower_shape = 8;   // forced shape when g_tower_mode == 1: 5 = 64x64 (4 waves), 8 = 128x64 (8 waves),
                          // 10 = 128x128 (16 waves, one workgroup per CU; C = 128)
 
-size_t tower_sync_bytes(int nlayers, int M)
+// [0] work counter (queue 0), [1] error word, [4 ..) per-(layer, M tile) counters, then
+// the counters of queues 1..7 (key 17 = 2)
+static size_t tower_tile_words(int nlayers, int M)
 {
     const int mtiles = (M + 63) / 64;   // the smallest BM (64) has the most M tiles
-    return ((size_t)(4 + nlayers * mtiles) * sizeof(unsigned) + 15) / 16 * 16;
+    return (size_t)(4 + nlayers * mtiles);
+}
+size_t tower_sync_bytes(int nlayers, int M)
+{
+    return ((tower_tile_words(nlayers, M) + 7) * sizeof(unsigned) + 15) / 16 * 16;
 }
 
 // Eval residual tower in one launch: NB blocks, conv1 X -> H (BN, ReLU), conv2
@@ -218,7 +254,8 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     a.sync = sync;
     a.status = status;
     a.spin_limit = g_tower_spin_limit;
-    a.group = g_tower_group ? C / (shape == 8 || shape == 5 ? 64 : 128) : 1;
+    a.group = g_tower_group == 1 ? C / (shape == 8 || shape == 5 ? 64 : 128) : 1;
+    a.xq = g_tower_group == 2 ? sync + tower_tile_words(2 * NB, M) : nullptr;
     if (shape == 10 && C != 128) return hipErrorInvalidValue;   // 16-wave tile: C = 128 only (C = 256 spills)
     a.abl = g_tower_ablation;
     float* X = act[0];
@@ -239,6 +276,16 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     hipError_t e = hipMemsetAsync(sync, 0, tower_sync_bytes(2 * NB, M), st);
     if (e != hipSuccess) return e;
 #ifdef AZG_AB_STUDIES
+    // traffic ablations of the 128x64 tower (key 8 bits 4 / 8: no weight / no halo loads)
+    if (shape == 8 && (a.abl & 12)) {
+        const bool nw = a.abl & 4, nh = a.abl & 8;
+        if (C == 256 && nw && nh) return launch_tower_t<256, 64, 4, 1, 8, 32, 3>(a, st, nullptr);
+        if (C == 256 && nw) return launch_tower_t<256, 64, 4, 1, 8, 32, 1>(a, st, nullptr);
+        if (C == 256 && nh) return launch_tower_t<256, 64, 4, 1, 8, 32, 2>(a, st, nullptr);
+        if (C == 128 && nw && nh) return launch_tower_t<128, 64, 4, 1, 8, 32, 3>(a, st, nullptr);
+        if (C == 128 && nw) return launch_tower_t<128, 64, 4, 1, 8, 32, 1>(a, st, nullptr);
+        if (C == 128 && nh) return launch_tower_t<128, 64, 4, 1, 8, 32, 2>(a, st, nullptr);
+    }
     if (g_tower_coh && (shape == 8 || shape == 5)) {   // study only: sc1 loads at 2-4 workgroups per CU
         if (C == 128 && shape == 8) return launch_tower_t<128, 64, 4, 1, 8, 16>(a, st, nullptr);
         if (C == 128) return launch_tower_t<128, 64, 2, 1, 4, 16>(a, st, nullptr);

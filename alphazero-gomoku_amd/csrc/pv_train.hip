@@ -45,6 +45,7 @@ int wgrad_splits(int C, int M);
 constexpr int kMaxWgradSplits = 64;   // wgrad_splits <= slots / tiles <= 56, rounded to 8
 
 constexpr int TROWS = 64;    // rows per tile of bn_bwd_reduce_kernel (a net without residual blocks)
+constexpr int kApplyU = 4;   // float4 per thread and pass of the BN apply kernels
 constexpr int HROWS = 128;   // rows per tile of the head-projection backward partials
 
 int g_train_fuse_apply = 1;   // key 23: 1 BN applies folded into the next conv's staging; 0 separate passes
@@ -168,24 +169,36 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
                                                        const float* __restrict__ shift, float* __restrict__ out,
                                                        int M)
 {
-    constexpr int F4 = C / 4;
+    // grid-stride, kApplyU float4 per thread and pass, loads first (as bn_bwd_apply_kernel)
+    constexpr int F4 = C / 4, U = kApplyU;
     const int total = M * F4;
+    const int stride = gridDim.x * blockDim.x;
     const __amdgpu_buffer_rsrc_t rs = wt_rsrc(out, padded_bytes(M, C));
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-        const int m = i / F4, c = (i - m * F4) * 4;
-        const int o = pad_off(m, C) + c;
-        f32x4 v = *(const f32x4*)(z + o);
-        const f32x4 s = *(const f32x4*)(scale + c);
-        const f32x4 t = *(const f32x4*)(shift + c);
-        f32x4 r;
-        if (RES) r = *(const f32x4*)(res + o);
+    const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const int c = (i0 % F4) * 4;
+    const f32x4 s = *(const f32x4*)(scale + c);
+    const f32x4 t = *(const f32x4*)(shift + c);
+    for (int ib = i0; ib < total; ib += U * stride) {
+        f32x4 v[U], r[U];
+        int o[U];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            float y = fmaf(v[k], s[k], t[k]);   // same arithmetic as the conv staging prologue (ProX)
-            if (RES) y += r[k];
-            v[k] = fmaxf(y, 0.f);
+        for (int u = 0; u < U; ++u) {
+            const int i = min(ib + u * stride, total - 1);
+            o[u] = pad_off(i / F4, C) + c;
+            v[u] = *(const f32x4*)(z + o[u]);
+            if (RES) r[u] = *(const f32x4*)(res + o[u]);
         }
-        store4<WT>(out, rs, o, v);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (ib + u * stride >= total) break;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float y = fmaf(v[u][k], s[k], t[k]);   // same arithmetic as the conv staging prologue (ProX)
+                if (RES) y += r[u][k];
+                v[u][k] = fmaxf(y, 0.f);
+            }
+            store4<WT>(out, rs, o[u], v[u]);
+        }
     }
 }
 
@@ -263,36 +276,53 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* __restrict__ iw, float* __restrict__ dz, float* __restrict__ gres, int M,
     const float* __restrict__ fscale = nullptr, const float* __restrict__ fshift = nullptr)
 {
-    constexpr int F4 = C / 4;
+    // grid-stride, kApplyU float4 per thread and pass with every load issued before the
+    // first store; the stride is a multiple of C/4, so a thread's channels are fixed and
+    // its per-channel coefficients are loaded once
+    constexpr int F4 = C / 4, U = kApplyU;
     const int total = M * F4;
+    const int stride = gridDim.x * blockDim.x;
     const __amdgpu_buffer_rsrc_t rz = wt_rsrc(dz, padded_bytes(M, C));
     const __amdgpu_buffer_rsrc_t rg = wt_rsrc(GRES ? gres : dz, padded_bytes(M, C));
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-        const int m = i / F4, c = (i - m * F4) * 4;
-        const int o = pad_off(m, C) + c;
-        const f32x4 gv = *(const f32x4*)(g + o);
-        const f32x4 zv = *(const f32x4*)(z + o);
-        f32x4 av;
-        if constexpr (MZ) {
-            const f32x4 sc = *(const f32x4*)(fscale + c), sh = *(const f32x4*)(fshift + c);
+    const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const int c = (i0 % F4) * 4;
+    const f32x4 mu = *(const f32x4*)(mean + c);
+    const f32x4 g_ = *(const f32x4*)(gm + c);
+    const f32x4 k_ = *(const f32x4*)(kk + c);
+    const f32x4 w_ = *(const f32x4*)(iw + c);
+    f32x4 sc = {0.f, 0.f, 0.f, 0.f}, sh = sc;
+    if constexpr (MZ) {
+        sc = *(const f32x4*)(fscale + c);
+        sh = *(const f32x4*)(fshift + c);
+    }
+    for (int ib = i0; ib < total; ib += U * stride) {
+        f32x4 gv[U], zv[U], av[U];
+        int o[U];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) av[q] = fmaf(zv[q], sc[q], sh[q]);
-        } else {
-            av = *(const f32x4*)(act + o);
+        for (int u = 0; u < U; ++u) {
+            const int i = min(ib + u * stride, total - 1);
+            o[u] = pad_off(i / F4, C) + c;
+            gv[u] = *(const f32x4*)(g + o[u]);
+            zv[u] = *(const f32x4*)(z + o[u]);
+            if constexpr (!MZ) av[u] = *(const f32x4*)(act + o[u]);
         }
-        const f32x4 mu = *(const f32x4*)(mean + c);
-        const f32x4 g_ = *(const f32x4*)(gm + c);
-        const f32x4 k_ = *(const f32x4*)(kk + c);
-        const f32x4 w_ = *(const f32x4*)(iw + c);
-        f32x4 out, dyv;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            float dy;
-            out[q] = bnbwd_elem(gv[q], av[q], zv[q], mu[q], g_[q], k_[q], w_[q], dy);
-            dyv[q] = dy;
+        for (int u = 0; u < U; ++u) {
+            if (ib + u * stride >= total) break;
+            if constexpr (MZ) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) av[u][q] = fmaf(zv[u][q], sc[q], sh[q]);
+            }
+            f32x4 out, dyv;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float dy;
+                out[q] = bnbwd_elem(gv[u][q], av[u][q], zv[u][q], mu[q], g_[q], k_[q], w_[q], dy);
+                dyv[q] = dy;
+            }
+            store4<WT>(dz, rz, o[u], out);
+            if (GRES) store4<WT>(gres, rg, o[u], dyv);
         }
-        store4<WT>(dz, rz, o, out);
-        if (GRES) store4<WT>(gres, rg, o, dyv);
     }
 }
 
@@ -703,8 +733,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     float* G = h->grads;
     const BnDesc* bd = h->bn_desc.data();
     const BnDesc* bdd = (const BnDesc*)h->bn_desc_dev;
-    const int gM = g_train_apply_grid > 0 ? std::min(grid_for((int64_t)M * C / 4), g_train_apply_grid)
-                                          : grid_for((int64_t)M * C / 4);
+    const int gM = g_train_apply_grid > 0 ? std::min(grid_for((int64_t)M * C / 4 / kApplyU), g_train_apply_grid)
+                                          : grid_for((int64_t)M * C / 4 / kApplyU);
     const int ntt = (M + TRAIN_BM - 1) / TRAIN_BM;   // M tiles of conv3x3_train (partials per tile)
     const size_t CC9 = (size_t)9 * C * C;
     // the conv3x3_train launch that produces a layer's partials also finalizes it (key

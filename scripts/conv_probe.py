@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--tower-shape", type=int, default=8, help="persistent tower tile shape (key 6)")
     ap.add_argument("--var", type=int, default=0, help="study build: tower tile-body variant (key 10)")
     ap.add_argument("--coh", type=int, default=0, help="study build: round-2 sc1 tower hand-off at 2 WG/CU (key 31)")
+    ap.add_argument("--abl", type=int, default=0, help="study build: tower ablation bits (key 8; 4 no weight loads, 8 no halo loads)")
+    ap.add_argument("--group", type=int, default=1, help="tower claims (key 17: 0 tile, 1 M tile, 2 per-XCD queues)")
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--channels", type=int, default=128)
     args = ap.parse_args()
@@ -36,6 +38,8 @@ def main():
     lib.azg_pv_set_tuning(0, args.shape)
     lib.azg_pv_set_tuning(10, args.var)
     lib.azg_pv_set_tuning(31, args.coh)
+    lib.azg_pv_set_tuning(8, args.abl)
+    lib.azg_pv_set_tuning(17, args.group)
     from network import PyTorchModel
     from synth import synth_encoded
     dev = torch.device("cuda", 0)
