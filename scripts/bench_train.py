@@ -26,13 +26,10 @@ def main():
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--channels", type=int, default=128)
     ap.add_argument("--cpu-steps", type=int, default=3)
-    ap.add_argument("--serial", action="store_true", help="conv weight grads on the caller's stream (key 12)")
     ap.add_argument("--tune", action="append", default=[], help="KEY=VALUE tuning key (include/azg_pv.h)")
     args = ap.parse_args()
     import _native
     lib = _native.load_library()
-    if args.serial:
-        lib.azg_pv_set_tuning(12, 1)
     for kv in args.tune:
         k, v = (int(t) for t in kv.split("="))
         lib.azg_pv_set_tuning(k, v)
@@ -76,7 +73,6 @@ def main():
     eng.profile_enable(False)
     fwd_flop = 2 * 225 * args.channels * 9 * args.channels * (2 * args.blocks)   # tower convs per sample
     out = {"net": f"{args.blocks}x{args.channels}", "batch": B, "steps": args.steps, "tune": args.tune,
-           "serial": args.serial,
            "ms_per_step_profiled": round(dt / args.steps * 1e3, 3), "samples_per_s": round(B * args.steps / dt, 1),
            "ms_per_step_sync": round(dt_sync / args.steps * 1e3, 3),
            "ms_per_step_pipelined": round(dt_pipe / args.steps * 1e3, 3),
