@@ -78,6 +78,16 @@ __device__ __forceinline__ size_t padded_bytes(int M, int C) {
     return (size_t)((M + PIX - 1) / PIX) * PADPIX * C * sizeof(float);
 }
 
+// BatchNorm backward apply of one element (reference network.py:12-25 autograd; shared
+// by bn_bwd_apply_kernel, the fused dgrad epilogue and the persistent backward):
+// dy = g * (act > 0); dz = ((dy - gm) - (z - mean) * k) * iw.
+__device__ __forceinline__ float bnbwd_elem(float g, float av, float z, float mu, float gm, float k, float iw,
+                                            float& dy)
+{
+    dy = av > 0.f ? g : 0.f;
+    return ((dy - gm) - (z - mu) * k) * iw;
+}
+
 enum Epi : int {
     EPI_BN_RELU = 0,      // relu(acc*scale + shift)
     EPI_BN_RES_RELU = 1,  // relu(acc*scale + shift + resid)

@@ -125,8 +125,10 @@ struct FinX {
     unsigned* cnt = nullptr;     // fused: arrival counter per N tile (0 at launch; reset by the last arriver).
                                  // XE_STATS: the tile is stored after the arrival count, so the
                                  // write-through drain of the 32 KB tile leaves the finalize's path
-    unsigned* done = nullptr;    // in-launch consumers (pv_bwd_tower.hip): the results are stored
+    unsigned* done = nullptr;    // in-launch consumers (pv_bwd_tower.hip, ApX): the results are stored
                                  // write-through, drained, and each finalizing workgroup then adds 1
+                                 // (to done[n tile] when done_nt, else to done[0])
+    int done_nt = 0;
     const float* gamma = nullptr;
     const float* beta = nullptr;                            // FWD
     float *rmean = nullptr, *rvar = nullptr;                // FWD running stats
@@ -135,6 +137,27 @@ struct FinX {
     float *ggamma = nullptr, *gbeta = nullptr;              // !FWD: parameter grads
     float *gm_o = nullptr, *k_o = nullptr, *iw_o = nullptr; // !FWD: bn_bwd_apply coefficients
 };
+// Dgrad + BatchNorm-backward apply in one launch (XE_BNBWD with APPLY, the train
+// backward's two-stream schedule, key 45): the dgrad's output g is the gradient of the
+// BN + ReLU output of the layer whose backward sums its epilogue produces, so once that
+// layer is finalized (by the last workgroup of each N tile, FinX) every workgroup applies
+// the BatchNorm backward to its own tile, still in registers -- dz = ((dy - gm) - (z -
+// mean) k) iw with dy = g (act > 0), bn_bwd_apply_kernel's arithmetic -- and stores dz
+// (and dy, the residual gradient, when gres is set); g itself is never stored.  Every
+// workgroup waits for its N tile's finalize (a grid-wide dependency: the host launches
+// this form only when every tile of the launch fits on the device at once).
+struct ApX {
+    const float* gm = nullptr;   // the layer's bn_bwd_apply coefficients (written by the finalize)
+    const float* kk = nullptr;
+    const float* iw = nullptr;
+    float* dz = nullptr;
+    float* gres = nullptr;
+    unsigned* done = nullptr;    // per N tile: finalizes published (monotonic over launches)
+    unsigned epoch = 0;          // the value done[n tile] reaches when this launch's finalize is published
+    unsigned* status = nullptr;  // sticky host-mapped status, set on a timed-out wait
+    unsigned spin = 0;           // polls before the wait is declared timed out (0: time out at once)
+};
+
 // partial sums of tiles t = j, j+8, ... (the tile class j of 8) for channel c.
 // COH: every load is an agent-scope relaxed atomic load (`global_load_dword sc1`,
 // L1 bypassed) -- the consumer form that may replace an acquire only inside the
@@ -277,13 +300,15 @@ __device__ __forceinline__ int halo_vkey(int row)
 // RBUF: how the residual is read -- 0 plain pointer loads; 1 buffer loads (default
 // cache policy); 2 buffer loads with sc1 (the tower's one-workgroup-per-CU hand-off)
 template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1, int ABL, int ELD, bool EARLY = false,
-          int XE = XE_NONE, int RBUF = 0>
+          int XE = XE_NONE, int RBUF = 0, bool APPLY = false>
 __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<C, BN_, WM_, TM_, NW_>::TN],
                                               const float* __restrict__ scale, const float* __restrict__ shift,
                                               const float* __restrict__ resid, float* __restrict__ out,
                                               __amdgpu_buffer_rsrc_t out_rs, int M, int m0, int n0, float* smem,
-                                              const EpiX& ex = EpiX{}, const FinX& fx = FinX{})
+                                              const EpiX& ex = EpiX{}, const FinX& fx = FinX{},
+                                              const ApX& ax = ApX{})
 {
+    static_assert(!APPLY || XE == XE_BNBWD, "the fused BN-backward apply follows a dgrad epilogue");
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
     constexpr int BM = T::BM, BN = T::BN, WN = T::WN, TM = T::TM, TN = T::TN;
     const int tid = threadIdx.x;
@@ -333,6 +358,7 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
     // XE partials of this thread's 4 channels over its rows
     f32x4 xa = {0.f, 0.f, 0.f, 0.f}, xb = {0.f, 0.f, 0.f, 0.f}, xmu = {0.f, 0.f, 0.f, 0.f};
     f32x4 vk[XE == XE_STATS ? NPASS : 1];
+    f32x4 gk[APPLY ? NPASS : 1], ak[APPLY ? NPASS : 1], zk[APPLY ? NPASS : 1];   // APPLY: g, act, z per pass
     // late store (XE_STATS + fused finalize): the raw tile (kept in vk) is stored after the
     // partials are published and counted, so the arrival waits only for the partials
     const bool late = XE == XE_STATS && EPI == EPI_RAW && fx.cnt != nullptr;
@@ -382,8 +408,13 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                     xa[e] += dy;
                     xb[e] = fmaf(xz[e] - xmu[e], dy, xb[e]);
                 }
+                if constexpr (APPLY) {
+                    gk[p] = v;
+                    ak[p] = xact;
+                    zk[p] = xz;
+                }
             }
-            if (!late) {
+            if (!late && !APPLY) {
                 if constexpr (SC1) {
                     __builtin_amdgcn_raw_buffer_store_b128(
                         __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), out_rs, o * 4, 0, 16);
@@ -504,7 +535,48 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                     // drains, a barrier, then one agent-scope add (consumers poll + acquire)
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __syncthreads();
-                    if (tid == 0) __hip_atomic_fetch_add(fx.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (tid == 0)
+                        __hip_atomic_fetch_add(fx.done + (fx.done_nt ? n0 / BN : 0), 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+        if constexpr (APPLY) {
+            // this N tile's BN finalize published (one polling lane, ONE agent acquire,
+            // vmcnt(0), barrier; bounded: a timeout sets the sticky status and proceeds)
+            if (tid == 0) {
+                const unsigned* d = ax.done + n0 / BN;
+                unsigned spins = 0;
+                while (ax.spin == 0 || __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - ax.epoch >
+                                           0x80000000u) {   // done < epoch, modulo 2^32
+                    if (++spins > ax.spin) {
+                        if (ax.status) __hip_atomic_store(ax.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
+            const f32x4 g_ = *(const f32x4*)(ax.gm + col), k_ = *(const f32x4*)(ax.kk + col);
+            const f32x4 w_ = *(const f32x4*)(ax.iw + col);
+            const __amdgpu_buffer_rsrc_t rz = wt_rsrc(ax.dz, padded_bytes(M, C));
+            const __amdgpu_buffer_rsrc_t rg = wt_rsrc(ax.gres ? ax.gres : ax.dz, padded_bytes(M, C));
+#pragma unroll
+            for (int p = 0; p < NPASS; ++p) {
+                const int m = m0 + er + p * RPI;
+                if (m < M) {
+                    const int o = pad_off(m, C) + col;
+                    f32x4 dz4, dy4;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float dy;
+                        dz4[e] = bnbwd_elem(gk[p][e], ak[p][e], zk[p][e], xmu[e], g_[e], k_[e], w_[e], dy);
+                        dy4[e] = dy;
+                    }
+                    store4<true>(ax.dz, rz, o, dz4);
+                    if (ax.gres) store4<true>(ax.gres, rg, o, dy4);
                 }
             }
         }
@@ -718,13 +790,13 @@ __device__ __forceinline__ void halo_mainloop_glds(const float* __restrict__ in,
 // barriers, bit 8 replaces LDS fragment reads by register values, bit 16 skips the
 // epilogue stores (kept live by a never-true compare).
 template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1 = false, int ABL = 0, int VAR = 0,
-          int XE = XE_NONE, int PRO = PRO_NONE>
+          int XE = XE_NONE, int PRO = PRO_NONE, bool APPLY = false>
 __device__ __forceinline__ void halo_tile(
     const float* __restrict__ in, const float* __restrict__ wp,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ resid, float* __restrict__ out, __amdgpu_buffer_rsrc_t out_rs,
     int M, int m0, int n0, float* smem, const EpiX& ex = EpiX{}, const ProX& px = ProX{},
-    const FinX& fx = FinX{})
+    const FinX& fx = FinX{}, const ApX& ax = ApX{})
 {
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
     if constexpr ((VAR & 4) != 0) {   // LDS-DMA staging
@@ -1023,8 +1095,8 @@ __device__ __forceinline__ void halo_tile(
 
     // the last chunk ended with a barrier: the staging buffers are free
     halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, (VSWZ ? BN : BN + 8), (VAR & 8) != 0, XE,
-                  (VAR & 16) ? 2 : (VAR & 32) ? 1 : 0>(
-        acc, scale, shift, resid, out, out_rs, M, m0, n0, smem, ex, fx);
+                  (VAR & 16) ? 2 : (VAR & 32) ? 1 : 0, APPLY>(
+        acc, scale, shift, resid, out, out_rs, M, m0, n0, smem, ex, fx, ax);
 }
 
 }  // namespace azg

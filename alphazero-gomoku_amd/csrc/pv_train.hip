@@ -50,6 +50,8 @@ constexpr int HROWS = 128;   // rows per tile of the head-projection backward pa
 
 int g_train_fuse_apply = 1;   // key 23: 1 BN applies folded into the next conv's staging; 0 separate passes
 int g_train_fuse_fin = 1;     // key 24: 1 BN finalize by the last workgroup of the producing conv; 0 separate kernels
+int g_train_dgrad_apply = 1;  // key 45: 1 each dgrad applies the next BN backward in its epilogue (when its tiles
+                              // fit the device at once); 0 separate bn_bwd_apply passes
 int g_train_apply_grid = 0;   // key 44: workgroup cap of the BN apply / BN-backward apply passes (0: one float4 per thread)
 int g_train_bwd_tower = 0;    // key 43 (study build): 1 the tower backward as one persistent launch (slower,
                               // measured); 0 the two-stream schedule (product)
@@ -73,6 +75,8 @@ struct TrainWS {
     float* slab[3] = {nullptr, nullptr, nullptr};  // weight-grad split-K slabs (two alternate; study build: three rotate)
     int slab_S = 0;                                // splits one slab holds
     unsigned* fincnt = nullptr;   // fused BN finalize arrival counters: [0..3] forward / two-stream, 4 per conv after
+    unsigned* apdone = nullptr;   // fused dgrad + BN-backward apply: finalizes published per N tile (monotonic)
+    unsigned ap_epoch = 0;        // launches of it so far
     // heads
     float *zh = nullptr, *fp = nullptr, *fv = nullptr, *hv = nullptr, *dpre = nullptr;
     float *dlogits = nullptr, *dfp = nullptr, *dfv = nullptr, *dhv = nullptr, *lossb = nullptr;
@@ -687,6 +691,8 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     A(w->scal, 4, true);
     A(t, 4 * (2 * kTowerMaxBlocks + 2), true);
     w->fincnt = (unsigned*)t;
+    A(t, 16, true);
+    w->apdone = (unsigned*)t;
     A(t, (size_t)head_proj_stats_groups(M) * 6 * 2, false);
     w->hsp1 = (double*)t;
     A(t, (size_t)head_dgrad_groups(cap) * 6 * 2, false);
@@ -985,6 +991,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     // epilogue of the dgrad conv that produces its gradient (XE_BNBWD, per 128-row
     // tile); the last block's bn2 sums come from heads_bwd_fused (per 128-row tile).
     bool done_fin = false;   // the stem's BN backward is finalized (by the last dgrad)
+    bool stem_dz_done = false;   // the stem's dz is in DH already (key 45)
     bool side_used = false;
     if (NB > 0) R(bwd_fin(h->bn_blk[NB - 1].second, hntile));
 #ifdef AZG_AB_STUDIES
@@ -1085,26 +1092,71 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             return 0;
         };
         bool fin_next = true;   // the next layer's finalize is already done (the first: above)
+        // key 45: every dgrad also applies the BN backward of the layer below in its
+        // epilogue once its in-kernel finalize is published (all its tiles must fit the
+        // device at once: they wait for each other); the next conv's dZ (and the residual
+        // gradient) come straight out of the dgrad, g itself is never stored
+        const bool dga = g_train_dgrad_apply && ffin && ntt * (C / 64) <= train_apply_capacity(C);
+        auto dgrad_apply = [&](int epi, const float* dz_in, const float* wd, const float* res, const float* xact,
+                               const float* xz, int xl, float* dz_out, float* gres_out) -> int32_t {
+            int pr = prof_begin(h, AZG_PROF_TRAIN_CONV, st, B);
+            const int o = bd[xl].out_off;
+            const EpiX ex{xact, xz, w->bmean + o, w->part_a, w->part_b};
+            FinX fx = fin_args(xl, false);
+            fx.cnt = w->fincnt;
+            fx.done = w->apdone;
+            fx.done_nt = 1;
+            ApX ax{};
+            ax.gm = w->bgm + o;
+            ax.kk = w->bk + o;
+            ax.iw = w->biw + o;
+            ax.dz = dz_out;
+            ax.gres = gres_out;
+            ax.done = w->apdone;
+            ax.epoch = ++w->ap_epoch;
+            ax.status = h->status_dev;
+            ax.spin = g_tower_spin_limit;
+            AZG_CK(launch_conv3x3_dgrad_apply(C, epi, dz_in, wd, res, w->DH, M, ex, fx, ax, st),
+                   "train: conv3x3 dgrad + BN backward apply");
+            prof_end(h, pr, st);
+            return 0;
+        };
         for (int i = NB - 1; i >= 0; --i) {
             const float* Xin = i == 0 ? w->a0 : w->xo[i - 1];
             const float* zin = i == 0 ? w->z0 : w->z2[i - 1];
             const int lin = i == 0 ? h->bn_stem : h->bn_blk[i - 1].second;
             const int l1 = h->bn_blk[i].first, l2 = h->bn_blk[i].second;
-            if (!fin_next) R(bwd_fin(l2, ntt));
             float* dz2 = w->dzs[2 * i + 1];
-            R(bwd_apply(w->gX, w->xo[i], w->z2[i], l2, dz2, w->GR));
-            R(wgrad(dz2, w->hh[i], h->t_blk[i].w2));
-            R(conv(EPI_RAW, XE_BNBWD, dz2, w->wdpack + (size_t)(2 * i + 1) * CC9, nullptr, w->DH, w->hh[i], w->z1[i],
-                   l1, ffin ? l1 : -1));
-            if (!ffin) R(bwd_fin(l1, ntt));
             float* dz1 = w->dzs[2 * i];
-            R(bwd_apply(w->DH, nullptr, w->z1[i], l1, dz1, nullptr));
+            if (!dga || i == NB - 1) {   // with dga, conv1's dgrad of block i + 1 produced dz2 and GR
+                if (!fin_next) R(bwd_fin(l2, ntt));
+                R(bwd_apply(w->gX, w->xo[i], w->z2[i], l2, dz2, w->GR));
+            }
+            R(wgrad(dz2, w->hh[i], h->t_blk[i].w2));
+            if (dga) {
+                R(dgrad_apply(EPI_RAW, dz2, w->wdpack + (size_t)(2 * i + 1) * CC9, nullptr, w->hh[i], w->z1[i], l1, dz1,
+                              nullptr));
+            } else {
+                R(conv(EPI_RAW, XE_BNBWD, dz2, w->wdpack + (size_t)(2 * i + 1) * CC9, nullptr, w->DH, w->hh[i],
+                       w->z1[i], l1, ffin ? l1 : -1));
+                if (!ffin) R(bwd_fin(l1, ntt));
+                R(bwd_apply(w->DH, nullptr, w->z1[i], l1, dz1, nullptr));
+            }
             R(wgrad(dz1, Xin, h->t_blk[i].w1));
-            R(conv(EPI_ADD, XE_BNBWD, dz1, w->wdpack + (size_t)(2 * i) * CC9, w->GR, w->gX, Xin, zin, lin,
-                   ffin ? lin : -1));
+            if (dga) {
+                // block i's conv1 dgrad (+ its residual gradient GR) -> the BN backward of
+                // block i - 1's bn2 (dz2 of block i - 1, and its dy as the next GR) or of
+                // the stem (the stem's dz into DH, the stem weight grad's operand)
+                R(dgrad_apply(EPI_ADD, dz1, w->wdpack + (size_t)(2 * i) * CC9, w->GR, Xin, zin, lin,
+                              i > 0 ? w->dzs[2 * (i - 1) + 1] : w->DH, i > 0 ? w->GR : nullptr));
+            } else {
+                R(conv(EPI_ADD, XE_BNBWD, dz1, w->wdpack + (size_t)(2 * i) * CC9, w->GR, w->gX, Xin, zin, lin,
+                       ffin ? lin : -1));
+            }
             fin_next = ffin;
             R(snap(NB - i));
         }
+        stem_dz_done = dga;
         if (pend.slab) AZG_CK(launch_wgrad_reduce(C, pend.slab, pend.dw, S, w->side), "train: wgrad reduce");
         done_fin = ffin;
     }
@@ -1131,7 +1183,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     } else if (!done_fin) {
         R(bwd_fin(h->bn_stem, ntt));
     }
-    R(bwd_apply(w->gX, nullptr, w->z0, h->bn_stem, w->DH, nullptr));
+    if (!stem_dz_done) R(bwd_apply(w->gX, nullptr, w->z0, h->bn_stem, w->DH, nullptr));
     hipLaunchKernelGGL((stem_wgrad_kernel<C>), dim3(B * STEM_WG_CHUNKS), dim3(256), 0, st, x, w->DH, w->spart);
     AZG_CK(hipGetLastError(), "train: stem_wgrad");
     hipLaunchKernelGGL(reduce_partials_kernel, dim3((27 * C + 15) / 16), dim3(256), 0, st, w->spart, B * STEM_WG_CHUNKS, 27 * C,

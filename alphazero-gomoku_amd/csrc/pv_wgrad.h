@@ -194,13 +194,4 @@ __device__ __forceinline__ void wgrad_reduce_elems(const float* __restrict__ sla
     }
 }
 
-// BatchNorm backward apply of one element (bn_bwd_apply_kernel, network.py:12-25
-// autograd): dy = g * (act > 0); dz = ((dy - gm) - (z - mean) * k) * iw.
-__device__ __forceinline__ float bnbwd_elem(float g, float av, float z, float mu, float gm, float k, float iw,
-                                            float& dy)
-{
-    dy = av > 0.f ? g : 0.f;
-    return ((dy - gm) - (z - mu) * k) * iw;
-}
-
 }  // namespace azg

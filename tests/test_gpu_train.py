@@ -333,9 +333,11 @@ def train_state_after(x, pi, z, blocks, ch, steps=2, seed=3):
     return got
 
 
-@pytest.mark.parametrize("key,values", [(23, (1, 0)), (24, (1, 0)), (44, (0, 512, 97))])
+@pytest.mark.parametrize("key,values", [(45, (1, 0)), (23, (1, 0)), (24, (1, 0)), (44, (0, 512, 97))])
 def test_train_schedule_keys_bitwise(key, values):
-    """The train step's product tuning keys change only the schedule: where the forward
+    """The train step's product tuning keys change only the schedule: where the backward
+    BN applies run (45: in the epilogue of the dgrad that produces their input, after its
+    in-kernel finalize, or separate bn_bwd_apply passes), where the forward
     BN applies run (23: folded into the next conv's halo staging, or separate passes),
     where the BN finalizes run (24: by the producing conv's last workgroup, or separate
     kernels) and how many workgroups the BN apply passes use (44, grid-stride): two
@@ -427,3 +429,47 @@ def test_train_sum_order_variants_match_oracle(key, value, tag, blocks, ch, B):
         test_gradients_match_oracle(tag, blocks, ch, B)
     finally:
         lib.azg_pv_set_tuning(key, prev)
+
+
+@pytest.mark.parametrize("blocks,ch,B", [(3, 64, 37), (2, 256, 16), (1, 128, 2), (6, 128, 144)])
+def test_dgrad_apply_bitwise_vs_separate_passes(blocks, ch, B):
+    """The dgrads with the BN backward applied in their epilogue (key 45 = 1: every
+    workgroup waits for its N tile's in-kernel finalize) are bitwise equal to the
+    separate bn_bwd_apply passes over three steps, at a ragged batch, C = 256 (four N
+    tiles), one block, and the largest 6x128 batch whose 508 dgrad tiles fit the device
+    at once (two workgroups per CU)."""
+    import _native
+    lib = _native.load_library()
+    b, p = synth_positions(B, seed=97 + B)
+    x = encode_batch(b, p)
+    pi, z = synth_targets(B, seed=98 + B)
+    prev = lib.azg_pv_set_tuning(45, 1)
+    try:
+        got = train_state_after(x, pi, z, blocks, ch, steps=3)
+        lib.azg_pv_set_tuning(45, 0)
+        ref = train_state_after(x, pi, z, blocks, ch, steps=3)
+    finally:
+        lib.azg_pv_set_tuning(45, prev)
+    bad = [i for i, (a, c) in enumerate(zip(ref, got)) if not torch.equal(a, c)]
+    assert not bad, bad
+
+
+def test_dgrad_apply_timeout_raises():
+    """A fused dgrad whose finalize wait times out (key 14 = 0 forces it) sets the sticky
+    status: train_batch raises, the launch drains, and a fresh model trains as before."""
+    import _native
+    lib = _native.load_library()
+    b, p = synth_positions(64, seed=99)
+    x = encode_batch(b, p)
+    pi, z = synth_targets(64, seed=100)
+    ref = train_state_after(x, pi, z, 2, 64, steps=1)
+    m = make_model(2, 64, seed=3)
+    try:
+        lib.azg_pv_set_tuning(14, 0)
+        with pytest.raises(RuntimeError, match="timed out"):
+            m.train_batch(x, pi, z)
+    finally:
+        lib.azg_pv_set_tuning(14, -1)
+        m.engine.clear_status()
+    got = train_state_after(x, pi, z, 2, 64, steps=1)
+    assert all(torch.equal(a, c) for a, c in zip(ref, got))
