@@ -840,6 +840,7 @@ static hipError_t launch_train_t(const float* in, const float* wp, const float* 
 {
     using T = typename TrainTile<C, 8>::T;
     constexpr int lds = halo_lds_bytes<C, T::BN, 4, 1, 8, 0, PRO>();
+    static_assert(!APPLY || (kApplyGofs + T::BM * T::BN) * 4 <= lds, "APPLY: the parked dy tile fits the staging LDS");
     static bool attr_done = false;
     if (!attr_done) {
         hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, true, PRO, 32, 8, APPLY>,
@@ -853,6 +854,7 @@ static hipError_t launch_train_t(const float* in, const float* wp, const float* 
     return hipGetLastError();
 }
 
+#ifdef AZG_AB_STUDIES   // key 45: measured slower, study build only
 // workgroups of the fused dgrad + BN-backward apply launch that can be resident at once
 // (its tiles wait for each other: the host launches it only when all of them fit)
 template <int C>
@@ -909,6 +911,8 @@ hipError_t launch_conv3x3_dgrad_apply(int C, int epi, const float* in, const flo
     }
 #undef AZG_DA
 }
+
+#endif
 
 // Train conv with fused BN partials: (EPI_RAW, XE_STATS) forward, optionally with
 // the input layer's BN applied in the staging (px: PRO_BN / PRO_BN_RES); (EPI_RAW |
@@ -1074,7 +1078,19 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         if (value >= 0) azg::g_train_apply_grid = value;
         return prev;
     }
-    if (key == 45) {  // train: dgrads with the next BN backward applied in their epilogue after an in-kernel finalize (1, default) or separate bn_bwd_apply passes (0); bitwise identical
+    if (key == 46) {  // study build: most workgroups a fused dgrad + apply launch may have (0 = automatic, the default); value -C queries the occupancy bound at C channels; 0 in the product
+#ifndef AZG_AB_STUDIES
+        return 0;
+#endif
+        if (value < 0) return azg::train_apply_capacity(-value);
+        const int prev = azg::g_train_apply_cap;
+        azg::g_train_apply_cap = value;
+        return prev;
+    }
+    if (key == 45) {  // study build: dgrads with the next BN backward applied in their epilogue after an in-kernel finalize (1) or separate bn_bwd_apply passes (0, default); bitwise identical, measured slower; 0 in the product
+#ifndef AZG_AB_STUDIES
+        return 0;
+#endif
         const int prev = azg::g_train_dgrad_apply;
         if (value == 0 || value == 1) azg::g_train_dgrad_apply = value;
         return prev;

@@ -143,9 +143,20 @@ struct FinX {
 // layer is finalized (by the last workgroup of each N tile, FinX) every workgroup applies
 // the BatchNorm backward to its own tile, still in registers -- dz = ((dy - gm) - (z -
 // mean) k) iw with dy = g (act > 0), bn_bwd_apply_kernel's arithmetic -- and stores dz
-// (and dy, the residual gradient, when gres is set); g itself is never stored.  Every
-// workgroup waits for its N tile's finalize (a grid-wide dependency: the host launches
-// this form only when every tile of the launch fits on the device at once).
+// (and dy, the residual gradient, when gres is set); g itself is never stored.
+// Every workgroup waits (bounded) for its N tile's finalize.  The host launches this
+// form only when the tiles should all fit the device at once, but residency is not
+// guaranteed (measured: 6x128 waits time out from ~490 of the 512 slots the occupancy
+// bound promises), so a timed-out wait DEFERS instead of failing: the workgroup stores
+// its dy (write-through, to `out`), drains, and CASes its tile word from any older value
+// to epoch*4 + 1; the finalizer, after publishing, exchanges every tile word of its N
+// tile to epoch*4 + 2 and applies the tiles whose old word was epoch*4 + 1 (acquire,
+// then plain loads of their dy).  A workgroup whose CAS fails saw the finalizer's
+// exchange, so the finalize is published: it acquires and applies its own tile.  Every
+// tile is applied exactly once with the same arithmetic: bitwise equal either way.
+// float offset of the finalizing workgroup's parked dy tile (past the fused finalize's
+// 2 x 8 x 64 fp64 combine buffer); the train launcher checks it fits the dynamic LDS
+constexpr int kApplyGofs = 2 * 8 * 64 * 2;
 struct ApX {
     const float* gm = nullptr;   // the layer's bn_bwd_apply coefficients (written by the finalize)
     const float* kk = nullptr;
@@ -153,9 +164,9 @@ struct ApX {
     float* dz = nullptr;
     float* gres = nullptr;
     unsigned* done = nullptr;    // per N tile: finalizes published (monotonic over launches)
+    unsigned* tword = nullptr;   // per (N tile, M tile): deferral words, epoch-tagged (never reset)
     unsigned epoch = 0;          // the value done[n tile] reaches when this launch's finalize is published
-    unsigned* status = nullptr;  // sticky host-mapped status, set on a timed-out wait
-    unsigned spin = 0;           // polls before the wait is declared timed out (0: time out at once)
+    unsigned spin = 0;           // polls before a wait defers (0: defer at once -- tests)
 };
 
 // partial sums of tiles t = j, j+8, ... (the tile class j of 8) for channel c.
@@ -358,7 +369,9 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
     // XE partials of this thread's 4 channels over its rows
     f32x4 xa = {0.f, 0.f, 0.f, 0.f}, xb = {0.f, 0.f, 0.f, 0.f}, xmu = {0.f, 0.f, 0.f, 0.f};
     f32x4 vk[XE == XE_STATS ? NPASS : 1];
-    f32x4 gk[APPLY ? NPASS : 1], ak[APPLY ? NPASS : 1], zk[APPLY ? NPASS : 1];   // APPLY: g, act, z per pass
+    // APPLY: the masked gradient dy per pass waits out the grid wait in registers (z is
+    // re-read after it, L2-resident); keeping g, act and z spilled to scratch
+    f32x4 gk[APPLY ? NPASS : 1];
     // late store (XE_STATS + fused finalize): the raw tile (kept in vk) is stored after the
     // partials are published and counted, so the arrival waits only for the partials
     const bool late = XE == XE_STATS && EPI == EPI_RAW && fx.cnt != nullptr;
@@ -407,11 +420,7 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                     const float dy = xact[e] > 0.f ? v[e] : 0.f;
                     xa[e] += dy;
                     xb[e] = fmaf(xz[e] - xmu[e], dy, xb[e]);
-                }
-                if constexpr (APPLY) {
-                    gk[p] = v;
-                    ak[p] = xact;
-                    zk[p] = xz;
+                    if constexpr (APPLY) gk[p][e] = dy;
                 }
             }
             if (!late && !APPLY) {
@@ -437,6 +446,22 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
         const __amdgpu_buffer_rsrc_t prs_a = wt_rsrc(ex.pa, (size_t)ntm * C * sizeof(float));
         const __amdgpu_buffer_rsrc_t prs_b = wt_rsrc(ex.pb, (size_t)ntm * C * sizeof(float));
         const int po = mt * C + n0 + tid;
+        // APPLY: dz (and dy as the residual gradient) of one 4-channel run from its
+        // masked dy -- bn_bwd_apply_kernel's arithmetic; coefficients read at the call
+        // (after this thread's acquire)
+        auto apply_store = [&](int o, const f32x4& dy4) {
+            const f32x4 g_ = *(const f32x4*)(ax.gm + col), k_ = *(const f32x4*)(ax.kk + col);
+            const f32x4 w_ = *(const f32x4*)(ax.iw + col);
+            const f32x4 xz = *(const f32x4*)(ex.z + o);
+            f32x4 dz4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float dy;   // dy4 is already masked: act = 1 keeps it
+                dz4[e] = bnbwd_elem(dy4[e], 1.f, xz[e], xmu[e], g_[e], k_[e], w_[e], dy);
+            }
+            store4<true>(ax.dz, wt_rsrc(ax.dz, padded_bytes(M, C)), o, dz4);
+            if (ax.gres) store4<true>(ax.gres, wt_rsrc(ax.gres, padded_bytes(M, C)), o, dy4);
+        };
         __syncthreads();                       // every thread is past its Es reads
         *(f32x4*)(R + er * BN + ec) = xa;
         if (XE == XE_BNBWD) *(f32x4*)(R + RPI * BN + er * BN + ec) = xb;
@@ -517,6 +542,14 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                 }
             }
             if (*flag) {
+                // APPLY: the finalizing workgroup parks its dy in LDS past the combine
+                // buffer while the finalize runs (kApplyGofs; every thread has read *flag)
+                float* Gs = smem + kApplyGofs;
+                if constexpr (APPLY) {
+                    __syncthreads();
+#pragma unroll
+                    for (int p = 0; p < NPASS; ++p) *(f32x4*)(Gs + (p * T::NT + tid) * 4) = gk[p];
+                }
                 // wave w sums tile class w % 8 of channels n0 + lane (coalesced rows of
                 // the [tile][C] partials), the classes combine through LDS in the order
                 // of bn_fin_combine8: bitwise equal to the stand-alone finalize
@@ -539,44 +572,98 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                         __hip_atomic_fetch_add(fx.done + (fx.done_nt ? n0 / BN : 0), 1u, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT);
                 }
+                if constexpr (APPLY) {
+                    // claim every tile word of this N tile (epoch*4 + 2); the tiles that
+                    // deferred (old word epoch*4 + 1) are applied here from their stored dy
+                    unsigned* nlist = (unsigned*)smem;          // the combine buffer is dead
+                    int* list = (int*)smem + 16;                // [ntm] deferred M tiles
+                    if (tid == 0) *nlist = 0u;
+                    __syncthreads();
+                    const unsigned tag = ax.epoch * 4u;
+                    unsigned* tw = ax.tword + (size_t)(n0 / BN) * ntm;
+                    for (int t = tid; t < ntm; t += T::NT) {
+                        const unsigned old =
+                            __hip_atomic_exchange(tw + t, tag + 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (old == tag + 1u) list[atomicAdd(nlist, 1u)] = t;
+                    }
+                    __syncthreads();
+                    const int nd = (int)*nlist;
+                    if (nd) {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        for (int i = 0; i < nd; ++i) {
+                            const int mb = list[i] * BM;
+#pragma unroll
+                            for (int p = 0; p < NPASS; ++p) {
+                                const int m = mb + er + p * RPI;
+                                if (m < M) {
+                                    const int o = pad_off(m, C) + col;
+                                    apply_store(o, *(const f32x4*)(out + o));
+                                }
+                            }
+                        }
+                    }
+                    __syncthreads();   // every thread is past *nlist / list
+#pragma unroll
+                    for (int p = 0; p < NPASS; ++p) gk[p] = *(const f32x4*)(Gs + (p * T::NT + tid) * 4);
+                }
             }
         }
         if constexpr (APPLY) {
-            // this N tile's BN finalize published (one polling lane, ONE agent acquire,
-            // vmcnt(0), barrier; bounded: a timeout sets the sticky status and proceeds)
+            // this N tile's BN finalize published: one polling lane, ONE agent acquire,
+            // vmcnt(0), barrier.  Bounded: past ax.spin polls the tile defers (ApX).
+            unsigned* amode = (unsigned*)smem;   // 0 apply, 1 defer, 2 deferred (done here)
             if (tid == 0) {
                 const unsigned* d = ax.done + n0 / BN;
-                unsigned spins = 0;
+                unsigned spins = 0, mode = 0;
                 while (ax.spin == 0 || __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - ax.epoch >
                                            0x80000000u) {   // done < epoch, modulo 2^32
                     if (++spins > ax.spin) {
-                        if (ax.status) __hip_atomic_store(ax.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        mode = 1;
                         break;
                     }
                     __builtin_amdgcn_s_sleep(2);
                 }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (mode == 0) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                *amode = mode;
             }
             __syncthreads();
-            const f32x4 g_ = *(const f32x4*)(ax.gm + col), k_ = *(const f32x4*)(ax.kk + col);
-            const f32x4 w_ = *(const f32x4*)(ax.iw + col);
-            const __amdgpu_buffer_rsrc_t rz = wt_rsrc(ax.dz, padded_bytes(M, C));
-            const __amdgpu_buffer_rsrc_t rg = wt_rsrc(ax.gres ? ax.gres : ax.dz, padded_bytes(M, C));
+            unsigned mode = *amode;
+            if (mode == 1) {
+                // R1 producer: dy write-through to `out`, every wave drains, a barrier,
+                // then the tile word's CAS (a failed CAS = the finalizer claimed it)
 #pragma unroll
-            for (int p = 0; p < NPASS; ++p) {
-                const int m = m0 + er + p * RPI;
-                if (m < M) {
-                    const int o = pad_off(m, C) + col;
-                    f32x4 dz4, dy4;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        float dy;
-                        dz4[e] = bnbwd_elem(gk[p][e], ak[p][e], zk[p][e], xmu[e], g_[e], k_[e], w_[e], dy);
-                        dy4[e] = dy;
+                for (int p = 0; p < NPASS; ++p) {
+                    const int m = m0 + er + p * RPI;
+                    if (m < M) store4<true>(out, out_rs, pad_off(m, C) + col, gk[p]);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (tid == 0) {
+                    unsigned* w = ax.tword + (size_t)(n0 / BN) * ntm + m0 / BM;
+                    const unsigned tag = ax.epoch * 4u;
+                    unsigned cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const bool deferred =
+                        cur != tag + 2u && __hip_atomic_compare_exchange_strong(w, &cur, tag + 1u, __ATOMIC_RELAXED,
+                                                                                __ATOMIC_RELAXED,
+                                                                                __HIP_MEMORY_SCOPE_AGENT);
+                    if (!deferred) {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     }
-                    store4<true>(ax.dz, rz, o, dz4);
-                    if (ax.gres) store4<true>(ax.gres, rg, o, dy4);
+                    *amode = deferred ? 2u : 0u;
+                }
+                __syncthreads();
+                mode = *amode;
+            }
+            if (mode == 0) {
+#pragma unroll
+                for (int p = 0; p < NPASS; ++p) {
+                    const int m = m0 + er + p * RPI;
+                    if (m < M) apply_store(pad_off(m, C) + col, gk[p]);
                 }
             }
         }

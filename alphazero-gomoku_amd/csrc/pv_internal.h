@@ -45,6 +45,7 @@ hipError_t launch_conv3x3_dgrad_apply(int C, int epi, const float* in, const flo
                                       int M, const EpiX& ex, const FinX& fx, const ApX& ax, hipStream_t st);
 int train_apply_capacity(int C);
 extern int g_train_dgrad_apply;
+extern int g_train_apply_cap;
 extern int g_tower_mode;
 extern int g_tower_shape;
 extern int g_tower_ablation;

@@ -50,8 +50,12 @@ constexpr int HROWS = 128;   // rows per tile of the head-projection backward pa
 
 int g_train_fuse_apply = 1;   // key 23: 1 BN applies folded into the next conv's staging; 0 separate passes
 int g_train_fuse_fin = 1;     // key 24: 1 BN finalize by the last workgroup of the producing conv; 0 separate kernels
-int g_train_dgrad_apply = 1;  // key 45: 1 each dgrad applies the next BN backward in its epilogue (when its tiles
+int g_train_dgrad_apply = 0;  // key 45 (study build): 1 each dgrad applies the next BN backward in its epilogue (when its tiles
                               // fit the device at once); 0 separate bn_bwd_apply passes
+int g_train_apply_cap = 0;    // key 46: most workgroups of a fused dgrad + apply launch (0: automatic)
+// polls (x s_sleep 2, ~1 us each under load) before a fused dgrad's finalize wait defers
+// its tile (pv_halo.h ApX): milliseconds, far above a legitimate wait (< 0.2 ms)
+constexpr unsigned kApplySpin = 1u << 12;
 int g_train_apply_grid = 0;   // key 44: workgroup cap of the BN apply / BN-backward apply passes (0: one float4 per thread)
 int g_train_bwd_tower = 0;    // key 43 (study build): 1 the tower backward as one persistent launch (slower,
                               // measured); 0 the two-stream schedule (product)
@@ -76,6 +80,7 @@ struct TrainWS {
     int slab_S = 0;                                // splits one slab holds
     unsigned* fincnt = nullptr;   // fused BN finalize arrival counters: [0..3] forward / two-stream, 4 per conv after
     unsigned* apdone = nullptr;   // fused dgrad + BN-backward apply: finalizes published per N tile (monotonic)
+    unsigned* aptword = nullptr;  // ... and its per-(N tile, M tile) deferral words (pv_halo.h ApX)
     unsigned ap_epoch = 0;        // launches of it so far
     // heads
     float *zh = nullptr, *fp = nullptr, *fv = nullptr, *hv = nullptr, *dpre = nullptr;
@@ -693,6 +698,8 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     w->fincnt = (unsigned*)t;
     A(t, 16, true);
     w->apdone = (unsigned*)t;
+    A(t, (size_t)((M + 127) / 128) * 4, true);
+    w->aptword = (unsigned*)t;
     A(t, (size_t)head_proj_stats_groups(M) * 6 * 2, false);
     w->hsp1 = (double*)t;
     A(t, (size_t)head_dgrad_groups(cap) * 6 * 2, false);
@@ -1096,7 +1103,16 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         // epilogue once its in-kernel finalize is published (all its tiles must fit the
         // device at once: they wait for each other); the next conv's dZ (and the residual
         // gradient) come straight out of the dgrad, g itself is never stored
-        const bool dga = g_train_dgrad_apply && ffin && ntt * (C / 64) <= train_apply_capacity(C);
+        // automatic bound: 15/16 of the occupancy bound (measured at 6x128: every wait
+        // met up to 480 of 512 workgroups, deferrals from ~490; past the bound the
+        // launch is still correct, ApX, only slower)
+#ifdef AZG_AB_STUDIES
+        const int occ = train_apply_capacity(C);
+        const int dga_cap = g_train_apply_cap > 0 ? std::min(g_train_apply_cap, occ) : occ - occ / 16;
+        const bool dga = g_train_dgrad_apply && ffin && ntt * (C / 64) <= dga_cap;
+#else
+        const bool dga = false;   // key 45 is a study-build variant (measured slower)
+#endif
         auto dgrad_apply = [&](int epi, const float* dz_in, const float* wd, const float* res, const float* xact,
                                const float* xz, int xl, float* dz_out, float* gres_out) -> int32_t {
             int pr = prof_begin(h, AZG_PROF_TRAIN_CONV, st, B);
@@ -1113,11 +1129,16 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             ax.dz = dz_out;
             ax.gres = gres_out;
             ax.done = w->apdone;
+            ax.tword = w->aptword;
             ax.epoch = ++w->ap_epoch;
-            ax.status = h->status_dev;
-            ax.spin = g_tower_spin_limit;
+            ax.spin = std::min(g_tower_spin_limit, kApplySpin);
+#ifdef AZG_AB_STUDIES
             AZG_CK(launch_conv3x3_dgrad_apply(C, epi, dz_in, wd, res, w->DH, M, ex, fx, ax, st),
                    "train: conv3x3 dgrad + BN backward apply");
+#else
+            (void)epi, (void)dz_in, (void)wd, (void)res, (void)ex, (void)ax;
+            return set_error("train: the fused dgrad + BN backward apply is in the study build only", hipErrorInvalidValue);
+#endif
             prof_end(h, pr, st);
             return 0;
         };

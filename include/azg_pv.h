@@ -183,7 +183,12 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          launch (pv_bwd_tower.hip, 1) or the product's two-stream schedule (0);
  *          bitwise identical, measured slower; returns 0 in the product library;
  *   key 44: train BN apply / BN-backward apply passes: workgroup cap of their
- *          grid-stride launch (0 = one float4 per thread, default); bitwise identical;
+ *          grid-stride launch (0 = four float4 per thread, default); bitwise identical;
+ *   keys 45, 46: study build only: train backward dgrads that apply the BN backward of
+ *          the layer below in their epilogue after an in-kernel finalize (45 = 1; 46 the
+ *          workgroup bound of that launch); bitwise identical, measured slower (the
+ *          waiting workgroups starve the concurrent weight-grad stream); return 0 in the
+ *          product library;
  *   key 31: study build only: the 64x64 / 128x64 towers with sc1 dependent loads
  *          and no acquire (two or more workgroups per CU: outside the microarch
  *          guide's measured envelope; the product uses the acquire there and the

@@ -16,4 +16,5 @@ python scripts/train_trace_segments.py $O/tr/run_kernel_trace.csv
 python scripts/train_step_timeline.py $O/tr/run_kernel_trace.csv > $O/timeline.txt
 timeout -k 10 300 python -u scripts/train_r3_probe.py --ab "45=1;45=0" > $O/probe.log 2>&1
 s=$?; tail -1 $O/probe.log; [ $s -eq 0 ] || exit $s
+timeout -k 10 300 python -u scripts/apply_cap_probe.py > $O/capprobe.log 2>&1; s=$?; cat $O/capprobe.log | tail -9; [ $s -eq 0 ] || exit $s
 echo done

@@ -129,6 +129,8 @@ def test_gradients_match_oracle(tag, blocks, ch, B):
     losses = torch.empty(3, device=dev)
     eng.train_backward(torch.from_numpy(x).to(dev), torch.from_numpy(pi).to(dev), torch.from_numpy(z).to(dev),
                        losses)
+    torch.cuda.synchronize()
+    eng.check_status()   # no in-kernel wait of the step timed out
     mk = gpu_masks(eng, blocks, B)
     want, (pl, vl), pre = masked_grads_fp64(st, blocks, ch, x, pi, z, mk, return_pre=True)
     np.testing.assert_allclose(losses.cpu().numpy(), [pl, vl, pl + vl], rtol=1e-5, atol=1e-7)
@@ -333,11 +335,9 @@ def train_state_after(x, pi, z, blocks, ch, steps=2, seed=3):
     return got
 
 
-@pytest.mark.parametrize("key,values", [(45, (1, 0)), (23, (1, 0)), (24, (1, 0)), (44, (0, 512, 97))])
+@pytest.mark.parametrize("key,values", [(23, (1, 0)), (24, (1, 0)), (44, (0, 512, 97))])
 def test_train_schedule_keys_bitwise(key, values):
-    """The train step's product tuning keys change only the schedule: where the backward
-    BN applies run (45: in the epilogue of the dgrad that produces their input, after its
-    in-kernel finalize, or separate bn_bwd_apply passes), where the forward
+    """The train step's product tuning keys change only the schedule: where the forward
     BN applies run (23: folded into the next conv's halo staging, or separate passes),
     where the BN finalizes run (24: by the producing conv's last workgroup, or separate
     kernels) and how many workgroups the BN apply passes use (44, grid-stride): two
@@ -431,45 +431,52 @@ def test_train_sum_order_variants_match_oracle(key, value, tag, blocks, ch, B):
         lib.azg_pv_set_tuning(key, prev)
 
 
-@pytest.mark.parametrize("blocks,ch,B", [(3, 64, 37), (2, 256, 16), (1, 128, 2), (6, 128, 144)])
-def test_dgrad_apply_bitwise_vs_separate_passes(blocks, ch, B):
+@pytest.mark.parametrize("blocks,ch,B,cap,spin", [
+    (3, 64, 37, 0, -1), (2, 256, 16, 0, -1), (1, 128, 2, 0, -1),
+    # the largest 6x128 batch under the automatic bound (480 of 512 workgroups)
+    (6, 128, 136, 0, -1),
+    # bound lifted to the occupancy bound: 508 workgroups, where waits are measured to
+    # time out and tiles defer to the finalizer
+    (6, 128, 144, 512, -1),
+    # every wait defers at once (key 14 = 0): the finalizers apply every other tile
+    (6, 128, 128, 0, 0), (2, 256, 16, 0, 0), (3, 64, 37, 0, 0)])
+def test_dgrad_apply_bitwise_vs_separate_passes(blocks, ch, B, cap, spin):
     """The dgrads with the BN backward applied in their epilogue (key 45 = 1: every
-    workgroup waits for its N tile's in-kernel finalize) are bitwise equal to the
-    separate bn_bwd_apply passes over three steps, at a ragged batch, C = 256 (four N
-    tiles), one block, and the largest 6x128 batch whose 508 dgrad tiles fit the device
-    at once (two workgroups per CU)."""
+    workgroup waits, bounded, for its N tile's in-kernel finalize, and defers its tile to
+    the finalizer if the wait times out -- pv_halo.h ApX) are bitwise equal to the
+    separate bn_bwd_apply passes over three steps: at a ragged batch, C = 256 (four N
+    tiles), one block, the largest 6x128 batch under the automatic bound, above it, and
+    with every tile deferred.  Study build only (measured slower: DESIGN.md §4)."""
     import _native
     lib = _native.load_library()
+    if lib.azg_pv_set_tuning(15, 0) != 1:
+        pytest.skip("the fused dgrad + BN backward apply is in the study build only (make study; AZG_PV_LIB)")
     b, p = synth_positions(B, seed=97 + B)
     x = encode_batch(b, p)
     pi, z = synth_targets(B, seed=98 + B)
     prev = lib.azg_pv_set_tuning(45, 1)
+    prev_cap = lib.azg_pv_set_tuning(46, cap)
     try:
+        lib.azg_pv_set_tuning(14, spin)
         got = train_state_after(x, pi, z, blocks, ch, steps=3)
+        lib.azg_pv_set_tuning(14, -1)
         lib.azg_pv_set_tuning(45, 0)
         ref = train_state_after(x, pi, z, blocks, ch, steps=3)
     finally:
+        lib.azg_pv_set_tuning(14, -1)
         lib.azg_pv_set_tuning(45, prev)
+        lib.azg_pv_set_tuning(46, prev_cap)
     bad = [i for i, (a, c) in enumerate(zip(ref, got)) if not torch.equal(a, c)]
     assert not bad, bad
 
 
-def test_dgrad_apply_timeout_raises():
-    """A fused dgrad whose finalize wait times out (key 14 = 0 forces it) sets the sticky
-    status: train_batch raises, the launch drains, and a fresh model trains as before."""
+def test_dgrad_apply_automatic_bound():
+    """Key 46's query: the occupancy bound the automatic 15/16 margin is taken from is
+    two 512-thread workgroups per CU on every CU.  Study build only."""
     import _native
     lib = _native.load_library()
-    b, p = synth_positions(64, seed=99)
-    x = encode_batch(b, p)
-    pi, z = synth_targets(64, seed=100)
-    ref = train_state_after(x, pi, z, 2, 64, steps=1)
-    m = make_model(2, 64, seed=3)
-    try:
-        lib.azg_pv_set_tuning(14, 0)
-        with pytest.raises(RuntimeError, match="timed out"):
-            m.train_batch(x, pi, z)
-    finally:
-        lib.azg_pv_set_tuning(14, -1)
-        m.engine.clear_status()
-    got = train_state_after(x, pi, z, 2, 64, steps=1)
-    assert all(torch.equal(a, c) for a, c in zip(ref, got))
+    if lib.azg_pv_set_tuning(15, 0) != 1:
+        pytest.skip("the fused dgrad + BN backward apply is in the study build only (make study; AZG_PV_LIB)")
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    for c in (64, 128, 256):
+        assert lib.azg_pv_set_tuning(46, -c) == 2 * cus
