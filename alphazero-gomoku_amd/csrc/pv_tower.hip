@@ -256,7 +256,9 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     a.spin_limit = g_tower_spin_limit;
     a.group = g_tower_group == 1 ? C / (shape == 8 || shape == 5 ? 64 : 128) : 1;
     a.xq = g_tower_group == 2 ? sync + tower_tile_words(2 * NB, M) : nullptr;
+#ifndef AZG_AB_STUDIES
     if (shape == 10 && C != 128) return hipErrorInvalidValue;   // 16-wave tile: C = 128 only (C = 256 spills)
+#endif
     a.abl = g_tower_ablation;
     float* X = act[0];
     float* H = act[1];
@@ -304,6 +306,10 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
         if (g_tower_var == 6) return launch_tower_t<128, 64, 4, 1, 8, 6>(a, st, nullptr);
         if (g_tower_var == 7) return launch_tower_t<128, 64, 4, 1, 8, 7>(a, st, nullptr);
         if (g_tower_var == 12) return launch_tower_t<128, 64, 4, 1, 8, 12>(a, st, nullptr);
+    }
+    if (C == 256 && shape == 10) {   // 16-wave 128x128 tile at C = 256 (spills; traffic study)
+        if (g_tower_var == 1) return launch_tower_t<256, 128, 4, 1, 16, 32>(a, st, nullptr);
+        return launch_tower_t<256, 128, 4, 1, 16, 16>(a, st, nullptr);
     }
     if (C == 128 && shape == 10 && g_tower_var == 1)   // 16-wave tile with the acquire instead of sc1 loads
         return launch_tower_t<128, 128, 4, 1, 16, 32>(a, st, nullptr);

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--group", type=int, default=1, help="tower claims (key 17: 0 tile, 1 M tile, 2 per-XCD queues)")
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--channels", type=int, default=128)
+    ap.add_argument("--check", action="store_true", help="compare the outputs bitwise with the 128x64 tower (shape 8)")
     args = ap.parse_args()
     import _native
     lib = _native.load_library()
@@ -71,6 +72,15 @@ def main():
         if k in ("conv3x3", "tower", "tower16"):
             per = flop * (2 * args.blocks if k.startswith("tower") else 1)
             out[k]["mfma_frac"] = round(per / (ms / n / 1e3) / 157.3e12, 4)
+    if args.check:
+        lib.azg_pv_set_tuning(6, 8)
+        lib.azg_pv_set_tuning(10, 0)
+        p8, v8 = torch.empty_like(probs), torch.empty_like(values)
+        eng.forward_into(x, p8, v8)
+        torch.cuda.synchronize()
+        eng.check_status()
+        out["bitwise_vs_shape8"] = bool(torch.equal(p8, probs) and torch.equal(v8, values))
+        out["max_abs_diff_vs_shape8"] = float(max((p8 - probs).abs().max(), (v8 - values).abs().max()))
     print(json.dumps(out), flush=True)
 
 
