@@ -1051,9 +1051,9 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         return 0;
 #endif
     }
-    if (key == 17) {  // persistent tower claims: 0 one tile, 1 one M tile x all N tiles, 2 one tile from eight per-XCD-group queues
+    if (key == 17) {  // persistent tower claims: 0 one tile, 1 one M tile x all N tiles (default)
         const int prev = azg::g_tower_group;
-        if (value >= 0 && value <= 2) azg::g_tower_group = value;
+        if (value >= 0 && value <= 1) azg::g_tower_group = value;
         return prev;
     }
     if (key == 22) {  // per-layer 128x64 conv tile-body variant (1 default; 0, 4, 5 A/B, bitwise identical)

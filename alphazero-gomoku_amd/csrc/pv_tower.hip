@@ -63,17 +63,11 @@ struct TowerArgs {
                          // N tile's halo rows are hits in that XCD's L2)
     int abl;             // timing studies only (0 in the product; results not valid otherwise):
                          // bit 1 skips the dependency wait + acquire, bit 2 the publish drain
-    unsigned* xq;        // non-null: eight claim queues, one per workgroup group blockIdx % 8 (the
-                         // workgroups of a group share an XCD -- observed placement, speed only):
-                         // queue q holds the M tiles [q*mtiles/8, (q+1)*mtiles/8) of every layer,
-                         // layer-major; its counter is sync[0] for q = 0, xq[q - 1] otherwise.  A
-                         // drained queue's workgroups steal from the next queues.
 };
 
 constexpr unsigned kSpinLimit = 1u << 22;    // x s_sleep(2): seconds, far above any tile time
 unsigned g_tower_spin_limit = kSpinLimit;    // tuning key 14 (tests: 0 forces the timeout path)
-int g_tower_group = 1;                       // tuning key 17: 1 (default) = claim an M tile with all its N tiles;
-                                             // 2 = one N tile per claim from eight per-XCD-group queues
+int g_tower_group = 1;                       // tuning key 17: 1 (default) = claim an M tile with all its N tiles
 #ifdef AZG_AB_STUDIES
 int g_tower_coh = 0;   // study key 31: sc1 dependent loads with 64x64 / 128x64 tiles (OUTSIDE the guide's envelope)
 #endif
@@ -108,40 +102,18 @@ __global__ __launch_bounds__(64 * NW_, (tower_min_waves<BN_, NW_>())) void conv_
     const int tid = threadIdx.x;
     const int mtiles = (a.M + T::BM - 1) / T::BM;
     const int grp = a.group;                     // N tiles per claim (1 or NTN)
+    const int tpl = mtiles * (NTN / grp);        // claims per layer
+    const int total = tpl * a.nlayers;
+    unsigned* work = a.sync;
     unsigned* err = a.sync + 1;
     unsigned* cnt = a.sync + 4;
-    // claim queue q: its first M tile, M tiles, claims per layer and in all, counter
-    const bool xq = a.xq != nullptr;
-    int q = xq ? (int)(blockIdx.x & 7) : 0, qtried = 1;
-    int qm0 = 0, tpl = 0, total = 0;
-    unsigned* work = a.sync;
-    auto set_queue = [&](int qq) {
-        qm0 = xq ? qq * mtiles / 8 : 0;
-        const int qn = xq ? (qq + 1) * mtiles / 8 - qm0 : mtiles;
-        tpl = qn * (NTN / grp);
-        total = tpl * a.nlayers;
-        work = (xq && qq > 0) ? a.xq + qq - 1 : a.sync;
-    };
-    set_queue(q);
 
     if (tid == 0) s_claim[0] = (int)__hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     int w = s_claim[0];
-    while (true) {
-        if (w >= total) {
-            // this queue is drained: steal from the next one (every queue once)
-            if (!xq || qtried == 8) break;
-            q = (q + 1) & 7;
-            ++qtried;
-            set_queue(q);
-            __syncthreads();                      // every wave has read s_claim
-            if (tid == 0) s_claim[0] = (int)__hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __syncthreads();
-            w = s_claim[0];
-            continue;
-        }
+    while (w < total) {
         const int l = w / tpl, t = w - l * tpl;
-        const int mt = qm0 + t / (NTN / grp), nt0 = (t % (NTN / grp)) * grp;
+        const int mt = t / (NTN / grp), nt0 = (t - mt * (NTN / grp)) * grp;
         __syncthreads();                          // every wave has read s_claim
         if (tid == 0) {
             // next claim now: its latency overlaps this tile (read after the tile)
@@ -224,16 +196,11 @@ int g_tower_var = 0;     // halo_tile VAR of the 128x64 C=128 tower (0 = product
 int g_tower_shape = 8;   // forced shape when g_tower_mode == 1: 5 = 64x64 (4 waves), 8 = 128x64 (8 waves),
                          // 10 = 128x128 (16 waves, one workgroup per CU; C = 128)
 
-// [0] work counter (queue 0), [1] error word, [4 ..) per-(layer, M tile) counters, then
-// the counters of queues 1..7 (key 17 = 2)
-static size_t tower_tile_words(int nlayers, int M)
-{
-    const int mtiles = (M + 63) / 64;   // the smallest BM (64) has the most M tiles
-    return (size_t)(4 + nlayers * mtiles);
-}
+// [0] work counter, [1] error word, [4 ..) per-(layer, M tile) counters
 size_t tower_sync_bytes(int nlayers, int M)
 {
-    return ((tower_tile_words(nlayers, M) + 7) * sizeof(unsigned) + 15) / 16 * 16;
+    const int mtiles = (M + 63) / 64;   // the smallest BM (64) has the most M tiles
+    return ((size_t)(4 + nlayers * mtiles) * sizeof(unsigned) + 15) / 16 * 16;
 }
 
 // Eval residual tower in one launch: NB blocks, conv1 X -> H (BN, ReLU), conv2
@@ -254,8 +221,7 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     a.sync = sync;
     a.status = status;
     a.spin_limit = g_tower_spin_limit;
-    a.group = g_tower_group == 1 ? C / (shape == 8 || shape == 5 ? 64 : 128) : 1;
-    a.xq = g_tower_group == 2 ? sync + tower_tile_words(2 * NB, M) : nullptr;
+    a.group = g_tower_group ? C / (shape == 8 || shape == 5 ? 64 : 128) : 1;
 #ifndef AZG_AB_STUDIES
     if (shape == 10 && C != 128) return hipErrorInvalidValue;   // 16-wave tile: C = 128 only (C = 256 spills)
 #endif

@@ -223,7 +223,7 @@ def test_persistent_tower_bitwise_equals_per_layer_launches(blocks, ch, batches)
             lib.azg_pv_set_tuning(5, 1)
             for shape in ((5, 8, 10) if ch == 128 else (5, 8)):
                 lib.azg_pv_set_tuning(6, shape)
-                for group in (0, 1, 2):   # claims (key 17): one tile, one M tile, per-XCD-group queues
+                for group in (0, 1):   # claims (key 17): one tile, one M tile
                     prev_group = lib.azg_pv_set_tuning(17, group)
                     for rep in range(3):
                         p1, v1, l1 = eng.forward(x, want_logits=True)

@@ -1,0 +1,101 @@
+"""Register / scratch budgets of the product library's hot kernels, read from the built
+code object (no GPU needed).
+
+Round 4 lost 5 % of the headline self-play rate to a change that only added claim-queue
+bookkeeping to the persistent tower: the kernel went from 32 to 200 bytes of scratch
+per lane and the self-play autotuner started picking the per-layer convs.  This test
+pins the scratch (spill) bytes and VGPR counts of the kernels the bench and the train
+step spend their time in, so such a regression fails on CPU before it reaches a GPU.
+Budgets are the measured values of the product build (round 4).
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(REPO, "alphazero-gomoku_amd", "libazg_pv.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+# (kernel-name regex on the mangled name, max private_segment_fixed_size bytes)
+SCRATCH_BUDGET = [
+    # persistent eval tower (the self-play / forward headline kernel)
+    (r"conv_towerILi128ELi64ELi4ELi1ELi8ELi32E", 32),
+    (r"conv_towerILi128ELi64ELi2ELi1ELi4ELi32E", 60),
+    (r"conv_towerILi256ELi64ELi4ELi1ELi8ELi32E", 32),
+    (r"conv_towerILi256ELi64ELi2ELi1ELi4ELi32E", 60),
+    (r"conv_towerILi64ELi64E", 0),
+    (r"conv_towerILi128ELi128ELi4ELi1ELi16E", 40),
+    # train convs at C <= 128 (the 6x128 train step) and the weight grad
+    (r"conv3x3_trainILi(64|128)E", 0),
+    (r"conv3x3_wgrad_natILi", 0),
+    (r"wgrad_reduce_kernel", 0),
+    (r"stem_mfma", 0),
+]
+
+
+def _kernels():
+    if not os.path.exists(LIB):
+        pytest.skip("libazg_pv.so not built (run __graft_entry__.build())")
+    objcopy = shutil.which("objcopy")
+    bundler = os.path.join(LLVM, "clang-offload-bundler")
+    readelf = os.path.join(LLVM, "llvm-readelf")
+    if not objcopy or not os.path.exists(bundler) or not os.path.exists(readelf):
+        pytest.skip("objcopy / clang-offload-bundler / llvm-readelf not available")
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        fb, co = os.path.join(d, "fb.bin"), os.path.join(d, "co.elf")
+        subprocess.run([objcopy, f"--dump-section=.hip_fatbin={fb}", LIB, os.path.join(d, "x.so")], check=True,
+                       capture_output=True)
+        # one offload bundle per translation unit, concatenated (4 KiB aligned)
+        raw = open(fb, "rb").read()
+        magic = b"__CLANG_OFFLOAD_BUNDLE__"
+        starts = [m.start() for m in re.finditer(re.escape(magic), raw)]
+        notes = ""
+        for i, st in enumerate(starts):
+            part = os.path.join(d, f"b{i}.bin")
+            with open(part, "wb") as f:
+                f.write(raw[st:starts[i + 1] if i + 1 < len(starts) else len(raw)])
+            subprocess.run([bundler, "--unbundle", "--type=o", f"--input={part}",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True,
+                           capture_output=True)
+            notes += subprocess.run([readelf, "--notes", co], check=True, capture_output=True, text=True).stdout
+    out = {}
+    name = None
+    for line in notes.splitlines():
+        m = re.match(r"\s*\.name:\s+(\S+)", line)
+        if m:
+            name = m.group(1)
+            out.setdefault(name, {})
+            continue
+        m = re.match(r"\s*\.(private_segment_fixed_size|vgpr_count|agpr_count|vgpr_spill_count):\s+(\d+)", line)
+        if m and name:
+            out[name][m.group(1)] = int(m.group(2))
+    return out
+
+
+def test_hot_kernels_within_scratch_budget():
+    ks = _kernels()
+    assert ks, "no kernels found in the code object"
+    bad, seen = [], set()
+    for pat, budget in SCRATCH_BUDGET:
+        hits = [n for n in ks if re.search(pat, n)]
+        assert hits, f"no kernel matches {pat}"
+        seen.add(pat)
+        for n in hits:
+            s = ks[n].get("private_segment_fixed_size", 0)
+            if s > budget:
+                bad.append((n, s, budget))
+    assert not bad, "kernels above their scratch budget (spills): " + "; ".join(
+        f"{n}: {s} B > {b} B" for n, s, b in bad)
+
+
+def test_hot_kernels_fit_two_workgroups_per_cu():
+    """The 8-wave tower / train tiles run two workgroups per CU: <= 128 VGPRs (+AGPRs)."""
+    ks = _kernels()
+    for n, v in ks.items():
+        if re.search(r"conv_towerILi(128|256)ELi64ELi4ELi1ELi8E|conv3x3_trainILi(64|128)E", n):
+            total = v.get("vgpr_count", 0) + v.get("agpr_count", 0)
+            assert total <= 128, (n, total)
