@@ -511,8 +511,9 @@ def train_leg(model, args, rank, world, dist, dev, local, blocks=BLOCKS, ch=CHAN
     model.grad_hook = None
     flop = train_flop(blocks, ch) * B
     nparam = model.engine.nparam
+    coll = "RCCL" if dist is not None and dist.get_backend() == "nccl" else "gloo (shared-GPU rehearsal)"
     return {"config": f"{blocks}x{ch}, {B} samples/GPU (global {B * world}), "
-                      f"{f'RCCL all-reduce of the flat fp32 gradient ({nparam * 4 / 1e6:.2f} MB) + ' if world > 1 else ''}"
+                      f"{f'{coll} all-reduce of the flat fp32 gradient ({nparam * 4 / 1e6:.2f} MB) + ' if world > 1 else ''}"
                       f"clip 3.0 + Adam",
             "samples_per_s": round(B * K * world / dt, 1), "ms_per_step": round(dt / K * 1e3, 3), "steps": K,
             "flop_per_step": flop, "mfma_frac": round(flop / (dt / K) / PEAK_F32_MFMA, 4)}
