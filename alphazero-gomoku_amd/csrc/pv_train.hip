@@ -278,7 +278,9 @@ __global__ __launch_bounds__(512) void bn_fin_tiles_kernel(const float* __restri
 // shift)), the same expression as the forward's apply): the mask is formed from z and
 // the layer's folded scale / shift instead of reading act -- bitwise the same mask,
 // one 4-B-per-channel tensor less to read.
-template <int C, bool GRES, bool WT = false, bool MZ = false>
+// (kApplyU = 4 float4 per thread measured fastest in the step: 2.843-2.851 ms vs 2.854-
+// 2.861 at 2 and 2.864-2.871 at 1, scripts/gpu_r4m.sh)
+template <int C, bool GRES, bool WT = false, bool MZ = false, int U = kApplyU>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* __restrict__ g, const float* __restrict__ act, const float* __restrict__ z,
     const float* __restrict__ mean, const float* __restrict__ gm, const float* __restrict__ kk,
@@ -288,7 +290,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     // grid-stride, kApplyU float4 per thread and pass with every load issued before the
     // first store; the stride is a multiple of C/4, so a thread's channels are fixed and
     // its per-channel coefficients are loaded once
-    constexpr int F4 = C / 4, U = kApplyU;
+    constexpr int F4 = C / 4;
     const int total = M * F4;
     const int stride = gridDim.x * blockDim.x;
     const __amdgpu_buffer_rsrc_t rz = wt_rsrc(dz, padded_bytes(M, C));

@@ -32,20 +32,21 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_nat(const float* __restr
     wgrad_nat_tile<C, true, 4>(dz, x, slab, M, S, split, tap, (t / W::NT) * W::BT, (t % W::NT) * W::BT, smem);
 }
 
-// dW = the S slabs summed in a fixed order (pv_wgrad.h wgrad_reduce_elems), 4
-// elements per thread
-constexpr int kReduceNV = 4;
+// dW = the S slabs summed in a fixed order (pv_wgrad.h wgrad_reduce_vec4: the per-element
+// order of wgrad_reduce_elems), one float4 run per thread.  In the step this pass shares
+// the chip with a dgrad; a quarter of the load instructions of the 4-scalar form made the
+// step 21 us faster (2.843-2.848 vs 2.864-2.872 ms, scripts/gpu_r4l.sh; two float4 per
+// thread: 2.875-2.882), bitwise equal.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ dw,
                                                            int C, int S)
 {
-    wgrad_reduce_elems<kReduceNV>(slab, dw, C, S, blockIdx.x * 256 * kReduceNV + threadIdx.x, 256);
+    wgrad_reduce_vec4<1>(slab, dw, C, S, blockIdx.x * 256 + threadIdx.x, 256);
 }
 
 hipError_t launch_wgrad_reduce(int C, const float* slab, float* dw, int S, hipStream_t st)
 {
-    const int total = 9 * C * C;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 256 * kReduceNV - 1) / (256 * kReduceNV)), dim3(256), 0, st,
-                       slab, dw, C, S);
+    const int total4 = 9 * C * C / 4;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total4 + 255) / 256), dim3(256), 0, st, slab, dw, C, S);
     return hipGetLastError();
 }
 
