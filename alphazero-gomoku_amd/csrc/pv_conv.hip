@@ -1125,7 +1125,7 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     if (key == 10) {  // persistent-tower tile body variant (A/B studies, bitwise identical)
         const int prev = azg::g_tower_var;
 #ifdef AZG_AB_STUDIES
-        if ((value >= 0 && value <= 8) || value == 12 || value == 13) azg::g_tower_var = value;
+        if ((value >= 0 && value <= 8) || value == 12 || value == 13 || value == 14 || value == 15 || value == 16) azg::g_tower_var = value;
 #else
         if (value == 0) azg::g_tower_var = value;
 #endif

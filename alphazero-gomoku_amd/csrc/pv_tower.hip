@@ -272,11 +272,20 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
         if (g_tower_var == 6) return launch_tower_t<128, 64, 4, 1, 8, 6>(a, st, nullptr);
         if (g_tower_var == 7) return launch_tower_t<128, 64, 4, 1, 8, 7>(a, st, nullptr);
         if (g_tower_var == 12) return launch_tower_t<128, 64, 4, 1, 8, 12>(a, st, nullptr);
+        if (g_tower_var == 14) return launch_tower_t<128, 64, 4, 1, 8, 33>(a, st, nullptr);
+        if (g_tower_var == 15) return launch_tower_t<128, 64, 4, 1, 8, 34>(a, st, nullptr);
     }
+    if (C == 256 && shape == 8 && g_tower_var == 2)   // weights staged two chunks ahead (VAR bit 2), C = 256
+        return launch_tower_t<256, 64, 4, 1, 8, 34>(a, st, nullptr);
+    if (C == 256 && shape == 8 && g_tower_var == 16)   // round-3 product body at C = 256 (VAR 32)
+        return launch_tower_t<256, 64, 4, 1, 8, 32>(a, st, nullptr);
+    if (C == 256 && shape == 5 && g_tower_var == 16)   // round-3 64x64 body at C = 256 (VAR 32)
+        return launch_tower_t<256, 64, 2, 1, 4, 32>(a, st, nullptr);
     if (C == 256 && shape == 10) {   // 16-wave 128x128 tile at C = 256 (spills; traffic study)
         if (g_tower_var == 1) return launch_tower_t<256, 128, 4, 1, 16, 32>(a, st, nullptr);
         return launch_tower_t<256, 128, 4, 1, 16, 16>(a, st, nullptr);
     }
+    if (C == 128 && shape == 5 && g_tower_var == 14) return launch_tower_t<128, 64, 2, 1, 4, 33>(a, st, nullptr);
     if (C == 128 && shape == 10 && g_tower_var == 1)   // 16-wave tile with the acquire instead of sc1 loads
         return launch_tower_t<128, 128, 4, 1, 16, 32>(a, st, nullptr);
     if (C == 128 && shape == 8 && g_tower_var == 13)   // round-2 acquire form: 64-bit pointer loads (VAR 0)
@@ -291,8 +300,14 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
             if (shape == 8) return launch_tower_t<128, 64, 4, 1, 8, 32>(a, st, nullptr);
             return launch_tower_t<128, 64, 2, 1, 4, 32>(a, st, nullptr);
         case 256:
-            if (shape == 8) return launch_tower_t<256, 64, 4, 1, 8, 32>(a, st, nullptr);
-            return launch_tower_t<256, 64, 2, 1, 4, 32>(a, st, nullptr);
+            // C = 256: halo rows keyed on the board position (VAR bit 1: conflict-free
+            // fragment reads, unpadded epilogue tile), bitwise equal, scripts/gpu_r4o.sh:
+            // 128x64 tile 90.0 vs 86.4 % of peak at B = 512, equal at 128 / 300 / 1024 /
+            // 2048; 64x64 tile 79.4 vs 77.4 % at B = 300, 89.5 vs 88.2 % at 512, 55.4 vs
+            // 56.4 % at 128.  At C = 128 the same body is slower (89.5 vs 91.2 % at B =
+            // 3456), so C = 128 keeps VAR 32.
+            if (shape == 8) return launch_tower_t<256, 64, 4, 1, 8, 33>(a, st, nullptr);
+            return launch_tower_t<256, 64, 2, 1, 4, 33>(a, st, nullptr);
         default: return hipErrorInvalidValue;
     }
 }

@@ -322,7 +322,7 @@ def tower_knames(ch, blocks):
     n = 2 * blocks
     return {"tower16": f"azg::conv_tower<{ch},128,4,1,16,16> (persistent residual tower, 16-wave 128x128 tiles, one "
                        f"workgroup per CU: {n} fused 3x3 conv + BN (+ residual) + ReLU layers per launch)",
-            "tower": f"azg::conv_tower<{ch},64,*,32> (persistent residual tower, 128x64 / 64x64 tiles, acquire "
+            "tower": f"azg::conv_tower<{ch},64,*,{33 if ch >= 256 else 32}> (persistent residual tower, 128x64 / 64x64 tiles, acquire "
                      f"hand-off: {n} fused 3x3 conv + BN (+ residual) + ReLU layers per launch)",
             "conv3x3": f"azg::conv3x3_halo<{ch},*> (per-layer fused 3x3 conv + BN (+ residual) + ReLU)"}
 
