@@ -833,25 +833,38 @@ hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, cons
 
 // Train convs: 128 x 64 tiles, 8 waves (two workgroups per CU), buffer-resource operand
 // addressing (halo_tile VAR 32), outputs stored write-through.
-template <int C, int EPI, int XE, int PRO = PRO_NONE, bool APPLY = false>
-static hipError_t launch_train_t(const float* in, const float* wp, const float* resid, float* out, int M,
-                                 const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st,
-                                 const ApX& ax = ApX{})
+template <int C, int EPI, int XE, int PRO, bool APPLY, int VAR>
+static hipError_t launch_train_v(const float* in, const float* wp, const float* resid, float* out, int M,
+                                 const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st, const ApX& ax)
 {
     using T = typename TrainTile<C, 8>::T;
-    constexpr int lds = halo_lds_bytes<C, T::BN, 4, 1, 8, 0, PRO>();
+    constexpr int lds = halo_lds_bytes<C, T::BN, 4, 1, 8, VAR, PRO>();
     static_assert(!APPLY || (kApplyGofs + T::BM * T::BN) * 4 <= lds, "APPLY: the parked dy tile fits the staging LDS");
     static bool attr_done = false;
     if (!attr_done) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, true, PRO, 32, 8, APPLY>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, true, PRO, VAR, 8, APPLY>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
         attr_done = true;
     }
     dim3 grid(((M + T::BM - 1) / T::BM) * (C / T::BN));
-    hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, true, PRO, 32, 8, APPLY>), grid, dim3(T::NT), lds, st, in, wp,
+    hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, true, PRO, VAR, 8, APPLY>), grid, dim3(T::NT), lds, st, in, wp,
                        resid, out, M, ex, px, fx, ax);
     return hipGetLastError();
+}
+
+int g_train_var = 32;   // key 50 (A/B): halo_tile VAR of the operand-prologue-free train convs (32, or 33: halo
+                        // rows keyed on the board position)
+
+template <int C, int EPI, int XE, int PRO = PRO_NONE, bool APPLY = false>
+static hipError_t launch_train_t(const float* in, const float* wp, const float* resid, float* out, int M,
+                                 const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st,
+                                 const ApX& ax = ApX{})
+{
+    if constexpr (PRO == PRO_NONE && !APPLY) {
+        if (g_train_var == 33) return launch_train_v<C, EPI, XE, PRO, APPLY, 33>(in, wp, resid, out, M, ex, px, fx, st, ax);
+    }
+    return launch_train_v<C, EPI, XE, PRO, APPLY, 32>(in, wp, resid, out, M, ex, px, fx, st, ax);
 }
 
 #ifdef AZG_AB_STUDIES   // key 45: measured slower, study build only
@@ -1076,6 +1089,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     if (key == 44) {  // train: workgroup cap of the BN apply / BN-backward apply passes (0 = one float4 per thread); bitwise identical
         const int prev = azg::g_train_apply_grid;
         if (value >= 0) azg::g_train_apply_grid = value;
+        return prev;
+    }
+    if (key == 50) {  // A/B: halo_tile VAR of the prologue-free train convs (32 default, 33 board-keyed halo rows); bitwise identical
+        const int prev = azg::g_train_var;
+        if (value == 32 || value == 33) azg::g_train_var = value;
         return prev;
     }
     if (key == 46) {  // study build: most workgroups a fused dgrad + apply launch may have (0 = automatic, the default); value -C queries the occupancy bound at C channels; 0 in the product
