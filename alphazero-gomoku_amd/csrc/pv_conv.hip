@@ -853,17 +853,13 @@ static hipError_t launch_train_v(const float* in, const float* wp, const float* 
     return hipGetLastError();
 }
 
-int g_train_var = 32;   // key 50 (A/B): halo_tile VAR of the operand-prologue-free train convs (32, or 33: halo
-                        // rows keyed on the board position)
-
 template <int C, int EPI, int XE, int PRO = PRO_NONE, bool APPLY = false>
 static hipError_t launch_train_t(const float* in, const float* wp, const float* resid, float* out, int M,
                                  const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st,
                                  const ApX& ax = ApX{})
 {
-    if constexpr (PRO == PRO_NONE && !APPLY) {
-        if (g_train_var == 33) return launch_train_v<C, EPI, XE, PRO, APPLY, 33>(in, wp, resid, out, M, ex, px, fx, st, ax);
-    }
+    // (the board-keyed halo body, VAR 33, measured equal for the prologue-free train convs:
+    // 2.865-2.869 vs 2.866-2.874 ms at 6x128 and within noise at 10x256, scripts/gpu_r4p.sh)
     return launch_train_v<C, EPI, XE, PRO, APPLY, 32>(in, wp, resid, out, M, ex, px, fx, st, ax);
 }
 
@@ -1089,11 +1085,6 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     if (key == 44) {  // train: workgroup cap of the BN apply / BN-backward apply passes (0 = one float4 per thread); bitwise identical
         const int prev = azg::g_train_apply_grid;
         if (value >= 0) azg::g_train_apply_grid = value;
-        return prev;
-    }
-    if (key == 50) {  // A/B: halo_tile VAR of the prologue-free train convs (32 default, 33 board-keyed halo rows); bitwise identical
-        const int prev = azg::g_train_var;
-        if (value == 32 || value == 33) azg::g_train_var = value;
         return prev;
     }
     if (key == 46) {  // study build: most workgroups a fused dgrad + apply launch may have (0 = automatic, the default); value -C queries the occupancy bound at C channels; 0 in the product

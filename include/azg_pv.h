@@ -184,9 +184,6 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          bitwise identical, measured slower; returns 0 in the product library;
  *   key 44: train BN apply / BN-backward apply passes: workgroup cap of their
  *          grid-stride launch (0 = four float4 per thread, default); bitwise identical;
- *   key 50: halo_tile body of the train convs without an operand prologue (every dgrad,
- *          the forward convs at C = 256): 32 (default) or 33 (halo rows keyed on the board
- *          position); bitwise identical;
  *   keys 45, 46: study build only: train backward dgrads that apply the BN backward of
  *          the layer below in their epilogue after an in-kernel finalize (45 = 1; 46 the
  *          workgroup bound of that launch); bitwise identical, measured slower (the
