@@ -89,6 +89,12 @@ def dist_setup(n_gpus: int):
             local = local % torch.cuda.device_count()
             torch.cuda.set_device(local)
             dist.init_process_group("gloo")
+            # the persistent tower assumes it owns the GPU (one process per GPU): with two
+            # processes on one card the driver time-slices their queues, and a suspended
+            # wave's claimed tiles can outlast the dependency spin bound (seen once in the
+            # round-4 rehearsal: the sticky status raised).  The rehearsal runs per-layer.
+            import _native
+            _native.load_library().azg_pv_set_tuning(5, 0)
         else:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
