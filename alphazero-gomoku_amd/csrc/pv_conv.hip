@@ -231,10 +231,10 @@ struct TrainTile {
     static constexpr int BN = NWT >= 16 ? 128 : 64;
     using T = ConvTile<C, BN, 4, 1, NWT>;
 };
-template <int C, int EPI, int XE, bool WT, int PRO = PRO_NONE, int VAR = 32, int NWT = 8, bool APPLY = false>
+template <int C, int EPI, int XE, bool WT, int PRO = PRO_NONE, int VAR = 32, int NWT = 8>
 __global__ __launch_bounds__(64 * NWT) __attribute__((amdgpu_waves_per_eu(4))) void conv3x3_train(
     const float* __restrict__ in, const float* __restrict__ wp, const float* __restrict__ resid,
-    float* __restrict__ out, int M, EpiX ex, ProX px, FinX fx, ApX ax)
+    float* __restrict__ out, int M, EpiX ex, ProX px, FinX fx)
 {
     using T = typename TrainTile<C, NWT>::T;
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -242,9 +242,9 @@ __global__ __launch_bounds__(64 * NWT) __attribute__((amdgpu_waves_per_eu(4))) v
     const int L = blockIdx.x, nt = gridDim.x;
     const int xcd = L & 7, q8 = nt >> 3, r8 = nt & 7;
     const int t = xcd * q8 + min(xcd, r8) + (L >> 3);
-    halo_tile<C, T::BN, 4, 1, NWT, EPI, WT, 0, VAR, XE, PRO, APPLY>(in, wp, nullptr, nullptr, resid, out,
-                                                                 wt_rsrc(out, padded_bytes(M, C)), M, (t / NTN) * T::BM,
-                                                                 (t % NTN) * T::BN, smem, ex, px, fx, ax);
+    halo_tile<C, T::BN, 4, 1, NWT, EPI, WT, 0, VAR, XE, PRO>(in, wp, nullptr, nullptr, resid, out,
+                                                          wt_rsrc(out, padded_bytes(M, C)), M, (t / NTN) * T::BM,
+                                                          (t % NTN) * T::BN, smem, ex, px, fx);
 }
 
 // Stem conv 3->C (K = 27) on the VALU: 0.2 % of the forward FLOPs.  One
@@ -833,95 +833,33 @@ hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, cons
 
 // Train convs: 128 x 64 tiles, 8 waves (two workgroups per CU), buffer-resource operand
 // addressing (halo_tile VAR 32), outputs stored write-through.
-template <int C, int EPI, int XE, int PRO, bool APPLY, int VAR>
+template <int C, int EPI, int XE, int PRO, int VAR>
 static hipError_t launch_train_v(const float* in, const float* wp, const float* resid, float* out, int M,
-                                 const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st, const ApX& ax)
+                                 const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st)
 {
     using T = typename TrainTile<C, 8>::T;
     constexpr int lds = halo_lds_bytes<C, T::BN, 4, 1, 8, VAR, PRO>();
-    static_assert(!APPLY || (kApplyGofs + T::BM * T::BN) * 4 <= lds, "APPLY: the parked dy tile fits the staging LDS");
     static bool attr_done = false;
     if (!attr_done) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, true, PRO, VAR, 8, APPLY>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv3x3_train<C, EPI, XE, true, PRO, VAR, 8>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
         attr_done = true;
     }
     dim3 grid(((M + T::BM - 1) / T::BM) * (C / T::BN));
-    hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, true, PRO, VAR, 8, APPLY>), grid, dim3(T::NT), lds, st, in, wp,
-                       resid, out, M, ex, px, fx, ax);
+    hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, true, PRO, VAR, 8>), grid, dim3(T::NT), lds, st, in, wp,
+                       resid, out, M, ex, px, fx);
     return hipGetLastError();
 }
 
-template <int C, int EPI, int XE, int PRO = PRO_NONE, bool APPLY = false>
+template <int C, int EPI, int XE, int PRO = PRO_NONE>
 static hipError_t launch_train_t(const float* in, const float* wp, const float* resid, float* out, int M,
-                                 const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st,
-                                 const ApX& ax = ApX{})
+                                 const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st)
 {
     // (the board-keyed halo body, VAR 33, measured equal for the prologue-free train convs:
     // 2.865-2.869 vs 2.866-2.874 ms at 6x128 and within noise at 10x256, scripts/gpu_r4p.sh)
-    return launch_train_v<C, EPI, XE, PRO, APPLY, 32>(in, wp, resid, out, M, ex, px, fx, st, ax);
+    return launch_train_v<C, EPI, XE, PRO, 32>(in, wp, resid, out, M, ex, px, fx, st);
 }
-
-#ifdef AZG_AB_STUDIES   // key 45: measured slower, study build only
-// workgroups of the fused dgrad + BN-backward apply launch that can be resident at once
-// (its tiles wait for each other: the host launches it only when all of them fit)
-template <int C>
-static int train_apply_capacity_t()
-{
-    using T = typename TrainTile<C, 8>::T;
-    constexpr int lds = halo_lds_bytes<C, T::BN, 4, 1, 8, 0, PRO_NONE>();
-    static int cap = -1;
-    if (cap < 0) {
-        int per_cu = 0, dev = 0, cus = 0;
-        if (hipFuncSetAttribute((const void*)conv3x3_train<C, EPI_ADD, XE_BNBWD, true, PRO_NONE, 32, 8, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &per_cu, (const void*)conv3x3_train<C, EPI_ADD, XE_BNBWD, true, PRO_NONE, 32, 8, true>, T::NT, lds) !=
-                hipSuccess ||
-            hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
-            cap = 0;
-        } else {
-            int per_cu2 = 0;
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &per_cu2, (const void*)conv3x3_train<C, EPI_RAW, XE_BNBWD, true, PRO_NONE, 32, 8, true>, T::NT, lds);
-            cap = std::min(per_cu, per_cu2) * cus;
-        }
-    }
-    return cap;
-}
-int train_apply_capacity(int C)
-{
-    switch (C) {
-        case 64: return train_apply_capacity_t<64>();
-        case 128: return train_apply_capacity_t<128>();
-        case 256: return train_apply_capacity_t<256>();
-        default: return 0;
-    }
-}
-
-// dgrad + the BN backward of the layer below applied in the epilogue (ApX), after the
-// in-kernel finalize of that layer (fx.cnt and fx.done must be set)
-hipError_t launch_conv3x3_dgrad_apply(int C, int epi, const float* in, const float* wp, const float* resid, float* out,
-                                      int M, const EpiX& ex, const FinX& fx, const ApX& ax, hipStream_t st)
-{
-    const ProX p0{};
-#define AZG_DA(CC)                                                                                              \
-    case CC:                                                                                                    \
-        if (epi == EPI_RAW) return launch_train_t<CC, EPI_RAW, XE_BNBWD, PRO_NONE, true>(in, wp, resid, out, M, ex, p0, fx, st, ax); \
-        if (epi == EPI_ADD) return launch_train_t<CC, EPI_ADD, XE_BNBWD, PRO_NONE, true>(in, wp, resid, out, M, ex, p0, fx, st, ax); \
-        return hipErrorInvalidValue;
-    switch (C) {
-        AZG_DA(64)
-        AZG_DA(128)
-        AZG_DA(256)
-        default: return hipErrorInvalidValue;
-    }
-#undef AZG_DA
-}
-
-#endif
 
 // Train conv with fused BN partials: (EPI_RAW, XE_STATS) forward, optionally with
 // the input layer's BN applied in the staging (px: PRO_BN / PRO_BN_RES); (EPI_RAW |
@@ -1075,33 +1013,9 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         azg::g_conv_tail_split = value ? 1 : 0;
         return prev;
     }
-    if (key == 43) {  // study build: tower backward as one persistent launch (1; slower, measured) or the two-stream schedule (0, product); bitwise identical
-        const int prev = azg::g_train_bwd_tower;
-#ifdef AZG_AB_STUDIES
-        if (value == 0 || value == 1) azg::g_train_bwd_tower = value;
-#endif
-        return prev;
-    }
     if (key == 44) {  // train: workgroup cap of the BN apply / BN-backward apply passes (0 = one float4 per thread); bitwise identical
         const int prev = azg::g_train_apply_grid;
         if (value >= 0) azg::g_train_apply_grid = value;
-        return prev;
-    }
-    if (key == 46) {  // study build: most workgroups a fused dgrad + apply launch may have (0 = automatic, the default); value -C queries the occupancy bound at C channels; 0 in the product
-#ifndef AZG_AB_STUDIES
-        return 0;
-#endif
-        if (value < 0) return azg::train_apply_capacity(-value);
-        const int prev = azg::g_train_apply_cap;
-        azg::g_train_apply_cap = value;
-        return prev;
-    }
-    if (key == 45) {  // study build: dgrads with the next BN backward applied in their epilogue after an in-kernel finalize (1) or separate bn_bwd_apply passes (0, default); bitwise identical, measured slower; 0 in the product
-#ifndef AZG_AB_STUDIES
-        return 0;
-#endif
-        const int prev = azg::g_train_dgrad_apply;
-        if (value == 0 || value == 1) azg::g_train_dgrad_apply = value;
         return prev;
     }
     if (key == 24) {  // train: BN finalize fused into the producing conv's last workgroup (1, default) or separate (0; two-stream backward); bitwise identical

@@ -82,10 +82,6 @@ constexpr int halo_lds_bytes()
 // Tower epilogue: BN scale/shift, residual added when `resid` is non-null, ReLU
 // (EPI_BN_RELU / EPI_BN_RES_RELU chosen at run time, same arithmetic).
 constexpr int EPI_BN_OPTRES_RELU = 4;
-// Dgrad epilogue with the residual gradient added when `resid` is non-null (EPI_ADD /
-// EPI_RAW chosen at run time, same arithmetic): one tile body for both dgrads of a
-// residual block in the persistent train backward (pv_bwd_tower.hip).
-constexpr int EPI_OPTADD = 5;
 
 // Train-step epilogue extras (template XE of halo_tile / halo_epilogue), computed
 // from the tile while it is on chip so no separate pass re-reads the conv output:
@@ -125,10 +121,6 @@ struct FinX {
     unsigned* cnt = nullptr;     // fused: arrival counter per N tile (0 at launch; reset by the last arriver).
                                  // XE_STATS: the tile is stored after the arrival count, so the
                                  // write-through drain of the 32 KB tile leaves the finalize's path
-    unsigned* done = nullptr;    // in-launch consumers (pv_bwd_tower.hip, ApX): the results are stored
-                                 // write-through, drained, and each finalizing workgroup then adds 1
-                                 // (to done[n tile] when done_nt, else to done[0])
-    int done_nt = 0;
     const float* gamma = nullptr;
     const float* beta = nullptr;                            // FWD
     float *rmean = nullptr, *rvar = nullptr;                // FWD running stats
@@ -137,48 +129,8 @@ struct FinX {
     float *ggamma = nullptr, *gbeta = nullptr;              // !FWD: parameter grads
     float *gm_o = nullptr, *k_o = nullptr, *iw_o = nullptr; // !FWD: bn_bwd_apply coefficients
 };
-// Dgrad + BatchNorm-backward apply in one launch (XE_BNBWD with APPLY, the train
-// backward's two-stream schedule, key 45): the dgrad's output g is the gradient of the
-// BN + ReLU output of the layer whose backward sums its epilogue produces, so once that
-// layer is finalized (by the last workgroup of each N tile, FinX) every workgroup applies
-// the BatchNorm backward to its own tile, still in registers -- dz = ((dy - gm) - (z -
-// mean) k) iw with dy = g (act > 0), bn_bwd_apply_kernel's arithmetic -- and stores dz
-// (and dy, the residual gradient, when gres is set); g itself is never stored.
-// Every workgroup waits (bounded) for its N tile's finalize.  The host launches this
-// form only when the tiles should all fit the device at once, but residency is not
-// guaranteed (measured: 6x128 waits time out from ~490 of the 512 slots the occupancy
-// bound promises), so a timed-out wait DEFERS instead of failing: the workgroup stores
-// its dy (write-through, to `out`), drains, and CASes its tile word from any older value
-// to epoch*4 + 1; the finalizer, after publishing, exchanges every tile word of its N
-// tile to epoch*4 + 2 and applies the tiles whose old word was epoch*4 + 1 (acquire,
-// then plain loads of their dy).  A workgroup whose CAS fails saw the finalizer's
-// exchange, so the finalize is published: it acquires and applies its own tile.  Every
-// tile is applied exactly once with the same arithmetic: bitwise equal either way.
-// float offset of the finalizing workgroup's parked dy tile (past the fused finalize's
-// 2 x 8 x 64 fp64 combine buffer); the train launcher checks it fits the dynamic LDS
-constexpr int kApplyGofs = 2 * 8 * 64 * 2;
-struct ApX {
-    const float* gm = nullptr;   // the layer's bn_bwd_apply coefficients (written by the finalize)
-    const float* kk = nullptr;
-    const float* iw = nullptr;
-    float* dz = nullptr;
-    float* gres = nullptr;
-    unsigned* done = nullptr;    // per N tile: finalizes published (monotonic over launches)
-    unsigned* tword = nullptr;   // per (N tile, M tile): deferral words, epoch-tagged (never reset)
-    unsigned epoch = 0;          // the value done[n tile] reaches when this launch's finalize is published
-    unsigned spin = 0;           // polls before a wait defers (0: defer at once -- tests)
-};
-
-// partial sums of tiles t = j, j+8, ... (the tile class j of 8) for channel c.
-// COH: every load is an agent-scope relaxed atomic load (`global_load_dword sc1`,
-// L1 bypassed) -- the consumer form that may replace an acquire only inside the
-// microarch guide's measured one-workgroup-per-CU envelope; the product's fused
-// finalize runs at two workgroups per CU and uses an acquire + plain loads instead.
-__device__ __forceinline__ float coh_load(const float* p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <bool FWD, bool COH = false>
+// partial sums of tiles t = j, j+8, ... (the tile class j of 8) for channel c
+template <bool FWD>
 __device__ __forceinline__ void bn_fin_accum(const float* __restrict__ pa, const float* __restrict__ pb, int ldc,
                                              int ntile, int prow, int M, int c, int j, double& v0, double& v1)
 {
@@ -192,8 +144,8 @@ __device__ __forceinline__ void bn_fin_accum(const float* __restrict__ pa, const
 #pragma unroll
         for (int k = 0; k < 32; ++k) {
             const int t = min(t0 + 8 * k, ntile - 1);
-            a[k] = COH ? coh_load(pa + (size_t)t * ldc + c) : pa[(size_t)t * ldc + c];
-            b[k] = COH ? coh_load(pb + (size_t)t * ldc + c) : pb[(size_t)t * ldc + c];
+            a[k] = pa[(size_t)t * ldc + c];
+            b[k] = pb[(size_t)t * ldc + c];
         }
         __builtin_amdgcn_sched_barrier(0);   // hipcc otherwise interleaves each load with its wait
 #pragma unroll
@@ -214,13 +166,6 @@ __device__ __forceinline__ void bn_fin_accum(const float* __restrict__ pa, const
 }
 // combine the 8 tile classes in the fixed order ((0+4)+(2+6))+((1+5)+(3+7)) and write
 // channel c's results
-// publish one result: write-through (agent-scope relaxed store = global_store sc1) when
-// a consumer of the same launch reads it (f.done), plain otherwise
-__device__ __forceinline__ void fin_put(float* p, float v, bool wt)
-{
-    if (wt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else *p = v;
-}
 template <bool FWD>
 __device__ __forceinline__ void bn_fin_out(double v0, double v1, int M, int c, const FinX& f)
 {
@@ -241,12 +186,11 @@ __device__ __forceinline__ void bn_fin_out(double v0, double v1, int M, int c, c
         f.rvar[c] = (float)((double)BN_MOMENTUM * unb + (1.0 - (double)BN_MOMENTUM) * (double)f.rvar[c]);
     } else {
         const double inv = (double)f.inv_i[c];
-        const bool wt = f.done != nullptr;
-        fin_put(f.ggamma + c, (float)(v1 * inv), wt);
-        fin_put(f.gbeta + c, (float)v0, wt);
-        fin_put(f.gm_o + c, (float)(v0 / (double)M), wt);
-        fin_put(f.k_o + c, (float)(v1 * inv * inv / (double)M), wt);
-        fin_put(f.iw_o + c, (float)inv * f.gamma[c], wt);
+        f.ggamma[c] = (float)(v1 * inv);
+        f.gbeta[c] = (float)v0;
+        f.gm_o[c] = (float)(v0 / (double)M);
+        f.k_o[c] = (float)(v1 * inv * inv / (double)M);
+        f.iw_o[c] = (float)inv * f.gamma[c];
     }
 }
 // 8 waves x 64 lanes: wave w holds tile class w of channel c (lane); the classes are
@@ -311,15 +255,13 @@ __device__ __forceinline__ int halo_vkey(int row)
 // RBUF: how the residual is read -- 0 plain pointer loads; 1 buffer loads (default
 // cache policy); 2 buffer loads with sc1 (the tower's one-workgroup-per-CU hand-off)
 template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1, int ABL, int ELD, bool EARLY = false,
-          int XE = XE_NONE, int RBUF = 0, bool APPLY = false>
+          int XE = XE_NONE, int RBUF = 0>
 __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<C, BN_, WM_, TM_, NW_>::TN],
                                               const float* __restrict__ scale, const float* __restrict__ shift,
                                               const float* __restrict__ resid, float* __restrict__ out,
                                               __amdgpu_buffer_rsrc_t out_rs, int M, int m0, int n0, float* smem,
-                                              const EpiX& ex = EpiX{}, const FinX& fx = FinX{},
-                                              const ApX& ax = ApX{})
+                                              const EpiX& ex = EpiX{}, const FinX& fx = FinX{})
 {
-    static_assert(!APPLY || XE == XE_BNBWD, "the fused BN-backward apply follows a dgrad epilogue");
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
     constexpr int BM = T::BM, BN = T::BN, WN = T::WN, TM = T::TM, TN = T::TN;
     const int tid = threadIdx.x;
@@ -334,8 +276,7 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
     const int ec = (tid % CPR) * 4;
     const int er = tid / CPR;
     const int col = n0 + ec;
-    const bool has_res = EPI == EPI_BN_RES_RELU || EPI == EPI_ADD ||
-                         ((EPI == EPI_BN_OPTRES_RELU || EPI == EPI_OPTADD) && resid);
+    const bool has_res = EPI == EPI_BN_RES_RELU || EPI == EPI_ADD || (EPI == EPI_BN_OPTRES_RELU && resid);
     // EARLY: the residual / scale / shift loads are issued before the accumulator
     // tile goes through LDS, so their latency overlaps the ds_write + barrier
     f32x4 rve[EARLY ? NPASS : 1];
@@ -369,9 +310,6 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
     // XE partials of this thread's 4 channels over its rows
     f32x4 xa = {0.f, 0.f, 0.f, 0.f}, xb = {0.f, 0.f, 0.f, 0.f}, xmu = {0.f, 0.f, 0.f, 0.f};
     f32x4 vk[XE == XE_STATS ? NPASS : 1];
-    // APPLY: the masked gradient dy per pass waits out the grid wait in registers (z is
-    // re-read after it, L2-resident); keeping g, act and z spilled to scratch
-    f32x4 gk[APPLY ? NPASS : 1];
     // late store (XE_STATS + fused finalize): the raw tile (kept in vk) is stored after the
     // partials are published and counted, so the arrival waits only for the partials
     const bool late = XE == XE_STATS && EPI == EPI_RAW && fx.cnt != nullptr;
@@ -408,8 +346,6 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                     x = has_res ? fmaxf(x * s4[e] + t4[e] + rv[e], 0.f) : fmaxf(x * s4[e] + t4[e], 0.f);
                 } else if (EPI == EPI_ADD) {
                     x = x + rv[e];
-                } else if (EPI == EPI_OPTADD) {
-                    if (has_res) x = x + rv[e];
                 }
                 v[e] = x;
             }
@@ -420,10 +356,9 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                     const float dy = xact[e] > 0.f ? v[e] : 0.f;
                     xa[e] += dy;
                     xb[e] = fmaf(xz[e] - xmu[e], dy, xb[e]);
-                    if constexpr (APPLY) gk[p][e] = dy;
                 }
             }
-            if (!late && !APPLY) {
+            if (!late) {
                 if constexpr (SC1) {
                     __builtin_amdgcn_raw_buffer_store_b128(
                         __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), out_rs, o * 4, 0, 16);
@@ -446,22 +381,6 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
         const __amdgpu_buffer_rsrc_t prs_a = wt_rsrc(ex.pa, (size_t)ntm * C * sizeof(float));
         const __amdgpu_buffer_rsrc_t prs_b = wt_rsrc(ex.pb, (size_t)ntm * C * sizeof(float));
         const int po = mt * C + n0 + tid;
-        // APPLY: dz (and dy as the residual gradient) of one 4-channel run from its
-        // masked dy -- bn_bwd_apply_kernel's arithmetic; coefficients read at the call
-        // (after this thread's acquire)
-        auto apply_store = [&](int o, const f32x4& dy4) {
-            const f32x4 g_ = *(const f32x4*)(ax.gm + col), k_ = *(const f32x4*)(ax.kk + col);
-            const f32x4 w_ = *(const f32x4*)(ax.iw + col);
-            const f32x4 xz = *(const f32x4*)(ex.z + o);
-            f32x4 dz4;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                float dy;   // dy4 is already masked: act = 1 keeps it
-                dz4[e] = bnbwd_elem(dy4[e], 1.f, xz[e], xmu[e], g_[e], k_[e], w_[e], dy);
-            }
-            store4<true>(ax.dz, wt_rsrc(ax.dz, padded_bytes(M, C)), o, dz4);
-            if (ax.gres) store4<true>(ax.gres, wt_rsrc(ax.gres, padded_bytes(M, C)), o, dy4);
-        };
         __syncthreads();                       // every thread is past its Es reads
         *(f32x4*)(R + er * BN + ec) = xa;
         if (XE == XE_BNBWD) *(f32x4*)(R + RPI * BN + er * BN + ec) = xb;
@@ -542,14 +461,6 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                 }
             }
             if (*flag) {
-                // APPLY: the finalizing workgroup parks its dy in LDS past the combine
-                // buffer while the finalize runs (kApplyGofs; every thread has read *flag)
-                float* Gs = smem + kApplyGofs;
-                if constexpr (APPLY) {
-                    __syncthreads();
-#pragma unroll
-                    for (int p = 0; p < NPASS; ++p) *(f32x4*)(Gs + (p * T::NT + tid) * 4) = gk[p];
-                }
                 // wave w sums tile class w % 8 of channels n0 + lane (coalesced rows of
                 // the [tile][C] partials), the classes combine through LDS in the order
                 // of bn_fin_combine8: bitwise equal to the stand-alone finalize
@@ -560,111 +471,9 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                 double* red = (double*)smem;   // [groups][2][8][64]
                 const int wv = (tid >> 6) & 7, ln = tid & 63, ch = n0 + (tid >> 9) * 64 + ln;
                 double v0, v1;
-                bn_fin_accum<XE == XE_STATS, false>(ex.pa, ex.pb, C, ntm, BM, M, ch, wv, v0, v1);
+                bn_fin_accum<XE == XE_STATS>(ex.pa, ex.pb, C, ntm, BM, M, ch, wv, v0, v1);
                 bn_fin_combine8<XE == XE_STATS>(v0, v1, red, M, ch, true, fx);
                 if (tid == 0) __hip_atomic_store(fx.cnt + n0 / BN, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (fx.done) {
-                    // R1 producer: the results were stored write-through; every storing wave
-                    // drains, a barrier, then one agent-scope add (consumers poll + acquire)
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __syncthreads();
-                    if (tid == 0)
-                        __hip_atomic_fetch_add(fx.done + (fx.done_nt ? n0 / BN : 0), 1u, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                }
-                if constexpr (APPLY) {
-                    // claim every tile word of this N tile (epoch*4 + 2); the tiles that
-                    // deferred (old word epoch*4 + 1) are applied here from their stored dy
-                    unsigned* nlist = (unsigned*)smem;          // the combine buffer is dead
-                    int* list = (int*)smem + 16;                // [ntm] deferred M tiles
-                    if (tid == 0) *nlist = 0u;
-                    __syncthreads();
-                    const unsigned tag = ax.epoch * 4u;
-                    unsigned* tw = ax.tword + (size_t)(n0 / BN) * ntm;
-                    for (int t = tid; t < ntm; t += T::NT) {
-                        const unsigned old =
-                            __hip_atomic_exchange(tw + t, tag + 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (old == tag + 1u) list[atomicAdd(nlist, 1u)] = t;
-                    }
-                    __syncthreads();
-                    const int nd = (int)*nlist;
-                    if (nd) {
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        for (int i = 0; i < nd; ++i) {
-                            const int mb = list[i] * BM;
-#pragma unroll
-                            for (int p = 0; p < NPASS; ++p) {
-                                const int m = mb + er + p * RPI;
-                                if (m < M) {
-                                    const int o = pad_off(m, C) + col;
-                                    apply_store(o, *(const f32x4*)(out + o));
-                                }
-                            }
-                        }
-                    }
-                    __syncthreads();   // every thread is past *nlist / list
-#pragma unroll
-                    for (int p = 0; p < NPASS; ++p) gk[p] = *(const f32x4*)(Gs + (p * T::NT + tid) * 4);
-                }
-            }
-        }
-        if constexpr (APPLY) {
-            // this N tile's BN finalize published: one polling lane, ONE agent acquire,
-            // vmcnt(0), barrier.  Bounded: past ax.spin polls the tile defers (ApX).
-            unsigned* amode = (unsigned*)smem;   // 0 apply, 1 defer, 2 deferred (done here)
-            if (tid == 0) {
-                const unsigned* d = ax.done + n0 / BN;
-                unsigned spins = 0, mode = 0;
-                while (ax.spin == 0 || __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - ax.epoch >
-                                           0x80000000u) {   // done < epoch, modulo 2^32
-                    if (++spins > ax.spin) {
-                        mode = 1;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                if (mode == 0) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-                *amode = mode;
-            }
-            __syncthreads();
-            unsigned mode = *amode;
-            if (mode == 1) {
-                // R1 producer: dy write-through to `out`, every wave drains, a barrier,
-                // then the tile word's CAS (a failed CAS = the finalizer claimed it)
-#pragma unroll
-                for (int p = 0; p < NPASS; ++p) {
-                    const int m = m0 + er + p * RPI;
-                    if (m < M) store4<true>(out, out_rs, pad_off(m, C) + col, gk[p]);
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (tid == 0) {
-                    unsigned* w = ax.tword + (size_t)(n0 / BN) * ntm + m0 / BM;
-                    const unsigned tag = ax.epoch * 4u;
-                    unsigned cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const bool deferred =
-                        cur != tag + 2u && __hip_atomic_compare_exchange_strong(w, &cur, tag + 1u, __ATOMIC_RELAXED,
-                                                                                __ATOMIC_RELAXED,
-                                                                                __HIP_MEMORY_SCOPE_AGENT);
-                    if (!deferred) {
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    }
-                    *amode = deferred ? 2u : 0u;
-                }
-                __syncthreads();
-                mode = *amode;
-            }
-            if (mode == 0) {
-#pragma unroll
-                for (int p = 0; p < NPASS; ++p) {
-                    const int m = m0 + er + p * RPI;
-                    if (m < M) apply_store(pad_off(m, C) + col, gk[p]);
-                }
             }
         }
     }
@@ -877,13 +686,13 @@ __device__ __forceinline__ void halo_mainloop_glds(const float* __restrict__ in,
 // barriers, bit 8 replaces LDS fragment reads by register values, bit 16 skips the
 // epilogue stores (kept live by a never-true compare).
 template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, bool SC1 = false, int ABL = 0, int VAR = 0,
-          int XE = XE_NONE, int PRO = PRO_NONE, bool APPLY = false>
+          int XE = XE_NONE, int PRO = PRO_NONE>
 __device__ __forceinline__ void halo_tile(
     const float* __restrict__ in, const float* __restrict__ wp,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ resid, float* __restrict__ out, __amdgpu_buffer_rsrc_t out_rs,
     int M, int m0, int n0, float* smem, const EpiX& ex = EpiX{}, const ProX& px = ProX{},
-    const FinX& fx = FinX{}, const ApX& ax = ApX{})
+    const FinX& fx = FinX{})
 {
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
     if constexpr ((VAR & 4) != 0) {   // LDS-DMA staging
@@ -1182,8 +991,8 @@ __device__ __forceinline__ void halo_tile(
 
     // the last chunk ended with a barrier: the staging buffers are free
     halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, (VSWZ ? BN : BN + 8), (VAR & 8) != 0, XE,
-                  (VAR & 16) ? 2 : (VAR & 32) ? 1 : 0, APPLY>(
-        acc, scale, shift, resid, out, out_rs, M, m0, n0, smem, ex, fx, ax);
+                  (VAR & 16) ? 2 : (VAR & 32) ? 1 : 0>(
+        acc, scale, shift, resid, out, out_rs, M, m0, n0, smem, ex, fx);
 }
 
 }  // namespace azg

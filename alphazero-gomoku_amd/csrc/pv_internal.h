@@ -40,19 +40,12 @@ constexpr int TRAIN_BM = 128;   // rows per M tile of conv3x3_train (BN partials
 hipError_t launch_conv3x3_train(int C, int epi, int xe, const float* in, const float* wp, const float* resid,
                                 float* out, int M, const EpiX& ex, hipStream_t st, const ProX* px = nullptr,
                                 const FinX* fx = nullptr);
-struct ApX;
-hipError_t launch_conv3x3_dgrad_apply(int C, int epi, const float* in, const float* wp, const float* resid, float* out,
-                                      int M, const EpiX& ex, const FinX& fx, const ApX& ax, hipStream_t st);
-int train_apply_capacity(int C);
-extern int g_train_dgrad_apply;
-extern int g_train_apply_cap;
 extern int g_tower_mode;
 extern int g_tower_shape;
 extern int g_tower_ablation;
 extern int g_tower_var;
 extern int g_train_fuse_apply;
 extern int g_train_fuse_fin;
-extern int g_train_bwd_tower;
 extern int g_train_apply_grid;
 extern int g_wgrad_splits;
 hipError_t launch_stem_stats(int C, const float* x, const float* ws, float* out, int B, float* pa, float* pb,

@@ -20,13 +20,10 @@
 // staging and finalizes its own BN in its last workgroup) -> the head chain
 // (pv_train_heads.hip) -> the tower backward on two streams (dgrads on the caller's,
 // weight grads on a low-priority side stream) -> head weight grads, stem backward;
-// train_apply: clip + Adam + the next step's weight packs.  (The study build also has
-// the tower backward as ONE persistent launch, pv_bwd_tower.hip, key 43: bitwise equal,
-// measured slower.)
+// train_apply: clip + Adam + the next step's weight packs.
 #include "pv_internal.h"
 #include "pv_halo.h"
 #include "pv_train_heads.h"
-#include "pv_bwd_tower.h"
 #include "pv_wgrad.h"
 
 #include <algorithm>
@@ -50,15 +47,7 @@ constexpr int HROWS = 128;   // rows per tile of the head-projection backward pa
 
 int g_train_fuse_apply = 1;   // key 23: 1 BN applies folded into the next conv's staging; 0 separate passes
 int g_train_fuse_fin = 1;     // key 24: 1 BN finalize by the last workgroup of the producing conv; 0 separate kernels
-int g_train_dgrad_apply = 0;  // key 45 (study build): 1 each dgrad applies the next BN backward in its epilogue (when its tiles
-                              // fit the device at once); 0 separate bn_bwd_apply passes
-int g_train_apply_cap = 0;    // key 46: most workgroups of a fused dgrad + apply launch (0: automatic)
-// polls (x s_sleep 2, ~1 us each under load) before a fused dgrad's finalize wait defers
-// its tile (pv_halo.h ApX): milliseconds, far above a legitimate wait (< 0.2 ms)
-constexpr unsigned kApplySpin = 1u << 12;
 int g_train_apply_grid = 0;   // key 44: workgroup cap of the BN apply / BN-backward apply passes (0: one float4 per thread)
-int g_train_bwd_tower = 0;    // key 43 (study build): 1 the tower backward as one persistent launch (slower,
-                              // measured); 0 the two-stream schedule (product)
 
 struct TrainWS {
     int cap = 0;
@@ -76,12 +65,9 @@ struct TrainWS {
     float *part_a = nullptr, *part_b = nullptr;   // [ntile][C]
     float* hpart = nullptr;                        // [ntile][3][C]
     float* spart = nullptr;                        // [B][27][C]
-    float* slab[3] = {nullptr, nullptr, nullptr};  // weight-grad split-K slabs (two alternate; study build: three rotate)
+    float* slab[2] = {nullptr, nullptr};           // weight-grad split-K slabs (two alternate)
     int slab_S = 0;                                // splits one slab holds
-    unsigned* fincnt = nullptr;   // fused BN finalize arrival counters: [0..3] forward / two-stream, 4 per conv after
-    unsigned* apdone = nullptr;   // fused dgrad + BN-backward apply: finalizes published per N tile (monotonic)
-    unsigned* aptword = nullptr;  // ... and its per-(N tile, M tile) deferral words (pv_halo.h ApX)
-    unsigned ap_epoch = 0;        // launches of it so far
+    unsigned* fincnt = nullptr;   // fused BN finalize arrival counters, one per N tile
     // heads
     float *zh = nullptr, *fp = nullptr, *fv = nullptr, *hv = nullptr, *dpre = nullptr;
     float *dlogits = nullptr, *dfp = nullptr, *dfv = nullptr, *dhv = nullptr, *lossb = nullptr;
@@ -93,15 +79,7 @@ struct TrainWS {
     // optimizer
     double* npart = nullptr;     // grad sq-sum partials
     float* scal = nullptr;       // [0] total norm, [1] clip coef
-    // persistent backward (pv_bwd_tower.hip): counters and the per-conv descriptors
-    unsigned* bsync = nullptr;
-    BwdConv* bdesc = nullptr;
-    std::vector<BwdConv> bdesc_host;   // what bdesc holds
-    // timing studies (AZG_BWD_TRACE=<file>): the last persistent launch's per-item trace,
-    // host-mapped, written to <file> with its geometry when the workspace is freed
-    unsigned long long* trace = nullptr;
-    int trace_hdr[4] = {0, 0, 0, 0};   // C, nconv, M, S of the last traced launch
-    // two-stream backward (key 43 = 0): weight grads on `side`
+    // two-stream backward: weight grads on `side`
     hipStream_t side = nullptr;
     hipEvent_t ev_ready = nullptr, ev_join = nullptr;
     // debug snapshots of gX (AZG_DEBUG_SNAP=1, two-stream schedule): after heads, after each block
@@ -115,13 +93,18 @@ static TrainWS* ws_of(azg_pv* h) { return (TrainWS*)h->train; }
 // its hand-off events release at device scope (they order two streams of one device)
 static hipError_t make_side_stream(TrainWS* w)
 {
-    if (w->side) return hipSuccess;
-    int least = 0, greatest = 0;
-    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&w->side, hipStreamNonBlocking, least);
+    if (w->side && w->ev_ready && w->ev_join) return hipSuccess;
+    hipError_t e = hipSuccess;
+    if (!w->side) {
+        int least = 0, greatest = 0;
+        e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&w->side, hipStreamNonBlocking, least);
+    }
+    // each object is created only if missing: a failed creation is retried by the next
+    // step instead of leaving a null event behind a live stream
     const unsigned flags = hipEventDisableTiming | hipEventReleaseToDevice;
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&w->ev_ready, flags);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&w->ev_join, flags);
+    if (e == hipSuccess && !w->ev_ready) e = hipEventCreateWithFlags(&w->ev_ready, flags);
+    if (e == hipSuccess && !w->ev_join) e = hipEventCreateWithFlags(&w->ev_join, flags);
     return e;
 }
 
@@ -134,21 +117,6 @@ void free_train_workspace(azg_pv* h)
     if (w->ev_ready) (void)hipEventDestroy(w->ev_ready);
     if (w->ev_join) (void)hipEventDestroy(w->ev_join);
     if (w->side) (void)hipStreamDestroy(w->side);
-#ifdef AZG_AB_STUDIES
-    if (w->trace) {
-        (void)hipDeviceSynchronize();
-        if (const char* path = getenv("AZG_BWD_TRACE")) {
-            if (FILE* f = fopen(path, "wb")) {
-                const int* g = w->trace_hdr;
-                const size_t n = g[0] ? (size_t)bwd_tower_items(g[0], g[1], g[2], g[3]) : 0;
-                fwrite(g, sizeof(int), 4, f);
-                fwrite(w->trace, sizeof(unsigned long long), n * 5, f);
-                fclose(f);
-            }
-        }
-        (void)hipHostFree(w->trace);
-    }
-#endif
     delete w;
     h->train = nullptr;
 }
@@ -676,12 +644,7 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     A(w->spart, (size_t)cap * STEM_WG_CHUNKS * 27 * C, false);
     // slabs for the automatic split count at this capacity (or the key-27 override)
     w->slab_S = std::max(wgrad_splits(C, M), std::min(g_wgrad_splits, kMaxWgradSplits));
-#ifdef AZG_AB_STUDIES
-    const int nslab = 3;
-#else
-    const int nslab = 2;
-#endif
-    for (int k = 0; k < nslab; ++k) A(w->slab[k], (size_t)w->slab_S * 9 * C * C, false);
+    for (int k = 0; k < 2; ++k) A(w->slab[k], (size_t)w->slab_S * 9 * C * C, false);
     A(w->zh, (size_t)cap * 3 * PIX, false);
     A(w->fp, (size_t)cap * 2 * PIX, false);
     A(w->fv, (size_t)cap * PIX, false);
@@ -698,10 +661,6 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     A(w->scal, 4, true);
     A(t, 4 * (2 * kTowerMaxBlocks + 2), true);
     w->fincnt = (unsigned*)t;
-    A(t, 16, true);
-    w->apdone = (unsigned*)t;
-    A(t, (size_t)((M + 127) / 128) * 4, true);
-    w->aptword = (unsigned*)t;
     A(t, (size_t)head_proj_stats_groups(M) * 6 * 2, false);
     w->hsp1 = (double*)t;
     A(t, (size_t)head_dgrad_groups(cap) * 6 * 2, false);
@@ -709,17 +668,6 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     A(w->feat, (size_t)cap * FC_FS, true);
     A(w->pre, (size_t)cap * FC_OUT, false);
     A(w->hbw, 16, false);
-#ifdef AZG_AB_STUDIES
-    A(t, bwd_sync_words(2 * NB), true);
-    w->bsync = (unsigned*)t;
-    A(t, (sizeof(BwdConv) * (2 * NB > 0 ? 2 * NB : 1) + 3) / 4, false);
-    w->bdesc = (BwdConv*)t;
-    if (getenv("AZG_BWD_TRACE") && NB > 0) {
-        const size_t n = (size_t)bwd_tower_items(C, 2 * NB, M, kMaxWgradSplits) * 5;
-        hipError_t e = hipHostMalloc((void**)&w->trace, n * sizeof(unsigned long long), hipHostMallocMapped);
-        if (e != hipSuccess) return set_error("train workspace: trace buffer", e);
-    }
-#endif
     if (getenv("AZG_DEBUG_SNAP")) {
         w->snap.assign(NB + 1, nullptr);
         for (int i = 0; i <= NB; ++i) A(w->snap[i], act, true);
@@ -1000,86 +948,10 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     // epilogue of the dgrad conv that produces its gradient (XE_BNBWD, per 128-row
     // tile); the last block's bn2 sums come from heads_bwd_fused (per 128-row tile).
     bool done_fin = false;   // the stem's BN backward is finalized (by the last dgrad)
-    bool stem_dz_done = false;   // the stem's dz is in DH already (key 45)
     bool side_used = false;
     if (NB > 0) R(bwd_fin(h->bn_blk[NB - 1].second, hntile));
-#ifdef AZG_AB_STUDIES
-    if (NB > 0 && g_train_bwd_tower && ffin) {
-        // ---- one persistent launch (pv_bwd_tower.hip) ----
-        const int nconv = 2 * NB;
-        const int S = wgrad_splits(C, M);
-        if (S > w->slab_S) return set_error("train: wgrad splits exceed the slab workspace (key 27 above the allocation)", hipErrorInvalidValue);
-        std::vector<BwdConv> ds(nconv);
-        for (int i = NB - 1; i >= 0; --i) {
-            const int p2 = 2 * (NB - 1 - i), p1 = p2 + 1;
-            const int l1 = h->bn_blk[i].first, l2 = h->bn_blk[i].second;
-            const int lin = i == 0 ? h->bn_stem : h->bn_blk[i - 1].second;
-            const float* Xin = i == 0 ? w->a0 : w->xo[i - 1];
-            const float* zin = i == 0 ? w->z0 : w->z2[i - 1];
-            const int o1 = bd[l1].out_off, o2 = bd[l2].out_off;
-            BwdConv c2{};   // conv2 of block i: g = gX, mask from the block output, dy also -> GR
-            c2.g = w->gX;
-            c2.act = w->xo[i];
-            c2.z = w->z2[i];
-            c2.mean = w->bmean + o2;
-            c2.gm = w->bgm + o2;
-            c2.kk = w->bk + o2;
-            c2.iw = w->biw + o2;
-            c2.dz = w->dzs[2 * i + 1];
-            c2.gres = w->GR;
-            c2.wd = w->wdpack + (size_t)(2 * i + 1) * CC9;
-            c2.out = w->DH;
-            c2.ex = EpiX{w->hh[i], w->z1[i], w->bmean + o1, w->part_a, w->part_b};
-            c2.fx = fin_args(l1, false);
-            c2.fx.cnt = w->fincnt + 4 * (p2 + 1);
-            c2.fx.done = bwd_fin_word(w->bsync, p2 + 1);
-            c2.wx = w->hh[i];
-            c2.slab = w->slab[p2 % 3];
-            c2.dw = G + h->poff[h->t_blk[i].w2];
-            BwdConv c1{};   // conv1 of block i: g = DH, mask from z1 (no residual), dgrad + GR -> gX
-            c1.g = w->DH;
-            c1.z = w->z1[i];
-            c1.mean = w->bmean + o1;
-            c1.gm = w->bgm + o1;
-            c1.kk = w->bk + o1;
-            c1.iw = w->biw + o1;
-            c1.fscale = w->bscale + o1;
-            c1.fshift = w->bshift + o1;
-            c1.dz = w->dzs[2 * i];
-            c1.wd = w->wdpack + (size_t)(2 * i) * CC9;
-            c1.resid = w->GR;
-            c1.out = w->gX;
-            c1.ex = EpiX{Xin, zin, w->bmean + bd[lin].out_off, w->part_a, w->part_b};
-            c1.fx = fin_args(lin, false);
-            c1.fx.cnt = w->fincnt + 4 * (p1 + 1);
-            c1.fx.done = bwd_fin_word(w->bsync, p1 + 1);
-            c1.wx = Xin;
-            c1.slab = w->slab[p1 % 3];
-            c1.dw = G + h->poff[h->t_blk[i].w1];
-            ds[p2] = c2;
-            ds[p1] = c1;
-        }
-        if (ds.size() != w->bdesc_host.size() ||
-            memcmp(ds.data(), w->bdesc_host.data(), ds.size() * sizeof(BwdConv)) != 0) {
-            // the pointer set changed (new workspace or rebound parameters): rare
-            AZG_CK(hipStreamSynchronize(st), "train: descriptor upload");
-            AZG_CK(hipMemcpy(w->bdesc, ds.data(), ds.size() * sizeof(BwdConv), hipMemcpyHostToDevice),
-                   "train: descriptor upload");
-            w->bdesc_host = ds;
-        }
-        int pr = prof_begin(h, AZG_PROF_TRAIN_CONV, st, B);
-        unsigned long long* tr = nullptr;
-        if (w->trace) {
-            AZG_CK(hipHostGetDevicePointer((void**)&tr, w->trace, 0), "train: trace buffer");
-            w->trace_hdr[0] = C, w->trace_hdr[1] = nconv, w->trace_hdr[2] = M, w->trace_hdr[3] = S;
-        }
-        AZG_CK(launch_bwd_tower(C, w->bdesc, nconv, M, S, w->bsync, h->status_dev, st, tr), "train: bwd tower");
-        prof_end(h, pr, st);
-        done_fin = true;
-    } else
-#endif
     if (NB > 0) {
-        // ---- the two-stream schedule (key 43 = 0): dgrads on the caller's stream, the
+        // ---- the two-stream schedule: dgrads on the caller's stream, the
         // weight grads on `side` (one event hand-off per conv), each slab reduction
         // deferred behind the next conv's weight-grad kernel ----
         AZG_CK(make_side_stream(w), "train: side stream");
@@ -1101,49 +973,6 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             return 0;
         };
         bool fin_next = true;   // the next layer's finalize is already done (the first: above)
-        // key 45: every dgrad also applies the BN backward of the layer below in its
-        // epilogue once its in-kernel finalize is published (all its tiles must fit the
-        // device at once: they wait for each other); the next conv's dZ (and the residual
-        // gradient) come straight out of the dgrad, g itself is never stored
-        // automatic bound: 15/16 of the occupancy bound (measured at 6x128: every wait
-        // met up to 480 of 512 workgroups, deferrals from ~490; past the bound the
-        // launch is still correct, ApX, only slower)
-#ifdef AZG_AB_STUDIES
-        const int occ = train_apply_capacity(C);
-        const int dga_cap = g_train_apply_cap > 0 ? std::min(g_train_apply_cap, occ) : occ - occ / 16;
-        const bool dga = g_train_dgrad_apply && ffin && ntt * (C / 64) <= dga_cap;
-#else
-        const bool dga = false;   // key 45 is a study-build variant (measured slower)
-#endif
-        auto dgrad_apply = [&](int epi, const float* dz_in, const float* wd, const float* res, const float* xact,
-                               const float* xz, int xl, float* dz_out, float* gres_out) -> int32_t {
-            int pr = prof_begin(h, AZG_PROF_TRAIN_CONV, st, B);
-            const int o = bd[xl].out_off;
-            const EpiX ex{xact, xz, w->bmean + o, w->part_a, w->part_b};
-            FinX fx = fin_args(xl, false);
-            fx.cnt = w->fincnt;
-            fx.done = w->apdone;
-            fx.done_nt = 1;
-            ApX ax{};
-            ax.gm = w->bgm + o;
-            ax.kk = w->bk + o;
-            ax.iw = w->biw + o;
-            ax.dz = dz_out;
-            ax.gres = gres_out;
-            ax.done = w->apdone;
-            ax.tword = w->aptword;
-            ax.epoch = ++w->ap_epoch;
-            ax.spin = std::min(g_tower_spin_limit, kApplySpin);
-#ifdef AZG_AB_STUDIES
-            AZG_CK(launch_conv3x3_dgrad_apply(C, epi, dz_in, wd, res, w->DH, M, ex, fx, ax, st),
-                   "train: conv3x3 dgrad + BN backward apply");
-#else
-            (void)epi, (void)dz_in, (void)wd, (void)res, (void)ex, (void)ax;
-            return set_error("train: the fused dgrad + BN backward apply is in the study build only", hipErrorInvalidValue);
-#endif
-            prof_end(h, pr, st);
-            return 0;
-        };
         for (int i = NB - 1; i >= 0; --i) {
             const float* Xin = i == 0 ? w->a0 : w->xo[i - 1];
             const float* zin = i == 0 ? w->z0 : w->z2[i - 1];
@@ -1151,35 +980,19 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             const int l1 = h->bn_blk[i].first, l2 = h->bn_blk[i].second;
             float* dz2 = w->dzs[2 * i + 1];
             float* dz1 = w->dzs[2 * i];
-            if (!dga || i == NB - 1) {   // with dga, conv1's dgrad of block i + 1 produced dz2 and GR
-                if (!fin_next) R(bwd_fin(l2, ntt));
-                R(bwd_apply(w->gX, w->xo[i], w->z2[i], l2, dz2, w->GR));
-            }
+            if (!fin_next) R(bwd_fin(l2, ntt));
+            R(bwd_apply(w->gX, w->xo[i], w->z2[i], l2, dz2, w->GR));
             R(wgrad(dz2, w->hh[i], h->t_blk[i].w2));
-            if (dga) {
-                R(dgrad_apply(EPI_RAW, dz2, w->wdpack + (size_t)(2 * i + 1) * CC9, nullptr, w->hh[i], w->z1[i], l1, dz1,
-                              nullptr));
-            } else {
-                R(conv(EPI_RAW, XE_BNBWD, dz2, w->wdpack + (size_t)(2 * i + 1) * CC9, nullptr, w->DH, w->hh[i],
-                       w->z1[i], l1, ffin ? l1 : -1));
-                if (!ffin) R(bwd_fin(l1, ntt));
-                R(bwd_apply(w->DH, nullptr, w->z1[i], l1, dz1, nullptr));
-            }
+            R(conv(EPI_RAW, XE_BNBWD, dz2, w->wdpack + (size_t)(2 * i + 1) * CC9, nullptr, w->DH, w->hh[i],
+                   w->z1[i], l1, ffin ? l1 : -1));
+            if (!ffin) R(bwd_fin(l1, ntt));
+            R(bwd_apply(w->DH, nullptr, w->z1[i], l1, dz1, nullptr));
             R(wgrad(dz1, Xin, h->t_blk[i].w1));
-            if (dga) {
-                // block i's conv1 dgrad (+ its residual gradient GR) -> the BN backward of
-                // block i - 1's bn2 (dz2 of block i - 1, and its dy as the next GR) or of
-                // the stem (the stem's dz into DH, the stem weight grad's operand)
-                R(dgrad_apply(EPI_ADD, dz1, w->wdpack + (size_t)(2 * i) * CC9, w->GR, Xin, zin, lin,
-                              i > 0 ? w->dzs[2 * (i - 1) + 1] : w->DH, i > 0 ? w->GR : nullptr));
-            } else {
-                R(conv(EPI_ADD, XE_BNBWD, dz1, w->wdpack + (size_t)(2 * i) * CC9, w->GR, w->gX, Xin, zin, lin,
-                       ffin ? lin : -1));
-            }
+            R(conv(EPI_ADD, XE_BNBWD, dz1, w->wdpack + (size_t)(2 * i) * CC9, w->GR, w->gX, Xin, zin, lin,
+                   ffin ? lin : -1));
             fin_next = ffin;
             R(snap(NB - i));
         }
-        stem_dz_done = dga;
         if (pend.slab) AZG_CK(launch_wgrad_reduce(C, pend.slab, pend.dw, S, w->side), "train: wgrad reduce");
         done_fin = ffin;
     }
@@ -1206,7 +1019,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     } else if (!done_fin) {
         R(bwd_fin(h->bn_stem, ntt));
     }
-    if (!stem_dz_done) R(bwd_apply(w->gX, nullptr, w->z0, h->bn_stem, w->DH, nullptr));
+    R(bwd_apply(w->gX, nullptr, w->z0, h->bn_stem, w->DH, nullptr));
     hipLaunchKernelGGL((stem_wgrad_kernel<C>), dim3(B * STEM_WG_CHUNKS), dim3(256), 0, st, x, w->DH, w->spart);
     AZG_CK(hipGetLastError(), "train: stem_wgrad");
     hipLaunchKernelGGL(reduce_partials_kernel, dim3((27 * C + 15) / 16), dim3(256), 0, st, w->spart, B * STEM_WG_CHUNKS, 27 * C,

@@ -362,66 +362,12 @@ def test_train_schedule_keys_bitwise(key, values):
         lib.azg_pv_set_tuning(key, prev)
 
 
-@pytest.mark.parametrize("blocks,ch,B", [(6, 128, 128), (3, 64, 37), (2, 256, 16), (1, 128, 2), (4, 128, 300)])
-def test_bwd_tower_bitwise_vs_two_stream(blocks, ch, B):
-    """The persistent train backward (pv_bwd_tower.hip, key 43 = 1) is bitwise equal to
-    the two-stream schedule of stand-alone kernels (key 43 = 0) over three steps: the
-    configs[3] shape, a ragged batch (37: a partial 128-row tile), C = 256 (four dgrad N
-    tiles, 36 weight-grad tiles per split), one block at the smallest batch, and a batch
-    above the workspace's first capacity (300: re-allocation, new descriptors)."""
-    import _native
-    lib = _native.load_library()
-    if lib.azg_pv_set_tuning(15, 0) != 1:
-        pytest.skip("the persistent train backward is in the study build only (make study; AZG_PV_LIB)")
-    b, p = synth_positions(B, seed=93 + B)
-    x = encode_batch(b, p)
-    pi, z = synth_targets(B, seed=94 + B)
-    prev = lib.azg_pv_set_tuning(43, 1)
-    try:
-        got = train_state_after(x, pi, z, blocks, ch, steps=3)
-        lib.azg_pv_set_tuning(43, 0)
-        ref = train_state_after(x, pi, z, blocks, ch, steps=3)
-    finally:
-        lib.azg_pv_set_tuning(43, prev)
-    bad = [i for i, (a, c) in enumerate(zip(ref, got)) if not torch.equal(a, c)]
-    assert not bad, bad
-
-
-def test_bwd_tower_timeout_raises_and_drains():
-    """A dependency wait of the persistent train backward that times out (tuning key 14
-    = 0 makes every poll time out) sets the sticky status: train_batch raises, the
-    launch still drains (the next steps run), and after clear_status a fresh model
-    trains to the same state as without the fault."""
-    import _native
-    lib = _native.load_library()
-    if lib.azg_pv_set_tuning(15, 0) != 1 or lib.azg_pv_set_tuning(43, 1) != 0:
-        pytest.skip("the persistent train backward is in the study build only (make study; AZG_PV_LIB)")
-    b, p = synth_positions(64, seed=95)
-    x = encode_batch(b, p)
-    pi, z = synth_targets(64, seed=96)
-    ref = train_state_after(x, pi, z, 2, 64, steps=1)
-    m = make_model(2, 64, seed=3)
-    try:
-        lib.azg_pv_set_tuning(14, 0)
-        with pytest.raises(RuntimeError, match="timed out"):
-            m.train_batch(x, pi, z)
-        lib.azg_pv_set_tuning(14, -1)
-        with pytest.raises(RuntimeError, match="timed out"):   # sticky
-            m.train_batch(x, pi, z)
-    finally:
-        lib.azg_pv_set_tuning(14, -1)
-        m.engine.clear_status()
-    got = train_state_after(x, pi, z, 2, 64, steps=1)
-    lib.azg_pv_set_tuning(43, 0)
-    assert all(torch.equal(a, c) for a, c in zip(ref, got))
-
-
 @pytest.mark.parametrize("key,value", [(27, 16), (27, 64)])
 @pytest.mark.parametrize("tag,blocks,ch,B", [("6x128", 6, 128, 128), ("3x64", 3, 64, 37)])
 def test_train_sum_order_variants_match_oracle(key, value, tag, blocks, ch, B):
     """The weight-grad split count (key 27) changes an fp32 summation order: it holds
-    the oracle tolerance of test_gradients_match_oracle (no bitwise test); 64 splits also
-    exercise the persistent backward's largest slab."""
+    the oracle tolerance of test_gradients_match_oracle (no bitwise test); 64 splits are
+    the largest slab the workspace holds."""
     import _native
     lib = _native.load_library()
     prev = lib.azg_pv_set_tuning(key, value)
@@ -429,54 +375,3 @@ def test_train_sum_order_variants_match_oracle(key, value, tag, blocks, ch, B):
         test_gradients_match_oracle(tag, blocks, ch, B)
     finally:
         lib.azg_pv_set_tuning(key, prev)
-
-
-@pytest.mark.parametrize("blocks,ch,B,cap,spin", [
-    (3, 64, 37, 0, -1), (2, 256, 16, 0, -1), (1, 128, 2, 0, -1),
-    # the largest 6x128 batch under the automatic bound (480 of 512 workgroups)
-    (6, 128, 136, 0, -1),
-    # bound lifted to the occupancy bound: 508 workgroups, where waits are measured to
-    # time out and tiles defer to the finalizer
-    (6, 128, 144, 512, -1),
-    # every wait defers at once (key 14 = 0): the finalizers apply every other tile
-    (6, 128, 128, 0, 0), (2, 256, 16, 0, 0), (3, 64, 37, 0, 0)])
-def test_dgrad_apply_bitwise_vs_separate_passes(blocks, ch, B, cap, spin):
-    """The dgrads with the BN backward applied in their epilogue (key 45 = 1: every
-    workgroup waits, bounded, for its N tile's in-kernel finalize, and defers its tile to
-    the finalizer if the wait times out -- pv_halo.h ApX) are bitwise equal to the
-    separate bn_bwd_apply passes over three steps: at a ragged batch, C = 256 (four N
-    tiles), one block, the largest 6x128 batch under the automatic bound, above it, and
-    with every tile deferred.  Study build only (measured slower: DESIGN.md §4)."""
-    import _native
-    lib = _native.load_library()
-    if lib.azg_pv_set_tuning(15, 0) != 1:
-        pytest.skip("the fused dgrad + BN backward apply is in the study build only (make study; AZG_PV_LIB)")
-    b, p = synth_positions(B, seed=97 + B)
-    x = encode_batch(b, p)
-    pi, z = synth_targets(B, seed=98 + B)
-    prev = lib.azg_pv_set_tuning(45, 1)
-    prev_cap = lib.azg_pv_set_tuning(46, cap)
-    try:
-        lib.azg_pv_set_tuning(14, spin)
-        got = train_state_after(x, pi, z, blocks, ch, steps=3)
-        lib.azg_pv_set_tuning(14, -1)
-        lib.azg_pv_set_tuning(45, 0)
-        ref = train_state_after(x, pi, z, blocks, ch, steps=3)
-    finally:
-        lib.azg_pv_set_tuning(14, -1)
-        lib.azg_pv_set_tuning(45, prev)
-        lib.azg_pv_set_tuning(46, prev_cap)
-    bad = [i for i, (a, c) in enumerate(zip(ref, got)) if not torch.equal(a, c)]
-    assert not bad, bad
-
-
-def test_dgrad_apply_automatic_bound():
-    """Key 46's query: the occupancy bound the automatic 15/16 margin is taken from is
-    two 512-thread workgroups per CU on every CU.  Study build only."""
-    import _native
-    lib = _native.load_library()
-    if lib.azg_pv_set_tuning(15, 0) != 1:
-        pytest.skip("the fused dgrad + BN backward apply is in the study build only (make study; AZG_PV_LIB)")
-    cus = torch.cuda.get_device_properties(0).multi_processor_count
-    for c in (64, 128, 256):
-        assert lib.azg_pv_set_tuning(46, -c) == 2 * cus
