@@ -19,6 +19,24 @@ class AzgConfig(ctypes.Structure):
                 ("board", ctypes.c_int32), ("in_ch", ctypes.c_int32)]
 
 
+class TowerDiag(ctypes.Structure):
+    """include/azg_pv.h azg_pv_tower_diag."""
+    _fields_ = [(n, ctypes.c_uint32) for n in (
+        "timeouts", "waits_over_100us", "waits_over_1ms", "waits_over_10ms", "waits_over_100ms", "max_wait_us",
+        "recovered", "seq", "layer", "mtile", "wait_mtile", "observed", "needed", "waited_us", "wall_us",
+        "waiter_hwid", "waiter_xcc", "claims", "producer_claimed", "producer_started", "producer_hwid",
+        "producer_xcc")] + [("producer_start_us", ctypes.c_int32), ("reserved", ctypes.c_uint32 * 9)]
+
+    def as_dict(self) -> dict:
+        d = {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}
+        for k in ("waiter_hwid", "producer_hwid"):   # gfx9 HW_ID fields
+            v = d[k]
+            d[k.replace("hwid", "cu")] = {"wave": v & 15, "simd": (v >> 4) & 3, "cu": (v >> 8) & 15,
+                                          "sh": (v >> 12) & 1, "se": (v >> 13) & 7, "vmid": (v >> 20) & 15,
+                                          "queue": (v >> 24) & 7}
+        return d
+
+
 _P = ctypes.c_void_p
 _SIGS = {
     "azg_pv_abi_version": (ctypes.c_int32, []),
@@ -44,13 +62,17 @@ _SIGS = {
     "azg_pv_profile_boards": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_int64)]),
     "azg_pv_set_tuning": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32]),
     "azg_pv_tower_status": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_void_p]),
+    "azg_pv_last_seq": (ctypes.c_uint32, [_P]),
+    "azg_pv_recover": (ctypes.c_int32, [_P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32), _P]),
     "azg_pv_status": (ctypes.c_int32, [_P]),
     "azg_pv_clear_status": (ctypes.c_int32, [_P]),
+    "azg_pv_tower_diag_read": (ctypes.c_int32, [_P, ctypes.POINTER(TowerDiag), _P]),
+    "azg_pv_tower_diag_clear": (ctypes.c_int32, [_P, _P]),
     "azg_pv_debug_copy": (ctypes.c_int32, [_P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32, _P]),
 }
 EXPORTS = tuple(_SIGS)
 PROF_CLASSES = ("conv3x3", "stem", "heads", "train_conv", "train_wgrad", "train_other", "tower", "tower16")
-ABI_VERSION = 1
+ABI_VERSION = 2   # 2: tower launch numbers, azg_pv_recover, the wait record (round 5)
 
 _lib = None
 

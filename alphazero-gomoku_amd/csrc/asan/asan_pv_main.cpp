@@ -20,7 +20,7 @@ static int fails = 0;
 
 int main()
 {
-    CHECK(azg_pv_abi_version() == 1);
+    CHECK(azg_pv_abi_version() == 2);
     const int shapes[4][2] = {{3, 64}, {6, 128}, {10, 256}, {0, 64}};
     const long long want[3] = {340010, 1892650, 11930922};
     for (int s = 0; s < 4; ++s) {
@@ -42,6 +42,17 @@ int main()
         CHECK(azg_pv_status(h) == 0);
         CHECK(azg_pv_clear_status(h) == 0);
         CHECK(azg_pv_mark_dirty(h) == 0);
+        // tower recovery / wait record before any launch: nothing posted, nothing to do
+        CHECK(azg_pv_last_seq(h) == 0);
+        int32_t rec = -1;
+        CHECK(azg_pv_recover(h, 0, &rec, nullptr) == 0 && rec == 0);
+        CHECK(azg_pv_recover(h, 7, &rec, nullptr) == 0 && rec == 0);
+        CHECK(azg_pv_recover(h, 7, nullptr, nullptr) != 0);
+        azg_pv_tower_diag d;
+        std::memset(&d, 0xff, sizeof(d));
+        CHECK(azg_pv_tower_diag_read(h, &d, nullptr) == 0 && d.timeouts == 0 && d.recovered == 0);
+        CHECK(azg_pv_tower_diag_read(h, nullptr, nullptr) != 0);
+        CHECK(azg_pv_tower_diag_clear(h, nullptr) == 0);
         // not bound yet: every compute entry point must fail cleanly
         float dummy = 0.f;
         CHECK(azg_pv_forward(h, &dummy, 1, &dummy, &dummy, nullptr, nullptr) != 0);
@@ -62,11 +73,16 @@ int main()
     CHECK(azg_pv_destroy(nullptr) == 0);
     CHECK(azg_pv_param_count(nullptr) == -1);
     CHECK(azg_pv_status(nullptr) == 0);
+    CHECK(azg_pv_last_seq(nullptr) == 0);
+    CHECK(azg_pv_tower_diag_clear(nullptr, nullptr) != 0);
     CHECK(azg_pv_bind(nullptr, nullptr, nullptr, nullptr) != 0);
     // tuning keys round-trip (previous value returned)
     const int prev = azg_pv_set_tuning(5, 0);
     CHECK(azg_pv_set_tuning(5, prev) == 0);
     CHECK(azg_pv_set_tuning(999, 1) == -1);
+    const int prev_wait = azg_pv_set_tuning(14, 0);   // wait bound (us): default 1 s
+    CHECK(prev_wait == 1000000);
+    CHECK(azg_pv_set_tuning(14, -1) == 0 && azg_pv_set_tuning(14, -1) == 1000000);
     std::printf("asan_pv: %s\n", fails ? "FAILED" : "ok");
     return fails ? 1 : 0;
 }

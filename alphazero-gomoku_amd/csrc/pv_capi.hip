@@ -35,7 +35,7 @@ static int32_t fail(const char* what, hipError_t e = hipSuccess)
 
 extern "C" {
 
-int32_t azg_pv_abi_version(void) { return 1; }
+int32_t azg_pv_abi_version(void) { return 2; }
 
 const char* azg_pv_last_error(void) { return g_err.c_str(); }
 
@@ -66,7 +66,8 @@ int32_t azg_pv_destroy(azg_pv* h)
     if (h->wbase) (void)hipFree(h->wbase);
     if (h->bn_desc_dev) (void)hipFree(h->bn_desc_dev);
     if (h->conv_off_dev) (void)hipFree(h->conv_off_dev);
-    if (h->status_host) (void)hipHostFree(h->status_host);
+    if (h->ring_host) (void)hipHostFree(h->ring_host);
+    if (h->tower_diag) (void)hipFree(h->tower_diag);
     for (auto& e : h->prof_ev) (void)hipEventDestroy(e);
     delete h;
     return 0;
@@ -119,14 +120,18 @@ int32_t azg_pv_bind(azg_pv* h, float* params, float* grads, float* bn_stats)
             e = hipMemcpy(h->conv_off_dev, offs.data(), sizeof(int64_t) * offs.size(), hipMemcpyHostToDevice);
         if (e != hipSuccess) return fail("azg_pv_bind: conv offset upload", e);
         void* sp = nullptr;
-        e = hipHostMalloc(&sp, 64, hipHostMallocMapped | hipHostMallocCoherent);
-        if (e != hipSuccess) return fail("azg_pv_bind: hipHostMalloc(status word)", e);
-        h->status_host = (unsigned*)sp;
-        *h->status_host = 0;
+        e = hipHostMalloc(&sp, kTowerRing * sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent);
+        if (e != hipSuccess) return fail("azg_pv_bind: hipHostMalloc(tower ring)", e);
+        h->ring_host = (unsigned*)sp;
+        memset(h->ring_host, 0, kTowerRing * sizeof(unsigned));
         void* dp = nullptr;
         e = hipHostGetDevicePointer(&dp, sp, 0);
-        if (e != hipSuccess) return fail("azg_pv_bind: hipHostGetDevicePointer(status word)", e);
-        h->status_dev = (unsigned*)dp;
+        if (e != hipSuccess) return fail("azg_pv_bind: hipHostGetDevicePointer(tower ring)", e);
+        h->ring_dev = (unsigned*)dp;
+        e = hipMalloc(&h->tower_diag, kTowerDiagWords * sizeof(unsigned));
+        if (e == hipSuccess) e = hipMemset(h->tower_diag, 0, kTowerDiagWords * sizeof(unsigned));
+        if (e != hipSuccess) return fail("azg_pv_bind: tower wait record", e);
+        h->launches.assign(kTowerRing, azg_pv::LaunchRec{});
     }
     h->params = params;
     h->grads = grads;
@@ -218,14 +223,17 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards)
 
 int32_t azg_pv_status(const azg_pv* h)
 {
-    if (!h || !h->status_host) return 0;
-    return (int32_t)__atomic_load_n(h->status_host, __ATOMIC_ACQUIRE);
+    if (!h || !h->ring_host) return 0;
+    int32_t n = 0;
+    for (unsigned i = 0; i < kTowerRing; ++i) n += __atomic_load_n(h->ring_host + i, __ATOMIC_ACQUIRE) != 0u;
+    return n;
 }
 
 int32_t azg_pv_clear_status(azg_pv* h)
 {
     if (!h) return fail("azg_pv_clear_status: null handle");
-    if (h->status_host) __atomic_store_n(h->status_host, 0u, __ATOMIC_RELEASE);
+    if (h->ring_host)
+        for (unsigned i = 0; i < kTowerRing; ++i) __atomic_store_n(h->ring_host + i, 0u, __ATOMIC_RELEASE);
     return 0;
 }
 
@@ -238,6 +246,76 @@ int32_t azg_pv_tower_status(azg_pv* h, void* stream)
     AZG_TRY(hipMemcpyAsync(w, h->tower_sync, sizeof(w), hipMemcpyDeviceToHost, st), "azg_pv_tower_status: copy");
     AZG_TRY(hipStreamSynchronize(st), "azg_pv_tower_status: sync");
     return (int32_t)w[1];
+}
+
+uint32_t azg_pv_last_seq(const azg_pv* h) { return h ? h->last_seq : 0u; }
+
+int32_t azg_pv_recover(azg_pv* h, uint32_t seq, int32_t* recovered, void* stream)
+{
+    if (!h || !recovered) return fail("azg_pv_recover: null argument");
+    *recovered = 0;
+    if (seq == 0 || !h->ring_host) return 0;
+    const unsigned slot = seq & (kTowerRing - 1);
+    if (__atomic_load_n(h->ring_host + slot, __ATOMIC_ACQUIRE) != seq) return 0;
+    const azg_pv::LaunchRec r = h->launches[slot];
+    if (r.seq != seq)
+        return fail("azg_pv_recover: the timed-out launch is older than the launch record ring (recover it sooner)");
+    // per-layer convs from the same inputs into the same outputs: bitwise what the tower
+    // computes when no wait times out
+    if (int32_t e = forward_eval(h, r.x, r.batch, r.probs, r.values, r.logits, (hipStream_t)stream, r.boards,
+                                 r.players, r.priors, true))
+        return e;
+    __atomic_store_n(h->ring_host + slot, 0u, __ATOMIC_RELEASE);
+    ++h->recovered;
+    *recovered = 1;
+    return 0;
+}
+
+int32_t azg_pv_tower_diag_read(azg_pv* h, azg_pv_tower_diag* out, void* stream)
+{
+    if (!h || !out) return fail("azg_pv_tower_diag_read: null argument");
+    memset(out, 0, sizeof(*out));
+    out->recovered = h->recovered;
+    if (!h->tower_diag) return 0;
+    unsigned w[kTowerDiagWords];
+    hipStream_t st = (hipStream_t)stream;
+    AZG_TRY(hipMemcpyAsync(w, h->tower_diag, sizeof(w), hipMemcpyDeviceToHost, st), "azg_pv_tower_diag_read: copy");
+    AZG_TRY(hipStreamSynchronize(st), "azg_pv_tower_diag_read: sync");
+    auto us = [](unsigned ticks) { return ticks / 100u; };   // s_memrealtime: 100 MHz
+    out->timeouts = w[1];
+    out->waits_over_100us = w[2];
+    out->waits_over_1ms = w[3];
+    out->waits_over_10ms = w[4];
+    out->waits_over_100ms = w[5];
+    out->max_wait_us = us(w[6]);
+    out->seq = w[7];
+    out->layer = w[8];
+    out->mtile = w[9];
+    out->wait_mtile = w[10];
+    out->observed = w[11];
+    out->needed = w[12];
+    out->waited_us = us(w[13]);
+    out->wall_us = us(w[14]);
+    out->waiter_hwid = w[15];
+    out->waiter_xcc = w[16];
+    out->claims = w[17];
+    out->producer_claimed = w[18];
+    out->producer_started = w[19];
+    out->producer_hwid = w[20];
+    out->producer_xcc = w[21];
+    out->producer_start_us = (int32_t)w[22] / 100;
+    return 0;
+}
+
+int32_t azg_pv_tower_diag_clear(azg_pv* h, void* stream)
+{
+    if (!h) return fail("azg_pv_tower_diag_clear: null handle");
+    h->recovered = 0;
+    if (!h->tower_diag) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    AZG_TRY(hipMemsetAsync(h->tower_diag, 0, kTowerDiagWords * sizeof(unsigned), st), "azg_pv_tower_diag_clear");
+    AZG_TRY(hipStreamSynchronize(st), "azg_pv_tower_diag_clear: sync");
+    return 0;
 }
 
 }  // extern "C"
@@ -350,6 +428,8 @@ void free_workspace(azg_pv* h)
     h->hbuf = nullptr;
     if (h->tower_sync) (void)hipFree(h->tower_sync);
     h->tower_sync = nullptr;
+    if (h->tower_prod) (void)hipFree(h->tower_prod);
+    h->tower_prod = nullptr;
     h->act_cap = 0;
     free_train_workspace(h);
 }
@@ -367,10 +447,15 @@ int32_t ensure_eval_workspace(azg_pv* h, int batch, hipStream_t st)
     h->hbuf = nullptr;
     if (h->tower_sync) (void)hipFree(h->tower_sync);
     h->tower_sync = nullptr;
+    if (h->tower_prod) (void)hipFree(h->tower_prod);
+    h->tower_prod = nullptr;
     h->act_cap = 0;
     {
         hipError_t e = hipMalloc(&h->tower_sync, tower_sync_bytes(2 * h->NB, cap * PIX));
         if (e != hipSuccess) return fail("ensure_eval_workspace: hipMalloc(tower sync)", e);
+        e = hipMalloc(&h->tower_prod, tower_prod_bytes(2 * h->NB, cap * PIX));
+        if (e == hipSuccess) e = hipMemsetAsync(h->tower_prod, 0, tower_prod_bytes(2 * h->NB, cap * PIX), st);
+        if (e != hipSuccess) return fail("ensure_eval_workspace: tower producer records", e);
     }
     {
         const size_t hb = (size_t)cap * (FC_FS + FC_OUT) * sizeof(float);
@@ -408,7 +493,7 @@ int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst, int part)
 // tower (pv_tower.hip) with 64x64 / 128x64 / 128x128 (16-wave) tiles.  All bitwise
 // identical.
 static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch, hipStream_t st,
-                              const int8_t* boards, const int8_t* players, float** out)
+                              const int8_t* boards, const int8_t* players, float** out, unsigned seq = 0)
 {
     const int C = h->C;
     const int M = batch * PIX;
@@ -429,8 +514,8 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
             out_off[2 * i + 1] = bd[h->bn_blk[i].second].out_off;
         }
         pr = prof_begin(h, variant == 10 ? AZG_PROF_TOWER_WIDE : AZG_PROF_TOWER, st, batch);
-        AZG_TRY(launch_tower(C, h->NB, variant, h->act, h->wpack, h->scale, h->shift, out_off, M, h->tower_sync,
-                             h->status_dev, st, &X),
+        const TowerSync ts{h->tower_sync, h->ring_dev, h->tower_diag, h->tower_prod, seq};
+        AZG_TRY(launch_tower(C, h->NB, variant, h->act, h->wpack, h->scale, h->shift, out_off, M, ts, st, &X),
                 "forward: tower");
         prof_end(h, pr, st);
         *out = X;
@@ -519,14 +604,24 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
 }
 
 int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* values, float* logits,
-                     hipStream_t st, const int8_t* boards, const int8_t* players, float* priors)
+                     hipStream_t st, const int8_t* boards, const int8_t* players, float* priors, bool per_layer)
 {
     const int C = h->C;
     const float* P = h->params;
     const BnDesc* bd = h->bn_desc.data();
-    const int variant = tower_variant(h, x, batch, st, boards, players);
+    const int variant = per_layer ? 0 : tower_variant(h, x, batch, st, boards, players);
+    // a tower launch gets a number and a record of its buffers (azg_pv_recover)
+    unsigned seq = 0;
+    if (variant != 0 && h->NB > 0 && !h->launches.empty()) {
+        seq = ++h->seq;
+        if (seq == 0) seq = ++h->seq;   // 0 means "not posted"
+        azg_pv::LaunchRec& r = h->launches[seq & (kTowerRing - 1)];
+        r = azg_pv::LaunchRec{seq, x, boards, players, batch, probs, values, logits, priors};
+        __atomic_store_n(h->ring_host + (seq & (kTowerRing - 1)), 0u, __ATOMIC_RELEASE);
+    }
+    if (!per_layer) h->last_seq = seq;
     float* X = nullptr;
-    if (int32_t r = stem_and_tower(h, variant, x, batch, st, boards, players, &X)) return r;
+    if (int32_t r = stem_and_tower(h, variant, x, batch, st, boards, players, &X, seq)) return r;
     const int ho = bd[h->bn_pol].out_off;   // policy (2) then value (1): contiguous
     int pr = prof_begin(h, AZG_PROF_HEADS, st, batch);
     AZG_TRY(launch_heads_fwd(C, X, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], h->scale + ho, h->shift + ho,

@@ -984,9 +984,9 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
 #endif
         return prev;
     }
-    if (key == 14) {  // tests: persistent-tower dependency spin bound (-1 restores the default)
-        const int prev = (int)azg::g_tower_spin_limit;
-        azg::g_tower_spin_limit = value < 0 ? (1u << 22) : (unsigned)value;
+    if (key == 14) {  // persistent-tower dependency wait bound in us of awake time (-1 restores the default, 0 forces timeouts)
+        const int prev = (int)azg::g_tower_wait_us;
+        azg::g_tower_wait_us = value < 0 ? azg::kTowerWaitUs : (unsigned)value;
         return prev;
     }
     if (key == 31) {  // study build only: 64x64 / 128x64 tower with sc1 dependent loads instead of the acquire

@@ -53,10 +53,21 @@ hipError_t launch_stem_stats(int C, const float* x, const float* ws, float* out,
 constexpr int kTowerMaxBlocks = 32;
 int conv_batch_bucket(int M);
 size_t tower_sync_bytes(int nlayers, int M);
+size_t tower_prod_bytes(int nlayers, int M);
+constexpr unsigned kTowerRing = 256;          // host ring of timed-out launch numbers (power of 2)
+constexpr int kTowerDiagWords = 64;           // device wait record (pv_tower.hip TowerDiag)
+constexpr unsigned kTowerWaitUs = 1000000u;   // default awake-time bound of one dependency wait: 1 s
+struct TowerSync {
+    unsigned* sync;   // tower_sync_bytes: memset per launch
+    unsigned* ring;   // host-mapped ring (device alias)
+    unsigned* diag;   // kTowerDiagWords, persistent
+    void* prod;       // tower_prod_bytes, persistent
+    unsigned seq;     // launch number (0: not posted)
+};
 hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const float* wpack, const float* scale,
-                        const float* shift, const int* out_off, int M, unsigned* sync, unsigned* status,
-                        hipStream_t st, float** result);
-extern unsigned g_tower_spin_limit;
+                        const float* shift, const int* out_off, int M, const TowerSync& ts, hipStream_t st,
+                        float** result);
+extern unsigned g_tower_wait_us;
 extern int g_tower_group;
 #ifdef AZG_AB_STUDIES
 extern int g_tower_coh;
@@ -127,8 +138,23 @@ struct azg_pv {
     float* act[3] = {nullptr, nullptr, nullptr};
     float* hbuf = nullptr;
     unsigned* tower_sync = nullptr;   // persistent tower: work counter, error word, tile counters
-    unsigned* status_host = nullptr;  // sticky status word, pinned + mapped (kernels write it, azg_pv_status reads)
-    unsigned* status_dev = nullptr;   // device alias of status_host
+    void* tower_prod = nullptr;       // persistent tower: per-tile producer records
+    unsigned* tower_diag = nullptr;   // persistent tower: wait record (kTowerDiagWords, device)
+    unsigned* ring_host = nullptr;    // timed-out launch numbers [kTowerRing], pinned + mapped (kernels post, host reads)
+    unsigned* ring_dev = nullptr;     // device alias of ring_host
+    unsigned seq = 0;                 // last tower launch number handed out (0 = none yet)
+    unsigned last_seq = 0;            // the last forward's launch number (0: it ran per-layer convs)
+    // what each posted launch read and wrote, by seq % kTowerRing (azg_pv_recover re-runs it)
+    struct LaunchRec {
+        unsigned seq = 0;
+        const float* x = nullptr;
+        const int8_t* boards = nullptr;
+        const int8_t* players = nullptr;
+        int batch = 0;
+        float *probs = nullptr, *values = nullptr, *logits = nullptr, *priors = nullptr;
+    };
+    std::vector<LaunchRec> launches;
+    uint32_t recovered = 0;           // launches recomputed per layer
     int act_cap = 0;
 
     // train workspace (pv_train.hip)
@@ -155,5 +181,6 @@ int prof_begin(azg_pv* h, int cls, hipStream_t st, int64_t boards = 0);   // ret
 hipError_t prof_harvest(azg_pv* h);
 void prof_end(azg_pv* h, int pair, hipStream_t st);
 int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* values, float* logits,
-                     hipStream_t st, const int8_t* boards, const int8_t* players, float* priors);
+                     hipStream_t st, const int8_t* boards, const int8_t* players, float* priors,
+                     bool per_layer = false);
 }  // namespace azg

@@ -28,8 +28,10 @@
 //    (static_assert below).
 // Deadlock freedom: a tile waits only on tiles claimed before it (all of layer
 // l-1 precedes layer l in claim order), and a claimed tile is always executed by a
-// running workgroup, so the oldest unfinished tile can always finish.  Spins are
-// bounded; a timeout sets the error word (read by azg_pv_tower_status) and the
+// running workgroup, so the oldest unfinished tile can always finish.  Waits are
+// bounded by the waiting wave's AWAKE time (tower_wait below); a timeout posts the
+// launch's sequence number to the handle's host ring (azg_pv_recover recomputes that
+// forward per layer), fills the self-describing record (azg_pv_tower_diag) and the
 // workgroup proceeds so the grid always drains.
 //
 // Buffer reuse (WAR): with X -> H -> Y(+X) -> H -> X(+Y) ..., a tile overwrites
@@ -56,8 +58,11 @@ struct TowerArgs {
     int M;
     int act_bytes;       // bytes of one activation buffer (buffer descriptor range)
     unsigned* sync;      // [0] work counter, [1] error word, [4..] per-(layer, M tile) counters
-    unsigned* status;    // sticky host-mapped status word of the handle (azg_pv_status); may be null
-    unsigned spin_limit; // polls before a dependency wait is declared timed out
+    unsigned* ring;      // host-mapped ring of timed-out launch numbers (azg_pv_recover); may be null
+    unsigned* diag;      // persistent wait record (TowerDiag layout, azg_pv_tower_diag); may be null
+    uint4* prod;         // per (layer, M tile): {seq, HW_ID, XCC_ID, start tick} of the workgroup running it
+    unsigned seq;        // launch sequence number (0: autotuning runs, never posted)
+    unsigned limit;      // awake-time bound of one dependency wait, in 10-ns ticks (0: time out at once)
     int group;           // 1: a claim is one (M, N) tile; NTN: one M tile with all its N
                          // tiles, run back to back by the claiming workgroup (the second
                          // N tile's halo rows are hits in that XCD's L2)
@@ -65,8 +70,7 @@ struct TowerArgs {
                          // bit 1 skips the dependency wait + acquire, bit 2 the publish drain
 };
 
-constexpr unsigned kSpinLimit = 1u << 22;    // x s_sleep(2): seconds, far above any tile time
-unsigned g_tower_spin_limit = kSpinLimit;    // tuning key 14 (tests: 0 forces the timeout path)
+unsigned g_tower_wait_us = kTowerWaitUs;     // tuning key 14 (tests: 0 forces the timeout path)
 int g_tower_group = 1;                       // tuning key 17: 1 (default) = claim an M tile with all its N tiles
 #ifdef AZG_AB_STUDIES
 int g_tower_coh = 0;   // study key 31: sc1 dependent loads with 64x64 / 128x64 tiles (OUTSIDE the guide's envelope)
@@ -85,6 +89,110 @@ constexpr int tower_lds_bytes()
 {
     constexpr int need = halo_lds_bytes<C, BN, WM, TM, NW, VAR>() + 16;
     return NW >= 16 && need <= 82 * 1024 ? 82 * 1024 : need;
+}
+
+// Device side of azg_pv_tower_diag (word offsets into a.diag; the host converts ticks
+// to microseconds).
+enum TowerDiag : int {
+    TD_TAKEN = 0,         // 0 until the first timed-out wait claims the record
+    TD_TIMEOUTS, TD_W100US, TD_W1MS, TD_W10MS, TD_W100MS, TD_MAXWAIT,
+    TD_SEQ, TD_LAYER, TD_MTILE, TD_WAIT_MTILE, TD_OBSERVED, TD_NEEDED, TD_WAITED, TD_WALL,
+    TD_WAITER_HW, TD_WAITER_XCC, TD_CLAIMS, TD_PCLAIMED, TD_PSTARTED, TD_PHW, TD_PXCC, TD_PSTART,
+    TD_WORDS
+};
+static_assert(TD_WORDS <= kTowerDiagWords, "tower diag record");
+
+__device__ __forceinline__ unsigned hw_id()
+{
+    unsigned v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
+    return v;
+}
+__device__ __forceinline__ unsigned xcc_id()
+{
+    unsigned v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return v & 15u;
+}
+
+// One dependency wait (lane 0 of the waiting workgroup): relaxed agent-scope polls
+// with s_sleep between them until the counter reaches `need`.  The bound is the
+// wave's AWAKE time: each s_memrealtime delta (100 MHz) counts at most kWaitStep
+// ticks, so a wave that was context-saved together with its producer (queue
+// preemption suspends every wave of the dispatch) does not time out on the gap.
+// The fast path (counter already complete) reads no clock.  Returns false on timeout.
+constexpr unsigned kWaitStep = 1000;   // 10 us
+__device__ __forceinline__ bool tower_wait(const unsigned* c, unsigned need, unsigned limit, unsigned& seen,
+                                           unsigned& waited, unsigned long long& t0, unsigned long long& t1)
+{
+    seen = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    waited = 0;
+    if (seen >= need && limit != 0) return true;
+    t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long prev = t0;
+    for (;;) {
+        __builtin_amdgcn_s_sleep(2);
+        seen = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long d = now - prev;
+        prev = now;
+        waited += d < kWaitStep ? (unsigned)d : kWaitStep;
+        t1 = now;
+        if (seen >= need && limit != 0) return true;
+        if (waited >= limit) return false;
+    }
+}
+
+// Book-keeping of a wait that took `waited` ticks (only slow waits get here)
+__device__ __forceinline__ void tower_wait_stats(unsigned* d, unsigned waited)
+{
+    if (!d) return;
+    if (waited > 10000u) __hip_atomic_fetch_add(d + TD_W100US, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (waited > 100000u) __hip_atomic_fetch_add(d + TD_W1MS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (waited > 1000000u) __hip_atomic_fetch_add(d + TD_W10MS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (waited > 10000000u) __hip_atomic_fetch_add(d + TD_W100MS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (waited > 10000u) __hip_atomic_fetch_max(d + TD_MAXWAIT, waited, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A timed-out wait of tile (l, mt) on tile (l - 1, j): post the launch to the host
+// ring and, if first since the record was cleared, describe it -- including what the
+// producer tile's workgroup had published about itself in this launch.
+__device__ __noinline__ void tower_timeout(unsigned* ring, unsigned* d, const unsigned* sync, const uint4* prod,
+                                              unsigned seq, int l, int mt, int j, int mtiles, int tpl, unsigned seen,
+                                              unsigned need, unsigned waited, unsigned long long t0,
+                                              unsigned long long t1)
+{
+    if (ring && seq)
+        __hip_atomic_store(ring + (seq & (kTowerRing - 1)), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (!d) return;
+    __hip_atomic_fetch_add(d + TD_TIMEOUTS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned zero = 0;
+    if (!__hip_atomic_compare_exchange_strong(d + TD_TAKEN, &zero, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT))
+        return;
+    auto ld = [](const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto st = [&](int k, unsigned v) { __hip_atomic_store(d + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    const unsigned claims = ld(sync);
+    const unsigned* pp = (const unsigned*)(prod + (size_t)(l - 1) * mtiles + j);
+    const bool started = ld(pp) == seq;
+    // claim index of the producer's (first) claim: layer-major, then M tile
+    const unsigned pidx = (unsigned)((l - 1) * tpl + j * (tpl / mtiles));
+    st(TD_SEQ, seq);
+    st(TD_LAYER, (unsigned)l);
+    st(TD_MTILE, (unsigned)mt);
+    st(TD_WAIT_MTILE, (unsigned)j);
+    st(TD_OBSERVED, seen);
+    st(TD_NEEDED, need);
+    st(TD_WAITED, waited);
+    st(TD_WALL, (unsigned)(t1 - t0));
+    st(TD_WAITER_HW, hw_id());
+    st(TD_WAITER_XCC, xcc_id());
+    st(TD_CLAIMS, claims);
+    st(TD_PCLAIMED, claims > pidx ? 1u : 0u);
+    st(TD_PSTARTED, started ? 1u : 0u);
+    st(TD_PHW, started ? ld(pp + 1) : 0u);
+    st(TD_PXCC, started ? ld(pp + 2) : 0u);
+    st(TD_PSTART, started ? ld(pp + 3) - (unsigned)t0 : 0u);   // signed on the host
 }
 
 // HABL (study build, timing / traffic ablations only: results invalid): halo_tile's ABL
@@ -122,25 +230,30 @@ __global__ __launch_bounds__(64 * NW_, (tower_min_waves<BN_, NW_>())) void conv_
                 const unsigned* c = cnt + (size_t)(l - 1) * mtiles;
                 const int j0 = max(mt - 1, 0), j1 = min(mt + 1, mtiles - 1);
                 for (int j = j0; j <= j1; ++j) {
-                    unsigned spins = 0;
-                    // spin_limit 0 (tuning key 14, tests only) forces the timeout path
-                    while (a.spin_limit == 0 ||
-                           __hip_atomic_load(c + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)NTN) {
-                        if (++spins > a.spin_limit) {
-                            // the tile computes on stale inputs: flag the launch and the
-                            // handle (sticky, host-visible: the product raises on it)
-                            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            if (a.status)
-                                __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(2);
+                    unsigned seen, waited;
+                    unsigned long long t0 = 0, t1 = 0;
+                    if (!tower_wait(c + j, (unsigned)NTN, a.limit, seen, waited, t0, t1)) {
+                        // the tile computes on stale inputs: flag the launch (the host
+                        // recomputes it per layer) and describe the wait
+                        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        tower_timeout(a.ring, a.diag, a.sync, a.prod, a.seq, l, mt, j, mtiles, tpl, seen, (unsigned)NTN,
+                                      waited, t0, t1);
                     }
+                    if (waited > 10000u) tower_wait_stats(a.diag, waited);
                 }
                 // VAR bit 16 (one workgroup per CU): every dependent read is an sc1 load,
                 // no acquire; otherwise ONE agent-scope acquire (L1 invalidate) here
                 if constexpr ((VAR & 16) == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            // what this tile's workgroup publishes about itself (read only by a timed-out
+            // waiter's record): one 16-B store per claim
+            if (a.prod) {
+                const uint4 pr = make_uint4(a.seq, hw_id(), xcc_id(), (unsigned)__builtin_amdgcn_s_memrealtime());
+                __hip_atomic_store((unsigned*)(a.prod + (size_t)l * mtiles + mt) + 1, pr.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((unsigned*)(a.prod + (size_t)l * mtiles + mt) + 2, pr.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((unsigned*)(a.prod + (size_t)l * mtiles + mt) + 3, pr.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((unsigned*)(a.prod + (size_t)l * mtiles + mt) + 0, pr.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         __syncthreads();
@@ -202,14 +315,20 @@ size_t tower_sync_bytes(int nlayers, int M)
     const int mtiles = (M + 63) / 64;   // the smallest BM (64) has the most M tiles
     return ((size_t)(4 + nlayers * mtiles) * sizeof(unsigned) + 15) / 16 * 16;
 }
+// per-(layer, M tile) producer records (never cleared: tagged with the launch number)
+size_t tower_prod_bytes(int nlayers, int M)
+{
+    const int mtiles = (M + 63) / 64;
+    return (size_t)nlayers * mtiles * sizeof(uint4);
+}
 
 // Eval residual tower in one launch: NB blocks, conv1 X -> H (BN, ReLU), conv2
 // H -> Y (BN, + X, ReLU), X <-> Y.  `act` are the three padded NHWC buffers
 // (act[0] holds the stem output; the result ends in act[0] or act[2], returned in
 // *result).  `sync` must hold tower_sync_bytes(2*NB, M) bytes.
 hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const float* wpack, const float* scale,
-                        const float* shift, const int* out_off, int M, unsigned* sync, unsigned* status,
-                        hipStream_t st, float** result)
+                        const float* shift, const int* out_off, int M, const TowerSync& ts, hipStream_t st,
+                        float** result)
 {
     if (2 * NB > kTowerMaxLayers) return hipErrorInvalidValue;
     const size_t act_bytes = (size_t)(M / PIX) * PADPIX * C * sizeof(float);
@@ -218,9 +337,14 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     a.nlayers = 2 * NB;
     a.M = M;
     a.act_bytes = (int)act_bytes;
-    a.sync = sync;
-    a.status = status;
-    a.spin_limit = g_tower_spin_limit;
+    a.sync = ts.sync;
+    a.ring = ts.ring;
+    a.diag = ts.diag;
+    a.prod = (uint4*)ts.prod;
+    a.seq = ts.seq;
+    // microseconds -> 10-ns ticks, saturating
+    a.limit = g_tower_wait_us >= 0xffffffffu / 100u ? 0xffffffffu : g_tower_wait_us * 100u;
+    unsigned* sync = ts.sync;
     a.group = g_tower_group ? C / (shape == 8 || shape == 5 ? 64 : 128) : 1;
 #ifndef AZG_AB_STUDIES
     if (shape == 10 && C != 128) return hipErrorInvalidValue;   // 16-wave tile: C = 128 only (C = 256 spills)

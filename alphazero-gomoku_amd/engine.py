@@ -21,6 +21,10 @@ def _stream(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+class TowerFault(RuntimeError):
+    """A persistent-tower forward computed on stale inputs and could not be recomputed."""
+
+
 class PolicyValueEngine:
     def __init__(self, net: nn.Module, blocks: int, channels: int, board: int, device):
         if board != 15:
@@ -82,6 +86,7 @@ class PolicyValueEngine:
         check(self.lib.azg_pv_bind_counters(h, ptr(self.flat_nbt)), self.lib)
         self._seen = self._versions()
         self._out_cache = {}
+        self.recoveries = 0   # tower launches recomputed per layer (recover)
 
     # -- housekeeping -------------------------------------------------------
     def _versions(self):
@@ -100,20 +105,49 @@ class PolicyValueEngine:
     def mark_dirty(self):
         check(self.lib.azg_pv_mark_dirty(self.h), self.lib)
 
+    def last_seq(self) -> int:
+        """Launch number of the last forward if it ran the persistent tower, else 0
+        (include/azg_pv.h azg_pv_last_seq)."""
+        return int(self.lib.azg_pv_last_seq(self.h))
+
+    def recover(self, seq: int) -> bool:
+        """Call after synchronising with forward `seq`: if one of its tower waits timed
+        out, recompute it with per-layer convs (bitwise what an undisturbed tower gives)
+        into the same device outputs, stream-ordered, and return True.  The forward's
+        input and output buffers must still be intact."""
+        if not seq:
+            return False
+        done = ctypes.c_int32(0)
+        check(self.lib.azg_pv_recover(self.h, int(seq), ctypes.byref(done), _stream(self.device)), self.lib)
+        if done.value:
+            self.recoveries += 1
+        return bool(done.value)
+
     def check_status(self):
-        """Raise if any forward on this handle computed on stale inputs (sticky
-        device status, include/azg_pv.h azg_pv_status).  A plain host load: call it
-        after synchronising with the forwards it should cover.  The status stays set
-        (every later check raises) until clear_status(): a caller that handles the
-        failure clears it once reported (train.train_alphazero does so after a failed
-        evaluation, which the reference counts as a loss)."""
+        """Raise TowerFault if a persistent-tower launch this handle ran timed out and was
+        not recovered (azg_pv_status: a plain host load, complete for every forward the
+        caller has synchronised with).  The product recovers every timed-out launch at
+        its host sync (recover), so this fires only for forwards nobody settled, e.g.
+        predict_device results consumed without a recover.  The posted launches stay
+        until clear_status()."""
         s = int(self.lib.azg_pv_status(self.h))
         if s:
-            raise RuntimeError(f"libazg_pv: persistent residual tower timed out waiting for its inputs "
-                               f"(status {s}); the outputs of the affected forward are invalid")
+            raise TowerFault(f"libazg_pv: {s} persistent-tower launch(es) timed out waiting for their inputs and "
+                             f"were not recomputed; their outputs are invalid ({self.tower_diag()})")
 
     def clear_status(self):
         check(self.lib.azg_pv_clear_status(self.h), self.lib)
+
+    def tower_diag(self) -> dict:
+        """The tower's wait record since the last tower_diag_clear (include/azg_pv.h
+        azg_pv_tower_diag): wait histogram, timeouts, and the first timed-out wait."""
+        from _native import TowerDiag
+        d = TowerDiag()
+        check(self.lib.azg_pv_tower_diag_read(self.h, ctypes.byref(d), _stream(self.device)), self.lib)
+        return d.as_dict()
+
+    def tower_diag_clear(self):
+        check(self.lib.azg_pv_tower_diag_clear(self.h, _stream(self.device)), self.lib)
 
     def reattach_grads(self):
         for p, g in zip(self.params, self.grad_views):

@@ -203,6 +203,7 @@ class BoardEvaluator:
         self.players = self.h_players.numpy()
         self.event = torch.cuda.Event()
         self.n = 0
+        self.seq = 0                             # tower launch number of the batch in flight
 
     def submit(self, n: int) -> None:
         self.n = n
@@ -210,17 +211,27 @@ class BoardEvaluator:
             return
         self.d_boards[:n].copy_(self.h_boards[:n], non_blocking=True)
         self.d_players[:n].copy_(self.h_players[:n], non_blocking=True)
-        self.model.engine.forward_boards_into(self.d_boards[:n], self.d_players[:n], self.d_probs[:n],
-                                              self.d_values[:n], self.d_priors[:n])
+        eng = self.model.engine
+        eng.forward_boards_into(self.d_boards[:n], self.d_players[:n], self.d_probs[:n],
+                                self.d_values[:n], self.d_priors[:n])
+        self.seq = eng.last_seq()
         self.h_priors[:n].copy_(self.d_priors[:n], non_blocking=True)
         self.h_values[:n].copy_(self.d_values[:n], non_blocking=True)
         self.event.record()
 
     def wait(self):
-        """-> (priors [n,225], values [n,1]) numpy views of the pinned buffers."""
+        """-> (priors [n,225], values [n,1]) numpy views of the pinned buffers.  A batch
+        whose persistent-tower forward timed out is recomputed per layer here (the device
+        inputs and outputs of this evaluator are intact until its next submit)."""
         if self.n:
             self.event.synchronize()
-            self.model.engine.check_status()
+            eng = self.model.engine
+            if eng.recover(self.seq):
+                n = self.n
+                self.h_priors[:n].copy_(self.d_priors[:n], non_blocking=True)
+                self.h_values[:n].copy_(self.d_values[:n], non_blocking=True)
+                self.event.record()
+                self.event.synchronize()
         return self.h_priors.numpy()[:self.n], self.h_values.numpy()[:self.n]
 
 
@@ -259,16 +270,19 @@ class PyTorchModel:
     def predict(self, encoded_states: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
         """network.py:168-183: (probs [B,225] float32, values [B,1] float32) with BN
         running stats; the module's train/eval flag is left as it was."""
-        x = torch.from_numpy(np.ascontiguousarray(encoded_states, dtype=np.float32))
+        eng = self.engine
+        x = torch.from_numpy(np.ascontiguousarray(encoded_states, dtype=np.float32)).to(eng.device)
         probs, values = self.predict_device(x)
+        seq = eng.last_seq()
         out = probs.cpu().numpy(), values.cpu().numpy()
-        self.engine.check_status()
+        if eng.recover(seq):   # a timed-out tower wait: recomputed per layer in place
+            out = probs.cpu().numpy(), values.cpu().numpy()
         return out
 
     def predict_device(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """Device-resident predict: x [B,3,15,15] -> (probs, values) on the GPU.
-        Asynchronous: the sticky tower status (engine.check_status) is checked by
-        the next host-synchronising call (predict, predict_boards, evaluator wait)."""
+        Asynchronous: a caller that synchronises should settle the forward with
+        engine.recover(engine.last_seq()) (x must still be intact), as predict does."""
         probs, values, _ = self.engine.forward(x)
         return probs, values
 
@@ -286,8 +300,10 @@ class PyTorchModel:
         values = torch.empty((B, 1), dtype=torch.float32, device=eng.device)
         priors = torch.empty_like(probs) if masked else None
         eng.forward_boards_into(b, pl, probs, values, priors)
+        seq = eng.last_seq()
         out = (priors if masked else probs).cpu().numpy(), values.cpu().numpy()
-        eng.check_status()
+        if eng.recover(seq):
+            out = (priors if masked else probs).cpu().numpy(), values.cpu().numpy()
         return out
 
     def board_evaluator(self, capacity: int) -> "BoardEvaluator":
@@ -328,9 +344,6 @@ class PyTorchModel:
         if return_tensor:
             return mean
         vals = (mean.double() if epochs == 1 else acc / float(epochs)).tolist()
-        # the persistent train backward shares the tower's sticky status word (a timed-out
-        # dependency wait): raise after the host sync above
-        eng.check_status()
         return {"policy_loss": vals[0], "value_loss": vals[1], "total_loss": vals[2]}
 
     train_step = train_batch

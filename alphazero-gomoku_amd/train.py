@@ -27,6 +27,7 @@ import torch
 import distributed as D
 from games.gomoku import Gomoku as GameClass
 from mcts.new_mcts_alpha import MCTS
+from engine import TowerFault
 from network import PyTorchModel
 from selfplay import (BatchedSelfPlay, ReplayBuffer, load_replay_buffer, play_game_and_collect,  # noqa: F401
                       sample_action_from_pi, save_replay_buffer, selfplay_games, softmax_temperature)
@@ -78,15 +79,18 @@ def evaluate_models(model_new: PyTorchModel, model_best: PyTorchModel, game_name
         winners = _play_eval_games(model_new, model_best, games, starts, n_simulations, cpuct, native)
     except Exception as e:   # every rank must still reach the collective below
         failure, winners = e, []
+    fault = isinstance(failure, TowerFault)
     if record is not None:
         record.extend(games)
     new_wins = sum(1 for w, s in zip(winners, starts) if (w == 1 and s) or (w == 2 and not s))
     draws = sum(1 for w in winners if w == 0)
     eng = getattr(model_new, "engine", None)
     dev = eng.device if eng is not None else "cpu"
-    tot = torch.tensor([new_wins, draws, int(failure is not None)], dtype=torch.int64, device=dev)
+    tot = torch.tensor([new_wins, draws, int(failure is not None), int(fault)], dtype=torch.int64, device=dev)
     D.allreduce_sum_(tot)
-    new_wins, draws, failed = (int(v) for v in tot.tolist())
+    new_wins, draws, failed, faults = (int(v) for v in tot.tolist())
+    if faults:   # an engine fault is never a lost game: every rank re-raises it
+        raise TowerFault(f"evaluation: engine fault on {faults} rank(s)" + (f": {failure}" if failure else ""))
     if failed:   # all ranks agree; the caller counts it as a loss (reference train.py:803-805)
         raise RuntimeError(f"evaluation failed on {failed} rank(s)" + (f": {failure}" if failure else ""))
     return new_wins, new_wins / float(n_games), draws
@@ -203,13 +207,13 @@ def train_alphazero(game_name: str = "gomoku", board_size: int = 15, num_iterati
         try:
             new_wins, win_rate, draws = evaluate_models(model_candidate, model_best, game_name, n_games=eval_games,
                                                         n_simulations=eval_mcts_simulations, cpuct=cpuct)
+        except TowerFault:
+            # a forward that computed on stale inputs and could not be recomputed: an
+            # engine fault, not a lost evaluation -- never counted as a rejection
+            raise
         except Exception as e:  # reference: evaluation failure counts as a loss (train.py:803-805)
             print(f"evaluation failed: {e}")
             new_wins, win_rate, draws = 0, 0.0, 0
-            # the failure is reported: clear the sticky tower status (engine.check_status)
-            # so the next generation's forwards are judged on their own
-            for mdl in (model_candidate, model_best):
-                mdl.engine.clear_status()
         if main:
             print(f"eval done: {(time.time() - te) / 60:.2f} min, win_rate={win_rate:.3f} "
                   f"({new_wins}/{eval_games}), draws={draws}")

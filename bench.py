@@ -89,12 +89,6 @@ def dist_setup(n_gpus: int):
             local = local % torch.cuda.device_count()
             torch.cuda.set_device(local)
             dist.init_process_group("gloo")
-            # the persistent tower assumes it owns the GPU (one process per GPU): with two
-            # processes on one card the driver time-slices their queues, and a suspended
-            # wave's claimed tiles can outlast the dependency spin bound (seen once in the
-            # round-4 rehearsal: the sticky status raised).  The rehearsal runs per-layer.
-            import _native
-            _native.load_library().azg_pv_set_tuning(5, 0)
         else:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -365,6 +359,7 @@ def selfplay_run(model, game_class, G, S, max_moves, seeds, profile=True):
                         groups=2 if G > 1 else 1)
     eng = model.engine
     eng.clear_status()
+    eng.tower_diag_clear()
     if profile:
         eng.profile_enable(True)
     t0 = time.perf_counter()
@@ -382,8 +377,24 @@ def selfplay_run(model, game_class, G, S, max_moves, seeds, profile=True):
     boards = eng.profile_boards() if profile else {}
     if profile:
         eng.profile_enable(False)
-    eng.check_status()
+    eng.check_status()   # every timed-out tower launch was recomputed at its evaluator's wait
+    sp.tower = tower_waits(eng)
     return sp, dt, prof, boards, results
+
+
+def tower_waits(eng) -> dict:
+    """The persistent tower's dependency waits in the leg just run (azg_pv_tower_diag):
+    the histogram, timeouts (each one a launch recomputed per layer) and, if any timed
+    out, the first one's record."""
+    d = eng.tower_diag()
+    out = {k: d[k] for k in ("waits_over_100us", "waits_over_1ms", "waits_over_10ms", "max_wait_us", "timeouts",
+                             "recovered")}
+    if d["timeouts"]:
+        out["first_timeout"] = {k: d[k] for k in ("layer", "mtile", "wait_mtile", "observed", "needed", "waited_us",
+                                                  "wall_us", "waiter_xcc", "waiter_cu", "producer_claimed",
+                                                  "producer_started", "producer_xcc", "producer_cu",
+                                                  "producer_start_us")}
+    return out
 
 
 PRETRAIN_STEPS = 20
@@ -445,6 +456,7 @@ def selfplay_leg(model, args, rank, world, dist, dev, local):
             "host_search_share_rank0": round(sp.search_seconds / dt, 3),
             "kernel_ms_rank0": {k: round(v[0], 1) for k, v in prof.items()},
             "kernel_launches_rank0": {k: v[1] for k, v in prof.items()},
+            "tower_waits_rank0": sp.tower,
             "settings": f"cpuct {SP_CPUCT}, Dirichlet alpha {SP_ALPHA} eps {SP_EPS} on the first {SP_NOISE_MOVES} "
                         f"moves, temperature max(0, 1 - n/{SP_TEMP_THRESHOLD}), 8 symmetries, leaf batch 32 "
                         f"per game (train.py:847-889, mcts/new_mcts_alpha.py:12)",
@@ -466,6 +478,8 @@ def forward_leg(model, args, rank, world, dist, dev, local, blocks=BLOCKS, ch=CH
     values = torch.empty((B, 1), device=dev)
     for _ in range(max(warmup, 1)):
         eng.forward_into(x, probs, values)
+    torch.cuda.synchronize()
+    eng.tower_diag_clear()
     barrier_sync(dist, local)
     eng.profile_enable(True)
     barrier_sync(dist, local)
@@ -477,7 +491,11 @@ def forward_leg(model, args, rank, world, dist, dev, local, blocks=BLOCKS, ch=CH
     prof = eng.profile_read()
     boards = eng.profile_boards()
     eng.profile_enable(False)
-    eng.check_status()
+    # every launch read x and wrote probs / values: recovering the last one settles the
+    # outputs; earlier timed-out launches are counted (tower_waits) and dropped
+    eng.recover(eng.last_seq())
+    waits = tower_waits(eng)
+    eng.clear_status()
     assert torch.isfinite(probs).all() and torch.isfinite(values).all()
     (elapsed,) = reduce_(dist, dev, [elapsed], op="max")
     roof = roofline_from_profile(prof, boards, blocks, ch, tower_knames(ch, blocks))
@@ -487,7 +505,7 @@ def forward_leg(model, args, rank, world, dist, dev, local, blocks=BLOCKS, ch=CH
             "steps": steps, "warmup": warmup,
             "whole_forward_mfma_frac": round(B * steps / elapsed * fwd_flop(blocks, ch) / PEAK_F32_MFMA, 4),
             "kernel_ms_per_step": {k: round(v[0] / steps, 4) for k, v in prof.items()},
-            "roofline": roof}
+            "tower_waits_rank0": waits, "roofline": roof}
 
 
 def train_leg(model, args, rank, world, dist, dev, local, blocks=BLOCKS, ch=CHANNELS, steps=None):
@@ -534,7 +552,11 @@ def pente_leg(args, rank, world, dist, dev, local):
     nb, ch = 10, 256
     torch.manual_seed(1)
     m = PyTorchModel(board_size=15, device=str(dev), n_res_blocks=nb, channels=ch)
-    out = {"net": f"{nb}x{ch}"}
+    # the benchmarked weights are the seeded init + the same synthetic
+    # train_batch steps as the 6x128 headline (pretrain), not a raw Kaiming init
+    pretrain(m, dev, args.pretrain_steps)
+    out = {"net": f"{nb}x{ch}",
+           "weights": f"torch.manual_seed(1) init + {args.pretrain_steps} train_batch steps on synthetic data"}
     out["forward_b512"] = forward_leg(m, args, rank, world, dist, dev, local, nb, ch, BATCH, args.big_steps, 2)
     out["train_b128"] = train_leg(m, args, rank, world, dist, dev, local, nb, ch, steps=args.big_train_steps)
     if args.pente_moves > 0:

@@ -179,42 +179,78 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          shared fp64 reduction order, bitwise identical;
  *   key 27: train conv weight-grad pixel splits (0 = automatic, default; 8..64, a
  *          multiple of 8); bitwise identical only at a fixed value;
- *   key 43: study build only: the train step's tower backward as ONE persistent
- *          launch (pv_bwd_tower.hip, 1) or the product's two-stream schedule (0);
- *          bitwise identical, measured slower; returns 0 in the product library;
  *   key 44: train BN apply / BN-backward apply passes: workgroup cap of their
  *          grid-stride launch (0 = four float4 per thread, default); bitwise identical;
- *   keys 45, 46: study build only: train backward dgrads that apply the BN backward of
- *          the layer below in their epilogue after an in-kernel finalize (45 = 1; 46 the
- *          workgroup bound of that launch); bitwise identical, measured slower (the
- *          waiting workgroups starve the concurrent weight-grad stream); return 0 in the
- *          product library;
  *   key 31: study build only: the 64x64 / 128x64 towers with sc1 dependent loads
  *          and no acquire (two or more workgroups per CU: outside the microarch
  *          guide's measured envelope; the product uses the acquire there and the
  *          sc1 form only for the one-workgroup-per-CU 16-wave tile); returns 0 in
  *          the product library;
- *   key 14: persistent-tower dependency spin bound (tests only: 0 makes every
- *          dependency wait time out at once, exercising the error path; -1
- *          restores the default).
+ *   key 14: persistent-tower dependency wait bound in microseconds of the waiting
+ *          wave's awake time (default 1000000 = 1 s; -1 restores it; 0 makes every
+ *          dependency wait time out at once, exercising the recovery path).
  *   Every call returns the previous value. */
 int32_t azg_pv_set_tuning(int32_t key, int32_t value);
 
-/* Persistent-tower health: 0, or nonzero if a tile of the last eval forward on
- * this handle timed out waiting for its inputs (synchronises `stream`). */
+/* Persistent-tower dependency waits (pv_tower.hip).  A tile of the one-launch eval
+ * tower waits for the three tiles of the previous layer whose rows its halo reads.
+ * The wait is bounded by the waiting wave's AWAKE time (s_memrealtime deltas, each
+ * capped at 10 us, so a wave that was suspended together with its producer resumes
+ * without timing out); past the bound (key 14) the tile computes on stale inputs, the
+ * launch drains, and the launch's sequence number is posted to a ring in pinned,
+ * mapped host memory.  Every forward that runs the tower gets a sequence number
+ * (azg_pv_last_seq: the last one on this handle, 0 if the last forward ran per-layer
+ * convs).  azg_pv_recover(seq) -- called after synchronising with that forward --
+ * recomputes a posted launch with per-layer convs (bitwise equal to a tower that did
+ * not time out) into the SAME output buffers on `stream`, provided the caller's input
+ * and output buffers of that forward are still intact; *recovered = 1 then (0: the
+ * launch did not time out).  The Python layer does this at every host-synchronising
+ * forward (predict, predict_boards, BoardEvaluator.wait), so a timeout costs one
+ * per-layer forward instead of an error. */
+/* Error word of the last tower launch on this handle: 1 if one of its waits timed
+ * out (synchronises `stream`). */
 int32_t azg_pv_tower_status(azg_pv* h, void* stream);
+uint32_t azg_pv_last_seq(const azg_pv* h);
+int32_t azg_pv_recover(azg_pv* h, uint32_t seq, int32_t* recovered, void* stream);
 
-/* Sticky device-side status of the handle: 0 = every forward so far was computed
- * on complete inputs; nonzero = a persistent-tower tile timed out waiting for its
- * inputs and computed on stale data (outputs of that forward are invalid).  Kernels
- * write it straight into pinned, mapped host memory, so reading it is a plain load
- * with no device call: it is complete for every forward the caller has already
- * synchronised with (event / stream sync / D2H copy).  The Python layer checks it
- * after every host-synchronising forward and raises RuntimeError (the reference
- * contract: errors are an int status + exception).  It stays set
- * until azg_pv_clear_status. */
+/* Number of posted (timed-out) tower launches not yet recovered (a plain host load of
+ * the pinned ring: complete for every forward the caller has synchronised with); the
+ * Python layer raises on a nonzero value it cannot recover.  azg_pv_clear_status drops
+ * every posted launch without recomputing it. */
 int32_t azg_pv_status(const azg_pv* h);
 int32_t azg_pv_clear_status(azg_pv* h);
+
+/* Self-describing record of the tower's waits since the last azg_pv_tower_diag_clear
+ * (device counters + the first timed-out wait; synchronises `stream`).  Times are
+ * microseconds from s_memrealtime (100 MHz).  hwid = the HW_ID hardware register of the
+ * wave (CU, SE, VMID, queue, ...), xcc = its XCD (HW_REG_XCC_ID). */
+typedef struct {
+    uint32_t timeouts;          /* waits that timed out */
+    uint32_t waits_over_100us;  /* waits whose awake time exceeded 0.1 / 1 / 10 / 100 ms */
+    uint32_t waits_over_1ms;
+    uint32_t waits_over_10ms;
+    uint32_t waits_over_100ms;
+    uint32_t max_wait_us;       /* longest awake wait */
+    uint32_t recovered;         /* launches recomputed by azg_pv_recover (host count) */
+    /* the first timed-out wait */
+    uint32_t seq;               /* its launch */
+    uint32_t layer;             /* the waiting tile: conv layer (1 .. 2*blocks-1) and M tile */
+    uint32_t mtile;
+    uint32_t wait_mtile;        /* the layer-1 M tile it waited on */
+    uint32_t observed;          /* that tile's completion counter when the wait gave up */
+    uint32_t needed;            /* ... and the value it waited for (N tiles per M tile) */
+    uint32_t waited_us;         /* awake time of the wait */
+    uint32_t wall_us;           /* wall time from the wait's start to its timeout */
+    uint32_t waiter_hwid, waiter_xcc;
+    uint32_t claims;            /* tiles claimed in the launch when it timed out */
+    uint32_t producer_claimed;  /* 1: the producer tile had been claimed */
+    uint32_t producer_started;  /* 1: its workgroup had started it in this launch */
+    uint32_t producer_hwid, producer_xcc;
+    int32_t producer_start_us;  /* its start relative to the wait's start */
+    uint32_t reserved[9];
+} azg_pv_tower_diag;
+int32_t azg_pv_tower_diag_read(azg_pv* h, azg_pv_tower_diag* out, void* stream);
+int32_t azg_pv_tower_diag_clear(azg_pv* h, void* stream);
 
 /* Debug/test access to train-workspace activations of the last train step:
  * copies the interior [batch][15][15][C] (NHWC) of buffer `which` (block `index`

@@ -310,45 +310,71 @@ def test_persistent_tower_under_concurrent_load():
         lib.azg_pv_set_tuning(5, prev_mode)
 
 
-def test_tower_timeout_is_a_hard_error():
-    """A persistent-tower tile whose dependency wait times out computes on stale
-    inputs; the sticky status word must turn that into a RuntimeError on every
-    host-synchronising product path (predict, predict_boards, BoardEvaluator.wait).
-    Tuning key 14 = 0 makes every unsatisfied dependency poll time out."""
+def test_tower_timeout_is_recovered_bitwise():
+    """A persistent-tower tile whose dependency wait times out computes on stale inputs.
+    Every host-synchronising product path (predict, predict_boards, BoardEvaluator.wait)
+    must detect its launch in the host ring and recompute it per layer: outputs bitwise
+    equal to an undisturbed forward, the recovery counted, the wait record filled in
+    (layer / M tile / counter vs N tiles / waiter and producer placement).  A forward
+    nobody settled (predict_device) is a TowerFault at check_status.  Tuning key 14 = 0
+    makes every dependency wait time out at once."""
     import _native
+    from engine import TowerFault
     lib = _native.load_library()
     m = make_model(6, 128, seed=6)
+    eng = m.engine
     boards, players = synth_positions(512, seed=61)
     x = encode_batch(boards, players)
     bi8, pl8 = np.asarray(boards, np.int8).reshape(512, 225), np.asarray(players, np.int8)
+    stream = torch.cuda.current_stream().cuda_stream
     prev_mode = lib.azg_pv_set_tuning(5, 1)
     prev_shape = lib.azg_pv_set_tuning(6, 8)
     try:
-        p_ok, v_ok = m.predict(x)                    # healthy: no error
-        assert lib.azg_pv_status(m.engine.h) == 0
+        p_ok, v_ok = m.predict(x)                    # healthy
+        pb_ok, vb_ok = m.predict_boards(bi8, pl8)
+        assert eng.last_seq() > 0 and lib.azg_pv_status(eng.h) == 0
+        eng.tower_diag_clear()
+        d0 = eng.tower_diag()
+        assert d0["timeouts"] == 0 and d0["recovered"] == 0
         lib.azg_pv_set_tuning(14, 0)
-        with pytest.raises(RuntimeError, match="timed out"):
-            m.predict(x)
-        lib.azg_pv_set_tuning(14, -1)
-        # sticky: stays raised until cleared, even for a healthy forward
-        with pytest.raises(RuntimeError, match="timed out"):
-            m.predict_boards(bi8, pl8)
+        r0 = eng.recoveries
+        p, v = m.predict(x)
+        assert lib.azg_pv_tower_status(eng.h, stream) == 0   # the recompute ran per layer
+        assert np.array_equal(p, p_ok) and np.array_equal(v, v_ok)
+        pb, vb = m.predict_boards(bi8, pl8)
+        assert np.array_equal(pb, pb_ok) and np.array_equal(vb, vb_ok)
         ev = m.board_evaluator(512)
         ev.boards[:] = bi8
         ev.players[:] = pl8
         ev.submit(512)
-        with pytest.raises(RuntimeError, match="timed out"):
-            ev.wait()
-        m.engine.clear_status()
-        p, v = m.predict(x)
+        pe, ve = ev.wait()
+        assert np.array_equal(pe, pb_ok) and np.array_equal(ve, vb_ok)
+        assert eng.recoveries == r0 + 3 and lib.azg_pv_status(eng.h) == 0
+        d = eng.tower_diag()
+        print("tower wait record:", d)
+        assert d["timeouts"] > 0 and d["recovered"] == 3
+        assert 1 <= d["layer"] < 12 and d["needed"] == 2 and d["observed"] <= 2
+        assert abs(int(d["mtile"]) - int(d["wait_mtile"])) <= 1 and d["seq"] > 0
+        assert 0 <= d["waiter_xcc"] < 8 and d["claims"] > 0
+        # an unsettled launch (device-side predict, nobody recovers it) is a TowerFault
+        xd = torch.from_numpy(x).cuda()              # kept alive: recover re-reads it
+        m.predict_device(xd)
+        torch.cuda.synchronize()
+        assert lib.azg_pv_status(eng.h) == 1
+        with pytest.raises(TowerFault, match="timed out"):
+            eng.check_status()
+        lib.azg_pv_set_tuning(14, -1)
+        assert eng.recover(eng.last_seq())           # still recoverable (buffers intact)
+        eng.check_status()
+        eng.tower_diag_clear()
+        p, v = m.predict(x)                          # healthy again
         assert np.array_equal(p, p_ok) and np.array_equal(v, v_ok)
-        ev.submit(512)
-        ev.wait()
+        assert eng.tower_diag()["timeouts"] == 0
     finally:
         lib.azg_pv_set_tuning(14, -1)
         lib.azg_pv_set_tuning(6, prev_shape)
         lib.azg_pv_set_tuning(5, prev_mode)
-        m.engine.clear_status()
+        eng.clear_status()
 
 
 @pytest.mark.parametrize("blocks,ch,B", [(3, 64, 37), (6, 128, 300), (2, 256, 20)])

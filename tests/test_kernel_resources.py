@@ -21,15 +21,18 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 
 # (kernel-name regex on the mangled name, max private_segment_fixed_size bytes)
 SCRATCH_BUDGET = [
-    # persistent eval tower (the self-play / forward headline kernel)
+    # persistent eval tower (the self-play / forward headline kernel).  Round 5: the
+    # figures include the stack frame of the never-taken timed-out-wait path
+    # (pv_tower.hip tower_timeout, noinline so it adds no spill to the tile body: the
+    # 128x64 tower keeps its 14 scratch instructions)
     (r"conv_towerILi128ELi64ELi4ELi1ELi8ELi32E", 32),
-    (r"conv_towerILi128ELi64ELi2ELi1ELi4ELi32E", 60),
-    # C = 256: the board-keyed halo body (VAR 33) spills 100 B outside the chunk loop and is
+    (r"conv_towerILi128ELi64ELi2ELi1ELi4ELi32E", 64),
+    # C = 256: the board-keyed halo body (VAR 33) spills ~100 B outside the chunk loop and is
     # still 4 % faster than VAR 32's 32 B
-    (r"conv_towerILi256ELi64ELi4ELi1ELi8ELi33E", 100),
-    (r"conv_towerILi256ELi64ELi2ELi1ELi4ELi33E", 140),
+    (r"conv_towerILi256ELi64ELi4ELi1ELi8ELi33E", 112),
+    (r"conv_towerILi256ELi64ELi2ELi1ELi4ELi33E", 144),
     (r"conv_towerILi64ELi64E", 0),
-    (r"conv_towerILi128ELi128ELi4ELi1ELi16E", 40),
+    (r"conv_towerILi128ELi128ELi4ELi1ELi16E", 48),
     # train convs at C <= 128 (the 6x128 train step) and the weight grad
     (r"conv3x3_trainILi(64|128)E", 0),
     (r"conv3x3_wgrad_natILi", 0),
