@@ -25,7 +25,8 @@ class TowerDiag(ctypes.Structure):
         "timeouts", "waits_over_100us", "waits_over_1ms", "waits_over_10ms", "waits_over_100ms", "max_wait_us",
         "recovered", "seq", "layer", "mtile", "wait_mtile", "observed", "needed", "waited_us", "wall_us",
         "waiter_hwid", "waiter_xcc", "claims", "producer_claimed", "producer_started", "producer_hwid",
-        "producer_xcc")] + [("producer_start_us", ctypes.c_int32), ("reserved", ctypes.c_uint32 * 9)]
+        "producer_xcc")] + [("producer_start_us", ctypes.c_int32), ("max_wall_us", ctypes.c_uint32),
+                             ("waits_suspended", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 7)]
 
     def as_dict(self) -> dict:
         d = {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}

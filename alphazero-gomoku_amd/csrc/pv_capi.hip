@@ -304,6 +304,8 @@ int32_t azg_pv_tower_diag_read(azg_pv* h, azg_pv_tower_diag* out, void* stream)
     out->producer_hwid = w[20];
     out->producer_xcc = w[21];
     out->producer_start_us = (int32_t)w[22] / 100;
+    out->max_wall_us = us(w[23]);
+    out->waits_suspended = w[24];
     return 0;
 }
 

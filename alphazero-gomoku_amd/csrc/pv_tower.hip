@@ -98,6 +98,8 @@ enum TowerDiag : int {
     TD_TIMEOUTS, TD_W100US, TD_W1MS, TD_W10MS, TD_W100MS, TD_MAXWAIT,
     TD_SEQ, TD_LAYER, TD_MTILE, TD_WAIT_MTILE, TD_OBSERVED, TD_NEEDED, TD_WAITED, TD_WALL,
     TD_WAITER_HW, TD_WAITER_XCC, TD_CLAIMS, TD_PCLAIMED, TD_PSTARTED, TD_PHW, TD_PXCC, TD_PSTART,
+    TD_MAXWALL,           // longest wall time of a wait (awake + suspended)
+    TD_SUSP,              // waits whose wall time exceeded their awake time by > 1 ms (the wave was suspended)
     TD_WORDS
 };
 static_assert(TD_WORDS <= kTowerDiagWords, "tower diag record");
@@ -143,10 +145,13 @@ __device__ __forceinline__ bool tower_wait(const unsigned* c, unsigned need, uns
     }
 }
 
-// Book-keeping of a wait that took `waited` ticks (only slow waits get here)
-__device__ __forceinline__ void tower_wait_stats(unsigned* d, unsigned waited)
+// Book-keeping of a wait that took `waited` awake ticks over `wall` ticks of wall time
+// (only slow waits get here)
+__device__ __forceinline__ void tower_wait_stats(unsigned* d, unsigned waited, unsigned wall)
 {
     if (!d) return;
+    __hip_atomic_fetch_max(d + TD_MAXWALL, wall, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wall - waited > 100000u) __hip_atomic_fetch_add(d + TD_SUSP, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (waited > 10000u) __hip_atomic_fetch_add(d + TD_W100US, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (waited > 100000u) __hip_atomic_fetch_add(d + TD_W1MS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (waited > 1000000u) __hip_atomic_fetch_add(d + TD_W10MS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -239,7 +244,7 @@ __global__ __launch_bounds__(64 * NW_, (tower_min_waves<BN_, NW_>())) void conv_
                         tower_timeout(a.ring, a.diag, a.sync, a.prod, a.seq, l, mt, j, mtiles, tpl, seen, (unsigned)NTN,
                                       waited, t0, t1);
                     }
-                    if (waited > 10000u) tower_wait_stats(a.diag, waited);
+                    if (waited > 10000u || t1 - t0 > 10000u) tower_wait_stats(a.diag, waited, (unsigned)(t1 - t0));
                 }
                 // VAR bit 16 (one workgroup per CU): every dependent read is an sc1 load,
                 // no acquire; otherwise ONE agent-scope acquire (L1 invalidate) here

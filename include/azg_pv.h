@@ -247,7 +247,9 @@ typedef struct {
     uint32_t producer_started;  /* 1: its workgroup had started it in this launch */
     uint32_t producer_hwid, producer_xcc;
     int32_t producer_start_us;  /* its start relative to the wait's start */
-    uint32_t reserved[9];
+    uint32_t max_wall_us;       /* longest WALL time of a wait (awake + suspended) */
+    uint32_t waits_suspended;   /* waits whose wall time exceeded their awake time by > 1 ms */
+    uint32_t reserved[7];
 } azg_pv_tower_diag;
 int32_t azg_pv_tower_diag_read(azg_pv* h, azg_pv_tower_diag* out, void* stream);
 int32_t azg_pv_tower_diag_clear(azg_pv* h, void* stream);
