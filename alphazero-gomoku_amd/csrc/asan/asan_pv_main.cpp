@@ -81,8 +81,10 @@ int main()
     CHECK(azg_pv_set_tuning(5, prev) == 0);
     CHECK(azg_pv_set_tuning(999, 1) == -1);
     const int prev_wait = azg_pv_set_tuning(14, 0);   // wait bound (us): default 1 s
-    CHECK(prev_wait == 1000000);
-    CHECK(azg_pv_set_tuning(14, -1) == 0 && azg_pv_set_tuning(14, -1) == 1000000);
+    CHECK(prev_wait == 100000);
+    CHECK(azg_pv_set_tuning(14, -1) == 0 && azg_pv_set_tuning(14, -1) == 100000);
+    const int prev_breaker = azg_pv_set_tuning(18, 0);   // breaker seconds: default 30
+    CHECK(prev_breaker == 30 && azg_pv_set_tuning(18, prev_breaker) == 0);
     std::printf("asan_pv: %s\n", fails ? "FAILED" : "ok");
     return fails ? 1 : 0;
 }

@@ -4,6 +4,7 @@
 #include "../../include/azg_pv.h"
 #include "pv_internal.h"
 
+#include <chrono>
 #include <map>
 #include <tuple>
 
@@ -16,6 +17,15 @@
 using namespace azg;
 
 static thread_local std::string g_err;
+
+static double now_s()
+{
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+namespace azg {
+int g_tower_breaker_s = 30;   // key 18 (0: off)
+}
 
 static int32_t fail(const char* what, hipError_t e = hipSuccess)
 {
@@ -234,6 +244,7 @@ int32_t azg_pv_clear_status(azg_pv* h)
     if (!h) return fail("azg_pv_clear_status: null handle");
     if (h->ring_host)
         for (unsigned i = 0; i < kTowerRing; ++i) __atomic_store_n(h->ring_host + i, 0u, __ATOMIC_RELEASE);
+    h->breaker_until = 0.0;   // and the per-layer breaker closes
     return 0;
 }
 
@@ -268,6 +279,10 @@ int32_t azg_pv_recover(azg_pv* h, uint32_t seq, int32_t* recovered, void* stream
     __atomic_store_n(h->ring_host + slot, 0u, __ATOMIC_RELEASE);
     ++h->recovered;
     *recovered = 1;
+    if (g_tower_breaker_s > 0) {
+        h->breaker_until = now_s() + g_tower_breaker_s;
+        ++h->breaker_trips;
+    }
     return 0;
 }
 
@@ -276,6 +291,8 @@ int32_t azg_pv_tower_diag_read(azg_pv* h, azg_pv_tower_diag* out, void* stream)
     if (!h || !out) return fail("azg_pv_tower_diag_read: null argument");
     memset(out, 0, sizeof(*out));
     out->recovered = h->recovered;
+    out->breaker_trips = h->breaker_trips;
+    out->breaker_launches = h->breaker_launches;
     if (!h->tower_diag) return 0;
     unsigned w[kTowerDiagWords];
     hipStream_t st = (hipStream_t)stream;
@@ -306,6 +323,8 @@ int32_t azg_pv_tower_diag_read(azg_pv* h, azg_pv_tower_diag* out, void* stream)
     out->producer_start_us = (int32_t)w[22] / 100;
     out->max_wall_us = us(w[23]);
     out->waits_suspended = w[24];
+    out->breaker_trips = h->breaker_trips;
+    out->breaker_launches = h->breaker_launches;
     return 0;
 }
 
@@ -313,6 +332,8 @@ int32_t azg_pv_tower_diag_clear(azg_pv* h, void* stream)
 {
     if (!h) return fail("azg_pv_tower_diag_clear: null handle");
     h->recovered = 0;
+    h->breaker_trips = 0;
+    h->breaker_launches = 0;
     if (!h->tower_diag) return 0;
     hipStream_t st = (hipStream_t)stream;
     AZG_TRY(hipMemsetAsync(h->tower_diag, 0, kTowerDiagWords * sizeof(unsigned), st), "azg_pv_tower_diag_clear");
@@ -611,7 +632,15 @@ int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* 
     const int C = h->C;
     const float* P = h->params;
     const BnDesc* bd = h->bn_desc.data();
-    const int variant = per_layer ? 0 : tower_variant(h, x, batch, st, boards, players);
+    int variant = per_layer ? 0 : tower_variant(h, x, batch, st, boards, players);
+    if (variant != 0 && h->breaker_until > 0.0) {
+        if (now_s() < h->breaker_until) {
+            variant = 0;
+            ++h->breaker_launches;
+        } else {
+            h->breaker_until = 0.0;
+        }
+    }
     // a tower launch gets a number and a record of its buffers (azg_pv_recover)
     unsigned seq = 0;
     if (variant != 0 && h->NB > 0 && !h->launches.empty()) {

@@ -998,6 +998,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         return 0;
 #endif
     }
+    if (key == 18) {  // seconds of per-layer convs after a recovered tower launch (0: off)
+        const int prev = azg::g_tower_breaker_s;
+        if (value >= 0) azg::g_tower_breaker_s = value;
+        return prev;
+    }
     if (key == 17) {  // persistent tower claims: 0 one tile, 1 one M tile x all N tiles (default)
         const int prev = azg::g_tower_group;
         if (value >= 0 && value <= 1) azg::g_tower_group = value;

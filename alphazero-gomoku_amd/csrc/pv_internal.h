@@ -56,7 +56,10 @@ size_t tower_sync_bytes(int nlayers, int M);
 size_t tower_prod_bytes(int nlayers, int M);
 constexpr unsigned kTowerRing = 256;          // host ring of timed-out launch numbers (power of 2)
 constexpr int kTowerDiagWords = 64;           // device wait record (pv_tower.hip TowerDiag)
-constexpr unsigned kTowerWaitUs = 1000000u;   // default awake-time bound of one dependency wait: 1 s
+constexpr unsigned kTowerWaitUs = 100000u;    // default awake-time bound of one dependency wait: 100 ms
+                                              // (longest legitimate wait measured: 7.3 ms, two processes
+                                              // sharing the GPU; 0.26 ms alone -- DESIGN.md section 7)
+extern int g_tower_breaker_s;                 // key 18: seconds of per-layer convs after a recovered launch
 struct TowerSync {
     unsigned* sync;   // tower_sync_bytes: memset per launch
     unsigned* ring;   // host-mapped ring (device alias)
@@ -155,6 +158,11 @@ struct azg_pv {
     };
     std::vector<LaunchRec> launches;
     uint32_t recovered = 0;           // launches recomputed per layer
+    // circuit breaker: a recovered launch means the dispatch did not run as one (the GPU is
+    // shared and parts of it were suspended); forwards run per-layer convs until then
+    double breaker_until = 0.0;       // steady-clock seconds
+    uint32_t breaker_trips = 0;
+    uint32_t breaker_launches = 0;    // forwards that ran per layer because of it
     int act_cap = 0;
 
     // train workspace (pv_train.hip)

@@ -390,7 +390,7 @@ def tower_waits(eng) -> dict:
     if d["timeouts"] or d["waits_suspended"] or d["max_wall_us"] > 1000:
         log(f"pid {os.getpid()} tower waits: {d}")
     out = {k: d[k] for k in ("waits_over_100us", "waits_over_1ms", "waits_over_10ms", "max_wait_us", "max_wall_us",
-                             "waits_suspended", "timeouts", "recovered")}
+                             "waits_suspended", "timeouts", "recovered", "breaker_trips", "breaker_launches")}
     if d["timeouts"]:
         out["first_timeout"] = {k: d[k] for k in ("layer", "mtile", "wait_mtile", "observed", "needed", "waited_us",
                                                   "wall_us", "waiter_xcc", "waiter_cu", "producer_claimed",

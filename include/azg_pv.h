@@ -187,8 +187,13 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          sc1 form only for the one-workgroup-per-CU 16-wave tile); returns 0 in
  *          the product library;
  *   key 14: persistent-tower dependency wait bound in microseconds of the waiting
- *          wave's awake time (default 1000000 = 1 s; -1 restores it; 0 makes every
- *          dependency wait time out at once, exercising the recovery path).
+ *          wave's awake time (default 100000 = 100 ms; -1 restores it; 0 makes every
+ *          dependency wait time out at once, exercising the recovery path);
+ *   key 18: seconds a handle runs per-layer convs after azg_pv_recover recomputed one
+ *          of its tower launches (default 30; 0 disables the breaker).  A timed-out
+ *          wait means parts of the dispatch were suspended while others ran (the GPU is
+ *          shared with another process); per-layer launches have no
+ *          cross-workgroup waits.
  *   Every call returns the previous value. */
 int32_t azg_pv_set_tuning(int32_t key, int32_t value);
 
@@ -216,7 +221,7 @@ int32_t azg_pv_recover(azg_pv* h, uint32_t seq, int32_t* recovered, void* stream
 /* Number of posted (timed-out) tower launches not yet recovered (a plain host load of
  * the pinned ring: complete for every forward the caller has synchronised with); the
  * Python layer raises on a nonzero value it cannot recover.  azg_pv_clear_status drops
- * every posted launch without recomputing it. */
+ * every posted launch without recomputing it and closes the per-layer breaker (key 18). */
 int32_t azg_pv_status(const azg_pv* h);
 int32_t azg_pv_clear_status(azg_pv* h);
 
@@ -249,7 +254,9 @@ typedef struct {
     int32_t producer_start_us;  /* its start relative to the wait's start */
     uint32_t max_wall_us;       /* longest WALL time of a wait (awake + suspended) */
     uint32_t waits_suspended;   /* waits whose wall time exceeded their awake time by > 1 ms */
-    uint32_t reserved[7];
+    uint32_t breaker_trips;     /* recoveries that switched the handle to per-layer convs (key 18) */
+    uint32_t breaker_launches;  /* forwards run per layer while the breaker was open */
+    uint32_t reserved[5];
 } azg_pv_tower_diag;
 int32_t azg_pv_tower_diag_read(azg_pv* h, azg_pv_tower_diag* out, void* stream);
 int32_t azg_pv_tower_diag_clear(azg_pv* h, void* stream);

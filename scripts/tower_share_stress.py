@@ -55,6 +55,7 @@ def worker(args):
         eng.forward_into(xs[B], *outs[B])
     torch.cuda.synchronize()
     lib.azg_pv_set_tuning(14, args.wait_us)
+    lib.azg_pv_set_tuning(18, 0)   # no per-layer breaker: every launch runs the tower
     eng.clear_status()
     eng.tower_diag_clear()
     launches = timeouts = mism = 0

@@ -329,6 +329,7 @@ def test_tower_timeout_is_recovered_bitwise():
     stream = torch.cuda.current_stream().cuda_stream
     prev_mode = lib.azg_pv_set_tuning(5, 1)
     prev_shape = lib.azg_pv_set_tuning(6, 8)
+    prev_breaker = lib.azg_pv_set_tuning(18, 0)     # breaker off: every forward runs the tower
     try:
         p_ok, v_ok = m.predict(x)                    # healthy
         pb_ok, vb_ok = m.predict_boards(bi8, pl8)
@@ -370,8 +371,22 @@ def test_tower_timeout_is_recovered_bitwise():
         p, v = m.predict(x)                          # healthy again
         assert np.array_equal(p, p_ok) and np.array_equal(v, v_ok)
         assert eng.tower_diag()["timeouts"] == 0
+        # the breaker (key 18): after a recovered launch the handle runs per-layer convs
+        # (no cross-workgroup waits) until it expires or clear_status closes it
+        lib.azg_pv_set_tuning(18, 30)
+        lib.azg_pv_set_tuning(14, 0)
+        p, v = m.predict(x)                          # times out, recovered, breaker opens
+        lib.azg_pv_set_tuning(14, -1)
+        assert eng.tower_diag()["breaker_trips"] == 1 and np.array_equal(p, p_ok)
+        p, v = m.predict(x)
+        assert eng.last_seq() == 0 and eng.tower_diag()["breaker_launches"] == 1
+        assert np.array_equal(p, p_ok) and np.array_equal(v, v_ok)
+        eng.clear_status()
+        m.predict(x)
+        assert eng.last_seq() > 0                    # the tower again
     finally:
         lib.azg_pv_set_tuning(14, -1)
+        lib.azg_pv_set_tuning(18, prev_breaker)
         lib.azg_pv_set_tuning(6, prev_shape)
         lib.azg_pv_set_tuning(5, prev_mode)
         eng.clear_status()
