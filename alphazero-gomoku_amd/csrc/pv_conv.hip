@@ -998,6 +998,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         return 0;
 #endif
     }
+    if (key == 48) {  // train weight-grad tile: 1 v2 (row table, buffer LDS-DMA, MFMA-layout slabs; default), 0 v1; bitwise identical
+        const int prev = azg::g_wgrad_variant;
+        if (value == 0 || value == 1) azg::g_wgrad_variant = value;
+        return prev;
+    }
     if (key == 18) {  // seconds of per-layer convs after a recovered tower launch (0: off)
         const int prev = azg::g_tower_breaker_s;
         if (value >= 0) azg::g_tower_breaker_s = value;

@@ -48,6 +48,7 @@ extern int g_train_fuse_apply;
 extern int g_train_fuse_fin;
 extern int g_train_apply_grid;
 extern int g_wgrad_splits;
+extern int g_wgrad_variant;
 hipError_t launch_stem_stats(int C, const float* x, const float* ws, float* out, int B, float* pa, float* pb,
                              hipStream_t st);
 constexpr int kTowerMaxBlocks = 32;

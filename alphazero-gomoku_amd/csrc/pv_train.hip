@@ -35,8 +35,9 @@
 
 namespace azg {
 
-hipError_t launch_wgrad(int C, const float* dz, const float* x, float* slab, float* dw, int M, int S,
-                        hipStream_t st, bool reduce);
+hipError_t launch_wgrad(int C, const float* dz, const float* x, const int* rowtab, float* slab, float* dw, int M,
+                        int S, hipStream_t st, bool reduce);
+hipError_t launch_rowtab(int* rowtab, int n, hipStream_t st);
 hipError_t launch_wgrad_reduce(int C, const float* slab, float* dw, int S, hipStream_t st);
 int wgrad_splits(int C, int M);
 constexpr int kMaxWgradSplits = 64;   // wgrad_splits <= slots / tiles <= 56, rounded to 8
@@ -67,6 +68,7 @@ struct TrainWS {
     float* spart = nullptr;                        // [B][27][C]
     float* slab[2] = {nullptr, nullptr};           // weight-grad split-K slabs (two alternate)
     int slab_S = 0;                                // splits one slab holds
+    int* rowtab = nullptr;                         // padded row of every pixel (weight grad v2)
     unsigned* fincnt = nullptr;   // fused BN finalize arrival counters, one per N tile
     // heads
     float *zh = nullptr, *fp = nullptr, *fv = nullptr, *hv = nullptr, *dpre = nullptr;
@@ -645,6 +647,12 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     // slabs for the automatic split count at this capacity (or the key-27 override)
     w->slab_S = std::max(wgrad_splits(C, M), std::min(g_wgrad_splits, kMaxWgradSplits));
     for (int k = 0; k < 2; ++k) A(w->slab[k], (size_t)w->slab_S * 9 * C * C, false);
+    {
+        float* rt = nullptr;
+        A(rt, (size_t)M + kRowTabPad, false);
+        w->rowtab = (int*)rt;
+    }
+    if (hipError_t e = launch_rowtab(w->rowtab, M, st)) return set_error("train workspace: row table", e);
     A(w->zh, (size_t)cap * 3 * PIX, false);
     A(w->fp, (size_t)cap * 2 * PIX, false);
     A(w->fv, (size_t)cap * PIX, false);
@@ -964,7 +972,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             AZG_CK(hipStreamWaitEvent(w->side, w->ev_ready, 0), "train: stream wait");
             int pr = prof_begin(h, AZG_PROF_TRAIN_WGRAD, w->side);
             float* sl = w->slab[slab_i];
-            AZG_CK(launch_wgrad(C, dz, xin, sl, nullptr, M, S, w->side, false), "train: wgrad");
+            AZG_CK(launch_wgrad(C, dz, xin, w->rowtab, sl, nullptr, M, S, w->side, false), "train: wgrad");
             if (pend.slab) AZG_CK(launch_wgrad_reduce(C, pend.slab, pend.dw, S, w->side), "train: wgrad reduce");
             pend = PendRed{sl, G + h->poff[tensor]};
             slab_i ^= 1;

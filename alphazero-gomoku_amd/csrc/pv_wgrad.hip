@@ -4,9 +4,8 @@
 // split over pixel slabs (split-K) so the grid fills the chip: every workgroup
 // writes its 128x128 (64x64 at C=64) partial tile to a slab; wgrad_reduce sums
 // the slabs in a fixed order (bitwise reproducible) into torch's [Cout][Cin][3][3].
-// The tile body and the reduction order live in pv_wgrad.h, shared with the
-// persistent train backward (pv_bwd_tower.hip); these are the stand-alone launches of
-// the two-stream backward schedule (tuning key 43 = 0).
+// The tile bodies and the reduction orders live in pv_wgrad.h; these are the launches
+// of the train step's two-stream backward schedule.
 #include "pv_internal.h"
 #include "pv_wgrad.h"
 
@@ -43,16 +42,65 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     wgrad_reduce_vec4<1>(slab, dw, C, S, blockIdx.x * 256 + threadIdx.x, 256);
 }
 
+// Round 5 (key 48 = 1, default): the v2 tile (pv_wgrad.h wgrad_nat_tile2 -- row table,
+// buffer LDS-DMA, MFMA-layout slabs), bitwise equal to v1's slabs summed in v1's order.
+int g_wgrad_variant = 1;
+
+template <int C>
+__global__ __launch_bounds__(256, 2) void conv3x3_wgrad_nat2(const float* __restrict__ dz, const float* __restrict__ x,
+                                                             const int* __restrict__ rowtab, float* __restrict__ slab,
+                                                             int M, int S)
+{
+    using W = WgNat<C>;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
+    const int split = (k / W::TILES) * 8 + xcd;
+    int t = k % W::TILES;
+    const int tap = t / (W::NT * W::NT);
+    t -= tap * W::NT * W::NT;
+    wgrad_nat_tile2<C, true, 4>(dz, x, rowtab, slab, M, S, split, tap, (t / W::NT) * W::BT, (t % W::NT) * W::BT,
+                                smem);
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void wgrad_reduce_mfma_kernel(const float* __restrict__ slab, float* __restrict__ dw,
+                                                                int S)
+{
+    wgrad_reduce_mfma<C, 4>(slab, dw, S, blockIdx.x * 256 + threadIdx.x);
+}
+
+// rowtab[m] = padded row of pixel m (pv_halo.h pad_row), m < n
+__global__ void rowtab_kernel(int* __restrict__ rowtab, int n)
+{
+    for (int m = blockIdx.x * blockDim.x + threadIdx.x; m < n; m += gridDim.x * blockDim.x)
+        rowtab[m] = (m / PIX) * PADPIX + ((m % PIX) / BOARD + 1) * PADW + (m % BOARD) + 1;
+}
+
+hipError_t launch_rowtab(int* rowtab, int n, hipStream_t st)
+{
+    hipLaunchKernelGGL(rowtab_kernel, dim3(256), dim3(256), 0, st, rowtab, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_wgrad_reduce(int C, const float* slab, float* dw, int S, hipStream_t st)
 {
     const int total4 = 9 * C * C / 4;
+    if (g_wgrad_variant == 1) {
+        switch (C) {
+            case 64: hipLaunchKernelGGL(wgrad_reduce_mfma_kernel<64>, dim3((total4 + 255) / 256), dim3(256), 0, st, slab, dw, S); break;
+            case 128: hipLaunchKernelGGL(wgrad_reduce_mfma_kernel<128>, dim3((total4 + 255) / 256), dim3(256), 0, st, slab, dw, S); break;
+            case 256: hipLaunchKernelGGL(wgrad_reduce_mfma_kernel<256>, dim3((total4 + 255) / 256), dim3(256), 0, st, slab, dw, S); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total4 + 255) / 256), dim3(256), 0, st, slab, dw, C, S);
     return hipGetLastError();
 }
 
 template <int C>
-static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, float* dw, int M, int S,
-                                 hipStream_t st, bool reduce)
+static hipError_t launch_wgrad_t(const float* dz, const float* x, const int* rowtab, float* slab, float* dw, int M,
+                                 int S, hipStream_t st, bool reduce)
 {
     using W = WgNat<C>;
     if (S % 8) return hipErrorInvalidValue;           // wgrad_splits guarantees S % 8 == 0
@@ -60,10 +108,19 @@ static hipError_t launch_wgrad_t(const float* dz, const float* x, float* slab, f
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void*)conv3x3_wgrad_nat<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            W::LDS_BYTES);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)conv3x3_wgrad_nat2<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    W::LDS_BYTES);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((conv3x3_wgrad_nat<C>), dim3(S * W::TILES), dim3(256), W::LDS_BYTES, st, dz, x, slab, M, S);
+    if (g_wgrad_variant == 1) {
+        if (!rowtab) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((conv3x3_wgrad_nat2<C>), dim3(S * W::TILES), dim3(256), W::LDS_BYTES, st, dz, x, rowtab,
+                           slab, M, S);
+    } else {
+        hipLaunchKernelGGL((conv3x3_wgrad_nat<C>), dim3(S * W::TILES), dim3(256), W::LDS_BYTES, st, dz, x, slab, M, S);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !reduce) return e;
     return launch_wgrad_reduce(C, slab, dw, S, st);
@@ -94,13 +151,13 @@ int wgrad_splits(int C, int M)
 }
 
 // slab must hold S*9*C*C floats, S = wgrad_splits(C, M)
-hipError_t launch_wgrad(int C, const float* dz, const float* x, float* slab, float* dw, int M, int S,
-                        hipStream_t st, bool reduce)
+hipError_t launch_wgrad(int C, const float* dz, const float* x, const int* rowtab, float* slab, float* dw, int M,
+                        int S, hipStream_t st, bool reduce)
 {
     switch (C) {
-        case 64: return launch_wgrad_t<64>(dz, x, slab, dw, M, S, st, reduce);
-        case 128: return launch_wgrad_t<128>(dz, x, slab, dw, M, S, st, reduce);
-        case 256: return launch_wgrad_t<256>(dz, x, slab, dw, M, S, st, reduce);
+        case 64: return launch_wgrad_t<64>(dz, x, rowtab, slab, dw, M, S, st, reduce);
+        case 128: return launch_wgrad_t<128>(dz, x, rowtab, slab, dw, M, S, st, reduce);
+        case 256: return launch_wgrad_t<256>(dz, x, rowtab, slab, dw, M, S, st, reduce);
         default: return hipErrorInvalidValue;
     }
 }

@@ -335,14 +335,16 @@ def train_state_after(x, pi, z, blocks, ch, steps=2, seed=3):
     return got
 
 
-@pytest.mark.parametrize("key,values", [(23, (1, 0)), (24, (1, 0)), (44, (0, 512, 97))])
+@pytest.mark.parametrize("key,values", [(23, (1, 0)), (24, (1, 0)), (44, (0, 512, 97)), (48, (1, 0))])
 def test_train_schedule_keys_bitwise(key, values):
     """The train step's product tuning keys change only the schedule: where the forward
     BN applies run (23: folded into the next conv's halo staging, or separate passes),
     where the BN finalizes run (24: by the producing conv's last workgroup, or separate
     kernels) and how many workgroups the BN apply passes use (44, grid-stride): two
     steps from one state must give bitwise-identical params, grads, BN buffers and Adam
-    moments under every value."""
+    moments under every value.  Key 48 selects the weight-grad tile (1: round 5's row-table /
+    buffer-DMA / MFMA-layout-slab form, 0: round 4's): the same MFMA chain per output and
+    the same slab sum order."""
     import _native
     lib = _native.load_library()
     b, p = synth_positions(128, seed=91)

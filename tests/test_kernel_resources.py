@@ -36,7 +36,9 @@ SCRATCH_BUDGET = [
     # train convs at C <= 128 (the 6x128 train step) and the weight grad
     (r"conv3x3_trainILi(64|128)E", 0),
     (r"conv3x3_wgrad_natILi", 0),
+    (r"conv3x3_wgrad_nat2ILi", 0),
     (r"wgrad_reduce_kernel", 0),
+    (r"wgrad_reduce_mfma_kernel", 0),
     (r"stem_mfma", 0),
 ]
 
