@@ -91,11 +91,16 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
             "`python -c 'import __graft_entry__ as g; g.build()'` (or `make -C alphazero-gomoku_amd/csrc`). "
             "There is no CPU fallback.")
     lib = ctypes.CDLL(p)
+    # AZG_PV_ALLOW_OLD_ABI=1 (bitwise cross-library studies only, scripts/train_lib_compare.py):
+    # an older library binds without the entry points it lacks
+    old_ok = os.environ.get("AZG_PV_ALLOW_OLD_ABI") == "1"
     for name, (res, args) in _SIGS.items():
+        if old_ok and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.azg_pv_abi_version() != ABI_VERSION:
+    if lib.azg_pv_abi_version() != ABI_VERSION and not old_ok:
         raise RuntimeError(f"libazg_pv ABI {lib.azg_pv_abi_version()} != expected {ABI_VERSION}")
     if path is None:
         _lib = lib

@@ -167,10 +167,11 @@ struct WgMfmaLayout {
     static constexpr int NT = C / BT;
     static constexpr int WNW = NWV == 8 ? 4 : 2;
     static constexpr int TA = BT / 64, TB = BT / (32 * WNW);
-    // float index inside one tap's C*C block of the slab
+    // float index inside one tap's C*C block of the slab of C/D register r = 4q + e of
+    // `lane`: one 16-B store instruction (fixed q) writes 1 KiB contiguous per wave
     __host__ __device__ static constexpr int index(int tco, int tci, int w, int i, int j, int lane, int r)
     {
-        return (((((tco * NT + tci) * NWV + w) * TA + i) * TB + j) * 64 + lane) * 16 + r;
+        return ((((((tco * NT + tci) * NWV + w) * TA + i) * TB + j) * 4 + (r >> 2)) * 64 + lane) * 4 + (r & 3);
     }
 };
 template <int C, bool WT, int NWV>
@@ -354,14 +355,14 @@ __device__ __forceinline__ void wgrad_reduce_mfma(const float* __restrict__ slab
     if (k + 1 < S) p1 += s4[(size_t)(k + 1) * total4 + f];
     if (k + 2 < S) p2 += s4[(size_t)(k + 2) * total4 + f];
     const f32x4 r = (p0 + p1) + (p2 + p3);
-    // decode the slab index of element 4f (r4 = 0)
+    // decode the slab index of element 4f (e = 0; L::index)
     const int idx = 4 * f;
     const int tap = idx / (C * C);
-    int rem = idx - tap * C * C;
-    const int rq = rem & 15;           // r of the first element (a multiple of 4)
-    rem >>= 4;
+    int rem = (idx - tap * C * C) >> 2;
     const int lane = rem & 63;
     rem >>= 6;
+    const int rq = (rem & 3) * 4;      // r of the first element
+    rem >>= 2;
     const int j = rem % L::TB;
     rem /= L::TB;
     const int i = rem % L::TA;
