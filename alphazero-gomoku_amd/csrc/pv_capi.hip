@@ -78,6 +78,10 @@ int32_t azg_pv_destroy(azg_pv* h)
     if (h->conv_off_dev) (void)hipFree(h->conv_off_dev);
     if (h->ring_host) (void)hipHostFree(h->ring_host);
     if (h->tower_diag) (void)hipFree(h->tower_diag);
+    if (h->wpack16) (void)hipFree(h->wpack16);
+    if (h->scale16) (void)hipFree(h->scale16);
+    if (h->h3exp) (void)hipFree(h->h3exp);
+    if (h->conv_bn_off_dev) (void)hipFree(h->conv_bn_off_dev);
     for (auto& e : h->prof_ev) (void)hipEventDestroy(e);
     delete h;
     return 0;
@@ -502,6 +506,7 @@ int32_t ensure_eval_workspace(azg_pv* h, int batch, hipStream_t st)
 int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst, int part)
 {
     const int C = h->C;
+    h->h3_dirty = true;
     const float* P = h->params;
     // stem, head FCs, every residual conv (+ its dgrad packing when training) and
     // the eval BN fold: one launch
@@ -515,6 +520,35 @@ int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst, int part)
 // Stem + residual tower.  variant 0: one launch per conv; 5 / 8 / 10: the persistent
 // tower (pv_tower.hip) with 64x64 / 128x64 / 128x128 (16-wave) tiles.  All bitwise
 // identical.
+// The split-fp16 (H3) eval weights of the current parameters (pv_pack.hip pack_h3):
+// allocated on first use, re-packed after every repack.
+static int32_t ensure_h3(azg_pv* h, hipStream_t st)
+{
+    const int C = h->C, nl = 2 * h->NB;
+    if (!h->wpack16) {
+        const BnDesc* bd = h->bn_desc.data();
+        std::vector<int> off(nl > 0 ? nl : 1, 0);
+        for (int i = 0; i < h->NB; ++i) {
+            off[2 * i] = bd[h->bn_blk[i].first].out_off;
+            off[2 * i + 1] = bd[h->bn_blk[i].second].out_off;
+        }
+        hipError_t e = hipMalloc(&h->wpack16, (size_t)(nl > 0 ? nl : 1) * 9 * C * C * sizeof(float));
+        if (e == hipSuccess) e = hipMalloc(&h->scale16, (size_t)h->nfold * sizeof(float));
+        if (e == hipSuccess) e = hipMalloc(&h->h3exp, (size_t)(nl > 0 ? nl : 1) * sizeof(int));
+        if (e == hipSuccess) e = hipMalloc(&h->conv_bn_off_dev, off.size() * sizeof(int));
+        if (e == hipSuccess) e = hipMemcpy(h->conv_bn_off_dev, off.data(), off.size() * sizeof(int), hipMemcpyHostToDevice);
+        if (e != hipSuccess) return fail("forward: split-fp16 weight buffers", e);
+        h->h3_dirty = true;
+    }
+    if (h->h3_dirty) {
+        AZG_TRY(launch_pack_h3(h->params, h->conv_off_dev, nl, C, h->conv_bn_off_dev, h->scale, h->h3exp, h->wpack16,
+                               h->scale16, st),
+                "forward: split-fp16 weight pack");
+        h->h3_dirty = false;
+    }
+    return 0;
+}
+
 static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch, hipStream_t st,
                               const int8_t* boards, const int8_t* players, float** out, unsigned seq = 0)
 {
@@ -538,7 +572,11 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
         }
         pr = prof_begin(h, variant == 10 ? AZG_PROF_TOWER_WIDE : AZG_PROF_TOWER, st, batch);
         const TowerSync ts{h->tower_sync, h->ring_dev, h->tower_diag, h->tower_prod, seq};
-        AZG_TRY(launch_tower(C, h->NB, variant, h->act, h->wpack, h->scale, h->shift, out_off, M, ts, st, &X),
+        const bool h3 = g_tower_h3 != 0;
+        if (h3)
+            if (int32_t r = ensure_h3(h, st)) return r;
+        AZG_TRY(launch_tower(C, h->NB, variant, h->act, h3 ? (const float*)h->wpack16 : h->wpack,
+                             h3 ? h->scale16 : h->scale, h->shift, out_off, M, ts, st, &X, h3),
                 "forward: tower");
         prof_end(h, pr, st);
         *out = X;

@@ -29,6 +29,8 @@ constexpr float BN_MOMENTUM = 0.1f;       // nn.BatchNorm2d default
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 // element offset of interior pixel m in a padded NHWC tensor with C channels
 __device__ __forceinline__ int pad_off(int m, int C) {

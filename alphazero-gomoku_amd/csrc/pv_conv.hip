@@ -1003,6 +1003,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         if (value == 0 || value == 1) azg::g_wgrad_variant = value;
         return prev;
     }
+    if (key == 19) {  // eval tower arithmetic: 0 fp32 MFMA (default), 1 split-fp16 products (H3, study)
+        const int prev = azg::g_tower_h3;
+        if (value == 0 || value == 1) azg::g_tower_h3 = value;
+        return prev;
+    }
     if (key == 18) {  // seconds of per-layer convs after a recovered tower launch (0: off)
         const int prev = azg::g_tower_breaker_s;
         if (value >= 0) azg::g_tower_breaker_s = value;

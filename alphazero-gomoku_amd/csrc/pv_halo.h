@@ -719,6 +719,17 @@ __device__ __forceinline__ void halo_tile(
     // staging (halo_mainloop_glds); bit 8 = epilogue loads issued before the LDS pass.  Every VAR computes bitwise-identical results.
     constexpr bool VSWZ = (VAR & 1) != 0;
     constexpr bool BPF2 = (VAR & 2) != 0;
+    // H3 (VAR bit 64, eval only): fp32-equivalent products from three fp16 MFMAs.  Every
+    // operand x is split into hi = fp16(x) and lo = fp16(x - hi) (x = hi + lo to 2^-22 of
+    // x, or 3e-8 absolute below fp16's normal range); a K16 step is acc += lo_a hi_b +
+    // hi_a lo_b + hi_a hi_b (v_mfma_f32_32x32x16_f16: exact 22-bit products, fp32
+    // accumulation), the dropped lo_a lo_b is 2^-22 of the product.  A 128-B LDS row of 32
+    // channels holds [hi 32 x fp16 | lo 32 x fp16]: the fp32 row geometry, so the 16-B slot
+    // swizzles are unchanged.  Halo rows are split while staged; weights are packed split
+    // (and scaled by a per-layer power of two so their lo parts stay normal,
+    // pv_pack.hip pack_h3; the epilogue's BN scale carries the inverse).
+    constexpr bool H3 = (VAR & 64) != 0;
+    static_assert(!H3 || (PRO == PRO_NONE && XE == XE_NONE), "H3: eval tiles only");
     constexpr int NCHK = 9 * CG;
 
     float* Ah = smem;                 // [HR][32]
@@ -857,8 +868,27 @@ __device__ __forceinline__ void halo_tile(
         }
     };
     auto hstore = [&](int cg) {
+        if constexpr (H3) {
+            // channels sc..sc+3 of the row: hi halves into slot sc/8 (byte 2*(sc%8)),
+            // lo halves into slot 4 + sc/8, both slots swizzled like the fp32 row's
 #pragma unroll
-        for (int i = 0; i < H_LD; ++i) *(f32x4*)(Ah + (sr + RPP * i) * BK + hwchunk[i]) = rh[i];
+            for (int i = 0; i < H_LD; ++i) {
+                const int key = (hwchunk[i] >> 2) ^ (tid & 7);   // the row's slot swizzle
+                f16x4 hi, lo;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    hi[e] = (_Float16)rh[i][e];
+                    lo[e] = (_Float16)(rh[i][e] - (float)hi[e]);
+                }
+                float* row = Ah + (sr + RPP * i) * BK;
+                const int q = (tid & 7) >> 1, half = ((tid & 7) & 1) * 2;
+                *(f16x4*)(row + ((q ^ key) * 4) + half) = hi;
+                *(f16x4*)(row + (((4 + q) ^ key) * 4) + half) = lo;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < H_LD; ++i) *(f32x4*)(Ah + (sr + RPP * i) * BK + hwchunk[i]) = rh[i];
+        }
     };
     auto bstore = [&](const f32x4 (&rb)[B_LD], int buf) {
         float* b = Bs + buf * BN * BK;
@@ -945,6 +975,30 @@ __device__ __forceinline__ void halo_tile(
                 aswz[i] = VSWZ ? ((vpix[i] + vd) >> 1) & 7 : (r >> 1) & 7;
             }
             const float* Bb = Bs + cur * BN * BK;
+            if constexpr (H3) {
+#pragma unroll
+                for (int st = 0; st < 2; ++st) {   // K16 steps: channels 16 st + 8 h + (0..7)
+                    f16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) {
+                        ah[i] = *(const f16x8*)(Ah + arow[i] + (((2 * st + h) ^ aswz[i]) * 4));
+                        al[i] = *(const f16x8*)(Ah + arow[i] + (((4 + 2 * st + h) ^ aswz[i]) * 4));
+                    }
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        bh[j] = *(const f16x8*)(Bb + brow + j * 32 * BK + (((2 * st + h) ^ bswz) * 4));
+                        bl[j] = *(const f16x8*)(Bb + brow + j * 32 * BK + (((4 + 2 * st + h) ^ bswz) * 4));
+                    }
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) {
+                            at[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], at[i][j], 0, 0, 0);
+                            at[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], at[i][j], 0, 0, 0);
+                            at[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], at[i][j], 0, 0, 0);
+                        }
+                }
+            } else
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 f32x4 a[TM], b[TN];

@@ -70,7 +70,7 @@ struct TowerSync {
 };
 hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const float* wpack, const float* scale,
                         const float* shift, const int* out_off, int M, const TowerSync& ts, hipStream_t st,
-                        float** result);
+                        float** result, bool h3 = false);
 extern unsigned g_tower_wait_us;
 extern int g_tower_group;
 #ifdef AZG_AB_STUDIES
@@ -99,6 +99,9 @@ hipError_t launch_repack_all(const float* params, const int64_t* conv_offs, int 
                              const float* stem_w, float* ws, const float* wpf, const float* wv1, float* wfc,
                              const float* stats, const void* desc, int nbn, float* scale, float* shift,
                              hipStream_t st, int part = 0);
+hipError_t launch_pack_h3(const float* params, const int64_t* offs, int nl, int C, const int* conv_bn_off,
+                          const float* scale, int* exps, void* wp16, float* scale16, hipStream_t st);
+extern int g_tower_h3;
 hipError_t launch_fold_bn(const float* params, const float* stats, const void* desc, int nlayers,
                           float* scale, float* shift, hipStream_t st);
 
@@ -137,6 +140,13 @@ struct azg_pv {
     float* wfc = nullptr;     // [FC_OUT][FC_KP] packed policy_fc + value_fc1 (pv_heads.hip heads_fc)
     float* scale = nullptr;   // folded BN (eval)
     float* shift = nullptr;
+    // split-fp16 (H3) eval weights: packed [hi | lo] rows of w * 2^e per conv, the BN
+    // scale times 2^-e, the exponents and each conv's BN offset (allocated on first use)
+    void* wpack16 = nullptr;
+    float* scale16 = nullptr;
+    int* h3exp = nullptr;
+    int* conv_bn_off_dev = nullptr;
+    bool h3_dirty = true;
 
     // eval activations: 3 padded NHWC buffers + head features [B][3][225]
     float* act[3] = {nullptr, nullptr, nullptr};

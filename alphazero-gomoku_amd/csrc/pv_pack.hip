@@ -154,6 +154,68 @@ hipError_t launch_repack_all(const float* params, const int64_t* conv_offs, int 
 
 static inline int nblk(int total) { int b = (total + 255) / 256; return b > 4096 ? 4096 : b; }
 
+// ---- split-fp16 (H3) eval weights (pv_halo.h halo_tile VAR bit 64) ----
+// exps[l] = 14 - floor(log2 max|w_l|): max|w_l| * 2^e < 2^15, so hi = fp16(w 2^e) never
+// overflows and the lo parts of every weight above 2^-10 of the layer's largest stay
+// normal fp16 (the rest carry 2^-25 absolute error)
+__global__ __launch_bounds__(256) void h3_exp_kernel(const float* __restrict__ params, const int64_t* __restrict__ offs,
+                                                     int C, int* __restrict__ exps)
+{
+    __shared__ float red[256];
+    const float* w = params + offs[blockIdx.x];
+    float m = 0.f;
+    for (int i = threadIdx.x; i < 9 * C * C; i += 256) m = fmaxf(m, fabsf(w[i]));
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) exps[blockIdx.x] = red[0] > 0.f ? 14 - ilogbf(red[0]) : 0;
+}
+
+// packed row (kc * C + n) of 32 K values -> 64 halves [hi 32 | lo 32] of w * 2^e, in
+// the fp32 packing's order (repack_all_kernel)
+__global__ __launch_bounds__(256) void pack_h3_kernel(const float* __restrict__ params, const int64_t* __restrict__ offs,
+                                                      int C, const int* __restrict__ exps, _Float16* __restrict__ out)
+{
+    const int total = 9 * C * C, cg_n = C / 32;
+    const int l = blockIdx.y;
+    const float* w = params + offs[l];
+    _Float16* o = out + (size_t)l * 2 * total;
+    const float sc = ldexpf(1.f, exps[l]);
+    for (int idx = blockIdx.x * 256 + threadIdx.x; idx < total; idx += gridDim.x * 256) {
+        const int k = idx & 31, n = (idx >> 5) % C, kc = idx / (32 * C);
+        const int tap = kc / cg_n, c2 = (kc - tap * cg_n) * 32 + k;
+        const float v = w[(n * C + c2) * 9 + tap] * sc;
+        const _Float16 hi = (_Float16)v;
+        const int row = idx >> 5;
+        o[row * 64 + k] = hi;
+        o[row * 64 + 32 + k] = (_Float16)(v - (float)hi);
+    }
+}
+
+// scale16 = the eval BN scale of every residual conv's BN times 2^-e (exact)
+__global__ void scale_h3_kernel(const float* __restrict__ scale, const int* __restrict__ conv_bn_off,
+                                const int* __restrict__ exps, int C, float* __restrict__ scale16)
+{
+    const int l = blockIdx.x, o = conv_bn_off[l];
+    const float f = ldexpf(1.f, -exps[l]);
+    for (int c = threadIdx.x; c < C; c += blockDim.x) scale16[o + c] = scale[o + c] * f;
+}
+
+hipError_t launch_pack_h3(const float* params, const int64_t* offs, int nl, int C, const int* conv_bn_off,
+                          const float* scale, int* exps, void* wp16, float* scale16, hipStream_t st)
+{
+    if (nl <= 0) return hipSuccess;
+    hipLaunchKernelGGL(h3_exp_kernel, dim3(nl), dim3(256), 0, st, params, offs, C, exps);
+    int nb = nblk(9 * C * C);
+    nb = nb > 256 ? 256 : nb;
+    hipLaunchKernelGGL(pack_h3_kernel, dim3(nb, nl), dim3(256), 0, st, params, offs, C, exps, (_Float16*)wp16);
+    hipLaunchKernelGGL(scale_h3_kernel, dim3(nl), dim3(256), 0, st, scale, conv_bn_off, exps, C, scale16);
+    return hipGetLastError();
+}
+
 hipError_t launch_pack_convs(const float* params, const int64_t* offs, int nl, float* wp, float* wd, int C,
                              hipStream_t st)
 {

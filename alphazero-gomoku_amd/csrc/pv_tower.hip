@@ -331,9 +331,11 @@ size_t tower_prod_bytes(int nlayers, int M)
 // H -> Y (BN, + X, ReLU), X <-> Y.  `act` are the three padded NHWC buffers
 // (act[0] holds the stem output; the result ends in act[0] or act[2], returned in
 // *result).  `sync` must hold tower_sync_bytes(2*NB, M) bytes.
+int g_tower_h3 = 0;   // key 19: split-fp16 (H3) eval tower (pv_halo.h VAR bit 64); 0 = fp32 MFMA
+
 hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const float* wpack, const float* scale,
                         const float* shift, const int* out_off, int M, const TowerSync& ts, hipStream_t st,
-                        float** result)
+                        float** result, bool h3)
 {
     if (2 * NB > kTowerMaxLayers) return hipErrorInvalidValue;
     const size_t act_bytes = (size_t)(M / PIX) * PADPIX * C * sizeof(float);
@@ -372,6 +374,17 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     *result = X;
     hipError_t e = hipMemsetAsync(sync, 0, tower_sync_bytes(2 * NB, M), st);
     if (e != hipSuccess) return e;
+    if (h3) {   // wpack / scale are the split-fp16 packs (pv_pack.hip pack_h3)
+        switch (C) {
+            case 128:
+                if (shape == 5) return launch_tower_t<128, 64, 2, 1, 4, 96>(a, st, nullptr);
+                return launch_tower_t<128, 64, 4, 1, 8, 96>(a, st, nullptr);
+            case 256:
+                if (shape == 5) return launch_tower_t<256, 64, 2, 1, 4, 97>(a, st, nullptr);
+                return launch_tower_t<256, 64, 4, 1, 8, 97>(a, st, nullptr);
+            default: return hipErrorInvalidValue;
+        }
+    }
 #ifdef AZG_AB_STUDIES
     // traffic ablations of the 128x64 tower (key 8 bits 4 / 8: no weight / no halo loads)
     if (shape == 8 && (a.abl & 12)) {
