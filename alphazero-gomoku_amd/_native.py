@@ -27,7 +27,8 @@ class TowerDiag(ctypes.Structure):
         "waiter_hwid", "waiter_xcc", "claims", "producer_claimed", "producer_started", "producer_hwid",
         "producer_xcc")] + [("producer_start_us", ctypes.c_int32), ("max_wall_us", ctypes.c_uint32),
                              ("waits_suspended", ctypes.c_uint32), ("breaker_trips", ctypes.c_uint32),
-                             ("breaker_launches", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 5)]
+                             ("breaker_launches", ctypes.c_uint32), ("h3_overflows", ctypes.c_uint32),
+                             ("reserved", ctypes.c_uint32 * 4)]
 
     def as_dict(self) -> dict:
         d = {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}

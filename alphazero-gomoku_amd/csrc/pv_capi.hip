@@ -134,14 +134,17 @@ int32_t azg_pv_bind(azg_pv* h, float* params, float* grads, float* bn_stats)
             e = hipMemcpy(h->conv_off_dev, offs.data(), sizeof(int64_t) * offs.size(), hipMemcpyHostToDevice);
         if (e != hipSuccess) return fail("azg_pv_bind: conv offset upload", e);
         void* sp = nullptr;
-        e = hipHostMalloc(&sp, kTowerRing * sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent);
+        // two rings in one pinned, mapped allocation: timed-out tower launches, H3 overflows
+        e = hipHostMalloc(&sp, 2 * kTowerRing * sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent);
         if (e != hipSuccess) return fail("azg_pv_bind: hipHostMalloc(tower ring)", e);
         h->ring_host = (unsigned*)sp;
-        memset(h->ring_host, 0, kTowerRing * sizeof(unsigned));
+        h->ovf_host = h->ring_host + kTowerRing;
+        memset(h->ring_host, 0, 2 * kTowerRing * sizeof(unsigned));
         void* dp = nullptr;
         e = hipHostGetDevicePointer(&dp, sp, 0);
         if (e != hipSuccess) return fail("azg_pv_bind: hipHostGetDevicePointer(tower ring)", e);
         h->ring_dev = (unsigned*)dp;
+        h->ovf_dev = h->ring_dev + kTowerRing;
         e = hipMalloc(&h->tower_diag, kTowerDiagWords * sizeof(unsigned));
         if (e == hipSuccess) e = hipMemset(h->tower_diag, 0, kTowerDiagWords * sizeof(unsigned));
         if (e != hipSuccess) return fail("azg_pv_bind: tower wait record", e);
@@ -239,7 +242,7 @@ int32_t azg_pv_status(const azg_pv* h)
 {
     if (!h || !h->ring_host) return 0;
     int32_t n = 0;
-    for (unsigned i = 0; i < kTowerRing; ++i) n += __atomic_load_n(h->ring_host + i, __ATOMIC_ACQUIRE) != 0u;
+    for (unsigned i = 0; i < 2 * kTowerRing; ++i) n += __atomic_load_n(h->ring_host + i, __ATOMIC_ACQUIRE) != 0u;
     return n;
 }
 
@@ -247,7 +250,7 @@ int32_t azg_pv_clear_status(azg_pv* h)
 {
     if (!h) return fail("azg_pv_clear_status: null handle");
     if (h->ring_host)
-        for (unsigned i = 0; i < kTowerRing; ++i) __atomic_store_n(h->ring_host + i, 0u, __ATOMIC_RELEASE);
+        for (unsigned i = 0; i < 2 * kTowerRing; ++i) __atomic_store_n(h->ring_host + i, 0u, __ATOMIC_RELEASE);
     h->breaker_until = 0.0;   // and the per-layer breaker closes
     return 0;
 }
@@ -271,16 +274,25 @@ int32_t azg_pv_recover(azg_pv* h, uint32_t seq, int32_t* recovered, void* stream
     *recovered = 0;
     if (seq == 0 || !h->ring_host) return 0;
     const unsigned slot = seq & (kTowerRing - 1);
-    if (__atomic_load_n(h->ring_host + slot, __ATOMIC_ACQUIRE) != seq) return 0;
+    const bool ovf = __atomic_load_n(h->ovf_host + slot, __ATOMIC_ACQUIRE) == seq;
+    const bool tmo = __atomic_load_n(h->ring_host + slot, __ATOMIC_ACQUIRE) == seq;
+    if (!ovf && !tmo) return 0;
     const azg_pv::LaunchRec r = h->launches[slot];
     if (r.seq != seq)
-        return fail("azg_pv_recover: the timed-out launch is older than the launch record ring (recover it sooner)");
+        return fail("azg_pv_recover: the posted launch is older than the launch record ring (recover it sooner)");
     // per-layer convs from the same inputs into the same outputs: bitwise what the tower
-    // computes when no wait times out
+    // computes when no wait times out; an H3 launch whose activations left fp16's range
+    // is recomputed with fp32 MFMA
     if (int32_t e = forward_eval(h, r.x, r.batch, r.probs, r.values, r.logits, (hipStream_t)stream, r.boards,
-                                 r.players, r.priors, true))
+                                 r.players, r.priors, true, ovf))
         return e;
     __atomic_store_n(h->ring_host + slot, 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(h->ovf_host + slot, 0u, __ATOMIC_RELEASE);
+    if (ovf) ++h->h3_overflows;
+    if (!tmo) {   // a range overflow alone: no breaker (the dispatch ran as one)
+        *recovered = 1;
+        return 0;
+    }
     ++h->recovered;
     *recovered = 1;
     if (g_tower_breaker_s > 0) {
@@ -297,6 +309,7 @@ int32_t azg_pv_tower_diag_read(azg_pv* h, azg_pv_tower_diag* out, void* stream)
     out->recovered = h->recovered;
     out->breaker_trips = h->breaker_trips;
     out->breaker_launches = h->breaker_launches;
+    out->h3_overflows = h->h3_overflows;
     if (!h->tower_diag) return 0;
     unsigned w[kTowerDiagWords];
     hipStream_t st = (hipStream_t)stream;
@@ -329,6 +342,7 @@ int32_t azg_pv_tower_diag_read(azg_pv* h, azg_pv_tower_diag* out, void* stream)
     out->waits_suspended = w[24];
     out->breaker_trips = h->breaker_trips;
     out->breaker_launches = h->breaker_launches;
+    out->h3_overflows = h->h3_overflows;
     return 0;
 }
 
@@ -338,6 +352,7 @@ int32_t azg_pv_tower_diag_clear(azg_pv* h, void* stream)
     h->recovered = 0;
     h->breaker_trips = 0;
     h->breaker_launches = 0;
+    h->h3_overflows = 0;
     if (!h->tower_diag) return 0;
     hipStream_t st = (hipStream_t)stream;
     AZG_TRY(hipMemsetAsync(h->tower_diag, 0, kTowerDiagWords * sizeof(unsigned), st), "azg_pv_tower_diag_clear");
@@ -549,8 +564,20 @@ static int32_t ensure_h3(azg_pv* h, hipStream_t st)
     return 0;
 }
 
+// H3 per-layer tile: the 64x64 / 4-wave tile (shape 5, up to 4 workgroups per CU) or the
+// 128x64 / 8-wave tile (shape 8, 2 per CU), whichever needs fewer 128-row-equivalent
+// rounds of resident slots (ties: the 128-row tile).  Both compute the same arithmetic.
+static int conv_tuned_shape_h3(azg_pv* h, int batch, hipStream_t, const float*, const int8_t*, const int8_t*)
+{
+    const int M = batch * PIX, ntn = h->C / 64;
+    const long t5 = (long)((M + 63) / 64) * ntn, t8 = (long)((M + 127) / 128) * ntn;
+    const long r5 = (t5 + 1023) / 1024, r8 = (t8 + 511) / 512;
+    return r5 < 2 * r8 ? 5 : 8;
+}
+
 static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch, hipStream_t st,
-                              const int8_t* boards, const int8_t* players, float** out, unsigned seq = 0)
+                              const int8_t* boards, const int8_t* players, float** out, unsigned seq = 0,
+                              bool h3 = false)
 {
     const int C = h->C;
     const int M = batch * PIX;
@@ -571,14 +598,33 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
             out_off[2 * i + 1] = bd[h->bn_blk[i].second].out_off;
         }
         pr = prof_begin(h, variant == 10 ? AZG_PROF_TOWER_WIDE : AZG_PROF_TOWER, st, batch);
-        const TowerSync ts{h->tower_sync, h->ring_dev, h->tower_diag, h->tower_prod, seq};
-        const bool h3 = g_tower_h3 != 0;
-        if (h3)
-            if (int32_t r = ensure_h3(h, st)) return r;
+        const TowerSync ts{h->tower_sync, h->ring_dev, h->ovf_dev, h->tower_diag, h->tower_prod, seq};
         AZG_TRY(launch_tower(C, h->NB, variant, h->act, h3 ? (const float*)h->wpack16 : h->wpack,
                              h3 ? h->scale16 : h->scale, h->shift, out_off, M, ts, st, &X, h3),
                 "forward: tower");
         prof_end(h, pr, st);
+        *out = X;
+        return 0;
+    }
+    if (h3) {   // split-fp16 per-layer convs: the tower's arithmetic, layer by layer
+        const int shape = conv_tuned_shape_h3(h, batch, st, x, boards, players);
+        const float* wp16 = (const float*)h->wpack16;
+        for (int i = 0; i < h->NB; ++i) {
+            const BnDesc& b1 = bd[h->bn_blk[i].first];
+            const BnDesc& b2 = bd[h->bn_blk[i].second];
+            pr = prof_begin(h, AZG_PROF_CONV3X3, st, batch);
+            AZG_TRY(launch_conv3x3_h3(shape, C, EPI_BN_RELU, X, wp16 + (size_t)(2 * i) * 9 * C * C,
+                                      h->scale16 + b1.out_off, h->shift + b1.out_off, nullptr, H, M, st, h->ovf_dev,
+                                      seq),
+                    "forward: conv1 (H3)");
+            prof_end(h, pr, st);
+            pr = prof_begin(h, AZG_PROF_CONV3X3, st, batch);
+            AZG_TRY(launch_conv3x3_h3(shape, C, EPI_BN_RES_RELU, H, wp16 + (size_t)(2 * i + 1) * 9 * C * C,
+                                      h->scale16 + b2.out_off, h->shift + b2.out_off, X, Y, M, st, h->ovf_dev, seq),
+                    "forward: conv2 (H3)");
+            prof_end(h, pr, st);
+            float* t = X; X = Y; Y = t;
+        }
         *out = X;
         return 0;
     }
@@ -614,15 +660,15 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
 // and is not a candidate; key 6 = 10 forces it.  While the stream is being captured
 // the untuned default is used.  All variants are bitwise identical.
 static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, const int8_t* boards,
-                         const int8_t* players)
+                         const int8_t* players, bool h3)
 {
     if (h->NB == 0 || h->NB > kTowerMaxBlocks) return 0;
     if ((size_t)batch * PADPIX * h->C * sizeof(float) >= (size_t)INT32_MAX) return 0;
     if (g_tower_mode == 0) return 0;
-    if (g_tower_mode == 1) return (g_tower_shape == 10 && h->C != 128) ? 8 : g_tower_shape;
+    if (g_tower_mode == 1) return (g_tower_shape == 10 && (h->C != 128 || h3)) ? 8 : g_tower_shape;
     const int bucket = conv_batch_bucket(batch * PIX);
-    static std::map<std::tuple<int, int, int>, int> cache;
-    const auto key = std::make_tuple(h->C, h->NB, bucket);
+    static std::map<std::tuple<int, int, int, int>, int> cache;
+    const auto key = std::make_tuple(h->C, h->NB, bucket, (int)h3);
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
     const int fallback = batch >= 128 ? 8 : 0;
@@ -642,7 +688,7 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
             for (int r = 0; r < 3 && ok; ++r)
                 for (int c = 0; c < ncand && ok; ++c) {
                     ok = hipEventRecord(e0, st) == hipSuccess &&
-                         stem_and_tower(h, cand[c], x, batch, st, boards, players, &out) == 0 &&
+                         stem_and_tower(h, cand[c], x, batch, st, boards, players, &out, 0, h3) == 0 &&
                          hipEventRecord(e1, st) == hipSuccess && hipEventSynchronize(e1) == hipSuccess;
                     float ms = 0.f;
                     if (ok && r > 0 && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms < best_ms[c]) best_ms[c] = ms;
@@ -665,12 +711,18 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
 }
 
 int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* values, float* logits,
-                     hipStream_t st, const int8_t* boards, const int8_t* players, float* priors, bool per_layer)
+                     hipStream_t st, const int8_t* boards, const int8_t* players, float* priors, bool per_layer,
+                     bool fp32_only)
 {
     const int C = h->C;
     const float* P = h->params;
     const BnDesc* bd = h->bn_desc.data();
-    int variant = per_layer ? 0 : tower_variant(h, x, batch, st, boards, players);
+    // split-fp16 residual convs (key 19, C = 128 / 256): every path of the forward -- tower,
+    // per-layer, the autotuner's candidates, a recompute -- then computes the same arithmetic
+    const bool h3 = g_tower_h3 != 0 && !fp32_only && (C == 128 || C == 256) && h->NB > 0;
+    if (h3)
+        if (int32_t r = ensure_h3(h, st)) return r;
+    int variant = per_layer ? 0 : tower_variant(h, x, batch, st, boards, players, h3);
     if (variant != 0 && h->breaker_until > 0.0) {
         if (now_s() < h->breaker_until) {
             variant = 0;
@@ -679,18 +731,20 @@ int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* 
             h->breaker_until = 0.0;
         }
     }
-    // a tower launch gets a number and a record of its buffers (azg_pv_recover)
+    // a tower or H3 launch gets a number and a record of its buffers (azg_pv_recover);
+    // a recompute (per_layer) posts nothing
     unsigned seq = 0;
-    if (variant != 0 && h->NB > 0 && !h->launches.empty()) {
+    if ((variant != 0 || h3) && h->NB > 0 && !h->launches.empty() && !per_layer) {
         seq = ++h->seq;
         if (seq == 0) seq = ++h->seq;   // 0 means "not posted"
         azg_pv::LaunchRec& r = h->launches[seq & (kTowerRing - 1)];
-        r = azg_pv::LaunchRec{seq, x, boards, players, batch, probs, values, logits, priors};
+        r = azg_pv::LaunchRec{seq, x, boards, players, batch, h3, probs, values, logits, priors};
         __atomic_store_n(h->ring_host + (seq & (kTowerRing - 1)), 0u, __ATOMIC_RELEASE);
+        __atomic_store_n(h->ovf_host + (seq & (kTowerRing - 1)), 0u, __ATOMIC_RELEASE);
     }
     if (!per_layer) h->last_seq = seq;
     float* X = nullptr;
-    if (int32_t r = stem_and_tower(h, variant, x, batch, st, boards, players, &X, seq)) return r;
+    if (int32_t r = stem_and_tower(h, variant, x, batch, st, boards, players, &X, seq, h3)) return r;
     const int ho = bd[h->bn_pol].out_off;   // policy (2) then value (1): contiguous
     int pr = prof_begin(h, AZG_PROF_HEADS, st, batch);
     AZG_TRY(launch_heads_fwd(C, X, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], h->scale + ho, h->shift + ho,

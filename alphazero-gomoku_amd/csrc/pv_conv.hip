@@ -207,7 +207,7 @@ template <int C, int BN_, int WM_, int TM_, int NW_, int EPI, int ABL = 0, int V
 __global__ __launch_bounds__(64 * NW_, 2) void conv3x3_halo(
     const float* __restrict__ in, const float* __restrict__ wp,
     const float* __restrict__ scale, const float* __restrict__ shift,
-    const float* __restrict__ resid, float* __restrict__ out, int M)
+    const float* __restrict__ resid, float* __restrict__ out, int M, H3Guard guard)
 {
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -217,7 +217,7 @@ __global__ __launch_bounds__(64 * NW_, 2) void conv3x3_halo(
     const int t = xcd * q8 + min(xcd, r8) + (L >> 3);
     halo_tile<C, BN_, WM_, TM_, NW_, EPI, false, ABL, VAR>(in, wp, scale, shift, resid, out,
                                           __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0, 0x00020000), M,
-                                          (t / NTN) * T::BM, (t % NTN) * T::BN, smem);
+                                          (t / NTN) * T::BM, (t % NTN) * T::BN, smem, EpiX{}, ProX{}, FinX{}, guard);
 }
 // Train-step conv (forward z = conv(a), dgrad = conv(dZ, flipped W) [+ resid]) with
 // the BatchNorm partial sums fused into the epilogue (pv_halo.h XE_STATS / XE_BNBWD):
@@ -510,7 +510,7 @@ static hipError_t launch_conv_t(const float* in, const float* wp, const float* s
 
 template <int C, int BN, int WM, int TM, int NW, int EPI, int VAR = 0>
 static hipError_t launch_halo_t(const float* in, const float* wp, const float* scale, const float* shift,
-                                const float* resid, float* out, int M, hipStream_t st)
+                                const float* resid, float* out, int M, hipStream_t st, const H3Guard& guard = H3Guard{})
 {
     using T = ConvTile<C, BN, WM, TM, NW>;
     constexpr int lds = halo_lds_bytes<C, BN, WM, TM, NW, VAR>();
@@ -523,7 +523,7 @@ static hipError_t launch_halo_t(const float* in, const float* wp, const float* s
     }
     dim3 grid(((M + T::BM - 1) / T::BM) * (C / T::BN));
     hipLaunchKernelGGL((conv3x3_halo<C, BN, WM, TM, NW, EPI, 0, VAR>), grid, dim3(T::NT), lds, st, in, wp, scale,
-                       shift, resid, out, M);
+                       shift, resid, out, M, guard);
     return hipGetLastError();
 }
 
@@ -687,6 +687,33 @@ hipError_t launch_conv3x3_shape(int shape, int C, int epi, const float* in, cons
 #undef AZG_SB_SHAPES
 }
 
+// Split-fp16 (H3) per-layer conv (pv_halo.h VAR bit 64; wp / scale = the H3 packs of
+// pv_pack.hip pack_h3): the eval tower's arithmetic per layer (bitwise equal to it), the
+// 64x64 / 4-wave tile (shape 5) or the 128x64 / 8-wave tile (shape 8), buffer addressing.
+template <int CC, int BN, int WM, int NW>
+static hipError_t launch_h3_t(int epi, const float* in, const float* wp, const float* scale, const float* shift,
+                              const float* resid, float* out, int M, hipStream_t st, const H3Guard& g)
+{
+    if (epi == EPI_BN_RELU) return launch_halo_t<CC, BN, WM, 1, NW, EPI_BN_RELU, 96>(in, wp, scale, shift, resid, out, M, st, g);
+    if (epi == EPI_BN_RES_RELU) return launch_halo_t<CC, BN, WM, 1, NW, EPI_BN_RES_RELU, 96>(in, wp, scale, shift, resid, out, M, st, g);
+    return hipErrorInvalidValue;
+}
+hipError_t launch_conv3x3_h3(int shape, int C, int epi, const float* in, const float* wp, const float* scale,
+                             const float* shift, const float* resid, float* out, int M, hipStream_t st,
+                             unsigned* ring, unsigned seq)
+{
+    const H3Guard g{ring, seq};
+    switch (C) {
+        case 128:
+            if (shape == 8) return launch_h3_t<128, 64, 4, 8>(epi, in, wp, scale, shift, resid, out, M, st, g);
+            return launch_h3_t<128, 64, 2, 4>(epi, in, wp, scale, shift, resid, out, M, st, g);
+        case 256:
+            if (shape == 8) return launch_h3_t<256, 64, 4, 8>(epi, in, wp, scale, shift, resid, out, M, st, g);
+            return launch_h3_t<256, 64, 2, 4>(epi, in, wp, scale, shift, resid, out, M, st, g);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 int g_conv_shape_override = -1;
 int g_conv_autotune = 1;
 int g_conv_ablation = 0;
@@ -706,7 +733,7 @@ static hipError_t launch_ablation_s(const float* in, const float* wp, const floa
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     dim3 grid(((M + T::BM - 1) / T::BM) * (128 / BN));
     hipLaunchKernelGGL((conv3x3_halo<128, BN, WM, TM, NW, EPI_BN_RELU, ABL>), grid, dim3(T::NT), lds, st, in, wp,
-                       scale, shift, resid, out, M);
+                       scale, shift, resid, out, M, H3Guard{});
     return hipGetLastError();
 }
 
@@ -1003,7 +1030,7 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         if (value == 0 || value == 1) azg::g_wgrad_variant = value;
         return prev;
     }
-    if (key == 19) {  // eval tower arithmetic: 0 fp32 MFMA (default), 1 split-fp16 products (H3, study)
+    if (key == 19) {  // eval residual-conv arithmetic: 1 split-fp16 products (H3, default), 0 fp32 MFMA
         const int prev = azg::g_tower_h3;
         if (value == 0 || value == 1) azg::g_tower_h3 = value;
         return prev;

@@ -236,6 +236,15 @@ struct ProX {
 };
 
 
+// H3 range guard: a staged activation at or above fp16's largest finite value (65504)
+// cannot be split; the tile posts its launch number to the handle's host ring (the
+// host recomputes that forward with fp32 MFMA, azg_pv_recover) and computes on.
+struct H3Guard {
+    unsigned* ring = nullptr;   // host-mapped, kTowerRing entries (device alias)
+    unsigned seq = 0;
+};
+constexpr unsigned kH3RingSize = 256;   // = kTowerRing (pv_internal.h)
+
 // key of the 16-B slot swizzle of halo row `row` (padded-pixel index): the padded
 // board position v = yy*15 + xx (see halo_tile)
 __device__ __forceinline__ int halo_vkey(int row)
@@ -692,7 +701,7 @@ __device__ __forceinline__ void halo_tile(
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ resid, float* __restrict__ out, __amdgpu_buffer_rsrc_t out_rs,
     int M, int m0, int n0, float* smem, const EpiX& ex = EpiX{}, const ProX& px = ProX{},
-    const FinX& fx = FinX{})
+    const FinX& fx = FinX{}, const H3Guard& guard = H3Guard{})
 {
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
     if constexpr ((VAR & 4) != 0) {   // LDS-DMA staging
@@ -867,6 +876,7 @@ __device__ __forceinline__ void halo_tile(
             if ((pown >> i) & 1) store4<true>(px.aout, ars, hsrc[i] + cg * BK, v);
         }
     };
+    bool h3big = false;   // H3: a staged value outside fp16's range (H3Guard)
     auto hstore = [&](int cg) {
         if constexpr (H3) {
             // channels sc..sc+3 of the row: hi halves into slot sc/8 (byte 2*(sc%8)),
@@ -877,6 +887,7 @@ __device__ __forceinline__ void halo_tile(
                 f16x4 hi, lo;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
+                    h3big |= !(fabsf(rh[i][e]) < 65504.f);   // also catches NaN
                     hi[e] = (_Float16)rh[i][e];
                     lo[e] = (_Float16)(rh[i][e] - (float)hi[e]);
                 }
@@ -1043,6 +1054,11 @@ __device__ __forceinline__ void halo_tile(
             for (int j = 0; j < TN; ++j) acc[i][j] += at[i][j];
     }
 
+    if constexpr (H3) {
+        if (h3big && guard.ring && guard.seq)
+            __hip_atomic_store(guard.ring + (guard.seq & (kH3RingSize - 1)), guard.seq, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     // the last chunk ended with a barrier: the staging buffers are free
     halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, (VSWZ ? BN : BN + 8), (VAR & 8) != 0, XE,
                   (VAR & 16) ? 2 : (VAR & 32) ? 1 : 0>(

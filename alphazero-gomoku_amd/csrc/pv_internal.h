@@ -64,6 +64,7 @@ extern int g_tower_breaker_s;                 // key 18: seconds of per-layer co
 struct TowerSync {
     unsigned* sync;   // tower_sync_bytes: memset per launch
     unsigned* ring;   // host-mapped ring (device alias)
+    unsigned* ring_ovf;   // host-mapped ring of H3 range overflows (device alias)
     unsigned* diag;   // kTowerDiagWords, persistent
     void* prod;       // tower_prod_bytes, persistent
     unsigned seq;     // launch number (0: not posted)
@@ -99,6 +100,9 @@ hipError_t launch_repack_all(const float* params, const int64_t* conv_offs, int 
                              const float* stem_w, float* ws, const float* wpf, const float* wv1, float* wfc,
                              const float* stats, const void* desc, int nbn, float* scale, float* shift,
                              hipStream_t st, int part = 0);
+hipError_t launch_conv3x3_h3(int shape, int C, int epi, const float* in, const float* wp, const float* scale,
+                             const float* shift, const float* resid, float* out, int M, hipStream_t st,
+                             unsigned* ring, unsigned seq);
 hipError_t launch_pack_h3(const float* params, const int64_t* offs, int nl, int C, const int* conv_bn_off,
                           const float* scale, int* exps, void* wp16, float* scale16, hipStream_t st);
 extern int g_tower_h3;
@@ -156,6 +160,8 @@ struct azg_pv {
     unsigned* tower_diag = nullptr;   // persistent tower: wait record (kTowerDiagWords, device)
     unsigned* ring_host = nullptr;    // timed-out launch numbers [kTowerRing], pinned + mapped (kernels post, host reads)
     unsigned* ring_dev = nullptr;     // device alias of ring_host
+    unsigned* ovf_host = nullptr;     // H3 launches whose activations left fp16's range [kTowerRing], same memory
+    unsigned* ovf_dev = nullptr;
     unsigned seq = 0;                 // last tower launch number handed out (0 = none yet)
     unsigned last_seq = 0;            // the last forward's launch number (0: it ran per-layer convs)
     // what each posted launch read and wrote, by seq % kTowerRing (azg_pv_recover re-runs it)
@@ -165,10 +171,12 @@ struct azg_pv {
         const int8_t* boards = nullptr;
         const int8_t* players = nullptr;
         int batch = 0;
+        bool h3 = false;
         float *probs = nullptr, *values = nullptr, *logits = nullptr, *priors = nullptr;
     };
     std::vector<LaunchRec> launches;
     uint32_t recovered = 0;           // launches recomputed per layer
+    uint32_t h3_overflows = 0;        // H3 launches recomputed with fp32 MFMA (activations beyond fp16's range)
     // circuit breaker: a recovered launch means the dispatch did not run as one (the GPU is
     // shared and parts of it were suspended); forwards run per-layer convs until then
     double breaker_until = 0.0;       // steady-clock seconds
@@ -201,5 +209,5 @@ hipError_t prof_harvest(azg_pv* h);
 void prof_end(azg_pv* h, int pair, hipStream_t st);
 int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* values, float* logits,
                      hipStream_t st, const int8_t* boards, const int8_t* players, float* priors,
-                     bool per_layer = false);
+                     bool per_layer = false, bool fp32_only = false);
 }  // namespace azg

@@ -59,6 +59,7 @@ struct TowerArgs {
     int act_bytes;       // bytes of one activation buffer (buffer descriptor range)
     unsigned* sync;      // [0] work counter, [1] error word, [4..] per-(layer, M tile) counters
     unsigned* ring;      // host-mapped ring of timed-out launch numbers (azg_pv_recover); may be null
+    unsigned* ring_ovf;  // host-mapped ring of H3 launches whose activations left fp16's range
     unsigned* diag;      // persistent wait record (TowerDiag layout, azg_pv_tower_diag); may be null
     uint4* prod;         // per (layer, M tile): {seq, HW_ID, XCC_ID, start tick} of the workgroup running it
     unsigned seq;        // launch sequence number (0: autotuning runs, never posted)
@@ -266,8 +267,9 @@ __global__ __launch_bounds__(64 * NW_, (tower_min_waves<BN_, NW_>())) void conv_
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Ly.out, (short)0, a.act_bytes, 0x00020000);
         for (int nt = nt0; nt < nt0 + grp; ++nt) {
             if (nt > nt0) __syncthreads();        // the previous tile's epilogue is done with LDS
-            halo_tile<C, BN_, WM_, TM_, NW_, EPI_BN_OPTRES_RELU, true, HABL, VAR>(Ly.in, Ly.wp, Ly.scale, Ly.shift, Ly.resid,
-                                                                      Ly.out, rs, a.M, mt * T::BM, nt * T::BN, smem);
+            halo_tile<C, BN_, WM_, TM_, NW_, EPI_BN_OPTRES_RELU, true, HABL, VAR>(
+                Ly.in, Ly.wp, Ly.scale, Ly.shift, Ly.resid, Ly.out, rs, a.M, mt * T::BM, nt * T::BN, smem, EpiX{},
+                ProX{}, FinX{}, H3Guard{a.ring_ovf, a.seq});
         }
         if (!(a.abl & 2)) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
@@ -331,7 +333,7 @@ size_t tower_prod_bytes(int nlayers, int M)
 // H -> Y (BN, + X, ReLU), X <-> Y.  `act` are the three padded NHWC buffers
 // (act[0] holds the stem output; the result ends in act[0] or act[2], returned in
 // *result).  `sync` must hold tower_sync_bytes(2*NB, M) bytes.
-int g_tower_h3 = 0;   // key 19: split-fp16 (H3) eval tower (pv_halo.h VAR bit 64); 0 = fp32 MFMA
+int g_tower_h3 = 1;   // key 19: split-fp16 (H3) eval residual convs (pv_halo.h VAR bit 64, default); 0 = fp32 MFMA
 
 hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const float* wpack, const float* scale,
                         const float* shift, const int* out_off, int M, const TowerSync& ts, hipStream_t st,
@@ -346,6 +348,7 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     a.act_bytes = (int)act_bytes;
     a.sync = ts.sync;
     a.ring = ts.ring;
+    a.ring_ovf = ts.ring_ovf;
     a.diag = ts.diag;
     a.prod = (uint4*)ts.prod;
     a.seq = ts.seq;

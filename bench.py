@@ -49,6 +49,20 @@ import torch
 METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
 BLOCKS, CHANNELS, BATCH = 6, 128, 512
 PEAK_F32_MFMA = 157.3e12                                 # MI355X_MICROARCH.md: FP32 matrix peak
+PEAK_F16_MFMA = 16 * PEAK_F32_MFMA                       # dense F16/BF16 MFMA (the guide: 16x the fp32 rate)
+# split-fp16 residual convs (key 19 = 1, the default): three fp16 MFMAs per fp32-equivalent
+# product, so their roofline is the fp16 peak / 3 in fp32-equivalent FLOP/s
+PEAK_H3 = PEAK_F16_MFMA / 3
+
+
+def conv_peak():
+    """(peak FLOP/s of the residual convs' instructions, dtype label) for the eval
+    arithmetic the library runs now (tuning key 19)."""
+    import _native
+    lib = _native.load_library()
+    if lib.azg_pv_set_tuning(19, -1) == 1:
+        return PEAK_H3, "f16x3->f32"
+    return PEAK_F32_MFMA, "f32"
 
 
 def conv_flop(ch: int) -> int:
@@ -277,6 +291,7 @@ def roofline_from_profile(prof, boards, blocks, ch, knames, traffic=True):
     launch from the committed PMC record of that kernel and net at the batch closest
     to this run's average launch, scaled per board to it."""
     cf = conv_flop(ch)
+    peak, _ = conv_peak()
     cls = {}
     for k, (mult, _) in TOWER_CLASSES.items():
         ms, n = prof.get(k, (0.0, 0))
@@ -286,20 +301,27 @@ def roofline_from_profile(prof, boards, blocks, ch, knames, traffic=True):
             cls[k] = {"kernel": knames.get(k, k), "launches": n, "device_ms": round(ms, 1),
                       "avg_launch_us": round(ms / n * 1e3, 2), "flop_per_launch": round(flop / n),
                       "boards_per_launch": round(boards.get(k, 0) / n, 1),
-                      "frac": round(flop / (ms / 1e3) / PEAK_F32_MFMA, 4), "_flop": flop, "_ms": ms}
+                      "frac": round(flop / (ms / 1e3) / peak, 4), "_flop": flop, "_ms": ms}
     if not cls:
         return None
     dom = max(cls, key=lambda k: cls[k]["_ms"])
     d = cls[dom]
     achieved = d["_flop"] / (d["_ms"] / 1e3)
-    out = {"bound": "mfma", "achieved": round(achieved / 1e12, 3), "peak": PEAK_F32_MFMA / 1e12,
-           "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA, 4), "traffic": None}
+    out = {"bound": "mfma", "achieved": round(achieved / 1e12, 3), "peak": round(peak / 1e12, 1),
+           "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None}
+    if peak == PEAK_H3:
+        out["peak_basis"] = ("split-fp16 products: 3 v_mfma_f32_32x32x16_f16 per fp32-equivalent product, "
+                             "dense F16 MFMA peak 2516.8 TFLOP/s / 3; achieved counts the fp32-equivalent conv "
+                             "FLOPs (2 x 225 x C x 9C per board per conv)")
+        out["frac_of_fp32_mfma_peak"] = round(achieved / PEAK_F32_MFMA, 4)
     out.update({k: v for k, v in d.items() if not k.startswith("_") and k != "frac"})
     pref = TOWER_CLASSES[dom][1]
     if traffic and pref:
         net = f"{blocks}x{ch}_B"
+        h3 = peak == PEAK_H3   # the split-fp16 towers (halo_tile VAR 96 / 97) have their own records
         recs = [r for r in traffic_records() if r.get("kernel") == "tower" and r.get("config", "").startswith(net)
-                and r.get("shape", "").startswith(pref) and (dom != "tower" or "16>" not in r["shape"])]
+                and r.get("shape", "").startswith(pref) and (dom != "tower" or "16>" not in r["shape"])
+                and any(f", {v}, 0>" in r["shape"] for v in ((96, 97) if h3 else (16, 32, 33)))]
         if recs:
             bpl = d["boards_per_launch"]
             r = min(recs, key=lambda r: abs(r["boards_per_launch"] - bpl))
@@ -313,7 +335,7 @@ def roofline_from_profile(prof, boards, blocks, ch, knames, traffic=True):
     if others:
         tot_f = sum(c["_flop"] for c in cls.values())
         tot_ms = sum(c["_ms"] for c in cls.values())
-        out["all_residual_convs_frac"] = round(tot_f / (tot_ms / 1e3) / PEAK_F32_MFMA, 4)
+        out["all_residual_convs_frac"] = round(tot_f / (tot_ms / 1e3) / peak, 4)
         out["other_classes"] = {k: {kk: vv for kk, vv in cls[k].items() if not kk.startswith("_")} for k in others}
     return out
 
@@ -322,8 +344,11 @@ def tower_knames(ch, blocks):
     n = 2 * blocks
     return {"tower16": f"azg::conv_tower<{ch},128,4,1,16,16> (persistent residual tower, 16-wave 128x128 tiles, one "
                        f"workgroup per CU: {n} fused 3x3 conv + BN (+ residual) + ReLU layers per launch)",
-            "tower": f"azg::conv_tower<{ch},64,*,{33 if ch >= 256 else 32}> (persistent residual tower, 128x64 / 64x64 tiles, acquire "
-                     f"hand-off: {n} fused 3x3 conv + BN (+ residual) + ReLU layers per launch)",
+            "tower": (f"azg::conv_tower<{ch},64,*,{97 if ch >= 256 else 96}> (persistent residual tower, 128x64 / 64x64 "
+                      f"tiles, split-fp16 products, acquire hand-off: {n} fused 3x3 conv + BN (+ residual) + ReLU layers "
+                      f"per launch)" if conv_peak()[0] == PEAK_H3 else
+                      f"azg::conv_tower<{ch},64,*,{33 if ch >= 256 else 32}> (persistent residual tower, 128x64 / 64x64 "
+                      f"tiles, acquire hand-off: {n} fused 3x3 conv + BN (+ residual) + ReLU layers per launch)"),
             "conv3x3": f"azg::conv3x3_halo<{ch},*> (per-layer fused 3x3 conv + BN (+ residual) + ReLU)"}
 
 
@@ -672,7 +697,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": conv_peak()[1],
         "data": (f"synthetic (self-play from the empty board; 6x128 weights = seeded init + {args.pretrain_steps} "
                  f"train_batch steps on synthetic boards / pi / z, SURVEY §8(d); no checkpoint)"),
         "config": {"workload": f"configs[2]: {args.sp_games} concurrent self-play games/GPU x {args.sp_sims} "

@@ -189,6 +189,15 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *   key 14: persistent-tower dependency wait bound in microseconds of the waiting
  *          wave's awake time (default 100000 = 100 ms; -1 restores it; 0 makes every
  *          dependency wait time out at once, exercising the recovery path);
+ *   key 19: eval residual-conv arithmetic: 1 (default) split-fp16 -- every fp32 operand x
+ *          is split into hi = fp16(x), lo = fp16(x - hi) and a product is lo*hi + hi*lo +
+ *          hi*hi by three v_mfma_f32_32x32x16_f16 with fp32 accumulation (weights scaled by
+ *          a per-layer power of two, undone in the BN scale; error ~2^-22 per product, the
+ *          fp32 MFMA chain's order of magnitude); 0 fp32 MFMA.  Every
+ *          eval path (tower, per-layer, recompute) uses the selected arithmetic, so the
+ *          tower and per-layer forms stay bitwise equal.  A staged activation at or above
+ *          65504 posts the launch and azg_pv_recover recomputes it with fp32 MFMA.  The
+ *          train step always uses fp32 MFMA;
  *   key 18: seconds a handle runs per-layer convs after azg_pv_recover recomputed one
  *          of its tower launches (default 30; 0 disables the breaker).  A timed-out
  *          wait means parts of the dispatch were suspended while others ran (the GPU is
@@ -256,7 +265,9 @@ typedef struct {
     uint32_t waits_suspended;   /* waits whose wall time exceeded their awake time by > 1 ms */
     uint32_t breaker_trips;     /* recoveries that switched the handle to per-layer convs (key 18) */
     uint32_t breaker_launches;  /* forwards run per layer while the breaker was open */
-    uint32_t reserved[5];
+    uint32_t h3_overflows;      /* split-fp16 forwards recomputed with fp32 MFMA (key 19: an activation
+                                   beyond fp16's range, 65504) */
+    uint32_t reserved[4];
 } azg_pv_tower_diag;
 int32_t azg_pv_tower_diag_read(azg_pv* h, azg_pv_tower_diag* out, void* stream);
 int32_t azg_pv_tower_diag_clear(azg_pv* h, void* stream);

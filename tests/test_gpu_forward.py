@@ -419,3 +419,70 @@ def test_mfma_stem_bitwise_equals_valu_stem(blocks, ch, B):
         lib.azg_pv_set_tuning(9, prev)
     for a, b in zip(outs[0], outs[1]):
         assert np.array_equal(a, b), float(np.abs(a - b).max())
+
+
+@pytest.mark.parametrize("tower", [1, 0])
+def test_h3_range_guard_recomputes_in_fp32(tower):
+    """Split-fp16 residual convs (key 19 = 1, the default) cannot represent an activation
+    at or above 65504: the staging posts the launch and predict / predict_boards recompute
+    it with fp32 MFMA, so the result is bitwise the fp32 forward (key 19 = 0).  The stem's
+    BN gamma scaled by 1e5 drives the first conv's inputs past fp16's range.  Both the
+    persistent tower and the per-layer launches (key 5) carry the guard."""
+    import _native
+    lib = _native.load_library()
+    m = make_model(3, 128, seed=8)
+    with torch.no_grad():
+        m.net.bn.weight.mul_(1e5)
+    m.engine.mark_dirty()
+    boards, players = synth_positions(256, seed=81)
+    x = encode_batch(boards, players)
+    bi8, pl8 = np.asarray(boards, np.int8).reshape(256, 225), np.asarray(players, np.int8)
+    prev_mode = lib.azg_pv_set_tuning(5, tower)
+    prev_h3 = lib.azg_pv_set_tuning(19, 0)
+    try:
+        p32, v32 = m.predict(x)
+        pb32, vb32 = m.predict_boards(bi8, pl8)
+        lib.azg_pv_set_tuning(19, 1)
+        m.engine.tower_diag_clear()
+        p, v = m.predict(x)
+        pb, vb = m.predict_boards(bi8, pl8)
+        d = m.engine.tower_diag()
+        assert d["h3_overflows"] == 2, d
+        assert np.array_equal(p, p32) and np.array_equal(v, v32)
+        assert np.array_equal(pb, pb32) and np.array_equal(vb, vb32)
+        assert lib.azg_pv_status(m.engine.h) == 0
+    finally:
+        lib.azg_pv_set_tuning(19, prev_h3)
+        lib.azg_pv_set_tuning(5, prev_mode)
+
+
+@pytest.mark.parametrize("blocks,ch,B", [(6, 128, 512), (10, 256, 96)])
+def test_h3_matches_fp32_forward_and_oracle(blocks, ch, B):
+    """Split-fp16 (key 19 = 1) against the fp32-MFMA forward (key 19 = 0) and the fp64
+    oracle on the same weights: within the forward parity budget (1e-5), and no further
+    from fp64 than 2x the fp32 path's own deviation (or 1e-6)."""
+    import _native
+    lib = _native.load_library()
+    ref = RefModel(blocks, ch)
+    torch.manual_seed(1)
+    calib_bn(ref, seed=blocks * 1000 + ch)
+    m = make_model(blocks, ch, state_to_numpy(ref.net))
+    b, p = synth_positions(B, seed=B + ch + 7)
+    x = encode_batch(b, p)
+    prev = lib.azg_pv_set_tuning(19, 0)
+    try:
+        p32, v32 = m.predict(x)
+        lib.azg_pv_set_tuning(19, 1)
+        p16, v16 = m.predict(x)
+    finally:
+        lib.azg_pv_set_tuning(19, prev)
+    r64 = RefModel(blocks, ch, dtype=torch.float64)
+    r64.net.load_state_dict({k: (v.double() if v.dtype.is_floating_point else v)
+                             for k, v in ref.net.state_dict().items()})
+    pr, vr = r64.predict(x)
+    for name, a32, a16, a64 in (("probs", p32, p16, pr), ("values", v32, v16, vr)):
+        e32, e16 = np.abs(a32 - a64).max(), np.abs(a16 - a64).max()
+        print(f"{blocks}x{ch} {name}: |fp32-fp64|={e32:.2e} |h3-fp64|={e16:.2e} |h3-fp32|={np.abs(a16 - a32).max():.2e}")
+        assert np.abs(a16 - a32).max() <= 1e-5
+        assert e16 <= max(2 * e32, 1e-6), (name, e16, e32)
+    argmax_check(p16, pr, b)
