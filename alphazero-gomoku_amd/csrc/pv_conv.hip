@@ -690,13 +690,24 @@ hipError_t launch_conv3x3_shape(int shape, int C, int epi, const float* in, cons
 // Split-fp16 (H3) per-layer conv (pv_halo.h VAR bit 64; wp / scale = the H3 packs of
 // pv_pack.hip pack_h3): the eval tower's arithmetic per layer (bitwise equal to it), the
 // 64x64 / 4-wave tile (shape 5) or the 128x64 / 8-wave tile (shape 8), buffer addressing.
+template <int CC, int BN, int WM, int NW, int VAR>
+static hipError_t launch_h3_v(int epi, const float* in, const float* wp, const float* scale, const float* shift,
+                              const float* resid, float* out, int M, hipStream_t st, const H3Guard& g)
+{
+    if (epi == EPI_BN_RELU) return launch_halo_t<CC, BN, WM, 1, NW, EPI_BN_RELU, VAR>(in, wp, scale, shift, resid, out, M, st, g);
+    if (epi == EPI_BN_RES_RELU) return launch_halo_t<CC, BN, WM, 1, NW, EPI_BN_RES_RELU, VAR>(in, wp, scale, shift, resid, out, M, st, g);
+    return hipErrorInvalidValue;
+}
 template <int CC, int BN, int WM, int NW>
 static hipError_t launch_h3_t(int epi, const float* in, const float* wp, const float* scale, const float* shift,
                               const float* resid, float* out, int M, hipStream_t st, const H3Guard& g)
 {
-    if (epi == EPI_BN_RELU) return launch_halo_t<CC, BN, WM, 1, NW, EPI_BN_RELU, 96>(in, wp, scale, shift, resid, out, M, st, g);
-    if (epi == EPI_BN_RES_RELU) return launch_halo_t<CC, BN, WM, 1, NW, EPI_BN_RES_RELU, 96>(in, wp, scale, shift, resid, out, M, st, g);
-    return hipErrorInvalidValue;
+    switch (g_h3_var) {   // key 20 (A/B study): pv_tower.hip launch_tower
+        case 1: return launch_h3_v<CC, BN, WM, NW, 98>(epi, in, wp, scale, shift, resid, out, M, st, g);
+        case 2: return launch_h3_v<CC, BN, WM, NW, 97>(epi, in, wp, scale, shift, resid, out, M, st, g);
+        case 3: return launch_h3_v<CC, BN, WM, NW, 99>(epi, in, wp, scale, shift, resid, out, M, st, g);
+        default: return launch_h3_v<CC, BN, WM, NW, 96>(epi, in, wp, scale, shift, resid, out, M, st, g);
+    }
 }
 hipError_t launch_conv3x3_h3(int shape, int C, int epi, const float* in, const float* wp, const float* scale,
                              const float* shift, const float* resid, float* out, int M, hipStream_t st,
@@ -1028,6 +1039,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     if (key == 48) {  // train weight-grad tile: 1 v2 (row table, buffer LDS-DMA, MFMA-layout slabs; default), 0 v1; bitwise identical
         const int prev = azg::g_wgrad_variant;
         if (value == 0 || value == 1) azg::g_wgrad_variant = value;
+        return prev;
+    }
+    if (key == 20) {  // split-fp16 tile-body variant (A/B study; bitwise identical): 0 default, 1 weights two chunks ahead, 2 board-keyed swizzle, 3 both
+        const int prev = azg::g_h3_var;
+        if (value >= 0 && value <= 3) azg::g_h3_var = value;
         return prev;
     }
     if (key == 19) {  // eval residual-conv arithmetic: 1 split-fp16 products (H3, default), 0 fp32 MFMA

@@ -236,9 +236,11 @@ struct ProX {
 };
 
 
-// H3 range guard: a staged activation at or above fp16's largest finite value (65504)
-// cannot be split; the tile posts its launch number to the handle's host ring (the
-// host recomputes that forward with fp32 MFMA, azg_pv_recover) and computes on.
+// H3 range guard: an activation at or above 65520 rounds to an infinite hi part, and
+// every product it enters becomes inf - inf or 0 * inf = NaN, so a non-finite
+// accumulator in the epilogue means an input left fp16's range: the tile posts its
+// launch number to the handle's host ring (the host recomputes that forward with fp32
+// MFMA, azg_pv_recover) and computes on.  (Below 65520 the split is exact as usual.)
 struct H3Guard {
     unsigned* ring = nullptr;   // host-mapped, kTowerRing entries (device alias)
     unsigned seq = 0;
@@ -269,7 +271,8 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                                               const float* __restrict__ scale, const float* __restrict__ shift,
                                               const float* __restrict__ resid, float* __restrict__ out,
                                               __amdgpu_buffer_rsrc_t out_rs, int M, int m0, int n0, float* smem,
-                                              const EpiX& ex = EpiX{}, const FinX& fx = FinX{})
+                                              const EpiX& ex = EpiX{}, const FinX& fx = FinX{},
+                                              const H3Guard* guard = nullptr)
 {
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
     constexpr int BM = T::BM, BN = T::BN, WN = T::WN, TM = T::TM, TN = T::TN;
@@ -328,6 +331,13 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
         const int row = er + p * RPI;
         const int m = m0 + row;
         f32x4 v = *(const f32x4*)(Es + row * ELD + ec);
+        if (guard) {   // H3: a non-finite accumulator = an input beyond fp16's range (H3Guard)
+            const bool fin = __builtin_isfinite(v[0]) && __builtin_isfinite(v[1]) && __builtin_isfinite(v[2]) &&
+                             __builtin_isfinite(v[3]);
+            if (!fin && m0 + row < M && guard->ring && guard->seq)
+                __hip_atomic_store(guard->ring + (guard->seq & (kH3RingSize - 1)), guard->seq, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         if (XE == XE_STATS) vk[p] = v;
         if (m < M && (!(ABL & 16) || v[0] == 1234.5f)) {
             const int o = pad_off(m, C) + col;
@@ -876,7 +886,6 @@ __device__ __forceinline__ void halo_tile(
             if ((pown >> i) & 1) store4<true>(px.aout, ars, hsrc[i] + cg * BK, v);
         }
     };
-    bool h3big = false;   // H3: a staged value outside fp16's range (H3Guard)
     auto hstore = [&](int cg) {
         if constexpr (H3) {
             // channels sc..sc+3 of the row: hi halves into slot sc/8 (byte 2*(sc%8)),
@@ -887,7 +896,6 @@ __device__ __forceinline__ void halo_tile(
                 f16x4 hi, lo;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    h3big |= !(fabsf(rh[i][e]) < 65504.f);   // also catches NaN
                     hi[e] = (_Float16)rh[i][e];
                     lo[e] = (_Float16)(rh[i][e] - (float)hi[e]);
                 }
@@ -1054,15 +1062,10 @@ __device__ __forceinline__ void halo_tile(
             for (int j = 0; j < TN; ++j) acc[i][j] += at[i][j];
     }
 
-    if constexpr (H3) {
-        if (h3big && guard.ring && guard.seq)
-            __hip_atomic_store(guard.ring + (guard.seq & (kH3RingSize - 1)), guard.seq, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-    }
     // the last chunk ended with a barrier: the staging buffers are free
     halo_epilogue<C, BN_, WM_, TM_, NW_, EPI, SC1, ABL, (VSWZ ? BN : BN + 8), (VAR & 8) != 0, XE,
                   (VAR & 16) ? 2 : (VAR & 32) ? 1 : 0>(
-        acc, scale, shift, resid, out, out_rs, M, m0, n0, smem, ex, fx);
+        acc, scale, shift, resid, out, out_rs, M, m0, n0, smem, ex, fx, H3 ? &guard : nullptr);
 }
 
 }  // namespace azg

@@ -1,0 +1,8 @@
+#!/bin/bash
+# Round 5: split-fp16 eval convs -- per-layer vs tower forms and tile-body variants (key 20)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/r5h
+mkdir -p $O
+timeout -k 10 400 python -u scripts/h3_tune_study.py > $O/study_6x128.log 2>&1 &&
+timeout -k 10 300 python -u scripts/h3_tune_study.py --net 10x256 --batches 64,256,512 --rounds 2 --reps 2 > $O/study_10x256.log 2>&1

@@ -1,0 +1,71 @@
+"""Split-fp16 eval convs: per-layer launches vs the persistent tower (64x64 / 128x64
+tiles) and the tile-body variants (key 20), device time of stem + residual convs per
+forward at the self-play batch range (6x128 after bench.py's pretraining; 10x256 with
+--net).  Every variant is bitwise identical (checked against the first).
+
+    python scripts/h3_tune_study.py [--batches 128,512,2048,3456] [--vars 0,1,2,3]
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "alphazero-gomoku_amd")]
+
+import torch
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batches", default="128,256,512,1024,2048,3456,4096")
+    ap.add_argument("--vars", default="0,1,2,3")
+    ap.add_argument("--net", default="6x128")
+    ap.add_argument("--reps", type=int, default=4)
+    ap.add_argument("--rounds", type=int, default=3)
+    args = ap.parse_args()
+    import _native
+    import bench
+    from network import PyTorchModel
+    from synth import synth_encoded
+    lib = _native.load_library()
+    nb, ch = (int(v) for v in args.net.split("x"))
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    m = PyTorchModel(board_size=15, device=str(dev), n_res_blocks=nb, channels=ch)
+    bench.pretrain(m, dev)
+    eng = m.engine
+    flop_per_board = 2 * 225 * ch * 9 * ch * 2 * nb
+    forms = [("per-layer", 0, 8), ("tower64x64", 1, 5), ("tower128x64", 1, 8)]
+    for B in (int(b) for b in args.batches.split(",")):
+        x = torch.from_numpy(synth_encoded(B, seed=B)).to(dev)
+        best, ref = {}, None
+        for r in range(args.rounds):
+            for v in (int(t) for t in args.vars.split(",")):
+                lib.azg_pv_set_tuning(20, v)
+                for name, mode, shape in forms:
+                    lib.azg_pv_set_tuning(5, mode)
+                    lib.azg_pv_set_tuning(6, shape)
+                    p, _, _ = eng.forward(x)
+                    torch.cuda.synchronize()
+                    if ref is None:
+                        ref = p.clone()
+                    assert torch.equal(p, ref), (B, v, name)
+                    eng.profile_enable(True)
+                    for _ in range(args.reps):
+                        eng.forward(x)
+                    prof = eng.profile_read()
+                    eng.profile_enable(False)
+                    ms = sum(prof[k][0] for k in ("tower", "conv3x3") if k in prof) / args.reps
+                    key = f"{name}/var{v}"
+                    best[key] = min(best.get(key, 1e9), ms)
+        lib.azg_pv_set_tuning(20, 0)
+        lib.azg_pv_set_tuning(5, 2)
+        out = {"batch": B, "net": args.net,
+               "ms": {k: round(v, 4) for k, v in sorted(best.items(), key=lambda kv: kv[1])},
+               "tflops_best": round(flop_per_board * B / (min(best.values()) * 1e-3) / 1e12, 1)}
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
