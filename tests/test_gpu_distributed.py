@@ -178,3 +178,64 @@ def test_bench_collectives_see_device_tensors_under_rccl(monkeypatch):
     assert [s[:3] for s in seen[:2]] == [("all_reduce", "cuda", torch.float64)] * 2
     assert seen[0][3] == dist.ReduceOp.SUM and seen[1][3] == dist.ReduceOp.MAX
     assert seen[2] == ("barrier", [0])
+
+
+def _loop_worker(rank, world, port, out_dir):
+    """One train_alphazero iteration (reference train.py:575-845) on this rank: sharded
+    self-play, DP training with the flat-gradient all-reduce, BN-stat sync, sharded
+    gating with the summed win count, and the accept/reject decision -- every collective
+    of the loop on HIP models, under gloo (two ranks share the box's GPU)."""
+    import sys
+    sys.path[:0] = [REPO, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    torch.set_num_threads(1)
+    torch.distributed.init_process_group("gloo")   # train_alphazero keeps an initialised group
+    import random
+    import train
+    random.seed(100 + rank)                        # rank-local opening moves of the gating games
+    np.random.seed(200 + rank)
+    torch.manual_seed(rank)                        # broadcast_model must make the replicas equal
+    seen = {}
+    play = train._play_eval_games
+    evaluate = train.evaluate_models
+
+    def play_wrap(model_new, model_best, games, starts, *a, **k):
+        winners = play(model_new, model_best, games, starts, *a, **k)
+        seen["local_wins"] = sum(1 for w, s in zip(winners, starts) if (w == 1 and s) or (w == 2 and not s))
+        seen["local_games"] = len(games)
+        return winners
+
+    def evaluate_wrap(*a, **k):
+        out = evaluate(*a, **k)
+        seen["global_wins"] = out[0]
+        return out
+
+    train._play_eval_games = play_wrap
+    train.evaluate_models = evaluate_wrap
+    best = train.train_alphazero(num_iterations=1, games_per_iteration=4, n_simulations=16, batch_size=64,
+                                 epochs_per_iter=2, eval_games=4, eval_mcts_simulations=12,
+                                 win_rate_threshold=0.0,
+                                 model_dir=os.path.join(out_dir, "models"), n_res_blocks=2, channels=128,
+                                 max_moves=24)
+    st = _state(best)
+    st.update({k: np.array([v]) for k, v in seen.items()})
+    np.savez(os.path.join(out_dir, f"loop_rank{rank}.npz"), **st)
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_train_alphazero_world2_through_hip_engine(tmp_path):
+    """train_alphazero at world size 2 end to end on HIP models
+    (gloo; both ranks on this box's GPU).  After one iteration both ranks hold bitwise-
+    identical params, BN buffers and counters, Adam moments and step (the accepted
+    candidate: win_rate_threshold 0 accepts), and the gating win count every rank saw
+    is the sum of the ranks' local wins over their shard of the games."""
+    port = _free_port()
+    mp.spawn(_loop_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = (dict(np.load(tmp_path / f"loop_rank{r}.npz")) for r in range(2))
+    for k in ("params", "bn", "nbt", "m", "v", "step"):
+        assert np.array_equal(r0[k], r1[k]), k
+    assert r0["global_wins"][0] == r1["global_wins"][0] == r0["local_wins"][0] + r1["local_wins"][0]
+    assert r0["local_games"][0] + r1["local_games"][0] == 4
+    assert r0["step"][0] > 0                                         # trained: Adam stepped
