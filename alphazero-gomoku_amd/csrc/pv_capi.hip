@@ -569,6 +569,7 @@ static int32_t ensure_h3(azg_pv* h, hipStream_t st)
 // rounds of resident slots (ties: the 128-row tile).  Both compute the same arithmetic.
 static int conv_tuned_shape_h3(azg_pv* h, int batch, hipStream_t, const float*, const int8_t*, const int8_t*)
 {
+    if (g_conv_shape_override == 5 || g_conv_shape_override == 8) return g_conv_shape_override;   // key 0
     const int M = batch * PIX, ntn = h->C / 64;
     const long t5 = (long)((M + 63) / 64) * ntn, t8 = (long)((M + 127) / 128) * ntn;
     const long r5 = (t5 + 1023) / 1024, r8 = (t8 + 511) / 512;

@@ -357,12 +357,16 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 float x = v[e];
+                // explicit fmaf: the same rounding in every epilogue form (a contracted
+                // x * s + t in one kernel and an uncontracted one in another made the
+                // tower and the per-layer launches differ by an ulp once BN shifts are
+                // nonzero -- trained nets; seeded ones have shift 0)
                 if (EPI == EPI_BN_RELU) {
-                    x = fmaxf(x * s4[e] + t4[e], 0.f);
+                    x = fmaxf(fmaf(x, s4[e], t4[e]), 0.f);
                 } else if (EPI == EPI_BN_RES_RELU) {
-                    x = fmaxf(x * s4[e] + t4[e] + rv[e], 0.f);
+                    x = fmaxf(fmaf(x, s4[e], t4[e]) + rv[e], 0.f);
                 } else if (EPI == EPI_BN_OPTRES_RELU) {
-                    x = has_res ? fmaxf(x * s4[e] + t4[e] + rv[e], 0.f) : fmaxf(x * s4[e] + t4[e], 0.f);
+                    x = has_res ? fmaxf(fmaf(x, s4[e], t4[e]) + rv[e], 0.f) : fmaxf(fmaf(x, s4[e], t4[e]), 0.f);
                 } else if (EPI == EPI_ADD) {
                     x = x + rv[e];
                 }

@@ -41,6 +41,7 @@ hipError_t launch_conv3x3_train(int C, int epi, int xe, const float* in, const f
                                 float* out, int M, const EpiX& ex, hipStream_t st, const ProX* px = nullptr,
                                 const FinX* fx = nullptr);
 extern int g_tower_mode;
+extern int g_conv_shape_override;
 extern int g_tower_shape;
 extern int g_tower_ablation;
 extern int g_tower_var;
