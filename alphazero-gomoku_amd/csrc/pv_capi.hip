@@ -9,6 +9,7 @@
 #include <tuple>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -701,6 +702,9 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
                 if (batch >= 128 && best_ms[2] <= 1.02f * best_ms[b]) b = 2;   // the 128x64 tower
                 choice = cand[b];
             }
+            if (getenv("AZG_TUNE_LOG"))
+                fprintf(stderr, "[azg tune] C=%d NB=%d batch=%d h3=%d ok=%d per-layer %.4f tower64 %.4f tower128 %.4f -> %d\n",
+                        h->C, h->NB, batch, (int)h3, (int)ok, best_ms[0], best_ms[1], best_ms[2], choice);
             (void)hipEventDestroy(e1);
         }
         (void)hipEventDestroy(e0);

@@ -698,16 +698,15 @@ static hipError_t launch_h3_v(int epi, const float* in, const float* wp, const f
     if (epi == EPI_BN_RES_RELU) return launch_halo_t<CC, BN, WM, 1, NW, EPI_BN_RES_RELU, VAR>(in, wp, scale, shift, resid, out, M, st, g);
     return hipErrorInvalidValue;
 }
+// VAR 99 = H3 + buffer addressing + weights two chunks ahead + board-keyed halo swizzle:
+// the fastest per-layer form (+10 % over 96 at 128 boards, scripts/h3_tune_study.py)
 template <int CC, int BN, int WM, int NW>
 static hipError_t launch_h3_t(int epi, const float* in, const float* wp, const float* scale, const float* shift,
                               const float* resid, float* out, int M, hipStream_t st, const H3Guard& g)
 {
-    switch (g_h3_var) {   // key 20 (A/B study): pv_tower.hip launch_tower
-        case 1: return launch_h3_v<CC, BN, WM, NW, 98>(epi, in, wp, scale, shift, resid, out, M, st, g);
-        case 2: return launch_h3_v<CC, BN, WM, NW, 97>(epi, in, wp, scale, shift, resid, out, M, st, g);
-        case 3: return launch_h3_v<CC, BN, WM, NW, 99>(epi, in, wp, scale, shift, resid, out, M, st, g);
-        default: return launch_h3_v<CC, BN, WM, NW, 96>(epi, in, wp, scale, shift, resid, out, M, st, g);
-    }
+    if (epi == EPI_BN_RELU) return launch_halo_t<CC, BN, WM, 1, NW, EPI_BN_RELU, 99>(in, wp, scale, shift, resid, out, M, st, g);
+    if (epi == EPI_BN_RES_RELU) return launch_halo_t<CC, BN, WM, 1, NW, EPI_BN_RES_RELU, 99>(in, wp, scale, shift, resid, out, M, st, g);
+    return hipErrorInvalidValue;
 }
 hipError_t launch_conv3x3_h3(int shape, int C, int epi, const float* in, const float* wp, const float* scale,
                              const float* shift, const float* resid, float* out, int M, hipStream_t st,
@@ -1039,11 +1038,6 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     if (key == 48) {  // train weight-grad tile: 1 v2 (row table, buffer LDS-DMA, MFMA-layout slabs; default), 0 v1; bitwise identical
         const int prev = azg::g_wgrad_variant;
         if (value == 0 || value == 1) azg::g_wgrad_variant = value;
-        return prev;
-    }
-    if (key == 20) {  // split-fp16 tile-body variant (A/B study; bitwise identical): 0 default, 1 weights two chunks ahead, 2 board-keyed swizzle, 3 both
-        const int prev = azg::g_h3_var;
-        if (value >= 0 && value <= 3) azg::g_h3_var = value;
         return prev;
     }
     if (key == 19) {  // eval residual-conv arithmetic: 1 split-fp16 products (H3, default), 0 fp32 MFMA

@@ -107,7 +107,6 @@ hipError_t launch_conv3x3_h3(int shape, int C, int epi, const float* in, const f
 hipError_t launch_pack_h3(const float* params, const int64_t* offs, int nl, int C, const int* conv_bn_off,
                           const float* scale, int* exps, void* wp16, float* scale16, hipStream_t st);
 extern int g_tower_h3;
-extern int g_h3_var;
 hipError_t launch_fold_bn(const float* params, const float* stats, const void* desc, int nlayers,
                           float* scale, float* shift, hipStream_t st);
 

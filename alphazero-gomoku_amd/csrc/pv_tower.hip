@@ -333,7 +333,6 @@ size_t tower_prod_bytes(int nlayers, int M)
 // H -> Y (BN, + X, ReLU), X <-> Y.  `act` are the three padded NHWC buffers
 // (act[0] holds the stem output; the result ends in act[0] or act[2], returned in
 // *result).  `sync` must hold tower_sync_bytes(2*NB, M) bytes.
-int g_h3_var = 0;    // key 20: split-fp16 tile-body variant (A/B study, bitwise identical)
 int g_tower_h3 = 1;   // key 19: split-fp16 (H3) eval residual convs (pv_halo.h VAR bit 64, default); 0 = fp32 MFMA
 
 hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const float* wpack, const float* scale,
@@ -379,25 +378,18 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     hipError_t e = hipMemsetAsync(sync, 0, tower_sync_bytes(2 * NB, M), st);
     if (e != hipSuccess) return e;
     if (h3) {   // wpack / scale are the split-fp16 packs (pv_pack.hip pack_h3)
-        // g_h3_var (key 20, A/B study): 0 VAR 96; 1 weights two chunks ahead (98); 2 board-keyed
-        // halo swizzle (97); 3 both (99) -- all bitwise identical
-#define AZG_H3T(CC, BN, WM, NW)                                                                   \
-        switch (g_h3_var) {                                                                       \
-            case 1: return launch_tower_t<CC, BN, WM, 1, NW, 98>(a, st, nullptr);                 \
-            case 2: return launch_tower_t<CC, BN, WM, 1, NW, 97>(a, st, nullptr);                 \
-            case 3: return launch_tower_t<CC, BN, WM, 1, NW, 99>(a, st, nullptr);                 \
-            default: return launch_tower_t<CC, BN, WM, 1, NW, (CC == 256 ? 97 : 96)>(a, st, nullptr); \
-        }
+        // VAR 98 = H3 + buffer addressing + weights staged two chunks ahead (bit 2): +2.5-3 %
+        // over 96 at 256-4096 boards, the board-keyed swizzle (bit 1) slower in the tower
+        // (scripts/h3_tune_study.py, profiles/r5_h3_study.md); bitwise equal to every other form
         switch (C) {
             case 128:
-                if (shape == 5) { AZG_H3T(128, 64, 2, 4) }
-                AZG_H3T(128, 64, 4, 8)
+                if (shape == 5) return launch_tower_t<128, 64, 2, 1, 4, 98>(a, st, nullptr);
+                return launch_tower_t<128, 64, 4, 1, 8, 98>(a, st, nullptr);
             case 256:
-                if (shape == 5) { AZG_H3T(256, 64, 2, 4) }
-                AZG_H3T(256, 64, 4, 8)
+                if (shape == 5) return launch_tower_t<256, 64, 2, 1, 4, 98>(a, st, nullptr);
+                return launch_tower_t<256, 64, 4, 1, 8, 98>(a, st, nullptr);
             default: return hipErrorInvalidValue;
         }
-#undef AZG_H3T
     }
 #ifdef AZG_AB_STUDIES
     // traffic ablations of the 128x64 tower (key 8 bits 4 / 8: no weight / no halo loads)
