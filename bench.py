@@ -318,10 +318,10 @@ def roofline_from_profile(prof, boards, blocks, ch, knames, traffic=True):
     pref = TOWER_CLASSES[dom][1]
     if traffic and pref:
         net = f"{blocks}x{ch}_B"
-        h3 = peak == PEAK_H3   # the split-fp16 towers (halo_tile VAR 96 / 97) have their own records
+        h3 = peak == PEAK_H3   # the split-fp16 towers (halo_tile VAR 98) have their own records
         recs = [r for r in traffic_records() if r.get("kernel") == "tower" and r.get("config", "").startswith(net)
                 and r.get("shape", "").startswith(pref) and (dom != "tower" or "16>" not in r["shape"])
-                and any(f", {v}, 0>" in r["shape"] for v in ((96, 97) if h3 else (16, 32, 33)))]
+                and any(f", {v}, 0>" in r["shape"] for v in ((98,) if h3 else (16, 32, 33)))]
         if recs:
             bpl = d["boards_per_launch"]
             r = min(recs, key=lambda r: abs(r["boards_per_launch"] - bpl))

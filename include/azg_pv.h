@@ -195,9 +195,12 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          a per-layer power of two, undone in the BN scale; error ~2^-22 per product, the
  *          fp32 MFMA chain's order of magnitude); 0 fp32 MFMA.  Every
  *          eval path (tower, per-layer, recompute) uses the selected arithmetic, so the
- *          tower and per-layer forms stay bitwise equal.  A staged activation at or above
- *          65504 posts the launch and azg_pv_recover recomputes it with fp32 MFMA.  The
- *          train step always uses fp32 MFMA;
+ *          tower and per-layer forms stay bitwise equal.  An activation at or above fp16's
+ *          range (65520 rounds to inf) makes its products non-finite: the epilogue posts
+ *          the launch and azg_pv_recover recomputes it with fp32 MFMA.  The train step
+ *          always uses fp32 MFMA;
+ *   key 48: train weight-grad tile (1 = padded-row table, buffer LDS-DMA, slabs in the
+ *          MFMA layout, default; 0 = round-4 form); bitwise identical;
  *   key 18: seconds a handle runs per-layer convs after azg_pv_recover recomputed one
  *          of its tower launches (default 30; 0 disables the breaker).  A timed-out
  *          wait means parts of the dispatch were suspended while others ran (the GPU is
