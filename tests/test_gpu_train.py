@@ -106,7 +106,10 @@ def gpu_masks(eng, blocks, B):
                                              # configs[4]'s net at the bench's train shape (B = 128)
                                              pytest.param(None, 10, 256, 128, marks=pytest.mark.timeout(900)),
                                              # fused BN apply / finalize at 160 and 48 samples (C = 64 / 256)
-                                             (None, 2, 64, 160), (None, 2, 256, 48)])
+                                             (None, 2, 64, 160), (None, 2, 256, 48),
+                                             # B > kHeadFoldMaxB (512): the unfolded head-BN backward
+                                             # (head_bn_bwd_fin_kernel -> heads_bwd_fused with dg_nwg = 0)
+                                             pytest.param(None, 1, 64, 520, marks=pytest.mark.timeout(600))])
 def test_gradients_match_oracle(tag, blocks, ch, B):
     """Gradients vs fp64 autograd with the GPU's ReLU masks (oracle.masked_grads_fp64):
     |g_gpu - g_64| <= 2e-5 * max|g_64| + 1e-8 per tensor.  The fp32 CPU oracle (own
