@@ -82,6 +82,7 @@ int32_t azg_pv_destroy(azg_pv* h)
     if (h->wpack16) (void)hipFree(h->wpack16);
     if (h->scale16) (void)hipFree(h->scale16);
     if (h->h3exp) (void)hipFree(h->h3exp);
+    if (h->h3inv) (void)hipFree(h->h3inv);
     if (h->conv_bn_off_dev) (void)hipFree(h->conv_bn_off_dev);
     for (auto& e : h->prof_ev) (void)hipEventDestroy(e);
     delete h;
@@ -538,7 +539,7 @@ int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst, int part)
 // identical.
 // The split-fp16 (H3) eval weights of the current parameters (pv_pack.hip pack_h3):
 // allocated on first use, re-packed after every repack.
-static int32_t ensure_h3(azg_pv* h, hipStream_t st)
+int32_t ensure_h3(azg_pv* h, hipStream_t st)
 {
     const int C = h->C, nl = 2 * h->NB;
     if (!h->wpack16) {
@@ -551,6 +552,7 @@ static int32_t ensure_h3(azg_pv* h, hipStream_t st)
         hipError_t e = hipMalloc(&h->wpack16, (size_t)(nl > 0 ? nl : 1) * 9 * C * C * sizeof(float));
         if (e == hipSuccess) e = hipMalloc(&h->scale16, (size_t)h->nfold * sizeof(float));
         if (e == hipSuccess) e = hipMalloc(&h->h3exp, (size_t)(nl > 0 ? nl : 1) * sizeof(int));
+        if (e == hipSuccess) e = hipMalloc(&h->h3inv, (size_t)(nl > 0 ? nl : 1) * C * sizeof(float));
         if (e == hipSuccess) e = hipMalloc(&h->conv_bn_off_dev, off.size() * sizeof(int));
         if (e == hipSuccess) e = hipMemcpy(h->conv_bn_off_dev, off.data(), off.size() * sizeof(int), hipMemcpyHostToDevice);
         if (e != hipSuccess) return fail("forward: split-fp16 weight buffers", e);
@@ -558,7 +560,7 @@ static int32_t ensure_h3(azg_pv* h, hipStream_t st)
     }
     if (h->h3_dirty) {
         AZG_TRY(launch_pack_h3(h->params, h->conv_off_dev, nl, C, h->conv_bn_off_dev, h->scale, h->h3exp, h->wpack16,
-                               h->scale16, st),
+                               h->scale16, h->h3inv, st),
                 "forward: split-fp16 weight pack");
         h->h3_dirty = false;
     }

@@ -315,6 +315,8 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
                 Es[row * ELD + wn * TN * 32 + j * 32 + r32] = acc[i][j][r];
             }
     __syncthreads();
+    f32x4 h3s = {1.f, 1.f, 1.f, 1.f};
+    if (EPI == EPI_RAW && guard) h3s = *(const f32x4*)(scale + col);
     if (!EARLY && (EPI == EPI_BN_RELU || EPI == EPI_BN_RES_RELU || EPI == EPI_BN_OPTRES_RELU)) {
         s4 = *(const f32x4*)(scale + col);
         t4 = *(const f32x4*)(shift + col);
@@ -331,6 +333,7 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
         const int row = er + p * RPI;
         const int m = m0 + row;
         f32x4 v = *(const f32x4*)(Es + row * ELD + ec);
+        if (EPI == EPI_RAW && guard) v *= h3s;   // split-fp16 weights carry 2^e: exact
         if (guard) {   // H3: a non-finite accumulator = an input beyond fp16's range (H3Guard)
             const bool fin = __builtin_isfinite(v[0]) && __builtin_isfinite(v[1]) && __builtin_isfinite(v[2]) &&
                              __builtin_isfinite(v[3]);
@@ -735,7 +738,8 @@ __device__ __forceinline__ void halo_tile(
     static_assert(RPP % 16 == 0, "halo staging rows must keep the row swizzle");
     static_assert(H_LD <= 9, "halo loads are spread over the 9 taps");
     static_assert(PRO == PRO_NONE || H_LD <= 8, "the operand prologue of a row runs one tap after its load");
-    static_assert(PRO == PRO_NONE || ((VAR == 0 || VAR == 32) && ABL == 0), "operand prologue: register staging only");
+    static_assert(PRO == PRO_NONE || (((VAR & ~65) == 0 || (VAR & ~65) == 32) && ABL == 0),
+                  "operand prologue: register staging only");
     // VAR (A/B studies; the product uses 0, measured fastest): bit 1 = halo rows
     // swizzled on the padded board position (conflict-free fragment reads) and an
     // unpadded epilogue tile; bit 2 = weights staged two chunks ahead; bit 4 = LDS-DMA
@@ -752,7 +756,10 @@ __device__ __forceinline__ void halo_tile(
     // (and scaled by a per-layer power of two so their lo parts stay normal,
     // pv_pack.hip pack_h3; the epilogue's BN scale carries the inverse).
     constexpr bool H3 = (VAR & 64) != 0;
-    static_assert(!H3 || (PRO == PRO_NONE && XE == XE_NONE), "H3: eval tiles only");
+    // train forward (EPI_RAW + XE_STATS, PRO): BN-normalised inputs; the raw output is
+    // multiplied by `scale` (2^-e of the layer) in the epilogue.  The dgrad convs (inputs
+    // not normalised) stay fp32.
+    static_assert(!H3 || XE == XE_NONE || XE == XE_STATS, "H3: eval and train-forward tiles only");
     constexpr int NCHK = 9 * CG;
 
     float* Ah = smem;                 // [HR][32]
@@ -988,6 +995,12 @@ __device__ __forceinline__ void halo_tile(
             // keep the next chunk's global loads at the top of the chunk: without this
             // fence hipcc sinks them to just before their vmcnt wait (latency exposed)
             __builtin_amdgcn_sched_barrier(0);
+            // H3: the fragment addresses of each tap are built at the tap (a few VALU ops)
+            // instead of 9 taps x 4 addresses hoisted and kept live across the groups
+            if constexpr (H3) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(hrow[i]), "+v"(vpix[i]));
+            }
             const int d = (tap / 3 - 1) * PADW + (tap % 3 - 1);
             const int vd = (tap / 3 - 1) * BOARD + (tap % 3 - 1);
             int arow[TM], aswz[TM];

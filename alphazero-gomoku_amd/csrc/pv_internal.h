@@ -37,9 +37,12 @@ struct EpiX;
 struct ProX;
 struct FinX;
 constexpr int TRAIN_BM = 128;   // rows per M tile of conv3x3_train (BN partials granularity)
+// oscale (forward convs only): the split-fp16 weights of pack_h3 are passed as wp and the
+// raw output is multiplied by oscale[c] (= 2^-e of the layer, exact); nullptr: fp32 weights
 hipError_t launch_conv3x3_train(int C, int epi, int xe, const float* in, const float* wp, const float* resid,
                                 float* out, int M, const EpiX& ex, hipStream_t st, const ProX* px = nullptr,
-                                const FinX* fx = nullptr);
+                                const FinX* fx = nullptr, const float* oscale = nullptr);
+extern int g_train_h3;   // key 49: the train step's forward convs in split-fp16 (1) or fp32 MFMA (0)
 extern int g_tower_mode;
 extern int g_conv_shape_override;
 extern int g_tower_shape;
@@ -105,8 +108,9 @@ hipError_t launch_conv3x3_h3(int shape, int C, int epi, const float* in, const f
                              const float* shift, const float* resid, float* out, int M, hipStream_t st,
                              unsigned* ring, unsigned seq);
 hipError_t launch_pack_h3(const float* params, const int64_t* offs, int nl, int C, const int* conv_bn_off,
-                          const float* scale, int* exps, void* wp16, float* scale16, hipStream_t st);
+                          const float* scale, int* exps, void* wp16, float* scale16, float* inv, hipStream_t st);
 extern int g_tower_h3;
+extern int g_h3_tower_var;
 hipError_t launch_fold_bn(const float* params, const float* stats, const void* desc, int nlayers,
                           float* scale, float* shift, hipStream_t st);
 
@@ -150,6 +154,7 @@ struct azg_pv {
     void* wpack16 = nullptr;
     float* scale16 = nullptr;
     int* h3exp = nullptr;
+    float* h3inv = nullptr;   // [2 NB][C]: 2^-e of each conv (train forward, raw outputs)
     int* conv_bn_off_dev = nullptr;
     bool h3_dirty = true;
 
@@ -205,6 +210,7 @@ void free_workspace(azg_pv* h);
 void free_train_workspace(azg_pv* h);
 int32_t ensure_eval_workspace(azg_pv* h, int batch, hipStream_t st);
 int32_t repack(azg_pv* h, hipStream_t st, float* dgrad_dst = nullptr, int part = 0);   // dgrad_dst: also pack dgrad weights
+int32_t ensure_h3(azg_pv* h, hipStream_t st);   // split-fp16 packs of the current parameters
 int prof_begin(azg_pv* h, int cls, hipStream_t st, int64_t boards = 0);   // returns pair index or -1
 hipError_t prof_harvest(azg_pv* h);
 void prof_end(azg_pv* h, int pair, hipStream_t st);

@@ -195,24 +195,29 @@ __global__ __launch_bounds__(256) void pack_h3_kernel(const float* __restrict__ 
     }
 }
 
-// scale16 = the eval BN scale of every residual conv's BN times 2^-e (exact)
+// scale16 = the eval BN scale of every residual conv's BN times 2^-e (exact); inv (train
+// forward, optional) = 2^-e per layer and output channel: the raw conv output's factor
 __global__ void scale_h3_kernel(const float* __restrict__ scale, const int* __restrict__ conv_bn_off,
-                                const int* __restrict__ exps, int C, float* __restrict__ scale16)
+                                const int* __restrict__ exps, int C, float* __restrict__ scale16,
+                                float* __restrict__ inv)
 {
     const int l = blockIdx.x, o = conv_bn_off[l];
     const float f = ldexpf(1.f, -exps[l]);
-    for (int c = threadIdx.x; c < C; c += blockDim.x) scale16[o + c] = scale[o + c] * f;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        scale16[o + c] = scale[o + c] * f;
+        if (inv) inv[l * C + c] = f;
+    }
 }
 
 hipError_t launch_pack_h3(const float* params, const int64_t* offs, int nl, int C, const int* conv_bn_off,
-                          const float* scale, int* exps, void* wp16, float* scale16, hipStream_t st)
+                          const float* scale, int* exps, void* wp16, float* scale16, float* inv, hipStream_t st)
 {
     if (nl <= 0) return hipSuccess;
     hipLaunchKernelGGL(h3_exp_kernel, dim3(nl), dim3(256), 0, st, params, offs, C, exps);
     int nb = nblk(9 * C * C);
     nb = nb > 256 ? 256 : nb;
     hipLaunchKernelGGL(pack_h3_kernel, dim3(nb, nl), dim3(256), 0, st, params, offs, C, exps, (_Float16*)wp16);
-    hipLaunchKernelGGL(scale_h3_kernel, dim3(nl), dim3(256), 0, st, scale, conv_bn_off, exps, C, scale16);
+    hipLaunchKernelGGL(scale_h3_kernel, dim3(nl), dim3(256), 0, st, scale, conv_bn_off, exps, C, scale16, inv);
     return hipGetLastError();
 }
 

@@ -224,7 +224,9 @@ __global__ __launch_bounds__(64 * NW_, (tower_min_waves<BN_, NW_>())) void conv_
 
     if (tid == 0) s_claim[0] = (int)__hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    int w = s_claim[0];
+    // the claim is workgroup-uniform: keep it (and the layer / tile indices and the
+    // layer's pointers derived from it) in scalar registers
+    int w = __builtin_amdgcn_readfirstlane(s_claim[0]);
     while (w < total) {
         const int l = w / tpl, t = w - l * tpl;
         const int mt = t / (NTN / grp), nt0 = (t - mt * (NTN / grp)) * grp;
@@ -277,7 +279,7 @@ __global__ __launch_bounds__(64 * NW_, (tower_min_waves<BN_, NW_>())) void conv_
         }
         if (tid == 0) __hip_atomic_fetch_add(cnt + (size_t)l * mtiles + mt, (unsigned)grp, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
-        w = s_claim[0];
+        w = __builtin_amdgcn_readfirstlane(s_claim[0]);
     }
 }
 
@@ -333,6 +335,7 @@ size_t tower_prod_bytes(int nlayers, int M)
 // H -> Y (BN, + X, ReLU), X <-> Y.  `act` are the three padded NHWC buffers
 // (act[0] holds the stem output; the result ends in act[0] or act[2], returned in
 // *result).  `sync` must hold tower_sync_bytes(2*NB, M) bytes.
+int g_h3_tower_var = 1;   // key 20: the H3 tower body, 1 = board-keyed halo swizzle (VAR 99, default), 0 = row-keyed (98)
 int g_tower_h3 = 1;   // key 19: split-fp16 (H3) eval residual convs (pv_halo.h VAR bit 64, default); 0 = fp32 MFMA
 
 hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const float* wpack, const float* scale,
@@ -378,16 +381,23 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     hipError_t e = hipMemsetAsync(sync, 0, tower_sync_bytes(2 * NB, M), st);
     if (e != hipSuccess) return e;
     if (h3) {   // wpack / scale are the split-fp16 packs (pv_pack.hip pack_h3)
-        // VAR 98 = H3 + buffer addressing + weights staged two chunks ahead (bit 2): +2.5-3 %
-        // over 96 at 256-4096 boards, the board-keyed swizzle (bit 1) slower in the tower
-        // (scripts/h3_tune_study.py, profiles/r5_h3_study.md); bitwise equal to every other form
+        // VAR 99 = H3 + buffer addressing + weights staged two chunks ahead (bit 2) + the
+        // board-keyed halo swizzle (bit 1): with the fragment addresses built per tap (no
+        // spills) 3.8-4.8 % faster than the row-keyed VAR 98, whose fragment reads conflict
+        // at board-row ends (32 % of its LDS cycles; scripts/h3_tune_study.py,
+        // profiles/r5_h3_study.md); bitwise equal to every other form.  Key 20 = 0: VAR 98.
+        const bool vs = g_h3_tower_var == 1;
         switch (C) {
             case 128:
-                if (shape == 5) return launch_tower_t<128, 64, 2, 1, 4, 98>(a, st, nullptr);
-                return launch_tower_t<128, 64, 4, 1, 8, 98>(a, st, nullptr);
+                if (shape == 5) return vs ? launch_tower_t<128, 64, 2, 1, 4, 99>(a, st, nullptr)
+                                          : launch_tower_t<128, 64, 2, 1, 4, 98>(a, st, nullptr);
+                return vs ? launch_tower_t<128, 64, 4, 1, 8, 99>(a, st, nullptr)
+                          : launch_tower_t<128, 64, 4, 1, 8, 98>(a, st, nullptr);
             case 256:
-                if (shape == 5) return launch_tower_t<256, 64, 2, 1, 4, 98>(a, st, nullptr);
-                return launch_tower_t<256, 64, 4, 1, 8, 98>(a, st, nullptr);
+                if (shape == 5) return vs ? launch_tower_t<256, 64, 2, 1, 4, 99>(a, st, nullptr)
+                                          : launch_tower_t<256, 64, 2, 1, 4, 98>(a, st, nullptr);
+                return vs ? launch_tower_t<256, 64, 4, 1, 8, 99>(a, st, nullptr)
+                          : launch_tower_t<256, 64, 4, 1, 8, 98>(a, st, nullptr);
             default: return hipErrorInvalidValue;
         }
     }

@@ -762,7 +762,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     // sums of the layer below: act / z / layer `xl`); partials land in part_a / part_b;
     // fin >= 0: the BN layer this launch's partials belong to, finalized in-kernel
     auto conv = [&](int epi, int xe, const float* in, const float* wp, const float* res, float* out,
-                    const float* xact, const float* xz, int xl, int fin) -> int32_t {
+                    const float* xact, const float* xz, int xl, int fin, const float* osc = nullptr) -> int32_t {
         int pr = prof_begin(h, AZG_PROF_TRAIN_CONV, st, B);
         const EpiX ex{xact, xz, xl >= 0 ? w->bmean + bd[xl].out_off : nullptr, w->part_a, w->part_b};
         FinX fx{};
@@ -770,7 +770,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             fx = fin_args(fin, xe == XE_STATS);
             fx.cnt = w->fincnt;
         }
-        AZG_CK(launch_conv3x3_train(C, epi, xe, in, wp, res, out, M, ex, st, nullptr, fin >= 0 ? &fx : nullptr),
+        AZG_CK(launch_conv3x3_train(C, epi, xe, in, wp, res, out, M, ex, st, nullptr, fin >= 0 ? &fx : nullptr, osc),
                "train: conv3x3");
         prof_end(h, pr, st);
         return 0;
@@ -800,6 +800,14 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     int32_t r;
 #define R(x) if ((r = (x))) return r
 
+    // forward conv weights: the split-fp16 packs (key 49; ensured by train_backward) with
+    // their per-layer 2^-e output factor, or the fp32 packs
+    const bool fh3 = g_train_h3 && h->wpack16;
+    auto fwd_w = [&](int ci) -> const float* {
+        return fh3 ? (const float*)h->wpack16 + (size_t)ci * CC9 : h->wpack + (size_t)ci * CC9;
+    };
+    auto fwd_s = [&](int ci) -> const float* { return fh3 ? h->h3inv + (size_t)ci * C : nullptr; };
+
     // ---- forward (train-mode BN) ----
     {
         int pr0 = prof_begin(h, AZG_PROF_TRAIN_OTHER, st);
@@ -819,24 +827,24 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         // (pv_halo.h ProX): `pend` = the activation still to be formed from its raw z
         struct Pend { const float* z; int layer; const float* res; float* out; };
         Pend pend{w->z0, h->bn_stem, nullptr, w->a0};
-        auto fused_conv = [&](const Pend& p, const float* wpk, float* out, int fin) -> int32_t {
+        auto fused_conv = [&](const Pend& p, int ci, float* out, int fin) -> int32_t {
             int pr = prof_begin(h, AZG_PROF_TRAIN_CONV, st, B);
             const int o = bd[p.layer].out_off;
             const EpiX ex{nullptr, nullptr, nullptr, w->part_a, w->part_b};
             const ProX px{p.res, w->bscale + o, w->bshift + o, p.out};
             FinX fx = fin_args(fin, true);
             fx.cnt = w->fincnt;
-            AZG_CK(launch_conv3x3_train(C, EPI_RAW, XE_STATS, p.z, wpk, nullptr, out, M, ex, st, &px,
-                                        ffin ? &fx : nullptr),
+            AZG_CK(launch_conv3x3_train(C, EPI_RAW, XE_STATS, p.z, fwd_w(ci), nullptr, out, M, ex, st, &px,
+                                        ffin ? &fx : nullptr, fwd_s(ci)),
                    "train: conv3x3 (fused BN apply)");
             prof_end(h, pr, st);
             if (!ffin) return fin_fwd(fin, TRAIN_BM, ntt);
             return 0;
         };
         for (int i = 0; i < NB; ++i) {
-            R(fused_conv(pend, h->wpack + (size_t)(2 * i) * CC9, w->z1[i], h->bn_blk[i].first));
+            R(fused_conv(pend, 2 * i, w->z1[i], h->bn_blk[i].first));
             pend = Pend{w->z1[i], h->bn_blk[i].first, nullptr, w->hh[i]};
-            R(fused_conv(pend, h->wpack + (size_t)(2 * i + 1) * CC9, w->z2[i], h->bn_blk[i].second));
+            R(fused_conv(pend, 2 * i + 1, w->z2[i], h->bn_blk[i].second));
             pend = Pend{w->z2[i], h->bn_blk[i].second, X, w->xo[i]};
             X = w->xo[i];
         }
@@ -850,12 +858,12 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         R(apply(w->z0, nullptr, h->bn_stem, w->a0));
         for (int i = 0; i < NB; ++i) {
             const int l1 = h->bn_blk[i].first, l2 = h->bn_blk[i].second;
-            R(conv(EPI_RAW, XE_STATS, X, h->wpack + (size_t)(2 * i) * CC9, nullptr, w->z1[i], nullptr, nullptr, -1,
-                   ffin ? l1 : -1));
+            R(conv(EPI_RAW, XE_STATS, X, fwd_w(2 * i), nullptr, w->z1[i], nullptr, nullptr, -1, ffin ? l1 : -1,
+                   fwd_s(2 * i)));
             if (!ffin) R(fin_fwd(l1, TRAIN_BM, ntt));
             R(apply(w->z1[i], nullptr, l1, w->hh[i]));
-            R(conv(EPI_RAW, XE_STATS, w->hh[i], h->wpack + (size_t)(2 * i + 1) * CC9, nullptr, w->z2[i], nullptr,
-                   nullptr, -1, ffin ? l2 : -1));
+            R(conv(EPI_RAW, XE_STATS, w->hh[i], fwd_w(2 * i + 1), nullptr, w->z2[i], nullptr, nullptr, -1,
+                   ffin ? l2 : -1, fwd_s(2 * i + 1)));
             if (!ffin) R(fin_fwd(l2, TRAIN_BM, ntt));
             R(apply(w->z2[i], X, l2, w->xo[i]));
             X = w->xo[i];
@@ -1054,6 +1062,8 @@ int32_t train_backward(azg_pv* h, const float* x, const float* pis, const float*
         if (int32_t r = repack(h, st, w->wdpack)) return r;
         h->train_packs = true;
     }
+    if (g_train_h3)
+        if (int32_t r = ensure_h3(h, st)) return r;
     const int C = h->C;
     int32_t r;
     switch (C) {

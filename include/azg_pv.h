@@ -199,6 +199,8 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          range (65520 rounds to inf) makes its products non-finite: the epilogue posts
  *          the launch and azg_pv_recover recomputes it with fp32 MFMA.  The train step
  *          always uses fp32 MFMA;
+ *   key 20: the split-fp16 tower's tile body (1 = halo rows keyed on the board position,
+ *          conflict-free fragment reads, default; 0 = row-keyed); bitwise identical;
  *   key 48: train weight-grad tile (1 = padded-row table, buffer LDS-DMA, slabs in the
  *          MFMA layout, default; 0 = round-4 form); bitwise identical;
  *   key 18: seconds a handle runs per-layer convs after azg_pv_recover recomputed one

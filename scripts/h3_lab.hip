@@ -18,6 +18,7 @@
 #include <string>
 
 #include "pv_halo.h"
+#include "pv_h3.h"
 
 using namespace azg;
 
@@ -48,6 +49,24 @@ __global__ __launch_bounds__(64 * NW_, WPE) void lab_conv(const float* __restric
         (t / NTN) * T::BM, (t % NTN) * T::BN, smem, EpiX{}, ProX{}, FinX{}, guard);
 }
 
+template <int C, int BN_, int WM_, int TM_, int NW_, int TPS, int NWB, int WPE, int ABL = 0>
+__global__ __launch_bounds__(64 * NW_, WPE) void lab_h3(const float* __restrict__ in, const float* __restrict__ wp,
+                                                        const float* __restrict__ scale,
+                                                        const float* __restrict__ shift,
+                                                        const float* __restrict__ resid, float* __restrict__ out,
+                                                        int M, H3Guard guard)
+{
+    using T = ConvTile<C, BN_, WM_, TM_, NW_>;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int NTN = C / T::BN;
+    const int L = blockIdx.x, nt = gridDim.x;
+    const int xcd = L & 7, q8 = nt >> 3, r8 = nt & 7;
+    const int t = xcd * q8 + min(xcd, r8) + (L >> 3);
+    h3_tile<C, BN_, WM_, TM_, NW_, TPS, NWB, EPI_BN_RES_RELU, false, 0, ABL & 7, ABL & ~7>(
+        in, wp, scale, shift, resid, out, __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0, 0x00020000), M,
+        (t / NTN) * T::BM, (t % NTN) * T::BN, smem, guard);
+}
+
 struct Variant {
     std::string name;
     int C;
@@ -75,6 +94,31 @@ static hipError_t prep_v()
     return hipFuncSetAttribute((const void*)lab_conv<C, BN, WM, TM, NW, VAR, WPE>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
+template <int C, int BN, int WM, int TM, int NW, int TPS, int NWB, int WPE, int ABL = 0>
+static void launch_h(const float* in, const float* wp, const float* sc, const float* sh, const float* rs, float* out,
+                     int M, H3Guard g, hipStream_t st)
+{
+    using T = ConvTile<C, BN, WM, TM, NW>;
+    constexpr int lds = h3_lds_bytes<C, BN, WM, TM, NW, TPS, NWB, ABL & ~7>();
+    dim3 grid(((M + T::BM - 1) / T::BM) * (C / T::BN));
+    hipLaunchKernelGGL((lab_h3<C, BN, WM, TM, NW, TPS, NWB, WPE, ABL>), grid, dim3(T::NT), lds, st, in, wp, sc, sh, rs,
+                       out, M, g);
+}
+template <int C, int BN, int WM, int TM, int NW, int TPS, int NWB, int WPE, int ABL = 0>
+static hipError_t prep_h()
+{
+    constexpr int lds = h3_lds_bytes<C, BN, WM, TM, NW, TPS, NWB, ABL & ~7>();
+    return hipFuncSetAttribute((const void*)lab_h3<C, BN, WM, TM, NW, TPS, NWB, WPE, ABL>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+#define VH(C, BN, WM, TM, NW, TPS, NWB, WPE)                                                                        \
+    Variant{"h3_tile " #BN "x" #WM "x" #TM " nw" #NW " tps" #TPS " nwb" #NWB " wpe" #WPE, C,                      \
+            ConvTile<C, BN, WM, TM, NW>::BM, BN, (size_t)H3Tile<C, BN, WM, TM, NW, TPS, NWB>::LDS,                  \
+            launch_h<C, BN, WM, TM, NW, TPS, NWB, WPE>, prep_h<C, BN, WM, TM, NW, TPS, NWB, WPE>}
+#define VA(C, BN, WM, TM, NW, TPS, NWB, WPE, ABL)                                                                   \
+    Variant{"h3_tile " #BN "x" #WM "x" #TM " nw" #NW " tps" #TPS " nwb" #NWB " wpe" #WPE " ABLATION " #ABL, C,     \
+            ConvTile<C, BN, WM, TM, NW>::BM, BN, (size_t)h3_lds_bytes<C, BN, WM, TM, NW, TPS, NWB, ABL & ~7>(),            \
+            launch_h<C, BN, WM, TM, NW, TPS, NWB, WPE, ABL>, prep_h<C, BN, WM, TM, NW, TPS, NWB, WPE, ABL>}
 #define V(C, BN, WM, TM, NW, VAR, WPE)                                                                              \
     Variant{#BN "x" #WM "x" #TM " nw" #NW " var" #VAR " wpe" #WPE, C, ConvTile<C, BN, WM, TM, NW>::BM, BN,         \
             (size_t)halo_lds_bytes<C, BN, WM, TM, NW, VAR>(), launch_v<C, BN, WM, TM, NW, VAR, WPE>,                \
@@ -85,20 +129,27 @@ static std::vector<Variant> variants()
 {
     return {
         V(C, 64, 4, 1, 8, 99, 2),    // product per-layer form: 128x64, 8 waves, wave 32x32
-        V(C, 64, 4, 1, 8, 98, 2),    // the tower's body (row-keyed halo swizzle)
-        V(C, 128, 4, 1, 8, 99, 2),   // 128x128, 8 waves as 4x2, wave 32x64
-        V(C, 128, 2, 2, 8, 99, 2),   // 128x128, 8 waves as 2x4, wave 64x32
-        V(C, 64, 4, 2, 8, 99, 2),    // 256x64, 8 waves as 4x2, wave 64x32
         V(C, 128, 2, 2, 4, 99, 2),   // 128x128, 4 waves as 2x2, wave 64x64
-        V(C, 128, 2, 2, 4, 99, 1),   // ... one workgroup per CU guaranteed (256 VGPRs)
-        V(C, 128, 4, 1, 16, 99, 1),  // 128x128, 16 waves, wave 32x32
-        V(C, 64, 2, 1, 4, 99, 2),    // 64x64, 4 waves (the small-batch tile)
-        // the launch-bounds second argument is the minimum waves per SIMD: 4 caps the tile at
-        // 128 VGPRs (two 8-wave workgroups per CU, the tower's budget)
-        V(C, 64, 4, 1, 8, 98, 4),
-        V(C, 128, 4, 1, 8, 99, 4),
-        V(C, 128, 2, 2, 8, 99, 4),
-        V(C, 64, 4, 2, 8, 99, 4),
+        // h3_tile (pv_h3.h): LDS-DMA weight stages, counted waits, raw barriers
+        VH(C, 64, 4, 1, 8, 1, 2, 4),     // 128x64, wave 32x32, 1-tap stages
+        VH(C, 64, 4, 1, 8, 1, 3, 4),     // ... three stage buffers
+        VH(C, 64, 4, 1, 8, 3, 2, 2),     // ... 3-tap stages (one workgroup per CU by LDS)
+        VH(C, 128, 2, 2, 4, 1, 2, 2),    // 128x128, wave 64x64, 1-tap stages
+        VH(C, 128, 2, 2, 4, 1, 3, 2),    // ... three stage buffers
+        VH(C, 128, 4, 1, 8, 1, 2, 2),    // 128x128, 8 waves, wave 32x64
+        VH(C, 128, 2, 2, 8, 1, 2, 2),    // 128x128, 8 waves as 2x4, wave 64x32
+        VH(C, 128, 2, 2, 4, 3, 2, 1),    // 128x128, wave 64x64, 3-tap stages, one workgroup per CU
+        // OPT (ablation value bits >= 8): 8 = next-group halo loads at the group's first stage,
+        // 16 = epilogue residual loads before the LDS pass -- bitwise identical
+        VA(C, 128, 2, 2, 4, 1, 3, 2, 8), VA(C, 128, 2, 2, 4, 1, 3, 2, 16), VA(C, 128, 2, 2, 4, 1, 3, 2, 24),
+        VA(C, 64, 4, 1, 8, 3, 2, 2, 8), VA(C, 64, 4, 1, 8, 3, 2, 2, 24), VA(C, 64, 4, 1, 8, 1, 3, 4, 24),
+        // OPT 32: direct epilogue (no LDS pass)
+        VA(C, 128, 2, 2, 4, 1, 3, 2, 32), VA(C, 128, 4, 1, 8, 1, 2, 4, 32), VA(C, 64, 4, 1, 8, 3, 2, 2, 32),
+        // 128x128 / 8 waves (wave 32x64) capped at 128 VGPRs: two workgroups per CU
+        VH(C, 128, 4, 1, 8, 1, 2, 4), VH(C, 128, 4, 1, 8, 1, 3, 4), VA(C, 128, 4, 1, 8, 1, 3, 4, 8),
+        VH(C, 128, 2, 2, 8, 1, 3, 4),
+        // timing ablations (results invalid): 1 no epilogue, 2 no halo loads, 7 neither nor weights
+        VA(C, 128, 2, 2, 4, 1, 3, 2, 1), VA(C, 128, 2, 2, 4, 1, 3, 2, 2), VA(C, 128, 2, 2, 4, 1, 3, 2, 7),
     };
 }
 

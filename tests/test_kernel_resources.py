@@ -31,12 +31,13 @@ SCRATCH_BUDGET = [
     # still 4 % faster than VAR 32's 32 B
     (r"conv_towerILi256ELi64ELi4ELi1ELi8ELi33E", 112),
     (r"conv_towerILi256ELi64ELi2ELi1ELi4ELi33E", 144),
-    # split-fp16 towers (halo_tile VAR 98, the eval default, key 19): 128 VGPRs at 4 waves per
-    # SIMD; the 8-wave 128x64 tile is the tuned one at >= 224 boards
-    (r"conv_towerILi128ELi64ELi4ELi1ELi8ELi98E", 96),
-    (r"conv_towerILi128ELi64ELi2ELi1ELi4ELi98E", 304),
-    (r"conv_towerILi256ELi64ELi4ELi1ELi8ELi98E", 112),
-    (r"conv_towerILi256ELi64ELi2ELi1ELi4ELi98E", 336),
+    # split-fp16 towers (halo_tile VAR 99, the eval default, key 19 / 20; VAR 98 the row-keyed
+    # form): 128 VGPRs at 4 waves per SIMD, fragment addresses built per tap (round 5: 96-336 B
+    # of spills before); the 8-wave 128x64 tile is the tuned one at >= 224 boards
+    (r"conv_towerILi128ELi64ELi4ELi1ELi8ELi99E", 0),
+    (r"conv_towerILi256ELi64ELi4ELi1ELi8ELi99E", 16),
+    (r"conv_towerILi(128|256)ELi64ELi2ELi1ELi4ELi99E", 80),
+    (r"conv_towerILi(128|256)ELi64ELi(2|4)ELi1ELi(4|8)ELi98E", 16),
     (r"conv3x3_haloILi(128|256)ELi64ELi(2|4)ELi1ELi(4|8)ELi[01]ELi0ELi99E", 0),
     (r"conv_towerILi64ELi64E", 0),
     (r"conv_towerILi128ELi128ELi4ELi1ELi16E", 48),
