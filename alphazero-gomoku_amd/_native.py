@@ -28,7 +28,7 @@ class TowerDiag(ctypes.Structure):
         "producer_xcc")] + [("producer_start_us", ctypes.c_int32), ("max_wall_us", ctypes.c_uint32),
                              ("waits_suspended", ctypes.c_uint32), ("breaker_trips", ctypes.c_uint32),
                              ("breaker_launches", ctypes.c_uint32), ("h3_overflows", ctypes.c_uint32),
-                             ("reserved", ctypes.c_uint32 * 4)]
+                             ("train_h3_overflows", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 3)]
 
     def as_dict(self) -> dict:
         d = {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}
@@ -69,6 +69,7 @@ _SIGS = {
     "azg_pv_recover": (ctypes.c_int32, [_P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32), _P]),
     "azg_pv_status": (ctypes.c_int32, [_P]),
     "azg_pv_clear_status": (ctypes.c_int32, [_P]),
+    "azg_pv_train_status": (ctypes.c_int32, [_P]),
     "azg_pv_tower_diag_read": (ctypes.c_int32, [_P, ctypes.POINTER(TowerDiag), _P]),
     "azg_pv_tower_diag_clear": (ctypes.c_int32, [_P, _P]),
     "azg_pv_debug_copy": (ctypes.c_int32, [_P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32, _P]),

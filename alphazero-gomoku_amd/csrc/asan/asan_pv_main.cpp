@@ -40,6 +40,7 @@ int main()
         CHECK(o == n);
         CHECK(azg_pv_bn_count(h) > 0 && azg_pv_num_bn_layers(h) == 2 * shapes[s][0] + 3);
         CHECK(azg_pv_status(h) == 0);
+        CHECK(azg_pv_train_status(h) == 0);
         CHECK(azg_pv_clear_status(h) == 0);
         CHECK(azg_pv_mark_dirty(h) == 0);
         // tower recovery / wait record before any launch: nothing posted, nothing to do
@@ -73,6 +74,7 @@ int main()
     CHECK(azg_pv_destroy(nullptr) == 0);
     CHECK(azg_pv_param_count(nullptr) == -1);
     CHECK(azg_pv_status(nullptr) == 0);
+    CHECK(azg_pv_train_status(nullptr) == 0);
     CHECK(azg_pv_last_seq(nullptr) == 0);
     CHECK(azg_pv_tower_diag_clear(nullptr, nullptr) != 0);
     CHECK(azg_pv_bind(nullptr, nullptr, nullptr, nullptr) != 0);

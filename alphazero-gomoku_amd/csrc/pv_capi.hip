@@ -137,16 +137,18 @@ int32_t azg_pv_bind(azg_pv* h, float* params, float* grads, float* bn_stats)
         if (e != hipSuccess) return fail("azg_pv_bind: conv offset upload", e);
         void* sp = nullptr;
         // two rings in one pinned, mapped allocation: timed-out tower launches, H3 overflows
-        e = hipHostMalloc(&sp, 2 * kTowerRing * sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent);
+        // (+ the train forward's overflow flags)
+        e = hipHostMalloc(&sp, kStatusWords * sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent);
         if (e != hipSuccess) return fail("azg_pv_bind: hipHostMalloc(tower ring)", e);
         h->ring_host = (unsigned*)sp;
         h->ovf_host = h->ring_host + kTowerRing;
-        memset(h->ring_host, 0, 2 * kTowerRing * sizeof(unsigned));
+        memset(h->ring_host, 0, kStatusWords * sizeof(unsigned));
         void* dp = nullptr;
         e = hipHostGetDevicePointer(&dp, sp, 0);
         if (e != hipSuccess) return fail("azg_pv_bind: hipHostGetDevicePointer(tower ring)", e);
         h->ring_dev = (unsigned*)dp;
         h->ovf_dev = h->ring_dev + kTowerRing;
+        h->train_ovf_dev = h->ring_dev + 2 * kTowerRing;
         e = hipMalloc(&h->tower_diag, kTowerDiagWords * sizeof(unsigned));
         if (e == hipSuccess) e = hipMemset(h->tower_diag, 0, kTowerDiagWords * sizeof(unsigned));
         if (e != hipSuccess) return fail("azg_pv_bind: tower wait record", e);
@@ -240,19 +242,34 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards)
     return 0;
 }
 
+// split-fp16 train-forward overflow flags set since the last azg_pv_clear_status
+static unsigned train_ovf_flags(const azg_pv* h)
+{
+    unsigned n = 0;
+    if (h->ring_host)
+        for (unsigned i = 0; i < kTrainOvfWords; ++i)
+            n += __atomic_load_n(h->ring_host + 2 * kTowerRing + i, __ATOMIC_ACQUIRE) != 0u;
+    return n;
+}
+
 int32_t azg_pv_status(const azg_pv* h)
 {
     if (!h || !h->ring_host) return 0;
     int32_t n = 0;
-    for (unsigned i = 0; i < 2 * kTowerRing; ++i) n += __atomic_load_n(h->ring_host + i, __ATOMIC_ACQUIRE) != 0u;
+    for (unsigned i = 0; i < kStatusWords; ++i) n += __atomic_load_n(h->ring_host + i, __ATOMIC_ACQUIRE) != 0u;
     return n;
+}
+
+int32_t azg_pv_train_status(const azg_pv* h)
+{
+    return h ? (int32_t)train_ovf_flags(h) : 0;
 }
 
 int32_t azg_pv_clear_status(azg_pv* h)
 {
     if (!h) return fail("azg_pv_clear_status: null handle");
     if (h->ring_host)
-        for (unsigned i = 0; i < 2 * kTowerRing; ++i) __atomic_store_n(h->ring_host + i, 0u, __ATOMIC_RELEASE);
+        for (unsigned i = 0; i < kStatusWords; ++i) __atomic_store_n(h->ring_host + i, 0u, __ATOMIC_RELEASE);
     h->breaker_until = 0.0;   // and the per-layer breaker closes
     return 0;
 }
@@ -312,6 +329,7 @@ int32_t azg_pv_tower_diag_read(azg_pv* h, azg_pv_tower_diag* out, void* stream)
     out->breaker_trips = h->breaker_trips;
     out->breaker_launches = h->breaker_launches;
     out->h3_overflows = h->h3_overflows;
+    out->train_h3_overflows = train_ovf_flags(h);
     if (!h->tower_diag) return 0;
     unsigned w[kTowerDiagWords];
     hipStream_t st = (hipStream_t)stream;
@@ -345,6 +363,7 @@ int32_t azg_pv_tower_diag_read(azg_pv* h, azg_pv_tower_diag* out, void* stream)
     out->breaker_trips = h->breaker_trips;
     out->breaker_launches = h->breaker_launches;
     out->h3_overflows = h->h3_overflows;
+    out->train_h3_overflows = train_ovf_flags(h);
     return 0;
 }
 

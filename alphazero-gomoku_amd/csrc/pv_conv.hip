@@ -234,7 +234,7 @@ struct TrainTile {
 template <int C, int EPI, int XE, bool WT, int PRO = PRO_NONE, int VAR = 32, int NWT = 8>
 __global__ __launch_bounds__(64 * NWT) __attribute__((amdgpu_waves_per_eu(4))) void conv3x3_train(
     const float* __restrict__ in, const float* __restrict__ wp, const float* __restrict__ resid,
-    float* __restrict__ out, int M, EpiX ex, ProX px, FinX fx, const float* __restrict__ oscale)
+    float* __restrict__ out, int M, EpiX ex, ProX px, FinX fx, const float* __restrict__ oscale, H3Guard guard)
 {
     using T = typename TrainTile<C, NWT>::T;
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(64 * NWT) __attribute__((amdgpu_waves_per_eu(4))) v
     const int t = xcd * q8 + min(xcd, r8) + (L >> 3);
     halo_tile<C, T::BN, 4, 1, NWT, EPI, WT, 0, VAR, XE, PRO>(in, wp, oscale, nullptr, resid, out,
                                                           wt_rsrc(out, padded_bytes(M, C)), M, (t / NTN) * T::BM,
-                                                          (t % NTN) * T::BN, smem, ex, px, fx);
+                                                          (t % NTN) * T::BN, smem, ex, px, fx, guard);
 }
 
 // Stem conv 3->C (K = 27) on the VALU: 0.2 % of the forward FLOPs.  One
@@ -873,7 +873,7 @@ hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, cons
 template <int C, int EPI, int XE, int PRO, int VAR>
 static hipError_t launch_train_v(const float* in, const float* wp, const float* resid, float* out, int M,
                                  const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st,
-                                 const float* oscale = nullptr)
+                                 const float* oscale = nullptr, unsigned* h3ovf = nullptr)
 {
     using T = typename TrainTile<C, 8>::T;
     constexpr int lds = halo_lds_bytes<C, T::BN, 4, 1, 8, VAR, PRO>();
@@ -886,25 +886,28 @@ static hipError_t launch_train_v(const float* in, const float* wp, const float* 
     }
     dim3 grid(((M + T::BM - 1) / T::BM) * (C / T::BN));
     hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, true, PRO, VAR, 8>), grid, dim3(T::NT), lds, st, in, wp,
-                       resid, out, M, ex, px, fx, oscale);
+                       resid, out, M, ex, px, fx, oscale, H3Guard{h3ovf, 1u});
     return hipGetLastError();
 }
 
 template <int C, int EPI, int XE, int PRO = PRO_NONE>
 static hipError_t launch_train_t(const float* in, const float* wp, const float* resid, float* out, int M,
                                  const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st,
-                                 const float* oscale = nullptr)
+                                 const float* oscale = nullptr, unsigned* h3ovf = nullptr)
 {
-    // split-fp16 forward (VAR 97 = 64 | 32 | 1: H3, buffer addressing, board-keyed halo rows)
+    // split-fp16 forward (VAR 97 = 64 | 32 | 1: H3, buffer addressing, board-keyed halo rows;
+    // + 128: the fourth, lo x lo product -- key 49 = 2)
     if constexpr (EPI == EPI_RAW && XE == XE_STATS) {
-        if (oscale) return launch_train_v<C, EPI, XE, PRO, 97>(in, wp, resid, out, M, ex, px, fx, st, oscale);
+        if (oscale && g_train_h3 == 2)
+            return launch_train_v<C, EPI, XE, PRO, 225>(in, wp, resid, out, M, ex, px, fx, st, oscale, h3ovf);
+        if (oscale) return launch_train_v<C, EPI, XE, PRO, 97>(in, wp, resid, out, M, ex, px, fx, st, oscale, h3ovf);
     }
     if (oscale) return hipErrorInvalidValue;
     // (the board-keyed halo body, VAR 33, measured equal for the prologue-free train convs:
     // 2.865-2.869 vs 2.866-2.874 ms at 6x128 and within noise at 10x256, scripts/gpu_r4p.sh)
     return launch_train_v<C, EPI, XE, PRO, 32>(in, wp, resid, out, M, ex, px, fx, st);
 }
-int g_train_h3 = 0;   // key 49 (default off until measured)
+int g_train_h3 = 2;   // key 49: 0 fp32 MFMA, 1 split-fp16 (3 products), 2 split-fp16 with 4 products (default)
 
 // Train conv with fused BN partials: (EPI_RAW, XE_STATS) forward, optionally with
 // the input layer's BN applied in the staging (px: PRO_BN / PRO_BN_RES); (EPI_RAW |
@@ -912,17 +915,17 @@ int g_train_h3 = 0;   // key 49 (default off until measured)
 // the last workgroup of each N tile also runs the BN finalize (pv_halo.h FinX).
 hipError_t launch_conv3x3_train(int C, int epi, int xe, const float* in, const float* wp, const float* resid,
                                 float* out, int M, const EpiX& ex, hipStream_t st, const ProX* px, const FinX* fxp,
-                                const float* oscale)
+                                const float* oscale, unsigned* h3ovf)
 {
     const ProX p0{};
     const FinX fx = fxp ? *fxp : FinX{};
 #define AZG_TRAIN_C(CC)                                                                            \
     case CC:                                                                                       \
         if (epi == EPI_RAW && xe == XE_STATS && px && px->res)                                     \
-            return launch_train_t<CC, EPI_RAW, XE_STATS, PRO_BN_RES>(in, wp, resid, out, M, ex, *px, fx, st, oscale); \
+            return launch_train_t<CC, EPI_RAW, XE_STATS, PRO_BN_RES>(in, wp, resid, out, M, ex, *px, fx, st, oscale, h3ovf); \
         if (epi == EPI_RAW && xe == XE_STATS && px)                                                \
-            return launch_train_t<CC, EPI_RAW, XE_STATS, PRO_BN>(in, wp, resid, out, M, ex, *px, fx, st, oscale); \
-        if (epi == EPI_RAW && xe == XE_STATS) return launch_train_t<CC, EPI_RAW, XE_STATS>(in, wp, resid, out, M, ex, p0, fx, st, oscale); \
+            return launch_train_t<CC, EPI_RAW, XE_STATS, PRO_BN>(in, wp, resid, out, M, ex, *px, fx, st, oscale, h3ovf); \
+        if (epi == EPI_RAW && xe == XE_STATS) return launch_train_t<CC, EPI_RAW, XE_STATS>(in, wp, resid, out, M, ex, p0, fx, st, oscale, h3ovf); \
         if (epi == EPI_RAW && xe == XE_BNBWD) return launch_train_t<CC, EPI_RAW, XE_BNBWD>(in, wp, resid, out, M, ex, p0, fx, st); \
         if (epi == EPI_ADD && xe == XE_BNBWD) return launch_train_t<CC, EPI_ADD, XE_BNBWD>(in, wp, resid, out, M, ex, p0, fx, st); \
         return hipErrorInvalidValue;
@@ -1056,7 +1059,7 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     }
     if (key == 49) {  // train forward convs: 1 split-fp16 products (H3), 0 fp32 MFMA
         const int prev = azg::g_train_h3;
-        if (value == 0 || value == 1) azg::g_train_h3 = value;
+        if (value >= 0 && value <= 2) azg::g_train_h3 = value;
         return prev;
     }
     if (key == 19) {  // eval residual-conv arithmetic: 1 split-fp16 products (H3, default), 0 fp32 MFMA

@@ -738,7 +738,7 @@ __device__ __forceinline__ void halo_tile(
     static_assert(RPP % 16 == 0, "halo staging rows must keep the row swizzle");
     static_assert(H_LD <= 9, "halo loads are spread over the 9 taps");
     static_assert(PRO == PRO_NONE || H_LD <= 8, "the operand prologue of a row runs one tap after its load");
-    static_assert(PRO == PRO_NONE || (((VAR & ~65) == 0 || (VAR & ~65) == 32) && ABL == 0),
+    static_assert(PRO == PRO_NONE || (((VAR & ~193) == 0 || (VAR & ~193) == 32) && ABL == 0),
                   "operand prologue: register staging only");
     // VAR (A/B studies; the product uses 0, measured fastest): bit 1 = halo rows
     // swizzled on the padded board position (conflict-free fragment reads) and an
@@ -1029,6 +1029,10 @@ __device__ __forceinline__ void halo_tile(
                     for (int i = 0; i < TM; ++i)
 #pragma unroll
                         for (int j = 0; j < TN; ++j) {
+                            // VAR bit 128 (train forward): the lo x lo term too -- products exact
+                            // to ~2^-33, smallest first
+                            if constexpr ((VAR & 128) != 0)
+                                at[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bl[j], at[i][j], 0, 0, 0);
                             at[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], at[i][j], 0, 0, 0);
                             at[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], at[i][j], 0, 0, 0);
                             at[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], at[i][j], 0, 0, 0);

@@ -41,7 +41,7 @@ constexpr int TRAIN_BM = 128;   // rows per M tile of conv3x3_train (BN partials
 // raw output is multiplied by oscale[c] (= 2^-e of the layer, exact); nullptr: fp32 weights
 hipError_t launch_conv3x3_train(int C, int epi, int xe, const float* in, const float* wp, const float* resid,
                                 float* out, int M, const EpiX& ex, hipStream_t st, const ProX* px = nullptr,
-                                const FinX* fx = nullptr, const float* oscale = nullptr);
+                                const FinX* fx = nullptr, const float* oscale = nullptr, unsigned* h3ovf = nullptr);
 extern int g_train_h3;   // key 49: the train step's forward convs in split-fp16 (1) or fp32 MFMA (0)
 extern int g_tower_mode;
 extern int g_conv_shape_override;
@@ -60,6 +60,8 @@ int conv_batch_bucket(int M);
 size_t tower_sync_bytes(int nlayers, int M);
 size_t tower_prod_bytes(int nlayers, int M);
 constexpr unsigned kTowerRing = 256;          // host ring of timed-out launch numbers (power of 2)
+constexpr unsigned kTrainOvfWords = 16;       // + the train forward's split-fp16 overflow flags (same memory)
+constexpr unsigned kStatusWords = 2 * kTowerRing + kTrainOvfWords;
 constexpr int kTowerDiagWords = 64;           // device wait record (pv_tower.hip TowerDiag)
 constexpr unsigned kTowerWaitUs = 100000u;    // default awake-time bound of one dependency wait: 100 ms
                                               // (longest legitimate wait measured: 7.3 ms, two processes
@@ -167,6 +169,7 @@ struct azg_pv {
     unsigned* ring_host = nullptr;    // timed-out launch numbers [kTowerRing], pinned + mapped (kernels post, host reads)
     unsigned* ring_dev = nullptr;     // device alias of ring_host
     unsigned* ovf_host = nullptr;     // H3 launches whose activations left fp16's range [kTowerRing], same memory
+    unsigned* train_ovf_dev = nullptr;   // [kTrainOvfWords] split-fp16 train forward overflow flags (device alias)
     unsigned* ovf_dev = nullptr;
     unsigned seq = 0;                 // last tower launch number handed out (0 = none yet)
     unsigned last_seq = 0;            // the last forward's launch number (0: it ran per-layer convs)

@@ -770,7 +770,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             fx = fin_args(fin, xe == XE_STATS);
             fx.cnt = w->fincnt;
         }
-        AZG_CK(launch_conv3x3_train(C, epi, xe, in, wp, res, out, M, ex, st, nullptr, fin >= 0 ? &fx : nullptr, osc),
+        AZG_CK(launch_conv3x3_train(C, epi, xe, in, wp, res, out, M, ex, st, nullptr, fin >= 0 ? &fx : nullptr, osc,
+                                    osc ? h->train_ovf_dev : nullptr),
                "train: conv3x3");
         prof_end(h, pr, st);
         return 0;
@@ -835,7 +836,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             FinX fx = fin_args(fin, true);
             fx.cnt = w->fincnt;
             AZG_CK(launch_conv3x3_train(C, EPI_RAW, XE_STATS, p.z, fwd_w(ci), nullptr, out, M, ex, st, &px,
-                                        ffin ? &fx : nullptr, fwd_s(ci)),
+                                        ffin ? &fx : nullptr, fwd_s(ci), fh3 ? h->train_ovf_dev : nullptr),
                    "train: conv3x3 (fused BN apply)");
             prof_end(h, pr, st);
             if (!ffin) return fin_fwd(fin, TRAIN_BM, ntt);

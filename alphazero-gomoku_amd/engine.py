@@ -132,8 +132,18 @@ class PolicyValueEngine:
         until clear_status()."""
         s = int(self.lib.azg_pv_status(self.h))
         if s:
+            self.check_train()
+            d = self.tower_diag()
             raise TowerFault(f"libazg_pv: {s} persistent-tower launch(es) timed out waiting for their inputs and "
-                             f"were not recomputed; their outputs are invalid ({self.tower_diag()})")
+                             f"were not recomputed; their outputs are invalid ({d})")
+
+    def check_train(self):
+        """Raise TowerFault if a split-fp16 train forward (key 49) of a step the caller has
+        synchronised with met an activation beyond fp16's range (azg_pv_train_status)."""
+        if int(self.lib.azg_pv_train_status(self.h)):
+            raise TowerFault("libazg_pv: a split-fp16 train forward met an activation beyond fp16's range "
+                             "(65504): that step's losses and gradients are not valid; set tuning key 49 = 0 "
+                             f"(fp32 MFMA train convs) to train this net ({self.tower_diag()})")
 
     def clear_status(self):
         check(self.lib.azg_pv_clear_status(self.h), self.lib)

@@ -344,6 +344,7 @@ class PyTorchModel:
         if return_tensor:
             return mean
         vals = (mean.double() if epochs == 1 else acc / float(epochs)).tolist()
+        eng.check_train()   # a split-fp16 train forward out of fp16's range raises here
         return {"policy_loss": vals[0], "value_loss": vals[1], "total_loss": vals[2]}
 
     train_step = train_batch

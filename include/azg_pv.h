@@ -238,6 +238,11 @@ int32_t azg_pv_recover(azg_pv* h, uint32_t seq, int32_t* recovered, void* stream
  * every posted launch without recomputing it and closes the per-layer breaker (key 18). */
 int32_t azg_pv_status(const azg_pv* h);
 int32_t azg_pv_clear_status(azg_pv* h);
+/* Split-fp16 train forwards (key 49) that met an activation beyond fp16's range since the
+ * last azg_pv_clear_status (a plain host load; complete for every train step the caller
+ * has synchronised with).  Such a step's losses and gradients are not valid: the Python
+ * layer raises (PyTorchModel.train_batch; pipelined callers check Engine.check_train). */
+int32_t azg_pv_train_status(const azg_pv* h);
 
 /* Self-describing record of the tower's waits since the last azg_pv_tower_diag_clear
  * (device counters + the first timed-out wait; synchronises `stream`).  Times are
@@ -272,7 +277,10 @@ typedef struct {
     uint32_t breaker_launches;  /* forwards run per layer while the breaker was open */
     uint32_t h3_overflows;      /* split-fp16 forwards recomputed with fp32 MFMA (key 19: an activation
                                    beyond fp16's range, 65504) */
-    uint32_t reserved[4];
+    uint32_t train_h3_overflows;   /* split-fp16 train forwards that met an activation beyond fp16's range
+                                      (key 49; that step's results are not finite: azg_pv_status counts it,
+                                      the Python layer raises, azg_pv_clear_status resets it) */
+    uint32_t reserved[3];
 } azg_pv_tower_diag;
 int32_t azg_pv_tower_diag_read(azg_pv* h, azg_pv_tower_diag* out, void* stream);
 int32_t azg_pv_tower_diag_clear(azg_pv* h, void* stream);

@@ -367,12 +367,14 @@ def test_train_schedule_keys_bitwise(key, values):
         lib.azg_pv_set_tuning(key, prev)
 
 
-@pytest.mark.parametrize("key,value", [(27, 16), (27, 64)])
+@pytest.mark.parametrize("key,value", [(27, 16), (27, 64), (49, 0), (49, 1)])
 @pytest.mark.parametrize("tag,blocks,ch,B", [("6x128", 6, 128, 128), ("3x64", 3, 64, 37)])
 def test_train_sum_order_variants_match_oracle(key, value, tag, blocks, ch, B):
-    """The weight-grad split count (key 27) changes an fp32 summation order: it holds
-    the oracle tolerance of test_gradients_match_oracle (no bitwise test); 64 splits are
-    the largest slab the workspace holds."""
+    """The weight-grad split count (key 27) changes an fp32 summation order, and key 49 = 0 / 1
+    runs the forward convs in fp32 MFMA / three split-fp16 products instead of the default
+    four: each holds the
+    oracle tolerance of test_gradients_match_oracle (no bitwise test); 64 splits are the
+    largest slab the workspace holds."""
     import _native
     lib = _native.load_library()
     prev = lib.azg_pv_set_tuning(key, value)
@@ -380,3 +382,30 @@ def test_train_sum_order_variants_match_oracle(key, value, tag, blocks, ch, B):
         test_gradients_match_oracle(tag, blocks, ch, B)
     finally:
         lib.azg_pv_set_tuning(key, prev)
+
+
+def test_train_h3_range_overflow_raises():
+    """Split-fp16 train forward convs (key 49 = 2, the default) cannot represent a staged
+    activation at or above 65504: the epilogue flags the step (azg_pv_tower_diag
+    train_h3_overflows, counted by azg_pv_status) and train_batch raises TowerFault instead
+    of returning non-finite losses silently; key 49 = 0 trains the same net in fp32 MFMA."""
+    import _native
+    from engine import TowerFault
+    lib = _native.load_library()
+    m = make_model(2, 64, seed=5)
+    with torch.no_grad():
+        m.net.bn.weight.mul_(1e6)
+        m.net.bn.bias.add_(1e5)
+    m.engine.mark_dirty()
+    b, p = synth_positions(32, seed=91)
+    x = encode_batch(b, p)
+    pi, z = synth_targets(32, seed=92)
+    prev = lib.azg_pv_set_tuning(49, 2)
+    try:
+        with pytest.raises(TowerFault, match="key 49"):
+            m.train_batch(x, pi, z)
+        assert m.engine.tower_diag()["train_h3_overflows"] >= 1 and lib.azg_pv_train_status(m.engine.h) >= 1
+        m.engine.clear_status()
+        assert lib.azg_pv_status(m.engine.h) == 0 and lib.azg_pv_train_status(m.engine.h) == 0
+    finally:
+        lib.azg_pv_set_tuning(49, prev)
