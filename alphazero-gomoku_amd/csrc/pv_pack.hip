@@ -155,35 +155,54 @@ hipError_t launch_repack_all(const float* params, const int64_t* conv_offs, int 
 static inline int nblk(int total) { int b = (total + 255) / 256; return b > 4096 ? 4096 : b; }
 
 // ---- split-fp16 (H3) eval weights (pv_halo.h halo_tile VAR bit 64) ----
-// exps[l] = 14 - floor(log2 max|w_l|): max|w_l| * 2^e < 2^15, so hi = fp16(w 2^e) never
+// e_l = 14 - floor(log2 max|w_l|): max|w_l| * 2^e < 2^15, so hi = fp16(w 2^e) never
 // overflows and the lo parts of every weight above 2^-10 of the layer's largest stay
-// normal fp16 (the rest carry 2^-25 absolute error)
-__global__ __launch_bounds__(256) void h3_exp_kernel(const float* __restrict__ params, const int64_t* __restrict__ offs,
-                                                     int C, int* __restrict__ exps)
+// normal fp16 (the rest carry 2^-25 absolute error).  The max runs on H3_MAXB workgroups
+// per layer (float4 loads, one atomicMax on the bits of a non-negative float: their
+// order is the floats' order); exps[l] holds those bits until scale_h3_kernel turns them
+// into e_l (the train step re-packs every step: one workgroup per layer took 90 us).
+constexpr int H3_MAXB = 32;
+__device__ __forceinline__ int h3_exp_of(unsigned maxbits)
+{
+    const float m = __uint_as_float(maxbits);
+    return m > 0.f ? 14 - ilogbf(m) : 0;
+}
+__global__ __launch_bounds__(256) void h3_max_kernel(const float* __restrict__ params, const int64_t* __restrict__ offs,
+                                                     int C, unsigned* __restrict__ maxbits)
 {
     __shared__ float red[256];
-    const float* w = params + offs[blockIdx.x];
+    const int l = blockIdx.y;
+    const float* wl = params + offs[l];
     float m = 0.f;
-    for (int i = threadIdx.x; i < 9 * C * C; i += 256) m = fmaxf(m, fabsf(w[i]));
+    if ((offs[l] & 3) == 0) {   // the conv weights of the parameter layout start 16-B aligned (C % 32 == 0)
+        const f32x4* w = (const f32x4*)wl;
+        for (int i = blockIdx.x * 256 + threadIdx.x; i < 9 * C * C / 4; i += H3_MAXB * 256) {
+            const f32x4 v = w[i];
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+        }
+    } else {
+        for (int i = blockIdx.x * 256 + threadIdx.x; i < 9 * C * C; i += H3_MAXB * 256) m = fmaxf(m, fabsf(wl[i]));
+    }
     red[threadIdx.x] = m;
     __syncthreads();
     for (int o = 128; o > 0; o >>= 1) {
         if ((int)threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
         __syncthreads();
     }
-    if (threadIdx.x == 0) exps[blockIdx.x] = red[0] > 0.f ? 14 - ilogbf(red[0]) : 0;
+    if (threadIdx.x == 0) atomicMax(maxbits + l, __float_as_uint(red[0]));
 }
 
 // packed row (kc * C + n) of 32 K values -> 64 halves [hi 32 | lo 32] of w * 2^e, in
 // the fp32 packing's order (repack_all_kernel)
 __global__ __launch_bounds__(256) void pack_h3_kernel(const float* __restrict__ params, const int64_t* __restrict__ offs,
-                                                      int C, const int* __restrict__ exps, _Float16* __restrict__ out)
+                                                      int C, const unsigned* __restrict__ maxbits,
+                                                      _Float16* __restrict__ out)
 {
     const int total = 9 * C * C, cg_n = C / 32;
     const int l = blockIdx.y;
     const float* w = params + offs[l];
     _Float16* o = out + (size_t)l * 2 * total;
-    const float sc = ldexpf(1.f, exps[l]);
+    const float sc = ldexpf(1.f, h3_exp_of(maxbits[l]));
     for (int idx = blockIdx.x * 256 + threadIdx.x; idx < total; idx += gridDim.x * 256) {
         const int k = idx & 31, n = (idx >> 5) % C, kc = idx / (32 * C);
         const int tap = kc / cg_n, c2 = (kc - tap * cg_n) * 32 + k;
@@ -196,27 +215,34 @@ __global__ __launch_bounds__(256) void pack_h3_kernel(const float* __restrict__ 
 }
 
 // scale16 = the eval BN scale of every residual conv's BN times 2^-e (exact); inv (train
-// forward, optional) = 2^-e per layer and output channel: the raw conv output's factor
+// forward, optional) = 2^-e per layer and output channel: the raw conv output's factor;
+// exps[l] <- e_l (it held the max bits)
 __global__ void scale_h3_kernel(const float* __restrict__ scale, const int* __restrict__ conv_bn_off,
-                                const int* __restrict__ exps, int C, float* __restrict__ scale16,
+                                int* __restrict__ exps, int C, float* __restrict__ scale16,
                                 float* __restrict__ inv)
 {
     const int l = blockIdx.x, o = conv_bn_off[l];
-    const float f = ldexpf(1.f, -exps[l]);
+    const int e = h3_exp_of((unsigned)exps[l]);
+    __syncthreads();   // every thread has read the bits before thread 0 replaces them
+    const float f = ldexpf(1.f, -e);
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
         scale16[o + c] = scale[o + c] * f;
         if (inv) inv[l * C + c] = f;
     }
+    if (threadIdx.x == 0) exps[l] = e;
 }
 
 hipError_t launch_pack_h3(const float* params, const int64_t* offs, int nl, int C, const int* conv_bn_off,
                           const float* scale, int* exps, void* wp16, float* scale16, float* inv, hipStream_t st)
 {
     if (nl <= 0) return hipSuccess;
-    hipLaunchKernelGGL(h3_exp_kernel, dim3(nl), dim3(256), 0, st, params, offs, C, exps);
+    hipError_t e = hipMemsetAsync(exps, 0, (size_t)nl * sizeof(int), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(h3_max_kernel, dim3(H3_MAXB, nl), dim3(256), 0, st, params, offs, C, (unsigned*)exps);
     int nb = nblk(9 * C * C);
     nb = nb > 256 ? 256 : nb;
-    hipLaunchKernelGGL(pack_h3_kernel, dim3(nb, nl), dim3(256), 0, st, params, offs, C, exps, (_Float16*)wp16);
+    hipLaunchKernelGGL(pack_h3_kernel, dim3(nb, nl), dim3(256), 0, st, params, offs, C, (const unsigned*)exps,
+                       (_Float16*)wp16);
     hipLaunchKernelGGL(scale_h3_kernel, dim3(nl), dim3(256), 0, st, scale, conv_bn_off, exps, C, scale16, inv);
     return hipGetLastError();
 }

@@ -318,10 +318,12 @@ def roofline_from_profile(prof, boards, blocks, ch, knames, traffic=True):
     pref = TOWER_CLASSES[dom][1]
     if traffic and pref:
         net = f"{blocks}x{ch}_B"
-        h3 = peak == PEAK_H3   # the split-fp16 towers (halo_tile VAR 98) have their own records
+        h3 = peak == PEAK_H3   # the split-fp16 towers (halo_tile VAR 99; 98 before round 5's end) have their own records
         recs = [r for r in traffic_records() if r.get("kernel") == "tower" and r.get("config", "").startswith(net)
                 and r.get("shape", "").startswith(pref) and (dom != "tower" or "16>" not in r["shape"])
-                and any(f", {v}, 0>" in r["shape"] for v in ((98,) if h3 else (16, 32, 33)))]
+                and any(f", {v}, 0>" in r["shape"] for v in ((99, 98) if h3 else (16, 32, 33)))]
+        if h3 and any(", 99, 0>" in r["shape"] for r in recs):   # the current body's record first
+            recs = [r for r in recs if ", 99, 0>" in r["shape"]]
         if recs:
             bpl = d["boards_per_launch"]
             r = min(recs, key=lambda r: abs(r["boards_per_launch"] - bpl))
@@ -344,7 +346,7 @@ def tower_knames(ch, blocks):
     n = 2 * blocks
     return {"tower16": f"azg::conv_tower<{ch},128,4,1,16,16> (persistent residual tower, 16-wave 128x128 tiles, one "
                        f"workgroup per CU: {n} fused 3x3 conv + BN (+ residual) + ReLU layers per launch)",
-            "tower": (f"azg::conv_tower<{ch},64,*,{97 if ch >= 256 else 96}> (persistent residual tower, 128x64 / 64x64 "
+            "tower": (f"azg::conv_tower<{ch},64,*,99> (persistent residual tower, 128x64 / 64x64 "
                       f"tiles, split-fp16 products, acquire hand-off: {n} fused 3x3 conv + BN (+ residual) + ReLU layers "
                       f"per launch)" if conv_peak()[0] == PEAK_H3 else
                       f"azg::conv_tower<{ch},64,*,{33 if ch >= 256 else 32}> (persistent residual tower, 128x64 / 64x64 "

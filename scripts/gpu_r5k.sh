@@ -1,6 +1,17 @@
 #!/bin/bash
+# Round 5 final-tree evidence: PMC traffic of the VAR 99 towers, then rocprofv3 kernel traces
+# of the headline self-play leg, the configs[1] forward leg and one train run
+# -> python scripts/summarize_pmc_r3.py gpurun_out/pmc_r5b r5b ; python scripts/summarize_r3.py gpurun_out/r5k gpurun_out/r5k/train r5
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/r5k
-mkdir -p $O
-AZG_TUNE_LOG=1 timeout -k 10 600 python -u bench.py --no-cpu-baseline --train-steps 0 --big-steps 0 --pente-moves 0 > $O/bench.json 2> $O/bench.err
+mkdir -p $O/sp $O/fwd $O/train
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+OUT=gpurun_out/pmc_r5b timeout -k 10 600 bash scripts/gpu_pmc_r5.sh > $O/pmc.log 2>&1
+s=$?; echo "pmc rc $s"; [ $s -eq 0 ] || exit $s
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $O/sp/trace -o run -- python3 bench.py --skip-forward --no-cpu-baseline --train-steps 0 --big-steps 0 > $O/sp/bench.json 2> $O/sp/bench.err
+s=$?; echo "sp trace rc $s"; [ $s -eq 0 ] || exit $s
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d $O/fwd/trace -o run -- python3 bench.py --steps 20 --warmup 5 --sp-games 0 --no-cpu-baseline --train-steps 0 --big-steps 0 > $O/fwd/bench.json 2> $O/fwd/bench.err
+s=$?; echo "fwd trace rc $s"; [ $s -eq 0 ] || exit $s
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d $O/train/train_trace -o run -- python3 scripts/bench_train.py --steps 10 --cpu-steps 0 > $O/train/train.log 2>&1
+s=$?; echo "train trace rc $s"; [ $s -eq 0 ] || exit $s
+echo done

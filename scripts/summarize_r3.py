@@ -55,12 +55,13 @@ def main():
     shutil.copy(os.path.join(fw_dir, "run_kernel_stats.csv"), os.path.join(PROF, f"{tag}_forward_kernel_stats.csv"))
     bench = json.loads(open(os.path.join(root, "sp", "bench.json")).read().strip().splitlines()[-1])
     sp, det, roof = bench["selfplay"], bench["selfplay"]["detail"], bench["roofline"]
+    peak = roof.get("peak", PEAK / 1e12) * 1e12   # the instruction's roofline (split-fp16: F16 peak / 3)
     by = window(rows(os.path.join(sp_dir, "run_kernel_trace.csv")), sp["seconds"],
                 ("conv_tower<128", "conv3x3_halo<128"))
     L = [f"# rocprofv3 evidence, {tag}", "",
          "## Headline: configs[2] self-play to game end", "",
          f"`rocprofv3 --kernel-trace --stats -- python3 bench.py --skip-forward --no-cpu-baseline --train-steps 0 "
-         f"--big-steps 0` (scripts/gpu_r3c.sh): {bench['value']:.0f} leaf boards/s over {sp['seconds']:.1f} s, "
+         f"--big-steps 0` (scripts/gpu_{tag}k.sh): {bench['value']:.0f} leaf boards/s over {sp['seconds']:.1f} s, "
          f"{sp['rounds']} move rounds, games {det['game_length_rank0']} moves long, mean leaf batch "
          f"{det['mean_batch_rank0']}.", "",
          f"Residual-conv launches inside the timed window (the last {sp['seconds']:.1f} s of the trace; the "
@@ -77,7 +78,7 @@ def main():
           f"* Dominant kernel, the persistent tower: rocprofv3 {tn} launches, {tms:.1f} ms; the bench's own hipEvents "
           f"on the tower's stream: {ev_n} launches, {ev_ms:.1f} ms ({(tms - ev_ms) / ev_ms * 100:+.2f} %).",
           f"* Its roofline from the rocprofv3 time: {flop / 1e12:.1f} TFLOP / {tms / 1e3:.3f} s = "
-          f"{flop / (tms / 1e3) / 1e12:.2f} TFLOP/s = {flop / (tms / 1e3) / PEAK * 100:.2f} % of 157.3 "
+          f"{flop / (tms / 1e3) / 1e12:.2f} TFLOP/s = {flop / (tms / 1e3) / peak * 100:.2f} % of {peak / 1e12:.1f} "
           f"(JSON `roofline.frac` {roof['frac'] * 100:.2f} %, from hipEvents).",
           f"* GPU busy {det['gpu_busy_share_rank0'] * 100:.1f} % of the wall time.", ""]
     # forward leg
@@ -90,7 +91,7 @@ def main():
         f512 = conv_flop(128) * 12 * 512
         L += ["## configs[1] forward, B = 512 (bench `forward_b512`)", "",
               f"* `{ft[-1]['Kernel_Name'].split('(')[0]}`: {len(ft)} timed launches, {us:.1f} us average = "
-              f"{f512 / (us * 1e-6) / 1e12:.2f} TFLOP/s = {f512 / (us * 1e-6) / PEAK * 100:.2f} % of peak "
+              f"{f512 / (us * 1e-6) / 1e12:.2f} TFLOP/s = {f512 / (us * 1e-6) / peak * 100:.2f} % of peak "
               f"(JSON: {fb['roofline']['avg_launch_us']} us, {fb['roofline']['frac'] * 100:.2f} %); "
               f"{fb['boards_per_s']:.0f} boards/s for the whole forward.", ""]
     # PMC records
