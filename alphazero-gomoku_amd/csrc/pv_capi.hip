@@ -688,7 +688,8 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
     if (h->NB == 0 || h->NB > kTowerMaxBlocks) return 0;
     if ((size_t)batch * PADPIX * h->C * sizeof(float) >= (size_t)INT32_MAX) return 0;
     if (g_tower_mode == 0) return 0;
-    if (g_tower_mode == 1) return (g_tower_shape == 10 && (h->C != 128 || h3)) ? 8 : g_tower_shape;
+    if (g_tower_mode == 1)
+        return ((g_tower_shape == 10 && (h->C != 128 || h3)) || (g_tower_shape == 12 && !h3)) ? 8 : g_tower_shape;
     const int bucket = conv_batch_bucket(batch * PIX);
     static std::map<std::tuple<int, int, int, int>, int> cache;
     const auto key = std::make_tuple(h->C, h->NB, bucket, (int)h3);
@@ -699,9 +700,10 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
     if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return fallback;
     const bool prof = h->prof_on;
     h->prof_on = false;
-    const int cand[3] = {0, 5, 8};
-    const int ncand = 3;
-    float best_ms[3] = {1e30f, 1e30f, 1e30f};
+    // split-fp16: + shape 12, the h3_tile 128x128 tower (pv_h3.h)
+    const int cand[4] = {0, 5, 8, 12};
+    const int ncand = h3 ? 4 : 3;
+    float best_ms[4] = {1e30f, 1e30f, 1e30f, 1e30f};
     hipEvent_t e0, e1;
     int choice = fallback;
     if (hipEventCreate(&e0) == hipSuccess) {
@@ -721,11 +723,13 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
                 for (int c = 1; c < ncand; ++c)
                     if (best_ms[c] < best_ms[b]) b = c;
                 if (batch >= 128 && best_ms[2] <= 1.02f * best_ms[b]) b = 2;   // the 128x64 tower
+                if (h3 && batch >= 128 && best_ms[3] < 0.98f * best_ms[b]) b = 3;   // unless h3_tile beats it by 2 %
                 choice = cand[b];
             }
             if (getenv("AZG_TUNE_LOG"))
-                fprintf(stderr, "[azg tune] C=%d NB=%d batch=%d h3=%d ok=%d per-layer %.4f tower64 %.4f tower128 %.4f -> %d\n",
-                        h->C, h->NB, batch, (int)h3, (int)ok, best_ms[0], best_ms[1], best_ms[2], choice);
+                fprintf(stderr, "[azg tune] C=%d NB=%d batch=%d h3=%d ok=%d per-layer %.4f tower64 %.4f tower128 %.4f "
+                        "h3tile %.4f -> %d\n", h->C, h->NB, batch, (int)h3, (int)ok, best_ms[0], best_ms[1], best_ms[2],
+                        best_ms[3], choice);
             (void)hipEventDestroy(e1);
         }
         (void)hipEventDestroy(e0);

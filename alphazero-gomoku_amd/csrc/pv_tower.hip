@@ -38,6 +38,7 @@
 // rows whose readers are exactly (or transitively) the tiles it waits on.
 #include "pv_internal.h"
 #include "pv_halo.h"
+#include "pv_h3.h"
 
 namespace azg {
 
@@ -85,10 +86,19 @@ constexpr int tower_min_waves() { return NW_ >= 16 ? 4 : BN_ >= 128 ? 2 : 4; }
 // dynamic LDS of a tower launch: the 16-wave tile asks for more than half of the CU's
 // 160 KiB so that one workgroup per CU is guaranteed by LDS alone (the sc1-load
 // hand-off is valid only there), whatever the register allocation
+// VAR bit 256: the tile body is h3_tile (pv_h3.h: split-fp16, LDS-DMA weight stages of one
+// tap, three stage buffers), else halo_tile
+constexpr int kH3TileTps = 1, kH3TileNwb = 3;
+template <int C, int BN, int WM, int TM, int NW, int VAR>
+constexpr int tower_body_lds()
+{
+    if constexpr ((VAR & 256) != 0) return H3Tile<C, BN, WM, TM, NW, kH3TileTps, kH3TileNwb>::LDS;
+    else return halo_lds_bytes<C, BN, WM, TM, NW, VAR & 255>();
+}
 template <int C, int BN, int WM, int TM, int NW, int VAR>
 constexpr int tower_lds_bytes()
 {
-    constexpr int need = halo_lds_bytes<C, BN, WM, TM, NW, VAR>() + 16;
+    constexpr int need = tower_body_lds<C, BN, WM, TM, NW, VAR>() + 16;
     return NW >= 16 && need <= 82 * 1024 ? 82 * 1024 : need;
 }
 
@@ -209,7 +219,7 @@ __global__ __launch_bounds__(64 * NW_, (tower_min_waves<BN_, NW_>())) void conv_
     using T = ConvTile<C, BN_, WM_, TM_, NW_>;
     static_assert(!((VAR & 48) && (VAR & 12)), "buffer halo / residual loads (VAR 16, 32) exclude LDS-DMA (4) and early epilogue loads (8)");
     constexpr int NTN = C / T::BN;
-    constexpr int LDS_FLOATS = halo_lds_bytes<C, BN_, WM_, TM_, NW_, VAR>() / 4;
+    constexpr int LDS_FLOATS = tower_body_lds<C, BN_, WM_, TM_, NW_, VAR>() / 4;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     int* s_claim = (int*)(smem + LDS_FLOATS);
 
@@ -269,9 +279,14 @@ __global__ __launch_bounds__(64 * NW_, (tower_min_waves<BN_, NW_>())) void conv_
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Ly.out, (short)0, a.act_bytes, 0x00020000);
         for (int nt = nt0; nt < nt0 + grp; ++nt) {
             if (nt > nt0) __syncthreads();        // the previous tile's epilogue is done with LDS
-            halo_tile<C, BN_, WM_, TM_, NW_, EPI_BN_OPTRES_RELU, true, HABL, VAR>(
-                Ly.in, Ly.wp, Ly.scale, Ly.shift, Ly.resid, Ly.out, rs, a.M, mt * T::BM, nt * T::BN, smem, EpiX{},
-                ProX{}, FinX{}, H3Guard{a.ring_ovf, a.seq});
+            if constexpr ((VAR & 256) != 0)
+                h3_tile<C, BN_, WM_, TM_, NW_, kH3TileTps, kH3TileNwb, EPI_BN_OPTRES_RELU, true, 1>(
+                    Ly.in, Ly.wp, Ly.scale, Ly.shift, Ly.resid, Ly.out, rs, a.M, mt * T::BM, nt * T::BN, smem,
+                    H3Guard{a.ring_ovf, a.seq});
+            else
+                halo_tile<C, BN_, WM_, TM_, NW_, EPI_BN_OPTRES_RELU, true, HABL, VAR>(
+                    Ly.in, Ly.wp, Ly.scale, Ly.shift, Ly.resid, Ly.out, rs, a.M, mt * T::BM, nt * T::BN, smem, EpiX{},
+                    ProX{}, FinX{}, H3Guard{a.ring_ovf, a.seq});
         }
         if (!(a.abl & 2)) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
@@ -359,6 +374,7 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
     a.limit = g_tower_wait_us >= 0xffffffffu / 100u ? 0xffffffffu : g_tower_wait_us * 100u;
     unsigned* sync = ts.sync;
     a.group = g_tower_group ? C / (shape == 8 || shape == 5 ? 64 : 128) : 1;
+    if (shape == 12 && !h3) return hipErrorInvalidValue;   // h3_tile: split-fp16 only
 #ifndef AZG_AB_STUDIES
     if (shape == 10 && C != 128) return hipErrorInvalidValue;   // 16-wave tile: C = 128 only (C = 256 spills)
 #endif
@@ -387,6 +403,12 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
         // at board-row ends (32 % of its LDS cycles; scripts/h3_tune_study.py,
         // profiles/r5_h3_study.md); bitwise equal to every other form.  Key 20 = 0: VAR 98.
         const bool vs = g_h3_tower_var == 1;
+        // shape 12: h3_tile 128x128, 4 waves of 64x64 (VAR 355 = 99 | 256), bitwise equal
+        if (shape == 12) {
+            if (C == 128) return launch_tower_t<128, 128, 2, 2, 4, 355>(a, st, nullptr);
+            if (C == 256) return launch_tower_t<256, 128, 2, 2, 4, 355>(a, st, nullptr);
+            return hipErrorInvalidValue;
+        }
         switch (C) {
             case 128:
                 if (shape == 5) return vs ? launch_tower_t<128, 64, 2, 1, 4, 99>(a, st, nullptr)

@@ -36,7 +36,7 @@ def main():
     bench.pretrain(m, dev)
     eng = m.engine
     flop_per_board = 2 * 225 * ch * 9 * ch * 2 * nb
-    forms = [("per-layer", 0, 8), ("tower64x64", 1, 5), ("tower128x64", 1, 8)]
+    forms = [("per-layer", 0, 8), ("tower64x64", 1, 5), ("tower128x64", 1, 8), ("tower128x128h3tile", 1, 12)]
     for B in (int(b) for b in args.batches.split(",")):
         x = torch.from_numpy(synth_encoded(B, seed=B)).to(dev)
         best, ref = {}, None

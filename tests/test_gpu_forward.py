@@ -230,7 +230,7 @@ def test_persistent_tower_bitwise_equals_per_layer_launches(blocks, ch, batches)
             lib.azg_pv_set_tuning(5, 0)
             p0, v0, l0 = eng.forward(x, want_logits=True)
             lib.azg_pv_set_tuning(5, 1)
-            for shape in ((5, 8, 10) if ch == 128 else (5, 8)):
+            for shape in ((5, 8, 10, 12) if ch == 128 else (5, 8, 12)):   # 12: h3_tile (split-fp16 only)
                 lib.azg_pv_set_tuning(6, shape)
                 for group in (0, 1):   # claims (key 17): one tile, one M tile
                     prev_group = lib.azg_pv_set_tuning(17, group)
@@ -306,7 +306,7 @@ def test_persistent_tower_under_concurrent_load():
         lib.azg_pv_set_tuning(5, 1)
         s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
         torch.cuda.synchronize()
-        for shape in (8, 10, 5):
+        for shape in (8, 10, 5, 12):
             lib.azg_pv_set_tuning(6, shape)
             for _ in range(4):
                 with torch.cuda.stream(s1):

@@ -38,6 +38,10 @@ SCRATCH_BUDGET = [
     (r"conv_towerILi256ELi64ELi4ELi1ELi8ELi99E", 16),
     (r"conv_towerILi(128|256)ELi64ELi2ELi1ELi4ELi99E", 80),
     (r"conv_towerILi(128|256)ELi64ELi(2|4)ELi1ELi(4|8)ELi98E", 16),
+    # h3_tile towers (VAR 355, shape 12: 4 waves of 64x64 at 256 VGPRs): spills outside the
+    # chunk loop only (tower claim / epilogue)
+    (r"conv_towerILi128ELi128ELi2ELi2ELi4ELi355E", 176),
+    (r"conv_towerILi256ELi128ELi2ELi2ELi4ELi355E", 272),
     (r"conv3x3_haloILi(128|256)ELi64ELi(2|4)ELi1ELi(4|8)ELi[01]ELi0ELi99E", 0),
     (r"conv_towerILi64ELi64E", 0),
     (r"conv_towerILi128ELi128ELi4ELi1ELi16E", 48),
