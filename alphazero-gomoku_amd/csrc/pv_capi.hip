@@ -620,7 +620,7 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
             out_off[2 * i] = bd[h->bn_blk[i].first].out_off;
             out_off[2 * i + 1] = bd[h->bn_blk[i].second].out_off;
         }
-        pr = prof_begin(h, variant == 10 ? AZG_PROF_TOWER_WIDE : AZG_PROF_TOWER, st, batch);
+        pr = prof_begin(h, variant == 10 || variant == 12 ? AZG_PROF_TOWER_WIDE : AZG_PROF_TOWER, st, batch);
         const TowerSync ts{h->tower_sync, h->ring_dev, h->ovf_dev, h->tower_diag, h->tower_prod, seq};
         AZG_TRY(launch_tower(C, h->NB, variant, h->act, h3 ? (const float*)h->wpack16 : h->wpack,
                              h3 ? h->scale16 : h->scale, h->shift, out_off, M, ts, st, &X, h3),

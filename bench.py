@@ -316,13 +316,16 @@ def roofline_from_profile(prof, boards, blocks, ch, knames, traffic=True):
         out["frac_of_fp32_mfma_peak"] = round(achieved / PEAK_F32_MFMA, 4)
     out.update({k: v for k, v in d.items() if not k.startswith("_") and k != "frac"})
     pref = TOWER_CLASSES[dom][1]
+    h3 = peak == PEAK_H3
+    if h3 and dom == "tower16":   # split-fp16: class 7 is the h3_tile 128x128 tower (shape 12, VAR 355)
+        pref = f"conv_tower<{ch}, 128, 2, 2, 4, 355"
     if traffic and pref:
         net = f"{blocks}x{ch}_B"
-        h3 = peak == PEAK_H3   # the split-fp16 towers (halo_tile VAR 99; 98 before round 5's end) have their own records
+        # the split-fp16 128x64 towers: halo_tile VAR 99 (98 before round 5's end); h3_tile VAR 355
         recs = [r for r in traffic_records() if r.get("kernel") == "tower" and r.get("config", "").startswith(net)
                 and r.get("shape", "").startswith(pref) and (dom != "tower" or "16>" not in r["shape"])
-                and any(f", {v}, 0>" in r["shape"] for v in ((99, 98) if h3 else (16, 32, 33)))]
-        if h3 and any(", 99, 0>" in r["shape"] for r in recs):   # the current body's record first
+                and any(f", {v}, 0>" in r["shape"] for v in ((99, 98, 355) if h3 else (16, 32, 33)))]
+        if h3 and dom == "tower" and any(", 99, 0>" in r["shape"] for r in recs):   # the current body's record first
             recs = [r for r in recs if ", 99, 0>" in r["shape"]]
         if recs:
             bpl = d["boards_per_launch"]
@@ -344,8 +347,11 @@ def roofline_from_profile(prof, boards, blocks, ch, knames, traffic=True):
 
 def tower_knames(ch, blocks):
     n = 2 * blocks
-    return {"tower16": f"azg::conv_tower<{ch},128,4,1,16,16> (persistent residual tower, 16-wave 128x128 tiles, one "
-                       f"workgroup per CU: {n} fused 3x3 conv + BN (+ residual) + ReLU layers per launch)",
+    return {"tower16": (f"azg::conv_tower<{ch},128,2,2,4,355> (persistent residual tower, h3_tile 128x128 tiles: 4 "
+                        f"waves of 64x64, split-fp16 products, LDS-DMA weight stages: {n} fused 3x3 conv + BN "
+                        f"(+ residual) + ReLU layers per launch)" if conv_peak()[0] == PEAK_H3 else
+                        f"azg::conv_tower<{ch},128,4,1,16,16> (persistent residual tower, 16-wave 128x128 tiles, one "
+                        f"workgroup per CU: {n} fused 3x3 conv + BN (+ residual) + ReLU layers per launch)"),
             "tower": (f"azg::conv_tower<{ch},64,*,99> (persistent residual tower, 128x64 / 64x64 "
                       f"tiles, split-fp16 products, acquire hand-off: {n} fused 3x3 conv + BN (+ residual) + ReLU layers "
                       f"per launch)" if conv_peak()[0] == PEAK_H3 else

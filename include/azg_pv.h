@@ -132,7 +132,8 @@ enum {
     AZG_PROF_TRAIN_OTHER = 5,
     AZG_PROF_TOWER = 6,      /* persistent residual tower (all 2*NB convs, one launch),
                                 64x64 / 128x64 tiles, 2-4 workgroups per CU          */
-    AZG_PROF_TOWER_WIDE = 7, /* the same with 16-wave 128x128 tiles, 1 workgroup per CU */
+    AZG_PROF_TOWER_WIDE = 7, /* the same with 128x128 tiles: 16 waves, 1 workgroup per CU
+                                (fp32), or h3_tile's 4 waves of 64x64 (split-fp16, shape 12) */
     AZG_PROF_NCLASS = 8
 };
 int32_t azg_pv_profile_enable(azg_pv* h, int32_t enable);
@@ -154,7 +155,9 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          (shape from key 6), 2 (default) chosen per (C, blocks, batch bucket) by
  *          timing every variant on first use -- all bitwise identical;
  *   key 6: persistent-tower tile shape for key 5 = 1 (8: 128x64 / 8 waves, default;
- *          5: 64x64 / 4 waves; 10: 128x128 / 16 waves, one workgroup per CU, C = 128);
+ *          5: 64x64 / 4 waves; 10: 128x128 / 16 waves, one workgroup per CU, C = 128, fp32
+ *          only; 12: h3_tile 128x128 / 4 waves of 64x64, split-fp16 only -- a shape the
+ *          current arithmetic lacks runs as 8);
  *   keys 3, 7, 8: timing-only ablation switches (results invalid while set);
  *   key 10: tile-body variant of the C=128 128x64 persistent tower (0 = default;
  *          1..5 = swizzle / prefetch / LDS-DMA staging variants for A/B timing, all
@@ -201,6 +204,10 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          always uses fp32 MFMA;
  *   key 20: the split-fp16 tower's tile body (1 = halo rows keyed on the board position,
  *          conflict-free fragment reads, default; 0 = row-keyed); bitwise identical;
+ *   key 49: train-step forward convs: 2 (default) split-fp16 with all four hi / lo products
+ *          (~2^-33 per product: the two-step goldens hold), 1 three products, 0 fp32 MFMA;
+ *          the dgrad convs and weight grads stay fp32; a staged activation beyond fp16's
+ *          range flags the step (azg_pv_train_status);
  *   key 48: train weight-grad tile (1 = padded-row table, buffer LDS-DMA, slabs in the
  *          MFMA layout, default; 0 = round-4 form); bitwise identical;
  *   key 18: seconds a handle runs per-layer convs after azg_pv_recover recomputed one

@@ -19,4 +19,4 @@ run() {   # tag, probe args
 mkdir -p $OUT/t_b3456 $OUT/t_b512 $OUT/t_256_b512
 run t_b3456 --batch 3456 --tower 1 --tower-shape ${SHAPE_128:-8} || exit 1
 run t_b512 --batch 512 --tower 1 --tower-shape ${SHAPE_128:-8} || exit 1
-run t_256_b512 --batch 512 --tower 1 --tower-shape 8 --blocks 10 --channels 256 || exit 1
+run t_256_b512 --batch 512 --tower 1 --tower-shape ${SHAPE_256:-8} --blocks 10 --channels 256 || exit 1
