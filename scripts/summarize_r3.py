@@ -95,7 +95,8 @@ def main():
               f"(JSON: {fb['roofline']['avg_launch_us']} us, {fb['roofline']['frac'] * 100:.2f} %); "
               f"{fb['boards_per_s']:.0f} boards/s for the whole forward.", ""]
     # PMC records
-    recs = [r for r in json.load(open(os.path.join(PROF, "conv_traffic.json")))["records"] if r.get("tag") == tag]
+    recs = [r for r in json.load(open(os.path.join(PROF, "conv_traffic.json")))["records"]
+            if r.get("tag") == tag or (len(r.get("tag", "")) == len(tag) + 1 and r["tag"].startswith(tag))]
     if recs:
         L += ["## HBM traffic of the tower (PMC, scripts/gpu_pmc_r3.sh; FETCH_SIZE x2 + WRITE_SIZE)", "",
               "| kernel | config | HBM MB / launch | algorithmic MB | ratio | SQ MFMA busy |", "|---|---|---|---|---|---|"]
