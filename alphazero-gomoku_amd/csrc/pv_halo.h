@@ -10,6 +10,9 @@
 #pragma once
 #include "pv_common.h"
 
+#ifndef AZG_EVAL_REMAT
+#define AZG_EVAL_REMAT 1
+#endif
 namespace azg {
 
 // Tile shape: BM = WM*TM*32 pixels x BN channels; NW waves as WM x WN (WN = NW/WM),
@@ -995,9 +998,12 @@ __device__ __forceinline__ void halo_tile(
             // keep the next chunk's global loads at the top of the chunk: without this
             // fence hipcc sinks them to just before their vmcnt wait (latency exposed)
             __builtin_amdgcn_sched_barrier(0);
-            // H3: the fragment addresses of each tap are built at the tap (a few VALU ops)
+            // the fragment addresses of each tap are built at the tap (a few VALU ops)
             // instead of 9 taps x 4 addresses hoisted and kept live across the groups
-            if constexpr (H3) {
+            // (round 5: that hoisting was every tower's spill -- 32-336 B/lane -- and cost
+            // the split-fp16 per-layer tile its second workgroup per CU).  Not in the fp32
+            // train convs (XE epilogues): +50 us per step there, measured.
+            if constexpr (H3 || (XE == XE_NONE && AZG_EVAL_REMAT)) {
 #pragma unroll
                 for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(hrow[i]), "+v"(vpix[i]));
             }
