@@ -383,13 +383,18 @@ def visit_buckets(model, top):
         model.predict_boards(z8[:b], np.ones(b, np.int8))
 
 
+SP_GROUPS = int(os.environ.get("AZG_SP_GROUPS", "2"))   # pipelined search / evaluate groups
+
+
 def selfplay_run(model, game_class, G, S, max_moves, seeds, profile=True):
     """One self-play generation of G concurrent games (native search, pipelined
-    int8-board evaluator, 2 groups) -> (driver, seconds, profile, boards per class)."""
+    int8-board evaluator, SP_GROUPS groups: the host searches one while the GPU
+    evaluates the others; results are identical for any grouping) -> (driver, seconds,
+    profile, boards per class)."""
     from mcts.native_mcts import NativeSelfPlay
     sp = NativeSelfPlay(None, game_class, G, S, cpuct=SP_CPUCT, dirichlet_alpha=SP_ALPHA, epsilon=SP_EPS,
                         apply_dirichlet_n_first_moves=SP_NOISE_MOVES, evaluator_factory=model.board_evaluator,
-                        groups=2 if G > 1 else 1)
+                        groups=min(SP_GROUPS, G))
     eng = model.engine
     eng.clear_status()
     eng.tower_diag_clear()
