@@ -11,7 +11,7 @@
 #include "pv_common.h"
 
 #ifndef AZG_EVAL_REMAT
-#define AZG_EVAL_REMAT 1
+#define AZG_EVAL_REMAT 0   // study: 1 = per-tap addresses in the fp32 bodies too
 #endif
 namespace azg {
 
@@ -998,12 +998,13 @@ __device__ __forceinline__ void halo_tile(
             // keep the next chunk's global loads at the top of the chunk: without this
             // fence hipcc sinks them to just before their vmcnt wait (latency exposed)
             __builtin_amdgcn_sched_barrier(0);
-            // the fragment addresses of each tap are built at the tap (a few VALU ops)
-            // instead of 9 taps x 4 addresses hoisted and kept live across the groups
-            // (round 5: that hoisting was every tower's spill -- 32-336 B/lane -- and cost
-            // the split-fp16 per-layer tile its second workgroup per CU).  Not in the fp32
-            // train convs (XE epilogues): +50 us per step there, measured.
-            if constexpr (H3 || (XE == XE_NONE && AZG_EVAL_REMAT)) {
+            // split-fp16: the fragment addresses of each tap are built at the tap (a few
+            // VALU ops) instead of 9 taps x 4 addresses hoisted and kept live across the
+            // groups (round 5: that hoisting was the H3 towers' 96-336 B/lane of spills and
+            // cost the per-layer H3 tile its second workgroup per CU).  Not in the fp32
+            // bodies: measured slower there (fp32 tower 82.6 vs 87.2 % of peak at B = 512
+            // spill-free, the fp32 train convs +50 us per step; scripts/gpu_r5ab.sh).
+            if constexpr (H3 || AZG_EVAL_REMAT) {
 #pragma unroll
                 for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(hrow[i]), "+v"(vpix[i]));
             }
