@@ -67,6 +67,186 @@ __global__ __launch_bounds__(64 * NW_, WPE) void lab_h3(const float* __restrict_
         (t / NTN) * T::BM, (t % NTN) * T::BN, smem, guard);
 }
 
+// ---- 16x16x32 study: h3_tile's 128x128 / 4-wave body with v_mfma_f32_16x16x32_f16 (4x4 blocks
+// of 16x16 per wave: the same LDS bytes per MFMA cycle, a different K order per instruction, so
+// not bitwise the product).  Lab only: does the smaller MFMA shape run faster here?
+template <int C>
+__global__ __launch_bounds__(256, 2) void lab_h3_16(const float* __restrict__ in, const float* __restrict__ wp,
+                                                    const float* __restrict__ scale, const float* __restrict__ shift,
+                                                    const float* __restrict__ resid, float* __restrict__ out, int M)
+{
+    using H = H3Tile<C, 128, 2, 2, 4, 1, 3>;
+    constexpr int BM = 128, BN = 128, BK = 32, CG = C / 32, NW = 4, NT = 256, RPP = H::RPP, H_LD = H::H_LD,
+                  HR = H::HR, NST = 9, NSTAGE = CG * 9, PPW = H::PPW, BNP = BN / 8, NWB = 3;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int NTN = C / BN;
+    const int L = blockIdx.x, nt = gridDim.x;
+    const int xcd = L & 7, q8 = nt >> 3, r8 = nt & 7;
+    const int t = xcd * q8 + min(xcd, r8) + (L >> 3);
+    const int m0 = (t / NTN) * BM, n0 = (t % NTN) * BN;
+    float* Ah = smem;
+    float* Bs = smem + HR * BK;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid / 2, wn = wid % 2;
+    const int mlast = min(m0 + BM, M) - 1;
+    const int hbase = pad_row(m0) - (PADW + 1);
+    const int hmax = pad_row(mlast) + (PADW + 1);
+    const int sr = tid >> 3, sc = (tid & 7) * 4;
+    int hsrc[H_LD], hkey[H_LD];
+#pragma unroll
+    for (int i = 0; i < H_LD; ++i) {
+        const int r = min(hbase + sr + RPP * i, hmax);
+        hsrc[i] = (r * C + sc) * 4;
+        hkey[i] = (halo_vkey(hbase + sr + RPP * i) >> 1) & 7;
+    }
+    const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in), (short)0,
+                                                                          0x7fffffff, 0x00020000);
+    f32x4 rh[H_LD];
+    auto hload = [&](int g, int i) {
+        rh[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, hsrc[i] + g * BK * 4, 0, 0));
+    };
+    auto hstore = [&]() {
+        const int q = (tid & 7) >> 1, half = (tid & 1) * 2;
+#pragma unroll
+        for (int i = 0; i < H_LD; ++i) {
+            f16x4 hi, lo;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                hi[e] = (_Float16)rh[i][e];
+                lo[e] = (_Float16)(rh[i][e] - (float)hi[e]);
+            }
+            float* row = Ah + (sr + RPP * i) * BK;
+            *(f16x4*)(row + ((q ^ hkey[i]) * 4) + half) = hi;
+            *(f16x4*)(row + (((4 + q) ^ hkey[i]) * 4) + half) = lo;
+        }
+    };
+    const int lr = lane >> 3, ls = lane & 7;
+    int woff[PPW], wdst[PPW];
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+        const int p = wid + NW * i;
+        const int tt = p / BNP, row = (p % BNP) * 8 + lr;
+        woff[i] = tt * C * BK * CG + (n0 + row) * BK + ((ls ^ ((row >> 1) & 7)) * 4);
+        wdst[i] = (tt * BN + (p % BNP) * 8) * BK;
+    }
+    auto dma_stage = [&](int s) {
+        const int g = s / NST, t0 = s % NST;
+        const float* src = wp + (size_t)(t0 * CG + g) * C * BK;
+        float* dst = Bs + (s % NWB) * BN * BK;
+#pragma unroll
+        for (int i = 0; i < PPW; ++i)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + woff[i]),
+                                             (__attribute__((address_space(3))) void*)(dst + wdst[i]), 16, 0, 0);
+    };
+    // 16x16x32 fragments: lane -> row / col (lane & 15), K slot (lane >> 4) of the 32-channel row
+    const int r16 = lane & 15, ks = lane >> 4;
+    int hrow[4], vpix[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int pr = pad_row(min(m0 + wm * 64 + i * 16 + r16, M - 1));
+        hrow[i] = pr - hbase;
+        vpix[i] = halo_vkey(pr);
+    }
+    const int bswz = (r16 >> 1) & 7;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dma_stage(0);
+    dma_stage(1);
+#pragma unroll
+    for (int i = 0; i < H_LD; ++i) hload(0, i);
+    h3_wait_vm(0);
+    hstore();
+    h3_raw_barrier();
+#pragma unroll
+    for (int cg = 0; cg < CG; ++cg) {
+        // (one accumulation chain: timing study -- no per-group partial sums, unlike the product)
+        f32x4 (&at)[4][4] = acc;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int s = cg * 9 + tap;
+            if (s + 2 < NSTAGE) dma_stage(s + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            if (cg + 1 < CG && tap < H_LD) hload(cg + 1, tap);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(hrow[i]), "+v"(vpix[i]));
+            const int d = (tap / 3 - 1) * PADW + (tap % 3 - 1);
+            const int vd = (tap / 3 - 1) * BOARD + (tap % 3 - 1);
+            const float* Bb = Bs + (s % NWB) * BN * BK;
+            f16x8 ah[4], al[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int ar = (hrow[i] + d) * BK, aw = ((vpix[i] + vd) >> 1) & 7;
+                ah[i] = *(const f16x8*)(Ah + ar + ((ks ^ aw) * 4));
+                al[i] = *(const f16x8*)(Ah + ar + (((4 + ks) ^ aw) * 4));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float* br = Bb + (wn * 64 + j * 16 + r16) * BK;
+                const f16x8 bh = *(const f16x8*)(br + ((ks ^ bswz) * 4));
+                const f16x8 bl = *(const f16x8*)(br + (((4 + ks) ^ bswz) * 4));
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    at[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh, at[i][j], 0, 0, 0);
+                    at[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl, at[i][j], 0, 0, 0);
+                    at[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh, at[i][j], 0, 0, 0);
+                }
+            }
+            if (s + 1 < NSTAGE) h3_wait_vm(h3_wait_next<C, 128, 2, 2, 4, 1, 3, 0>(s));
+            else h3_wait_vm(0);
+            h3_raw_barrier();
+        }
+        if (cg + 1 < CG) {
+            h3_wait_vm(h3_wait_halo<C, 128, 2, 2, 4, 1, 3, 0>(cg));
+            hstore();
+            h3_raw_barrier();
+        }
+    }
+    // epilogue through LDS: [BM][BN] tile, then 16-B runs of 4 channels per thread
+    float* Es = smem;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                Es[(wm * 64 + i * 16 + 4 * ks + r) * BN + wn * 64 + j * 16 + r16] = acc[i][j][r];
+    __syncthreads();
+    constexpr int CPR = BN / 4, RPI = NT / CPR, NPASS = BM / RPI;
+    const int ec = (tid % CPR) * 4, er = tid / CPR, col = n0 + ec;
+    const f32x4 s4 = *(const f32x4*)(scale + col), t4 = *(const f32x4*)(shift + col);
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+        const int m = m0 + er + p * RPI;
+        if (m < M) {
+            f32x4 v = *(const f32x4*)(Es + (er + p * RPI) * BN + ec);
+            const int o = pad_off(m, C) + col;
+            const f32x4 rv = *(const f32x4*)(resid + o);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(fmaf(v[e], s4[e], t4[e]) + rv[e], 0.f);
+            *(f32x4*)(out + o) = v;
+        }
+    }
+}
+template <int C>
+static void launch_16(const float* in, const float* wp, const float* sc, const float* sh, const float* rs, float* out,
+                      int M, H3Guard, hipStream_t st)
+{
+    constexpr int lds = H3Tile<C, 128, 2, 2, 4, 1, 3>::LDS;
+    dim3 grid(((M + 127) / 128) * (C / 128));
+    hipLaunchKernelGGL((lab_h3_16<C>), grid, dim3(256), lds, st, in, wp, sc, sh, rs, out, M);
+}
+template <int C>
+static hipError_t prep_16()
+{
+    return hipFuncSetAttribute((const void*)lab_h3_16<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               H3Tile<C, 128, 2, 2, 4, 1, 3>::LDS);
+}
+
 struct Variant {
     std::string name;
     int C;
@@ -129,6 +309,8 @@ static std::vector<Variant> variants()
 {
     return {
         V(C, 64, 4, 1, 8, 99, 2),    // product per-layer form: 128x64, 8 waves, wave 32x32
+        Variant{"h3_tile 128x128 nw4 16x16x32 (not bitwise)", C, 128, 128,
+                (size_t)H3Tile<C, 128, 2, 2, 4, 1, 3>::LDS, launch_16<C>, prep_16<C>},
         V(C, 128, 2, 2, 4, 99, 2),   // 128x128, 4 waves as 2x2, wave 64x64
         // h3_tile (pv_h3.h): LDS-DMA weight stages, counted waits, raw barriers
         VH(C, 64, 4, 1, 8, 1, 2, 4),     // 128x64, wave 32x32, 1-tap stages
