@@ -56,7 +56,7 @@ def main():
                         eng.forward(x)
                     prof = eng.profile_read()
                     eng.profile_enable(False)
-                    ms = sum(prof[k][0] for k in ("tower", "conv3x3") if k in prof) / args.reps
+                    ms = sum(prof[k][0] for k in ("tower", "tower16", "conv3x3") if k in prof) / args.reps
                     key = f"{name}/var{v}"
                     best[key] = min(best.get(key, 1e9), ms)
         lib.azg_pv_set_tuning(20, 0)
