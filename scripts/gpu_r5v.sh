@@ -1,8 +1,7 @@
 #!/bin/bash
-# per-tap fragment addresses in every halo_tile body (fp32 towers / train convs spill-free):
-# train step, the full GPU suite, the default bench
+# final round-5 validation: train step, full GPU suite, default bench, N=2 rehearsal, smoke
 set -o pipefail
-O=gpurun_out/r5z; mkdir -p $O
+O=gpurun_out/r5v; mkdir -p $O
 timeout -k 10 200 python -u scripts/bench_train.py --steps 30 --cpu-steps 0 > $O/bt_a.log 2>&1 &&
 timeout -k 10 200 python -u scripts/bench_train.py --steps 30 --cpu-steps 0 --tune 49=0 > $O/bt_fp32.log 2>&1 &&
 timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 900 --timeout-method thread > $O/tests.log 2>&1 &&

@@ -61,7 +61,7 @@ def main():
     L = [f"# rocprofv3 evidence, {tag}", "",
          "## Headline: configs[2] self-play to game end", "",
          f"`rocprofv3 --kernel-trace --stats -- python3 bench.py --skip-forward --no-cpu-baseline --train-steps 0 "
-         f"--big-steps 0` (scripts/gpu_{tag}k.sh): {bench['value']:.0f} leaf boards/s over {sp['seconds']:.1f} s, "
+         f"--big-steps 0` (scripts/{os.environ.get('AZG_TRACE_SCRIPT', f'gpu_{tag}k.sh')}): {bench['value']:.0f} leaf boards/s over {sp['seconds']:.1f} s, "
          f"{sp['rounds']} move rounds, games {det['game_length_rank0']} moves long, mean leaf batch "
          f"{det['mean_batch_rank0']}.", "",
          f"Residual-conv launches inside the timed window (the last {sp['seconds']:.1f} s of the trace; the "
@@ -98,7 +98,7 @@ def main():
     recs = [r for r in json.load(open(os.path.join(PROF, "conv_traffic.json")))["records"]
             if r.get("tag") == tag or (len(r.get("tag", "")) == len(tag) + 1 and r["tag"].startswith(tag))]
     if recs:
-        L += ["## HBM traffic of the tower (PMC, scripts/gpu_pmc_r3.sh; FETCH_SIZE x2 + WRITE_SIZE)", "",
+        L += ["## HBM traffic of the tower (PMC, scripts/gpu_pmc_r3.sh / gpu_pmc_r5.sh; FETCH_SIZE x2 + WRITE_SIZE)", "",
               "| kernel | config | HBM MB / launch | algorithmic MB | ratio | SQ MFMA busy |", "|---|---|---|---|---|---|"]
         for r in recs:
             L.append(f"| `{r['shape']}` | {r['config']} | {r['hbm_bytes_per_launch'] / 1e6:.0f} | "
