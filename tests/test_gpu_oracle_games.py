@@ -10,7 +10,10 @@ visit or two, and a game diverges only where that changes the played move.  A
 divergence is therefore exempt only when it is explained by a near-tie: both
 searches' root visit counts at that move differ by at most TIE_VISITS per action, and
 the move was sampled (temperature > 0) or the root's top-2 visit gap is at most
-TIE_VISITS.  The exempt count is printed; any other divergence fails.
+TIE_VISITS.  Any other divergence fails, and the exempt games are gated too: at most
+MAX_EXEMPT_FRAC of a case's games may diverge, and the moves played identically before
+any divergence must be at least MIN_MATCHED_FRAC of all moves.  The
+headline case runs configs[2]'s settings: 6x128, 400 sims/move, every game to its end.
 
   * self-play: NativeSelfPlay over the HIP int8 board evaluators (train.py's path,
     reference train.py:360-412) vs NativeSelfPlay over the oracle's predict;
@@ -30,6 +33,8 @@ from conftest import golden_state, has_gpu, load_golden
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")]
 
 TIE_VISITS = 2
+MAX_EXEMPT_FRAC = 0.34
+MIN_MATCHED_FRAC = 0.6
 
 
 def _pair(tag, blocks, ch):
@@ -52,7 +57,7 @@ def _top2_gap(visits):
 
 
 def _compare(moves_h, moves_o, pis_h, pis_o, sims, sampled):
-    """(identical, exempt, max visit difference before the games part)"""
+    """(identical, exempt, max visit difference before the games part, moves matched)"""
     n = min(len(moves_h), len(moves_o))
     maxdv = 0.0
     for k in range(n):
@@ -62,14 +67,15 @@ def _compare(moves_h, moves_o, pis_h, pis_o, sims, sampled):
             tie = dv <= TIE_VISITS and (sampled(k) or min(_top2_gap(vh), _top2_gap(vo)) <= TIE_VISITS)
             assert tie, f"divergence at move {k} not explained by a near-tie: visit diff {dv}, " \
                         f"top-2 gaps {_top2_gap(vh)} / {_top2_gap(vo)}"
-            return False, True, max(maxdv, dv)
+            return False, True, max(maxdv, dv), k
         maxdv = max(maxdv, dv)
     assert len(moves_h) == len(moves_o), "one game ended before the other without a divergence"
-    return True, False, maxdv
+    return True, False, maxdv, n
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("tag,blocks,ch,games,sims,moves", [("3x64", 3, 64, 8, 100, 60), ("6x128", 6, 128, 4, 100, 30)])
+@pytest.mark.parametrize("tag,blocks,ch,games,sims,moves", [("3x64", 3, 64, 8, 100, 60), ("6x128", 6, 128, 4, 100, 30),
+                                                           ("6x128", 6, 128, 3, 400, 225)])
 def test_selfplay_games_match_oracle(tag, blocks, ch, games, sims, moves):
     from games.gomoku import Gomoku
     from mcts.native_mcts import NativeSelfPlay
@@ -91,24 +97,30 @@ def test_selfplay_games_match_oracle(tag, blocks, ch, games, sims, moves):
     hip_games, hip_res = play(evaluate=None, evaluator_factory=m.board_evaluator)
     m.engine.check_status()
     ora_games, ora_res = play(evaluate=ref.predict)
-    same = exempt = 0
+    same = exempt = matched = 0
     worst = 0.0
     for g in range(games):
         pis_h = [pi for _, pi, _ in hip_res[g][0]]
         pis_o = [pi for _, pi, _ in ora_res[g][0]]
-        ident, ex, dv = _compare(hip_games[g].move_history, ora_games[g].move_history, pis_h, pis_o, sims,
-                                 lambda k: temp(k) > 0)
+        ident, ex, dv, nm = _compare(hip_games[g].move_history, ora_games[g].move_history, pis_h, pis_o, sims,
+                                     lambda k: temp(k) > 0)
         worst = max(worst, dv)
+        matched += nm
         same += ident
         exempt += ex
         if ident:
             assert hip_res[g][1] == ora_res[g][1]
             assert all(np.array_equal(a[2], b[2]) for a, b in zip(hip_res[g][0], ora_res[g][0]))
     nmoves = sum(len(g.move_history) for g in hip_games)
-    print(f"{tag}: {games} self-play games, {nmoves} moves: {same} identical to the oracle's, "
-          f"{exempt} diverged at a near-tie (exempt); max root visit difference before a divergence {worst:.0f}")
+    print(f"{tag}: {games} self-play games x {sims} sims, {nmoves} moves: {same} identical to the oracle's, "
+          f"{exempt} diverged at a near-tie (exempt), {matched} moves matched before any divergence; "
+          f"max root visit difference before a divergence {worst:.0f}")
     assert same + exempt == games
     assert nmoves > games * 10
+    assert exempt <= MAX_EXEMPT_FRAC * games, f"{exempt} of {games} games exempt"
+    assert matched >= MIN_MATCHED_FRAC * nmoves, f"only {matched} of {nmoves} moves matched"
+    if moves == 225:                       # to game end: every identical game finished on both sides
+        assert all(g.is_game_over() for g in hip_games)
 
 
 class _Predict:
@@ -150,7 +162,7 @@ def test_gating_games_match_oracle():
     played = []
     train.evaluate_models(new, best, "gomoku", n_games=n, n_simulations=sims, cpuct=1.0, native=True, record=played)
     openings = [g.move_history[0] for g in played]
-    same = exempt = 0
+    same = exempt = matched = total = 0
     for i, op in enumerate(openings):
         runs = {}
         for name, en, eb in (("hip", new.predict, best.predict), ("oracle", ref_new.predict, ref_best.predict)):
@@ -161,8 +173,12 @@ def test_gating_games_match_oracle():
         (gh, ph), (go, po) = runs["hip"], runs["oracle"]
         # the product path is the HIP lockstep game, move for move
         assert list(gh.move_history) == list(played[i].move_history), i
-        ident, ex, _ = _compare(gh.move_history[1:], go.move_history[1:], ph, po, sims, lambda k: False)
+        ident, ex, _, nm = _compare(gh.move_history[1:], go.move_history[1:], ph, po, sims, lambda k: False)
+        matched += nm
+        total += len(gh.move_history) - 1
         same += ident
         exempt += ex
     print(f"gating: {n} games (3x64 vs 6x128, {sims} sims): {same} identical to the oracle's, {exempt} exempt")
     assert same + exempt == n
+    assert exempt <= MAX_EXEMPT_FRAC * n, f"{exempt} of {n} games exempt"
+    assert matched >= MIN_MATCHED_FRAC * total, f"only {matched} of {total} moves matched"
