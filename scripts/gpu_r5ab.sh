@@ -1,5 +1,7 @@
 #!/bin/bash
-# fp32 eval towers (key 19 = 0) with / without per-tap fragment addresses (AZG_EVAL_REMAT)
+# fp32 eval towers (key 19 = 0) with / without per-tap fragment addresses (AZG_EVAL_REMAT),
+# then 2 vs 3 self-play groups.  scripts/_ab/libazg_pv_noremat.so was the product built with
+# -DAZG_EVAL_REMAT=0 for this A/B only; it is not kept (rebuild it to rerun)
 set -o pipefail
 O=gpurun_out/r5ab; mkdir -p $O
 A="--sp-games 0 --train-steps 0 --big-steps 0 --no-cpu-baseline --tune 19=0"
