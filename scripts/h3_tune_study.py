@@ -19,7 +19,7 @@ import torch
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batches", default="128,256,512,1024,2048,3456,4096")
-    ap.add_argument("--vars", default="0", help="key 20: H3 tower body, 0 = VAR 98, 1 = VAR 99")
+    ap.add_argument("--vars", default="1", help="key 20: H3 tower body, 1 = VAR 99 (the product default), 0 = VAR 98")
     ap.add_argument("--net", default="6x128")
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--rounds", type=int, default=3)
