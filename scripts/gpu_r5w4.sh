@@ -1,5 +1,5 @@
 #!/bin/bash
-# tower shape 13 (128x64, 4 waves of 64x32, 256 VGPRs): forward parity first, then tower timings
+# tower shape 13 (128x64, 4 waves of 64x32, 256 VGPRs; removed after this measurement): forward parity first, then tower timings
 set -o pipefail
 O=gpurun_out/r5w4; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_forward.py -x -q --timeout 300 --timeout-method thread > $O/tests_fwd.log 2>&1 &&

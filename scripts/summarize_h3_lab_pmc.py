@@ -1,6 +1,8 @@
-"""SQ counters of the H3 tile lab variants (scripts/gpu_r5n.sh -> gpurun_out/r5n/p1, p2).
+"""SQ counters of the H3 tile lab variants (scripts/gpu_r5n.sh -> gpurun_out/r5n/p1, p2) and of
+the product towers (scripts/gpu_r5s.sh -> gpurun_out/r5s/<tag>/p1, p2).
 
     python scripts/summarize_h3_lab_pmc.py gpurun_out/r5n
+    python scripts/summarize_h3_lab_pmc.py gpurun_out/r5s/t_b3456
 """
 import collections
 import csv
@@ -18,7 +20,7 @@ def main():
         if not os.path.exists(f):
             continue
         for r in csv.DictReader(open(f)):
-            m = re.search(r"(lab_conv|lab_h3)<([\d, ]+)>", r["Kernel_Name"])
+            m = re.search(r"(lab_conv|lab_h3|conv_tower)<([\d, ]+)>", r["Kernel_Name"])
             if m:
                 acc[m.group(1) + "<" + m.group(2) + ">"][r["Counter_Name"]].append(float(r["Counter_Value"]))
     print("| lab_conv<C, BN, WM, TM, NW, VAR, WPE> | MFMA busy | LDS-array busy | wait_any | wait_inst | "
