@@ -73,10 +73,14 @@ _SIGS = {
     "azg_pv_tower_diag_read": (ctypes.c_int32, [_P, ctypes.POINTER(TowerDiag), _P]),
     "azg_pv_tower_diag_clear": (ctypes.c_int32, [_P, _P]),
     "azg_pv_debug_copy": (ctypes.c_int32, [_P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32, _P]),
+    "azg_pv_grad_count": (ctypes.c_int64, [_P]),
+    "azg_pv_train_fp32_once": (ctypes.c_int32, [_P]),
+    "azg_pv_posted": (ctypes.c_int32, [_P, ctypes.c_uint32]),
 }
 EXPORTS = tuple(_SIGS)
 PROF_CLASSES = ("conv3x3", "stem", "heads", "train_conv", "train_wgrad", "train_other", "tower", "tower16")
-ABI_VERSION = 2   # 2: tower launch numbers, azg_pv_recover, the wait record (round 5)
+ABI_VERSION = 3   # 2: tower launch numbers, azg_pv_recover, the wait record (round 5); 3: the gradient
+                  # buffer's skip word, azg_pv_train_fp32_once, azg_pv_posted (round 6)
 
 _lib = None
 
@@ -93,16 +97,11 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
             "`python -c 'import __graft_entry__ as g; g.build()'` (or `make -C alphazero-gomoku_amd/csrc`). "
             "There is no CPU fallback.")
     lib = ctypes.CDLL(p)
-    # AZG_PV_ALLOW_OLD_ABI=1 (bitwise cross-library studies only, scripts/train_lib_compare.py):
-    # an older library binds without the entry points it lacks
-    old_ok = os.environ.get("AZG_PV_ALLOW_OLD_ABI") == "1"
     for name, (res, args) in _SIGS.items():
-        if old_ok and not hasattr(lib, name):
-            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.azg_pv_abi_version() != ABI_VERSION and not old_ok:
+    if lib.azg_pv_abi_version() != ABI_VERSION:
         raise RuntimeError(f"libazg_pv ABI {lib.azg_pv_abi_version()} != expected {ABI_VERSION}")
     if path is None:
         _lib = lib

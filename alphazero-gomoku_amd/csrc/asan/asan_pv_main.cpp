@@ -20,7 +20,7 @@ static int fails = 0;
 
 int main()
 {
-    CHECK(azg_pv_abi_version() == 2);
+    CHECK(azg_pv_abi_version() == 3);
     const int shapes[4][2] = {{3, 64}, {6, 128}, {10, 256}, {0, 64}};
     const long long want[3] = {340010, 1892650, 11930922};
     for (int s = 0; s < 4; ++s) {
@@ -29,6 +29,7 @@ int main()
         CHECK(azg_pv_create(&cfg, &h) == 0 && h);
         const int64_t n = azg_pv_param_count(h);
         if (s < 3) CHECK(n == want[s]);
+        CHECK(azg_pv_grad_count(h) == n + 1);   // + the step's skip word (ABI 3)
         const int nt = azg_pv_num_param_tensors(h);
         std::vector<int64_t> off(nt), num(nt);
         CHECK(azg_pv_param_layout(h, off.data(), num.data()) == 0);
@@ -45,6 +46,8 @@ int main()
         CHECK(azg_pv_mark_dirty(h) == 0);
         // tower recovery / wait record before any launch: nothing posted, nothing to do
         CHECK(azg_pv_last_seq(h) == 0);
+        CHECK(azg_pv_posted(h, 0) == 0 && azg_pv_posted(h, 7) == 0);
+        CHECK(azg_pv_train_fp32_once(h) == 0);
         int32_t rec = -1;
         CHECK(azg_pv_recover(h, 0, &rec, nullptr) == 0 && rec == 0);
         CHECK(azg_pv_recover(h, 7, &rec, nullptr) == 0 && rec == 0);
@@ -75,6 +78,9 @@ int main()
     CHECK(azg_pv_param_count(nullptr) == -1);
     CHECK(azg_pv_status(nullptr) == 0);
     CHECK(azg_pv_train_status(nullptr) == 0);
+    CHECK(azg_pv_posted(nullptr, 3) == 0);
+    CHECK(azg_pv_grad_count(nullptr) == -1);
+    CHECK(azg_pv_train_fp32_once(nullptr) != 0);
     CHECK(azg_pv_last_seq(nullptr) == 0);
     CHECK(azg_pv_tower_diag_clear(nullptr, nullptr) != 0);
     CHECK(azg_pv_bind(nullptr, nullptr, nullptr, nullptr) != 0);

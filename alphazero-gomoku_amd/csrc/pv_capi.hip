@@ -46,7 +46,7 @@ static int32_t fail(const char* what, hipError_t e = hipSuccess)
 
 extern "C" {
 
-int32_t azg_pv_abi_version(void) { return 2; }
+int32_t azg_pv_abi_version(void) { return 3; }
 
 const char* azg_pv_last_error(void) { return g_err.c_str(); }
 
@@ -159,6 +159,7 @@ int32_t azg_pv_bind(azg_pv* h, float* params, float* grads, float* bn_stats)
     h->bn = bn_stats;
     h->dirty = true;
     h->train_packs = false;
+    h->bn_bak_ok = false;
     return 0;
 }
 
@@ -166,6 +167,7 @@ int32_t azg_pv_bind_counters(azg_pv* h, int64_t* num_batches_tracked)
 {
     if (!h) return fail("azg_pv_bind_counters: null handle");
     h->nbt = num_batches_tracked;
+    h->bn_bak_ok = false;
     return 0;
 }
 
@@ -176,6 +178,7 @@ int32_t azg_pv_mark_dirty(azg_pv* h)
     if (!h) return fail("azg_pv_mark_dirty: null handle");
     h->dirty = true;
     h->train_packs = false;
+    h->bn_bak_ok = false;
     return 0;
 }
 
@@ -242,27 +245,43 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards)
     return 0;
 }
 
-// split-fp16 train-forward overflow flags set since the last azg_pv_clear_status
-static unsigned train_ovf_flags(const azg_pv* h)
+// train steps the Adam kernel skipped (a split-fp16 train forward met an activation
+// beyond fp16's range on some rank) since the last azg_pv_clear_status
+static unsigned train_skips(const azg_pv* h)
 {
-    unsigned n = 0;
-    if (h->ring_host)
-        for (unsigned i = 0; i < kTrainOvfWords; ++i)
-            n += __atomic_load_n(h->ring_host + 2 * kTowerRing + i, __ATOMIC_ACQUIRE) != 0u;
-    return n;
+    return h->ring_host ? __atomic_load_n(h->ring_host + 2 * kTowerRing + kTrainSkips, __ATOMIC_ACQUIRE) : 0u;
 }
 
+// posted eval launches not yet recovered: timed-out tower launches and split-fp16 launches
+// whose activations left fp16's range (their outputs are invalid until recomputed)
 int32_t azg_pv_status(const azg_pv* h)
 {
     if (!h || !h->ring_host) return 0;
     int32_t n = 0;
-    for (unsigned i = 0; i < kStatusWords; ++i) n += __atomic_load_n(h->ring_host + i, __ATOMIC_ACQUIRE) != 0u;
+    for (unsigned i = 0; i < 2 * kTowerRing; ++i) n += __atomic_load_n(h->ring_host + i, __ATOMIC_ACQUIRE) != 0u;
     return n;
+}
+
+int32_t azg_pv_posted(const azg_pv* h, uint32_t seq)
+{
+    if (!h || !h->ring_host || seq == 0) return 0;
+    const unsigned slot = seq & (kTowerRing - 1);
+    return (__atomic_load_n(h->ring_host + slot, __ATOMIC_ACQUIRE) == seq ? 1 : 0) |
+           (__atomic_load_n(h->ovf_host + slot, __ATOMIC_ACQUIRE) == seq ? 2 : 0);
 }
 
 int32_t azg_pv_train_status(const azg_pv* h)
 {
-    return h ? (int32_t)train_ovf_flags(h) : 0;
+    return h ? (int32_t)train_skips(h) : 0;
+}
+
+int64_t azg_pv_grad_count(const azg_pv* h) { return h ? h->nparams + 1 : -1; }
+
+int32_t azg_pv_train_fp32_once(azg_pv* h)
+{
+    if (!h) return fail("azg_pv_train_fp32_once: null handle");
+    h->train_fp32_once = true;
+    return 0;
 }
 
 int32_t azg_pv_clear_status(azg_pv* h)
@@ -301,12 +320,28 @@ int32_t azg_pv_recover(azg_pv* h, uint32_t seq, int32_t* recovered, void* stream
         return fail("azg_pv_recover: the posted launch is older than the launch record ring (recover it sooner)");
     // per-layer convs from the same inputs into the same outputs: bitwise what the tower
     // computes when no wait times out; an H3 launch whose activations left fp16's range
-    // is recomputed with fp32 MFMA
-    if (int32_t e = forward_eval(h, r.x, r.batch, r.probs, r.values, r.logits, (hipStream_t)stream, r.boards,
-                                 r.players, r.priors, true, ovf))
-        return e;
+    // is recomputed with fp32 MFMA.  A timed-out split-fp16 launch is recomputed split
+    // under its own number, so a range overflow the stale-input tower could not see is
+    // posted by the recompute and settled here with fp32 MFMA as well.
     __atomic_store_n(h->ring_host + slot, 0u, __ATOMIC_RELEASE);
     __atomic_store_n(h->ovf_host + slot, 0u, __ATOMIC_RELEASE);
+    hipStream_t rst = (hipStream_t)stream;
+    const bool guard = !ovf && r.h3;
+    if (int32_t e = forward_eval(h, r.x, r.batch, r.probs, r.values, r.logits, rst, r.boards, r.players, r.priors,
+                                 true, ovf, guard ? seq : 0u))
+        return e;
+    bool late_ovf = false;
+    if (guard) {
+        AZG_TRY(hipStreamSynchronize(rst), "azg_pv_recover: sync");
+        late_ovf = __atomic_load_n(h->ovf_host + slot, __ATOMIC_ACQUIRE) == seq;
+        if (late_ovf) {
+            __atomic_store_n(h->ovf_host + slot, 0u, __ATOMIC_RELEASE);
+            if (int32_t e = forward_eval(h, r.x, r.batch, r.probs, r.values, r.logits, rst, r.boards, r.players,
+                                         r.priors, true, true))
+                return e;
+        }
+    }
+    if (late_ovf) ++h->h3_overflows;
     if (ovf) ++h->h3_overflows;
     if (!tmo) {   // a range overflow alone: no breaker (the dispatch ran as one)
         *recovered = 1;
@@ -329,7 +364,7 @@ int32_t azg_pv_tower_diag_read(azg_pv* h, azg_pv_tower_diag* out, void* stream)
     out->breaker_trips = h->breaker_trips;
     out->breaker_launches = h->breaker_launches;
     out->h3_overflows = h->h3_overflows;
-    out->train_h3_overflows = train_ovf_flags(h);
+    out->train_h3_overflows = train_skips(h);
     if (!h->tower_diag) return 0;
     unsigned w[kTowerDiagWords];
     hipStream_t st = (hipStream_t)stream;
@@ -363,7 +398,7 @@ int32_t azg_pv_tower_diag_read(azg_pv* h, azg_pv_tower_diag* out, void* stream)
     out->breaker_trips = h->breaker_trips;
     out->breaker_launches = h->breaker_launches;
     out->h3_overflows = h->h3_overflows;
-    out->train_h3_overflows = train_ovf_flags(h);
+    out->train_h3_overflows = train_skips(h);
     return 0;
 }
 
@@ -742,7 +777,7 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
 
 int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* values, float* logits,
                      hipStream_t st, const int8_t* boards, const int8_t* players, float* priors, bool per_layer,
-                     bool fp32_only)
+                     bool fp32_only, unsigned guard_seq)
 {
     const int C = h->C;
     const float* P = h->params;
@@ -763,7 +798,7 @@ int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* 
     }
     // a tower or H3 launch gets a number and a record of its buffers (azg_pv_recover);
     // a recompute (per_layer) posts nothing
-    unsigned seq = 0;
+    unsigned seq = per_layer ? guard_seq : 0u;
     if ((variant != 0 || h3) && h->NB > 0 && !h->launches.empty() && !per_layer) {
         seq = ++h->seq;
         if (seq == 0) seq = ++h->seq;   // 0 means "not posted"

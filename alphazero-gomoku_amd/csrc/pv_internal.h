@@ -60,7 +60,11 @@ int conv_batch_bucket(int M);
 size_t tower_sync_bytes(int nlayers, int M);
 size_t tower_prod_bytes(int nlayers, int M);
 constexpr unsigned kTowerRing = 256;          // host ring of timed-out launch numbers (power of 2)
-constexpr unsigned kTrainOvfWords = 16;       // + the train forward's split-fp16 overflow flags (same memory)
+constexpr unsigned kTrainOvfWords = 16;       // + the train step's words (same memory): [kTrainFlag] the split-fp16
+                                              // train forward's overflow flag of the step in flight (moved into the
+                                              // gradient buffer's skip slot and cleared by heads_small_grads),
+                                              // [kTrainSkips] steps the Adam kernel skipped (azg_pv_train_status)
+constexpr unsigned kTrainFlag = 1, kTrainSkips = 2;
 constexpr unsigned kStatusWords = 2 * kTowerRing + kTrainOvfWords;
 constexpr int kTowerDiagWords = 64;           // device wait record (pv_tower.hip TowerDiag)
 constexpr unsigned kTowerWaitUs = 100000u;    // default awake-time bound of one dependency wait: 100 ms
@@ -143,6 +147,8 @@ struct azg_pv {
     int64_t* nbt = nullptr;   // optional: num_batches_tracked per BN layer (azg_pv_bind_counters)
     bool dirty = true;
     bool train_packs = false;   // wpack / wdpack / wstem / wfc hold the current parameters (train_apply, key 36)
+    bool bn_bak_ok = false;     // the train workspace's BN backup holds the running stats the next step starts from
+    bool train_fp32_once = false;   // azg_pv_train_fp32_once: the next train step's forward convs in fp32 MFMA
 
     // packed / derived weights (one allocation)
     float* wbase = nullptr;
@@ -219,5 +225,5 @@ hipError_t prof_harvest(azg_pv* h);
 void prof_end(azg_pv* h, int pair, hipStream_t st);
 int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* values, float* logits,
                      hipStream_t st, const int8_t* boards, const int8_t* players, float* priors,
-                     bool per_layer = false, bool fp32_only = false);
+                     bool per_layer = false, bool fp32_only = false, unsigned guard_seq = 0);
 }  // namespace azg

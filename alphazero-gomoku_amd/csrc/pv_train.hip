@@ -81,6 +81,10 @@ struct TrainWS {
     // optimizer
     double* npart = nullptr;     // grad sq-sum partials
     float* scal = nullptr;       // [0] total norm, [1] clip coef
+    // the BN running stats / num_batches_tracked the step in flight started from: a step
+    // the Adam kernel skips (split-fp16 range overflow on some rank) restores them
+    float* bn_bak = nullptr;
+    int64_t* nbt_bak = nullptr;
     // two-stream backward: weight grads on `side`
     hipStream_t side = nullptr;
     hipEvent_t ev_ready = nullptr, ev_join = nullptr;
@@ -386,12 +390,22 @@ constexpr int HSG_OUT = ACTIONS + VHID + VHID + 2;
 __global__ __launch_bounds__(256) void heads_small_grads_kernel(
     const float* __restrict__ dlogits, const float* __restrict__ dhv, const float* __restrict__ dpre,
     const float* __restrict__ hv, const float* __restrict__ lossb, int B, float* __restrict__ g_pfb,
-    float* __restrict__ g_v1b, float* __restrict__ g_v2w, float* __restrict__ g_v2b, float* __restrict__ losses)
+    float* __restrict__ g_v1b, float* __restrict__ g_v2w, float* __restrict__ g_v2b, float* __restrict__ losses,
+    unsigned* __restrict__ ovf, float* __restrict__ skip)
 {
     const int lane = threadIdx.x & 63;
     const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (o >= HSG_OUT) return;
     if (o == HSG_OUT - 1) {
+        // every forward conv of this step ran before this kernel (same stream): the split-
+        // fp16 range flag of the step moves into the gradient buffer's skip slot, so a DP
+        // all-reduce of the gradient carries it to every rank (train_apply skips the step
+        // where it is nonzero), and is cleared for the next step
+        if (lane == 0 && skip) {
+            const unsigned f = ovf ? __hip_atomic_load(ovf + kTrainFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+            *skip = f ? 1.f : 0.f;
+            if (f) __hip_atomic_store(ovf + kTrainFlag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         double pl = 0.0, vl = 0.0;
         for (int b = lane; b < B; b += 64) {
             pl += (double)lossb[2 * b];
@@ -554,13 +568,38 @@ __global__ __launch_bounds__(256) void grad_sqsum_kernel(const float* __restrict
 // grad_sqsum partials itself (one fixed-order block reduction, the same in every workgroup, so all
 // workgroups hold the same coefficient, bitwise) and workgroup 0 publishes the norm --
 // one launch boundary less on the step's critical path.
+// The step's skip word (g[n], after any DP all-reduce: nonzero iff some rank's split-fp16
+// train forward met an activation beyond fp16's range) decides, uniformly in every
+// workgroup, whether the step commits: a skipped step leaves params, grads and moments
+// as they are and restores the BN running stats and counters the step started from
+// (BnKeep, saved when the previous step committed); a committed step saves them.
+struct BnKeep {
+    float* bn;            // running stats [nbn]
+    float* bn_bak;
+    int nbn;
+    int64_t* nbt;         // num_batches_tracked [nlayers] (may be null)
+    int64_t* nbt_bak;
+    int nlayers;
+    unsigned* skips;      // host-mapped count of skipped steps (azg_pv_train_status)
+};
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                    const double* __restrict__ part, int nb, float max_norm,
                                                    float* __restrict__ scal, float* __restrict__ total_norm,
                                                    float lr_bc1, float b1w, float b2, float one_m_b2, float bc2_sqrt,
-                                                   float eps, float wd)
+                                                   float eps, float wd, BnKeep k)
 {
+    const int64_t gtid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, gstride = (int64_t)gridDim.x * blockDim.x;
+    if (g[n] != 0.f) {   // skip: undo the step's running-stat updates
+        for (int64_t i = gtid; i < k.nbn; i += gstride) k.bn[i] = k.bn_bak[i];
+        if (k.nbt)
+            for (int64_t i = gtid; i < k.nlayers; i += gstride) k.nbt[i] = k.nbt_bak[i];
+        if (gtid == 0 && k.skips) __hip_atomic_fetch_add(k.skips, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    for (int64_t i = gtid; i < k.nbn; i += gstride) k.bn_bak[i] = k.bn[i];
+    if (k.nbt)
+        for (int64_t i = gtid; i < k.nlayers; i += gstride) k.nbt_bak[i] = k.nbt[i];
     __shared__ double red[8];
     double s = 0.0;
     for (int i = threadIdx.x; i < nb; i += blockDim.x) s += part[i];
@@ -667,6 +706,10 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     A(t, 2 * 1024, false);
     w->npart = (double*)t;
     A(w->scal, 4, true);
+    A(w->bn_bak, (size_t)h->nbn, false);
+    A(t, 2 * h->bn_desc.size() + 2, false);
+    w->nbt_bak = (int64_t*)t;
+    h->bn_bak_ok = false;
     A(t, 4 * (2 * kTowerMaxBlocks + 2), true);
     w->fincnt = (unsigned*)t;
     A(t, (size_t)head_proj_stats_groups(M) * 6 * 2, false);
@@ -803,7 +846,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
 
     // forward conv weights: the split-fp16 packs (key 49; ensured by train_backward) with
     // their per-layer 2^-e output factor, or the fp32 packs
-    const bool fh3 = g_train_h3 && h->wpack16;
+    const bool fh3 = g_train_h3 && h->wpack16 && !h->train_fp32_once;
     auto fwd_w = [&](int ci) -> const float* {
         return fh3 ? (const float*)h->wpack16 + (size_t)ci * CC9 : h->wpack + (size_t)ci * CC9;
     };
@@ -1019,7 +1062,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
            "train: head fc wgrad");
     hipLaunchKernelGGL(heads_small_grads_kernel, dim3((HSG_OUT + 3) / 4), dim3(256), 0, st, w->dlogits, w->dhv,
                        w->dpre, w->hv, w->lossb, B, G + h->poff[h->t_pfc_b], G + h->poff[h->t_vfc1_b],
-                       G + h->poff[h->t_vfc2_w], G + h->poff[h->t_vfc2_b], losses);
+                       G + h->poff[h->t_vfc2_w], G + h->poff[h->t_vfc2_b], losses, h->train_ovf_dev,
+                       G + h->nparams);
     AZG_CK(hipGetLastError(), "train: heads_small_grads");
     // policy_conv.weight [2][C] then value_conv.weight [C]: partial layout [t][3][C]
     hipLaunchKernelGGL(reduce_partials_kernel, dim3((3 * C + 15) / 16), dim3(256), 0, st, w->hpart, hntile, 3 * C,
@@ -1063,16 +1107,28 @@ int32_t train_backward(azg_pv* h, const float* x, const float* pis, const float*
         if (int32_t r = repack(h, st, w->wdpack)) return r;
         h->train_packs = true;
     }
-    if (g_train_h3)
+    if (g_train_h3 && !h->train_fp32_once)
         if (int32_t r = ensure_h3(h, st)) return r;
+    // the running stats this step starts from (a skipped step restores them): refreshed
+    // whenever they may have changed outside the library; a step the Adam kernel commits
+    // refreshes them itself
+    if (!h->bn_bak_ok) {
+        AZG_CK(hipMemcpyAsync(w->bn_bak, h->bn, (size_t)h->nbn * sizeof(float), hipMemcpyDeviceToDevice, st),
+               "train: BN backup");
+        if (h->nbt)
+            AZG_CK(hipMemcpyAsync(w->nbt_bak, h->nbt, h->bn_desc.size() * sizeof(int64_t), hipMemcpyDeviceToDevice, st),
+                   "train: BN counter backup");
+        h->bn_bak_ok = true;
+    }
     const int C = h->C;
     int32_t r;
     switch (C) {
         case 64: r = train_backward_t<64>(h, x, pis, zs, B, losses, st); break;
         case 128: r = train_backward_t<128>(h, x, pis, zs, B, losses, st); break;
         case 256: r = train_backward_t<256>(h, x, pis, zs, B, losses, st); break;
-        default: return set_error("train: bad channels", hipErrorInvalidValue);
+        default: r = set_error("train: bad channels", hipErrorInvalidValue); break;
     }
+    h->train_fp32_once = false;
     h->dirty = true;   // running stats changed -> eval fold must be redone
     return r;
 }
@@ -1092,9 +1148,11 @@ int32_t train_apply(azg_pv* h, float* exp_avg, float* exp_avg_sq, int64_t step, 
     const float lr_bc1 = (float)((double)lr / bc1);
     const float bc2_sqrt = (float)std::sqrt(bc2);
     // 1024 workgroups, grid-stride: each reduces the 1024 norm partials (8 KB) itself
+    const BnKeep keep{h->bn, w->bn_bak, (int)h->nbn, h->nbt, w->nbt_bak, (int)h->bn_desc.size(),
+                      h->train_ovf_dev ? h->train_ovf_dev + kTrainSkips : nullptr};
     hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n) < 1024 ? grid_for(n) : 1024), dim3(256), 0, st, h->params,
                        h->grads, exp_avg, exp_avg_sq, n, w->npart, nb, max_norm, w->scal, total_norm, lr_bc1,
-                       (float)(1.0 - (double)beta1), beta2, (float)(1.0 - (double)beta2), bc2_sqrt, eps, wd);
+                       (float)(1.0 - (double)beta1), beta2, (float)(1.0 - (double)beta2), bc2_sqrt, eps, wd, keep);
     AZG_CK(hipGetLastError(), "apply: adam");
     // every pack of the next step (and the eval BN fold) from the new parameters, on
     // this stream right behind Adam: the next train step starts without a repack

@@ -50,7 +50,14 @@ class PolicyValueEngine:
         dev = self.device
         with torch.no_grad():
             self.flat_params = torch.empty(self.nparam, dtype=torch.float32, device=dev)
-            self.flat_grads = torch.zeros(self.nparam, dtype=torch.float32, device=dev)
+            # the gradients + ONE skip word (include/azg_pv.h azg_pv_bind, ABI 3): a DP
+            # all-reduce of flat_grads_ext carries a rank's split-fp16 range overflow to
+            # every rank, and train_apply commits the step only where the word is 0
+            ng = int(self.lib.azg_pv_grad_count(h))
+            if ng != self.nparam + 1:
+                raise RuntimeError("libazg_pv: unexpected gradient buffer layout")
+            self.flat_grads_ext = torch.zeros(ng, dtype=torch.float32, device=dev)
+            self.flat_grads = self.flat_grads_ext[:self.nparam]
             self.param_views = []
             self.grad_views = []
             for i, p in enumerate(params):
@@ -79,14 +86,16 @@ class PolicyValueEngine:
                 b.num_batches_tracked = self.flat_nbt[i]
                 o += 2 * c
         self.params = params
-        check(self.lib.azg_pv_bind(h, ptr(self.flat_params), ptr(self.flat_grads), ptr(self.flat_bn)), self.lib)
+        check(self.lib.azg_pv_bind(h, ptr(self.flat_params), ptr(self.flat_grads_ext), ptr(self.flat_bn)), self.lib)
         if self.lib.azg_pv_num_bn_layers(h) != len(bns):
             raise RuntimeError("BatchNorm layer count does not match the engine layout")
         # num_batches_tracked advances inside the train kernels (no extra launch)
         check(self.lib.azg_pv_bind_counters(h, ptr(self.flat_nbt)), self.lib)
         self._seen = self._versions()
         self._out_cache = {}
-        self.recoveries = 0   # tower launches recomputed per layer (recover)
+        self.recoveries = 0         # tower launches recomputed per layer (recover)
+        self.train_recoveries = 0   # train steps skipped on the device and redone in fp32 (network.train_batch)
+        self._unsettled = []        # launch numbers of forwards no host sync has settled yet (predict_device)
 
     # -- housekeeping -------------------------------------------------------
     def _versions(self):
@@ -117,33 +126,59 @@ class PolicyValueEngine:
         input and output buffers must still be intact."""
         if not seq:
             return False
+        if seq in self._unsettled:
+            self._unsettled.remove(seq)
         done = ctypes.c_int32(0)
         check(self.lib.azg_pv_recover(self.h, int(seq), ctypes.byref(done), _stream(self.device)), self.lib)
         if done.value:
             self.recoveries += 1
         return bool(done.value)
 
+    def track(self, seq: int) -> None:
+        """Register a forward whose caller synchronises later without settling it
+        (PyTorchModel.predict_device): the next settle point checks it."""
+        if seq:
+            self._unsettled.append(int(seq))
+            del self._unsettled[:-1024]
+
+    def check_orphans(self, upto: int = 0) -> None:
+        """Settle point (the caller has synchronised this engine's stream): raise
+        TowerFault if a tracked forward older than `upto` (0: every tracked one) timed out
+        or met a split-fp16 range overflow -- its buffers may be gone, so it cannot be
+        recomputed, and its outputs are invalid."""
+        keep, bad = [], []
+        for s in self._unsettled:
+            if upto and s >= upto:
+                keep.append(s)
+            elif int(self.lib.azg_pv_posted(self.h, s)):
+                bad.append(s)
+        self._unsettled = keep
+        if bad:
+            raise TowerFault(f"libazg_pv: forward launch(es) {bad} timed out or left fp16's range and were never "
+                             f"settled (predict_device outputs consumed without recover); their outputs are invalid "
+                             f"({self.tower_diag()})")
+
     def check_status(self):
-        """Raise TowerFault if a persistent-tower launch this handle ran timed out and was
-        not recovered (azg_pv_status: a plain host load, complete for every forward the
-        caller has synchronised with).  The product recovers every timed-out launch at
-        its host sync (recover), so this fires only for forwards nobody settled, e.g.
-        predict_device results consumed without a recover.  The posted launches stay
-        until clear_status()."""
+        """Raise TowerFault if an eval launch this handle ran timed out or met a split-fp16
+        range overflow and was not recovered (azg_pv_status: a plain host load, complete
+        for every forward the caller has synchronised with).  The product recovers every
+        such launch at its host sync (recover), so this fires only for forwards nobody
+        settled.  The posted launches stay until clear_status()."""
         s = int(self.lib.azg_pv_status(self.h))
         if s:
-            self.check_train()
             d = self.tower_diag()
-            raise TowerFault(f"libazg_pv: {s} persistent-tower launch(es) timed out waiting for their inputs and "
-                             f"were not recomputed; their outputs are invalid ({d})")
+            raise TowerFault(f"libazg_pv: {s} eval launch(es) timed out or left fp16's range and were not "
+                             f"recomputed; their outputs are invalid ({d})")
 
-    def check_train(self):
-        """Raise TowerFault if a split-fp16 train forward (key 49) of a step the caller has
-        synchronised with met an activation beyond fp16's range (azg_pv_train_status)."""
-        if int(self.lib.azg_pv_train_status(self.h)):
-            raise TowerFault("libazg_pv: a split-fp16 train forward met an activation beyond fp16's range "
-                             "(65504): that step's losses and gradients are not valid; set tuning key 49 = 0 "
-                             f"(fp32 MFMA train convs) to train this net ({self.tower_diag()})")
+    def train_skips(self) -> int:
+        """Train steps the Adam kernel skipped since clear_status (azg_pv_train_status: a
+        plain host load, complete for every step the caller has synchronised with)."""
+        return int(self.lib.azg_pv_train_status(self.h))
+
+    def train_fp32_once(self):
+        """The next train_backward runs its forward convs with fp32 MFMA (the redo of a
+        skipped step)."""
+        check(self.lib.azg_pv_train_fp32_once(self.h), self.lib)
 
     def clear_status(self):
         check(self.lib.azg_pv_clear_status(self.h), self.lib)

@@ -103,7 +103,15 @@ class AlphaZeroNet(nn.Module):
         if self.training:
             raise RuntimeError("train-mode forward is fused into PyTorchModel.train_batch; "
                                "call .eval() for inference")
-        _, value, logits = self.engine.forward(x, want_logits=True)
+        eng = self.engine
+        x = x.to(eng.device, torch.float32).contiguous()
+        _, value, logits = eng.forward(x, want_logits=True)
+        # a host-visible result, like the reference's: settle the launch now (x is alive)
+        seq = eng.last_seq()
+        if seq:
+            torch.cuda.current_stream(eng.device).synchronize()
+            eng.recover(seq)
+            eng.check_orphans()
         return logits, value
 
     def predict(self, state):
@@ -123,6 +131,15 @@ class HipAdam(torch.optim.Adam):
         eng = net.engine
         self.flat_exp_avg = torch.zeros_like(eng.flat_params)
         self.flat_exp_avg_sq = torch.zeros_like(eng.flat_params)
+
+    def get_step(self) -> int:
+        self._ensure_state()
+        return int(self.state[self._net.engine.params[0]]["step"].item())
+
+    def set_step(self, step: int) -> None:
+        self._ensure_state()
+        for p in self._net.engine.params:
+            self.state[p]["step"].fill_(float(step))
 
     def _views(self, p, i):
         eng = self._net.engine
@@ -232,6 +249,7 @@ class BoardEvaluator:
                 self.h_values[:n].copy_(self.d_values[:n], non_blocking=True)
                 self.event.record()
                 self.event.synchronize()
+            eng.check_orphans(self.seq)
         return self.h_priors.numpy()[:self.n], self.h_values.numpy()[:self.n]
 
 
@@ -259,8 +277,9 @@ class PyTorchModel:
         self.value_loss_fn = nn.MSELoss()
         self.policy_loss_fn = nn.KLDivLoss(reduction="batchmean")
         self.max_grad_norm = 3.0                        # network.py:223
-        self.grad_hook = None                           # DP: all-reduce of the flat grads
+        self.grad_hook = None                           # DP: all-reduce of the flat grads (+ skip word)
         self._losses = None
+        self._skips_seen = 0                            # device-skipped steps already accounted for
 
     @property
     def engine(self) -> PolicyValueEngine:
@@ -277,13 +296,18 @@ class PyTorchModel:
         out = probs.cpu().numpy(), values.cpu().numpy()
         if eng.recover(seq):   # a timed-out tower wait: recomputed per layer in place
             out = probs.cpu().numpy(), values.cpu().numpy()
+        eng.check_orphans()
         return out
 
     def predict_device(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """Device-resident predict: x [B,3,15,15] -> (probs, values) on the GPU.
         Asynchronous: a caller that synchronises should settle the forward with
-        engine.recover(engine.last_seq()) (x must still be intact), as predict does."""
-        probs, values, _ = self.engine.forward(x)
+        engine.recover(engine.last_seq()) (x must still be intact), as predict does;
+        a forward nobody settles is checked at the engine's next settle point
+        (check_orphans: a posted one raises TowerFault there)."""
+        eng = self.engine
+        probs, values, _ = eng.forward(x)
+        eng.track(eng.last_seq())
         return probs, values
 
     policy_value = predict
@@ -304,6 +328,7 @@ class PyTorchModel:
         out = (priors if masked else probs).cpu().numpy(), values.cpu().numpy()
         if eng.recover(seq):
             out = (priors if masked else probs).cpu().numpy(), values.cpu().numpy()
+        eng.check_orphans()
         return out
 
     def board_evaluator(self, capacity: int) -> "BoardEvaluator":
@@ -328,24 +353,60 @@ class PyTorchModel:
                            return_tensor: bool = False):
         """train_batch on device-resident tensors.  return_tensor=True returns the
         mean losses as a float32 [3] device tensor (policy, value, total) without a
-        host sync, so consecutive steps pipeline on the stream."""
+        host sync, so consecutive steps pipeline on the stream.
+
+        A step whose split-fp16 forward (tuning key 49) met an activation beyond fp16's
+        range on any rank does not commit on the device (include/azg_pv.h
+        azg_pv_train_apply: params, moments and BN buffers keep the values it started
+        from).  Synchronous callers (return_tensor=False) see it with the losses and redo
+        the step with fp32 forward convs on every rank -- the result is the key-49 = 0
+        step, bitwise.  Pipelined callers (return_tensor=True) do not wait for it: the
+        skipped step's batch is dropped, its Adam step number is given back at the next
+        call (steps already queued behind it used numbers one higher), and
+        engine.train_skips() counts it."""
         self.net.train()
         eng = self.engine
+        self._settle_skips()
         losses = torch.empty(3, dtype=torch.float32, device=eng.device)
         acc = None
+        vals = None
         for _ in range(epochs):
-            eng.train_backward(s, t, z, losses)
-            if self.grad_hook is not None:
-                self.grad_hook(eng.flat_grads)
-            self.optimizer.hip_step(self.max_grad_norm)
-            if epochs > 1:
+            step0 = self.optimizer.get_step()
+            self._one_step(s, t, z, losses)
+            if not return_tensor:
+                # one host sync per step (the reference reads its losses per step too)
+                v = torch.cat((losses, eng.flat_grads_ext[-1:])).double().tolist()
+                if v[3] != 0.0:
+                    # skipped on the device on every rank (the all-reduced skip word): redo in fp32
+                    self.optimizer.set_step(step0)
+                    eng.train_recoveries += 1
+                    self._skips_seen += 1
+                    eng.train_fp32_once()
+                    self._one_step(s, t, z, losses)
+                    v = losses.double().tolist()
+                vals = v[:3] if vals is None else [a + b for a, b in zip(vals, v[:3])]
+            elif epochs > 1:
                 acc = losses.double() if acc is None else acc + losses
-        mean = losses if epochs == 1 else (acc / float(epochs)).float()
         if return_tensor:
-            return mean
-        vals = (mean.double() if epochs == 1 else acc / float(epochs)).tolist()
-        eng.check_train()   # a split-fp16 train forward out of fp16's range raises here
+            return losses if epochs == 1 else (acc / float(epochs)).float()
+        vals = [a / float(epochs) for a in vals]
         return {"policy_loss": vals[0], "value_loss": vals[1], "total_loss": vals[2]}
+
+    def _one_step(self, s, t, z, losses):
+        eng = self.engine
+        eng.train_backward(s, t, z, losses)
+        if self.grad_hook is not None:
+            self.grad_hook(eng.flat_grads_ext)   # the gradients AND the step's skip word
+        self.optimizer.hip_step(self.max_grad_norm)
+
+    def _settle_skips(self):
+        """Give back the Adam step numbers of pipelined steps the device skipped."""
+        n = self.engine.train_skips()
+        if n < self._skips_seen:       # clear_status reset the count
+            self._skips_seen = n
+        elif n > self._skips_seen:
+            self.optimizer.set_step(self.optimizer.get_step() - (n - self._skips_seen))
+            self._skips_seen = n
 
     train_step = train_batch
 
@@ -355,6 +416,8 @@ class PyTorchModel:
         d = os.path.dirname(path)
         if d:
             os.makedirs(d, exist_ok=True)
+        torch.cuda.current_stream(self.engine.device).synchronize()
+        self._settle_skips()
         net_sd = {k: v.detach().clone() for k, v in self.net.state_dict().items()}
         opt_sd = self.optimizer.state_dict()
         opt_sd = {"state": {i: {k: (v.detach().clone() if torch.is_tensor(v) else v) for k, v in st.items()}

@@ -67,9 +67,15 @@ int32_t azg_pv_num_param_tensors(const azg_pv* h);
  * parameter tensor inside the flat buffer, in nn.Module.parameters() order. */
 int32_t azg_pv_param_layout(const azg_pv* h, int64_t* offsets, int64_t* numels);
 
-/* Bind torch-owned flat buffers.  params/grads: azg_pv_param_count floats each;
- * bn_stats: azg_pv_bn_count floats.  grads may be NULL for inference-only use. */
+/* Bind torch-owned flat buffers.  params: azg_pv_param_count floats; grads:
+ * azg_pv_grad_count floats = the parameter gradients followed by ONE skip word
+ * (ABI 3): azg_pv_train_backward writes 1.0 there when its split-fp16 forward (key 49)
+ * met an activation beyond fp16's range, else 0.0; a data-parallel caller all-reduces
+ * the whole buffer (any nonzero result skips the step on every rank) and
+ * azg_pv_train_apply commits the step only where the word is 0.  bn_stats:
+ * azg_pv_bn_count floats.  grads may be NULL for inference-only use. */
 int32_t azg_pv_bind(azg_pv* h, float* params, float* grads, float* bn_stats);
+int64_t azg_pv_grad_count(const azg_pv* h);
 
 /* Optional: bind the int64 num_batches_tracked counters, one per BatchNorm layer
  * in module order (azg_pv_num_bn_layers of them, device).  Each
@@ -113,11 +119,20 @@ int32_t azg_pv_train_backward(azg_pv* h, const float* x, const float* pis,
  * of the grad buffer), then one Adam step (torch semantics: L2-coupled weight
  * decay, bias correction for `step`, which is the post-increment step count).
  * exp_avg / exp_avg_sq: flat buffers like params.  total_norm (device, 1 float,
- * may be NULL) receives the pre-clip global L2 norm. */
+ * may be NULL) receives the pre-clip global L2 norm.
+ * If the grad buffer's skip word (azg_pv_bind) is nonzero the step does NOT commit:
+ * params, grads and moments are left as they are, the BN running stats and counters
+ * are restored to what the step started from, and the skipped-step count
+ * (azg_pv_train_status) advances.  The caller then redoes the step, e.g. after
+ * azg_pv_train_fp32_once, with the same `step`. */
 int32_t azg_pv_train_apply(azg_pv* h, float* exp_avg, float* exp_avg_sq,
                            int64_t step, float lr, float beta1, float beta2,
                            float eps, float weight_decay, float max_norm,
                            float* total_norm, void* stream);
+
+/* The next azg_pv_train_backward on this handle runs its forward convs with fp32
+ * MFMA (tuning key 49 = 0 for that one step): the redo of a skipped step. */
+int32_t azg_pv_train_fp32_once(azg_pv* h);
 
 /* Kernel-class event timing (bench / roofline instrumentation).  When enabled,
  * every launch of a profiled class is bracketed by hipEvents on the stream it is
@@ -207,7 +222,8 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *   key 49: train-step forward convs: 2 (default) split-fp16 with all four hi / lo products
  *          (~2^-33 per product: the two-step goldens hold), 1 three products, 0 fp32 MFMA;
  *          the dgrad convs and weight grads stay fp32; a staged activation beyond fp16's
- *          range flags the step (azg_pv_train_status);
+ *          range sets the step's skip word (azg_pv_bind): the step does not commit and the
+ *          caller redoes it in fp32 (azg_pv_train_fp32_once);
  *   key 48: train weight-grad tile (1 = padded-row table, buffer LDS-DMA, slabs in the
  *          MFMA layout, default; 0 = round-4 form); bitwise identical;
  *   key 18: seconds a handle runs per-layer convs after azg_pv_recover recomputed one
@@ -239,16 +255,21 @@ int32_t azg_pv_tower_status(azg_pv* h, void* stream);
 uint32_t azg_pv_last_seq(const azg_pv* h);
 int32_t azg_pv_recover(azg_pv* h, uint32_t seq, int32_t* recovered, void* stream);
 
-/* Number of posted (timed-out) tower launches not yet recovered (a plain host load of
- * the pinned ring: complete for every forward the caller has synchronised with); the
- * Python layer raises on a nonzero value it cannot recover.  azg_pv_clear_status drops
- * every posted launch without recomputing it and closes the per-layer breaker (key 18). */
+/* Number of posted eval launches not yet recovered -- timed-out tower launches and
+ * split-fp16 launches whose activations left fp16's range (a plain host load of the
+ * pinned rings: complete for every forward the caller has synchronised with).
+ * azg_pv_posted(seq): bit 0 = launch `seq` timed out, bit 1 = it met a range overflow,
+ * both not yet recovered (0: nothing to settle).  The Python layer raises on a posted
+ * launch it cannot recover (its buffers are gone).  azg_pv_clear_status drops every
+ * posted launch without recomputing it, zeroes the skipped-step count and closes the
+ * per-layer breaker (key 18). */
 int32_t azg_pv_status(const azg_pv* h);
+int32_t azg_pv_posted(const azg_pv* h, uint32_t seq);
 int32_t azg_pv_clear_status(azg_pv* h);
-/* Split-fp16 train forwards (key 49) that met an activation beyond fp16's range since the
- * last azg_pv_clear_status (a plain host load; complete for every train step the caller
- * has synchronised with).  Such a step's losses and gradients are not valid: the Python
- * layer raises (PyTorchModel.train_batch; pipelined callers check Engine.check_train). */
+/* Train steps azg_pv_train_apply skipped because their skip word was set (a split-fp16
+ * train forward, key 49, met an activation beyond fp16's range on some rank) since the
+ * last azg_pv_clear_status (a plain host load; complete for every step the caller has
+ * synchronised with). */
 int32_t azg_pv_train_status(const azg_pv* h);
 
 /* Self-describing record of the tower's waits since the last azg_pv_tower_diag_clear
@@ -284,9 +305,9 @@ typedef struct {
     uint32_t breaker_launches;  /* forwards run per layer while the breaker was open */
     uint32_t h3_overflows;      /* split-fp16 forwards recomputed with fp32 MFMA (key 19: an activation
                                    beyond fp16's range, 65504) */
-    uint32_t train_h3_overflows;   /* split-fp16 train forwards that met an activation beyond fp16's range
-                                      (key 49; that step's results are not finite: azg_pv_status counts it,
-                                      the Python layer raises, azg_pv_clear_status resets it) */
+    uint32_t train_h3_overflows;   /* train steps skipped because a split-fp16 train forward (key 49) met an
+                                      activation beyond fp16's range (= azg_pv_train_status; the Python layer
+                                      redoes each in fp32; azg_pv_clear_status resets it) */
     uint32_t reserved[3];
 } azg_pv_tower_diag;
 int32_t azg_pv_tower_diag_read(azg_pv* h, azg_pv_tower_diag* out, void* stream);

@@ -18,7 +18,7 @@ HEADER = os.path.join(REPO, "include", "azg_pv.h")
 
 def header_symbols():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\*?\s+\**(azg_pv_[a-z_]+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\*?\s+\**(azg_pv_[a-z_0-9]+)\s*\(", txt, re.M)))
 
 
 def test_header_declares_expected_entry_points():

@@ -239,3 +239,93 @@ def test_train_alphazero_world2_through_hip_engine(tmp_path):
     assert r0["global_wins"][0] == r1["global_wins"][0] == r0["local_wins"][0] + r1["local_wins"][0]
     assert r0["local_games"][0] + r1["local_games"][0] == 4
     assert r0["step"][0] > 0                                         # trained: Adam stepped
+
+
+def _ovf_batches(B=32):
+    """Rank 0: 31 empty boards and one with a single stone (a pixel class the batch
+    statistics see 9 times in 7,200: its normalised stem output is ~28 sigma); rank 1:
+    random legal positions (a few sigma at most)."""
+    from oracle.boards import encode_batch, synth_positions, synth_targets
+    b0 = np.zeros((B, 15, 15), np.int8)
+    b0[0, 7, 7] = 1
+    p0 = np.full(B, 2, np.int8)
+    b1, p1 = synth_positions(B, seed=4242)
+    pi, z = synth_targets(B, seed=4243)
+    return [(encode_batch(b0, p0), pi, z), (encode_batch(b1, p1), pi, z)]
+
+
+def _stem_gamma(m, batches):
+    """Per-channel stem BN gamma that drives rank 0's largest activation beyond fp16's
+    range (65504) and keeps rank 1's below it: the geometric mean of 65520 / (the two
+    batches' largest normalised stem outputs), where rank 0's is at least 4x rank 1's;
+    other channels keep gamma 1 (train-mode BN statistics, float64)."""
+    import torch.nn.functional as F
+    w = m.net.conv.weight.detach().double().cpu()
+    mx = []
+    for x, _, _ in batches:
+        zz = F.conv2d(torch.from_numpy(np.asarray(x, np.float64)), w, padding=1)
+        mean = zz.mean(dim=(0, 2, 3), keepdim=True)
+        var = zz.var(dim=(0, 2, 3), unbiased=False, keepdim=True)
+        mx.append(((zz - mean) / torch.sqrt(var + 1e-5)).amax(dim=(0, 2, 3)))
+    sel = mx[0] > 4 * mx[1].clamp_min(1e-3)
+    gamma = torch.where(sel, 65520.0 / torch.sqrt(mx[0] * mx[1].clamp_min(1e-3)), torch.ones_like(mx[0]))
+    return gamma.float(), int(sel.sum())
+
+
+def _ovf_worker(rank, world, port, out_dir):
+    import sys
+    sys.path[:0] = [REPO, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    torch.set_num_threads(1)
+    torch.distributed.init_process_group("gloo")
+    import _native
+    import distributed as D
+    from network import PyTorchModel
+    lib = _native.load_library()
+    batches = _ovf_batches()
+    x, pi, z = batches[rank]
+    out = {}
+    for tag, key49 in (("split", 2), ("fp32", 0)):
+        torch.manual_seed(11)
+        m = PyTorchModel(board_size=15, device="cuda:0", n_res_blocks=2, channels=64)
+        gamma, nsel = _stem_gamma(m, batches)
+        with torch.no_grad():
+            m.net.bn.weight.copy_(gamma.to(m.engine.device))
+        m.engine.mark_dirty()
+        m.grad_hook = D.grad_hook()
+        prev = lib.azg_pv_set_tuning(49, key49)
+        try:
+            losses = m.train_batch(x, pi, z)
+        finally:
+            lib.azg_pv_set_tuning(49, prev)
+        out.update({f"{tag}_{k}": v for k, v in _state(m).items()})
+        out[f"{tag}_losses"] = np.array([losses[k] for k in ("policy_loss", "value_loss", "total_loss")])
+        out[f"{tag}_recoveries"] = np.array([m.engine.train_recoveries])
+        out[f"{tag}_skips"] = np.array([m.engine.train_skips()])
+        out["channels"] = np.array([nsel])
+    np.savez(os.path.join(out_dir, f"ovf_rank{rank}.npz"), **out)
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_dp_train_overflow_on_one_rank_skips_everywhere(tmp_path):
+    """a split-fp16 train-forward range overflow on ONE rank must not
+    hang or split the replicas.  Its skip word rides the gradient all-reduce, so every rank
+    skips the step on the device and redoes it in fp32 -- rank 0 overflows (its stem BN
+    drives one channel past 65504 on its batch only), rank 1 does not.  Checked: both
+    ranks redid the step (one recovery, one skipped step each), the replicas are bitwise
+    identical, and bitwise equal to a world-2 run with key 49 = 0."""
+    port = _free_port()
+    mp.spawn(_ovf_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = (dict(np.load(tmp_path / f"ovf_rank{r}.npz")) for r in range(2))
+    assert r0["channels"][0] >= 1, "no stem channel separates the two batches"
+    for r in (r0, r1):
+        assert r["split_recoveries"][0] == 1 and r["split_skips"][0] == 1, r
+        assert r["fp32_recoveries"][0] == 0 and r["fp32_skips"][0] == 0, r
+        assert np.isfinite(r["split_losses"]).all()
+        for k in ("params", "bn", "nbt", "m", "v", "step", "losses"):
+            assert np.array_equal(r[f"split_{k}"], r[f"fp32_{k}"]), k
+    for k in ("params", "bn", "nbt", "m", "v", "step"):
+        assert np.array_equal(r0[f"split_{k}"], r1[f"split_{k}"]), k
+    print(f"one-rank overflow: {int(r0['channels'][0])} stem channels, both ranks redid the step in fp32")

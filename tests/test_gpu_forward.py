@@ -83,6 +83,59 @@ def test_forward_matches_oracle(blocks, ch, B):
     argmax_check(probs, rp, b)
 
 
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("blocks,ch,seed,B,shape", [(6, 128, 0, 512, 8), (6, 128, 0, 3456, 8),
+                                                     (10, 256, 1, 512, 12)])
+def test_split_forward_on_trained_weights_matches_oracle32(blocks, ch, seed, B, shape):
+    """the split-fp16 eval arithmetic (key 19 = 1, the default) on weights
+    that are NOT on the fp16 grid -- the benchmarked ones: seeded init (seed 0 for 6x128,
+    1 for the 10x256 Pente net) + bench.pretrain's 20 train_batch steps -- so every product
+    term (lo_a hi_b, hi_a lo_b, hi_a hi_b) is live.  The tower runs with the shape the
+    bench's launches use: 128x64 (shape 8) at 512 and 3,456 boards (the self-play batch),
+    h3_tile 128x128 (shape 12) for 10x256 at 512.  Asserted: |gpu - oracle fp32| <= 1e-5
+    on probs and values (the north star's literal bar); printed: both against fp64 on the
+    first 256 boards."""
+    import _native
+    import bench
+    from network import PyTorchModel
+    lib = _native.load_library()
+    torch.set_num_threads(16)
+    torch.manual_seed(seed)
+    m = PyTorchModel(board_size=15, device="cuda", n_res_blocks=blocks, channels=ch)
+    bench.pretrain(m, m.engine.device)
+    st = state_to_numpy(m.net)
+    conv = np.asarray(st["res_blocks.0.conv1.weight"])
+    off = float(np.mean(conv.astype(np.float16).astype(np.float32) != conv))
+    assert off > 0.9, off                      # the weights' lo halves are live
+    ref = RefModel(blocks, ch)
+    load_numpy_state(ref.net, st)
+    b, p = synth_positions(B, seed=B + 7 * ch)
+    x = encode_batch(b, p)
+    assert lib.azg_pv_set_tuning(19, -1) == 1   # split-fp16 is the arithmetic under test
+    prev5, prev6 = lib.azg_pv_set_tuning(5, 1), lib.azg_pv_set_tuning(6, shape)
+    try:
+        m.engine.profile_enable(True)
+        probs, values = m.predict(x)
+        ran = m.engine.profile_read()
+        m.engine.profile_enable(False)
+    finally:
+        lib.azg_pv_set_tuning(5, prev5)
+        lib.azg_pv_set_tuning(6, prev6)
+    assert ("tower16" if shape == 12 else "tower") in ran, ran
+    rp, rv = ref.predict(x)
+    n64 = min(B, 256)
+    r64 = RefModel(blocks, ch, dtype=torch.float64)
+    r64.net.load_state_dict({k: (v.double() if v.dtype.is_floating_point else v)
+                             for k, v in ref.net.state_dict().items()})
+    p64, v64 = r64.predict(x[:n64])
+    for name, got, r32, r_64 in (("probs", probs, rp, p64), ("values", values, rv, v64)):
+        d32 = float(np.abs(got - r32).max())
+        print(f"{blocks}x{ch} B={B} shape {shape} {name}: |gpu-cpu32|={d32:.2e} "
+              f"|gpu-fp64|={np.abs(got[:n64] - r_64).max():.2e} |cpu32-fp64|={np.abs(r32[:n64] - r_64).max():.2e}")
+        assert d32 <= TOL, (name, d32)
+    argmax_check(probs, rp, b)
+
+
 def calib_bn(ref, seed):
     """Give BN running stats the statistics of real activations (train-mode passes
     without optimizer steps), as a trained net has."""
