@@ -648,6 +648,22 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
     float* X = h->act[0];
     float* H = h->act[1];
     float* Y = h->act[2];
+    if (variant == 13 && h->NB > 0) {
+        // the board-resident tower (pv_board.hip): every conv of one board from LDS,
+        // the tower output in place over the stem output
+        int out_off[2 * kTowerMaxBlocks];
+        for (int i = 0; i < h->NB; ++i) {
+            out_off[2 * i] = bd[h->bn_blk[i].first].out_off;
+            out_off[2 * i + 1] = bd[h->bn_blk[i].second].out_off;
+        }
+        pr = prof_begin(h, AZG_PROF_BOARD, st, batch);
+        AZG_TRY(launch_board_tower(h->NB, (const float*)h->wpack16, h->scale16, h->shift, out_off, X, batch, h->ovf_dev,
+                                   seq, st),
+                "forward: board tower");
+        prof_end(h, pr, st);
+        *out = X;
+        return 0;
+    }
     if (variant != 0 && h->NB > 0) {
         // the whole residual tower in one persistent launch
         int out_off[2 * kTowerMaxBlocks];
@@ -723,8 +739,12 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
     if (h->NB == 0 || h->NB > kTowerMaxBlocks) return 0;
     if ((size_t)batch * PADPIX * h->C * sizeof(float) >= (size_t)INT32_MAX) return 0;
     if (g_tower_mode == 0) return 0;
+    const bool board_ok = h3 && h->C == 128;   // the board-resident tower: split-fp16, C = 128 (LDS)
     if (g_tower_mode == 1)
-        return ((g_tower_shape == 10 && (h->C != 128 || h3)) || (g_tower_shape == 12 && !h3)) ? 8 : g_tower_shape;
+        return ((g_tower_shape == 10 && (h->C != 128 || h3)) || (g_tower_shape == 12 && !h3) ||
+                (g_tower_shape == 13 && !board_ok))
+                   ? 8
+                   : g_tower_shape;
     const int bucket = conv_batch_bucket(batch * PIX);
     static std::map<std::tuple<int, int, int, int>, int> cache;
     const auto key = std::make_tuple(h->C, h->NB, bucket, (int)h3);
@@ -735,10 +755,11 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
     if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return fallback;
     const bool prof = h->prof_on;
     h->prof_on = false;
-    // split-fp16: + shape 12, the h3_tile 128x128 tower (pv_h3.h)
-    const int cand[4] = {0, 5, 8, 12};
-    const int ncand = h3 ? 4 : 3;
-    float best_ms[4] = {1e30f, 1e30f, 1e30f, 1e30f};
+    // split-fp16: + shape 12, the h3_tile 128x128 tower (pv_h3.h); C = 128: + 13, the
+    // board-resident tower (pv_board.hip)
+    const int cand[5] = {0, 5, 8, 12, 13};
+    const int ncand = board_ok ? 5 : h3 ? 4 : 3;
+    float best_ms[5] = {1e30f, 1e30f, 1e30f, 1e30f, 1e30f};
     hipEvent_t e0, e1;
     int choice = fallback;
     if (hipEventCreate(&e0) == hipSuccess) {
@@ -759,12 +780,13 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
                     if (best_ms[c] < best_ms[b]) b = c;
                 if (batch >= 128 && best_ms[2] <= 1.02f * best_ms[b]) b = 2;   // the 128x64 tower
                 if (h3 && batch >= 128 && best_ms[3] < 0.98f * best_ms[b]) b = 3;   // unless h3_tile beats it by 2 %
+                if (board_ok && best_ms[4] < 0.98f * best_ms[b]) b = 4;            // or the board tower does
                 choice = cand[b];
             }
             if (getenv("AZG_TUNE_LOG"))
                 fprintf(stderr, "[azg tune] C=%d NB=%d batch=%d h3=%d ok=%d per-layer %.4f tower64 %.4f tower128 %.4f "
-                        "h3tile %.4f -> %d\n", h->C, h->NB, batch, (int)h3, (int)ok, best_ms[0], best_ms[1], best_ms[2],
-                        best_ms[3], choice);
+                        "h3tile %.4f board %.4f -> %d\n", h->C, h->NB, batch, (int)h3, (int)ok, best_ms[0], best_ms[1],
+                        best_ms[2], best_ms[3], best_ms[4], choice);
             (void)hipEventDestroy(e1);
         }
         (void)hipEventDestroy(e0);

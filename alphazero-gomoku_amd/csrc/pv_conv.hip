@@ -1014,8 +1014,14 @@ hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const fl
 
 }  // namespace azg
 
+namespace azg { extern int g_board_abl; }
 extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
 {
+    if (key == 51) {  // TEMPORARY: board-tower timing ablations
+        const int prev = azg::g_board_abl;
+        azg::g_board_abl = value;
+        return prev;
+    }
     if (key == 0) {
         const int prev = azg::g_conv_shape_override;
         azg::g_conv_shape_override = value;
@@ -1149,7 +1155,7 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     }
     if (key == 6) {   // persistent tower tile shape
         const int prev = azg::g_tower_shape;
-        if (value == 5 || value == 8 || value == 10 || value == 12) azg::g_tower_shape = value;
+        if (value == 5 || value == 8 || value == 10 || value == 12 || value == 13) azg::g_tower_shape = value;
 #ifdef AZG_AB_STUDIES
         if (value == 9) azg::g_tower_shape = value;
 #endif

@@ -82,6 +82,10 @@ struct TowerSync {
 hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const float* wpack, const float* scale,
                         const float* shift, const int* out_off, int M, const TowerSync& ts, hipStream_t st,
                         float** result, bool h3 = false);
+// board-resident split-fp16 tower (pv_board.hip, C = 128): x = the stem output, overwritten in
+// place with the tower output
+hipError_t launch_board_tower(int NB, const float* wp16, const float* scale16, const float* shift, const int* out_off,
+                              float* x, int B, unsigned* ring_ovf, unsigned seq, hipStream_t st);
 extern unsigned g_tower_wait_us;
 extern int g_tower_group;
 #ifdef AZG_AB_STUDIES

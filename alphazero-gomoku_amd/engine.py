@@ -269,14 +269,16 @@ class PolicyValueEngine:
     def profile_read(self) -> dict:
         """{class: (ms_total, launches)} since the last profile_enable (synchronises)."""
         from _native import PROF_CLASSES
-        ms = (ctypes.c_double * 8)()
-        n = (ctypes.c_int64 * 8)()
+        k = len(PROF_CLASSES)
+        ms = (ctypes.c_double * k)()
+        n = (ctypes.c_int64 * k)()
         check(self.lib.azg_pv_profile_read(self.h, ms, n), self.lib)
-        return {PROF_CLASSES[i]: (ms[i], int(n[i])) for i in range(8) if n[i]}
+        return {PROF_CLASSES[i]: (ms[i], int(n[i])) for i in range(k) if n[i]}
 
     def profile_boards(self) -> dict:
         """{class: boards processed} since the last profile_enable."""
         from _native import PROF_CLASSES
-        b = (ctypes.c_int64 * 8)()
+        k = len(PROF_CLASSES)
+        b = (ctypes.c_int64 * k)()
         check(self.lib.azg_pv_profile_boards(self.h, b), self.lib)
-        return {PROF_CLASSES[i]: int(b[i]) for i in range(8) if b[i]}
+        return {PROF_CLASSES[i]: int(b[i]) for i in range(k) if b[i]}

@@ -65,6 +65,14 @@ def conv_peak():
     return PEAK_F32_MFMA, "f32"
 
 
+def train_fwd_peak():
+    """(peak FLOP/s of the train step's forward convs, label) for tuning key 49: 2 (default)
+    split-fp16 with four products (the F16 MFMA peak / 4), 1 three products, 0 fp32 MFMA."""
+    import _native
+    k = _native.load_library().azg_pv_set_tuning(49, -1)
+    return {2: (PEAK_F16_MFMA / 4, "f16x4"), 1: (PEAK_F16_MFMA / 3, "f16x3")}.get(k, (PEAK_F32_MFMA, "f32"))
+
+
 def conv_flop(ch: int) -> int:
     """One 3x3 C->C conv on one 15x15 board: 2 * 225 * C * 9C."""
     return 2 * 225 * ch * 9 * ch
@@ -280,7 +288,8 @@ def traffic_records():
 
 
 # profile class -> (convs per launch as a multiple of blocks (0: one conv), PMC record shape prefix)
-TOWER_CLASSES = {"tower16": (2, "conv_tower<128, 128, 4, 1, 16"), "tower": (2, "conv_tower<"), "conv3x3": (0, None)}
+TOWER_CLASSES = {"tower16": (2, "conv_tower<128, 128, 4, 1, 16"), "tower": (2, "conv_tower<"),
+                 "board": (2, "board_tower"), "conv3x3": (0, None)}
 
 
 def roofline_from_profile(prof, boards, blocks, ch, knames, traffic=True):
@@ -313,12 +322,26 @@ def roofline_from_profile(prof, boards, blocks, ch, knames, traffic=True):
         out["peak_basis"] = ("split-fp16 products: 3 v_mfma_f32_32x32x16_f16 per fp32-equivalent product, "
                              "dense F16 MFMA peak 2516.8 TFLOP/s / 3; achieved counts the fp32-equivalent conv "
                              "FLOPs (2 x 225 x C x 9C per board per conv)")
-        out["frac_of_fp32_mfma_peak"] = round(achieved / PEAK_F32_MFMA, 4)
+        # a ratio, not a fraction: the split tower's fp32-equivalent rate over the fp32-MFMA peak
+        out["speedup_over_fp32_mfma_peak"] = round(achieved / PEAK_F32_MFMA, 4)
     out.update({k: v for k, v in d.items() if not k.startswith("_") and k != "frac"})
     pref = TOWER_CLASSES[dom][1]
     h3 = peak == PEAK_H3
     if h3 and dom == "tower16":   # split-fp16: class 7 is the h3_tile 128x128 tower (shape 12, VAR 355)
         pref = f"conv_tower<{ch}, 128, 2, 2, 4, 355"
+    if dom == "board":            # traffic records of the board-resident tower are keyed "board_tower"
+        pref = None
+        recs = [r for r in traffic_records() if r.get("kernel") == "board" and
+                r.get("config", "").startswith(f"{blocks}x{ch}_B")]
+        if traffic and recs:
+            bpl = d["boards_per_launch"]
+            r = min(recs, key=lambda r: abs(r["boards_per_launch"] - bpl))
+            out["traffic"] = round(r["hbm_bytes_per_launch"] / r["boards_per_launch"] * bpl)
+            out["traffic_over_algorithmic"] = r["traffic_over_algorithmic"]
+            out["traffic_basis"] = (f"PMC FETCH_SIZE x2 + WRITE_SIZE of board_tower at {r['config']} ({r['tag']}): "
+                                    f"{r['hbm_bytes_per_launch'] / 1e6:.1f} MB per launch, "
+                                    f"{r['traffic_over_algorithmic']}x algorithmic; scaled per board to this run's "
+                                    f"average launch ({bpl} boards)")
     if traffic and pref:
         net = f"{blocks}x{ch}_B"
         # the split-fp16 128x64 towers: halo_tile VAR 99 (98 before round 5's end); h3_tile VAR 355
@@ -347,7 +370,10 @@ def roofline_from_profile(prof, boards, blocks, ch, knames, traffic=True):
 
 def tower_knames(ch, blocks):
     n = 2 * blocks
-    return {"tower16": (f"azg::conv_tower<{ch},128,2,2,4,355> (persistent residual tower, h3_tile 128x128 tiles: 4 "
+    return {"board": (f"azg::board_tower (board-resident residual tower: one board per 16-wave workgroup, its "
+                      f"activations in LDS as split fp16 through all {n} fused 3x3 conv + BN (+ residual) + ReLU "
+                      f"layers, split-fp16 products, LDS-DMA weight stages)"),
+            "tower16": (f"azg::conv_tower<{ch},128,2,2,4,355> (persistent residual tower, h3_tile 128x128 tiles: 4 "
                         f"waves of 64x64, split-fp16 products, LDS-DMA weight stages: {n} fused 3x3 conv + BN "
                         f"(+ residual) + ReLU layers per launch)" if conv_peak()[0] == PEAK_H3 else
                         f"azg::conv_tower<{ch},128,4,1,16,16> (persistent residual tower, 16-wave 128x128 tiles, one "
@@ -543,7 +569,11 @@ def forward_leg(model, args, rank, world, dist, dev, local, blocks=BLOCKS, ch=CH
                       f"inputs resident in HBM",
             "boards_per_s": round(B * steps * world / elapsed, 1), "ms_per_step": round(elapsed / steps * 1e3, 4),
             "steps": steps, "warmup": warmup,
-            "whole_forward_mfma_frac": round(B * steps / elapsed * fwd_flop(blocks, ch) / PEAK_F32_MFMA, 4),
+            # the whole forward against the peaks of the instructions it issues: its residual
+            # convs at the conv roofline (split-fp16: F16 peak / 3), stem and heads at fp32
+            "whole_forward_frac_of_instruction_peak": round(
+                (2 * blocks * conv_flop(ch) / conv_peak()[0] + (fwd_flop(blocks, ch) - 2 * blocks * conv_flop(ch))
+                 / PEAK_F32_MFMA) * B * steps / elapsed, 4),
             "kernel_ms_per_step": {k: round(v[0] / steps, 4) for k, v in prof.items()},
             "tower_waits_rank0": waits, "roofline": roof}
 
@@ -574,13 +604,21 @@ def train_leg(model, args, rank, world, dist, dev, local, blocks=BLOCKS, ch=CHAN
     assert torch.isfinite(losses).all()
     model.grad_hook = None
     flop = train_flop(blocks, ch) * B
+    fwd_conv = 2 * blocks * conv_flop(ch) * B
+    fwd_peak, fwd_label = train_fwd_peak()
     nparam = model.engine.nparam
     coll = "RCCL" if dist is not None and dist.get_backend() == "nccl" else "gloo (shared-GPU rehearsal)"
     return {"config": f"{blocks}x{ch}, {B} samples/GPU (global {B * world}), "
                       f"{f'{coll} all-reduce of the flat fp32 gradient ({nparam * 4 / 1e6:.2f} MB) + ' if world > 1 else ''}"
                       f"clip 3.0 + Adam",
             "samples_per_s": round(B * K * world / dt, 1), "ms_per_step": round(dt / K * 1e3, 3), "steps": K,
-            "flop_per_step": flop, "mfma_frac": round(flop / (dt / K) / PEAK_F32_MFMA, 4)}
+            "flop_per_step": flop,
+            # against the peaks of the instructions the step issues: the forward convs at the
+            # key-49 arithmetic's roofline (default: four split-fp16 products, F16 peak / 4),
+            # data and weight gradients, stem and heads at the fp32-MFMA peak
+            "frac_of_instruction_peak": round((fwd_conv / fwd_peak + (flop - fwd_conv) / PEAK_F32_MFMA) / (dt / K), 4),
+            "peak_basis": f"forward convs {fwd_label} ({fwd_peak / 1e12:.1f} TFLOP/s), everything else fp32 MFMA "
+                          f"({PEAK_F32_MFMA / 1e12:.1f} TFLOP/s)"}
 
 
 def pente_leg(args, rank, world, dist, dev, local):

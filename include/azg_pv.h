@@ -149,14 +149,16 @@ enum {
                                 64x64 / 128x64 tiles, 2-4 workgroups per CU          */
     AZG_PROF_TOWER_WIDE = 7, /* the same with 128x128 tiles: 16 waves, 1 workgroup per CU
                                 (fp32), or h3_tile's 4 waves of 64x64 (split-fp16, shape 12) */
-    AZG_PROF_NCLASS = 8
+    AZG_PROF_BOARD = 8,      /* the board-resident tower (split-fp16, C = 128, shape 13): one
+                                board's activations in LDS through all 2*NB convs */
+    AZG_PROF_NCLASS = 9
 };
 int32_t azg_pv_profile_enable(azg_pv* h, int32_t enable);
 int32_t azg_pv_profile_read(azg_pv* h, double* ms, int64_t* launches);
 /* Boards (eval) / samples (train) processed per class since the last enable, so a
  * caller can price launches of varying batch (self-play) in algorithmic FLOPs.
- * A residual-conv launch (CONV3X3) counts its batch once per conv; a TOWER launch
- * counts its batch once for all 2*blocks convs. */
+ * A residual-conv launch (CONV3X3) counts its batch once per conv; a TOWER / TOWER_WIDE /
+ * BOARD launch counts its batch once for all 2*blocks convs. */
 int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
 
 /* Process-wide tuning knobs (benchmarks / A-B tests).  Returns the previous value.
@@ -171,8 +173,10 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          timing every variant on first use -- all bitwise identical;
  *   key 6: persistent-tower tile shape for key 5 = 1 (8: 128x64 / 8 waves, default;
  *          5: 64x64 / 4 waves; 10: 128x128 / 16 waves, one workgroup per CU, C = 128, fp32
- *          only; 12: h3_tile 128x128 / 4 waves of 64x64, split-fp16 only -- a shape the
- *          current arithmetic lacks runs as 8);
+ *          only; 12: h3_tile 128x128 / 4 waves of 64x64, split-fp16 only; 13: the
+ *          board-resident tower (pv_board.hip: one board per 16-wave workgroup, its
+ *          activations in LDS through every conv), split-fp16 and C = 128 only -- a shape
+ *          the current arithmetic lacks runs as 8);
  *   keys 3, 7, 8: timing-only ablation switches (results invalid while set);
  *   key 10: tile-body variant of the C=128 128x64 persistent tower (0 = default;
  *          1..5 = swizzle / prefetch / LDS-DMA staging variants for A/B timing, all

@@ -1,0 +1,40 @@
+"""TEMPORARY: timing ablations of the board-resident tower (key 51; results invalid while set)."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "alphazero-gomoku_amd")]
+import torch  # noqa: E402
+
+
+def main():
+    import _native
+    import bench
+    from network import PyTorchModel
+    from synth import synth_encoded
+    lib = _native.load_library()
+    torch.manual_seed(0)
+    m = PyTorchModel(board_size=15, device="cuda", n_res_blocks=6, channels=128)
+    eng = m.engine
+    lib.azg_pv_set_tuning(5, 1)
+    lib.azg_pv_set_tuning(6, 13)
+    flop = 12 * bench.conv_flop(128)
+    for B in (2048, 4096):
+        x = torch.from_numpy(synth_encoded(B, seed=B)).cuda()
+        for abl in [int(a) for a in os.environ.get('ABLS', '0,1,2,4,7,8,16,24,0').split(',')]:
+            lib.azg_pv_set_tuning(51, abl)
+            eng.forward(x)
+            torch.cuda.synchronize()
+            eng.profile_enable(True)
+            for _ in range(5):
+                eng.forward(x)
+            prof = eng.profile_read()
+            eng.profile_enable(False)
+            ms = prof["board"][0] / 5
+            print(f"B={B} abl {abl}: {ms:.3f} ms = {flop * B / ms / 1e9:.1f} TFLOP/s", flush=True)
+        lib.azg_pv_set_tuning(51, 0)
+        eng.clear_status()
+
+
+if __name__ == "__main__":
+    main()

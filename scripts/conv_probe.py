@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--coh", type=int, default=0, help="study build: round-2 sc1 tower hand-off at 2 WG/CU (key 31)")
     ap.add_argument("--abl", type=int, default=0, help="study build: tower ablation bits (key 8; 4 no weight loads, 8 no halo loads)")
     ap.add_argument("--group", type=int, default=1, help="tower claims (key 17: 0 tile, 1 M tile)")
+    ap.add_argument("--board-abl", type=int, default=0, help="board tower timing ablations (key 51; results invalid)")
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--channels", type=int, default=128)
     ap.add_argument("--check", action="store_true", help="compare the outputs bitwise with the 128x64 tower (shape 8)")
@@ -41,6 +42,8 @@ def main():
     lib.azg_pv_set_tuning(31, args.coh)
     lib.azg_pv_set_tuning(8, args.abl)
     lib.azg_pv_set_tuning(17, args.group)
+    if args.board_abl:
+        lib.azg_pv_set_tuning(51, args.board_abl)
     from network import PyTorchModel
     from synth import synth_encoded
     dev = torch.device("cuda", 0)

@@ -20,7 +20,7 @@ def main():
         if not os.path.exists(f):
             continue
         for r in csv.DictReader(open(f)):
-            m = re.search(r"(lab_conv|lab_h3|conv_tower)<([\d, ]+)>", r["Kernel_Name"])
+            m = re.search(r"(lab_conv|lab_h3|conv_tower|board_tower)<([\d, ]+)>", r["Kernel_Name"])
             if m:
                 acc[m.group(1) + "<" + m.group(2) + ">"][r["Counter_Name"]].append(float(r["Counter_Value"]))
     print("| lab_conv<C, BN, WM, TM, NW, VAR, WPE> | MFMA busy | LDS-array busy | wait_any | wait_inst | "
@@ -32,6 +32,8 @@ def main():
         mf = g("SQ_VALU_MFMA_BUSY_CYCLES") / (256 * 4 * gui)
         lds = g("SQ_LDS_IDX_ACTIVE") / (256 * gui)
         wc = g("SQ_WAVE_CYCLES")
+        if d.get("GRBM_GUI_ACTIVE") and d.get("_dur"):
+            pass
         print(f"| {k} | {mf:.3f} | {lds:.3f} | {g('SQ_WAIT_ANY') / wc:.3f} | {g('SQ_WAIT_INST_ANY') / wc:.3f} | "
               f"{g('SQ_WAIT_INST_LDS') / wc:.3f} | {g('SQ_ACTIVE_INST_ANY') / wc:.3f} | "
               f"{g('SQ_INSTS_LDS') / g('SQ_INSTS_MFMA'):.2f} | {g('SQ_INSTS_VALU') / g('SQ_INSTS_MFMA'):.2f} | "

@@ -283,7 +283,8 @@ def test_persistent_tower_bitwise_equals_per_layer_launches(blocks, ch, batches)
             lib.azg_pv_set_tuning(5, 0)
             p0, v0, l0 = eng.forward(x, want_logits=True)
             lib.azg_pv_set_tuning(5, 1)
-            for shape in ((5, 8, 10, 12) if ch == 128 else (5, 8, 12)):   # 12: h3_tile (split-fp16 only)
+            # 12: h3_tile, 13: the board-resident tower (split-fp16 only; 13 needs C = 128)
+            for shape in ((5, 8, 10, 12, 13) if ch == 128 else (5, 8, 12)):
                 lib.azg_pv_set_tuning(6, shape)
                 for group in (0, 1):   # claims (key 17): one tile, one M tile
                     prev_group = lib.azg_pv_set_tuning(17, group)
