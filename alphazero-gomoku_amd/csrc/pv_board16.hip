@@ -1,0 +1,410 @@
+// Board-resident residual tower on 16x16x32 products (split fp16, C = 128): the eval
+// forward's 2*NB residual convs (network.py:98-99, ResidualBlock network.py:9-26), one
+// board per 12-wave workgroup with the board's activations in LDS from the stem output to
+// the tower output -- pv_board.hip's structure on v_mfma_f32_16x16x32_f16.
+//
+// Why a second board tower: on gfx950 a CU streaming 16x16x32 f16 MFMAs sustains ~1.2x the
+// FLOP/s of one streaming 32x32x16 (scripts/lab/mfma_clock.hip: 2.05 vs 1.69 PFLOP/s
+// chip-wide, the same instruction peak -- the clock the power limit allows), and 16-row
+// fragments pad a board's 225 pixels to 240 rows instead of 256.  A 16x16x32 product sums
+// 32 channels per instruction, so this tower is its own arithmetic class (key 19 = 2):
+// within it every batch and every board computes the same MFMA sequence per element
+// (batch-independent, as the K16 forms are among themselves), and it matches the fp32
+// oracle to the split-fp16 tolerance.
+//
+// Work split: 15 M fragments of 16 pixels (the last holds pixel 224 only) x 8 N fragments
+// of 16 channels; wave w owns M fragments 5 (w % 3) .. +4 and the output channel group
+// w / 3 (32 channels: 2 N fragments) -- an 80x32 wave tile, per K32 step 10 A and 4 B
+// fragment reads for 30 MFMAs.
+//
+// Numerics: per output element one chain over channel groups cg, taps 0..8 and the three
+// products lo_a hi_b, hi_a lo_b, hi_a hi_b (channels 32 cg + 8 (lane >> 4) + 0..7 of each
+// lane, the pack_h3 order), then the eval epilogue relu(fmaf(acc, scale, shift) [+ the
+// block input]).  A non-finite accumulator (an activation at or above 65520) posts the
+// launch to the H3 overflow ring; azg_pv_recover recomputes it in fp32.
+//
+// LDS rows: per channel group a [226][128 B] image (pixels 0..224, then a zero row: the
+// neighbour of an off-board tap); a row's 16-B slots are {hi c 0-7, 8-15, 16-23, 24-31, lo
+// ...} stored at slot ^ (row & 6).  That key keeps every ds_read_b128 of an A fragment
+// conflict-free for every tap shift (a 16-lane bank group reads rows b + {0-3, 12-15} at
+// slot k and b + {4-11} at slot k ^ 1, for any b), the B reads (weight rows, b = 0) and the
+// epilogue's 4-B stores too.
+#include "pv_internal.h"
+
+namespace azg {
+
+constexpr int kB16C = 128;
+constexpr int kB16Groups = kB16C / 32;
+constexpr int kB16Rows = PIX + 1;                             // 225 pixels + the zero row
+constexpr int kB16Stage = kB16C * 128;                        // one (tap, cg) weight chunk: 128 rows x [hi 32 | lo 32]
+constexpr int kB16Act = 2 * kB16Stage;                        // LDS: [2] weight stages, then the activations
+constexpr int kB16Prow = kB16Act + kB16Groups * kB16Rows * 128;
+constexpr int kB16Lds = kB16Prow + 240 * 4;                   // 149,440 B: one workgroup per CU
+constexpr int kB16Waves = 12;
+constexpr int kB16Threads = 64 * kB16Waves;
+constexpr int kB16MaxLayers = 2 * kTowerMaxBlocks;
+constexpr int kB16Steps = 9 * kB16Groups;                     // K32 steps (weight chunks) per conv
+static_assert((kB16Groups * kB16Rows * 128) % 256 == 0, "a group's image keeps the 256-B bank phase");
+static_assert(kB16Steps % 2 == 0, "step s of every conv uses stage s & 1");
+
+struct Board16Args {
+    const float* wp[kB16MaxLayers];     // split-fp16 packs (pack_h3: [tap*CG + cg][cout][hi 32 | lo 32])
+    const float* scale[kB16MaxLayers];  // H3 BN scale (carries the pack's 2^-e) and shift
+    const float* shift[kB16MaxLayers];
+    float* x;                           // padded NHWC [B][17][17][128]: stem output in, tower output out
+    int B;
+    int nlayers;
+    unsigned* ring_ovf;                 // host-mapped H3 overflow ring (device alias)
+    unsigned seq;                       // launch number (0: autotuning runs, never posted)
+};
+
+typedef float b16_f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 b16_f16x2 __attribute__((ext_vector_type(2)));
+
+// Eval epilogue of one conv for a wave's 80x32 tile: element i of tile (f, n) is pixel
+// 80 mg + 16 f + 4 kb + i, channel 32 cg + 16 n + r16.  RES (conv2): the block input is
+// read from and the block output written to the board's padded NHWC rows in HBM (in place,
+// the same lane reads then writes each element) through a buffer resource: a padding
+// pixel's row offset lies past the resource, so its load returns 0 and its store is
+// dropped (no branches).  TO_LDS: y becomes the next conv's operand, [hi | lo] fp16 in the
+// keyed rows: lane pairs (channels 2k, 2k + 1 of one pixel) exchange y by DPP, both split
+// the pair (own value first), and the even lane stores the hi pair, the odd lane the lo
+// pair with its halves swapped (one v_perm).  Element pairs (i, i + 1) go through packed
+// fp32 math (v_pk_fma / v_pk_add: per element the same fmaf and add).  Returns whether an
+// accumulator was non-finite (their sum is: padding accumulators are exactly 0).
+template <bool RES, bool TO_LDS>
+__device__ __forceinline__ bool b16_epilogue(const f32x4 (&acc)[5][2], const float* __restrict__ scale,
+                                             const float* __restrict__ shift, __amdgpu_buffer_rsrc_t xr, char* lds,
+                                             const int* poff, int mg, int cg, int lane)
+{
+    asm volatile("" : "+v"(lane));   // the epilogue's addresses are rebuilt per conv, not hoisted (they would spill)
+    const int r16 = lane & 15, kb = lane >> 4, odd = r16 & 1, ce = r16 & 14;
+    // the lane's part of a store offset in a keyed row: slot (ce >> 3) ^ 4 (kb & 1), channel
+    // ce & 7, lo half for the odd lane; the tile's 32 (n ^ (i >> 1)) and the row i * 128 are
+    // immediates (row m = m0 + i has key 4 (kb & 1) | (i & 2))
+    const int lpart = (16 * ((ce >> 3) ^ (4 * (kb & 1))) + 2 * (ce & 7)) ^ (odd ? 64 : 0);
+    const unsigned sel = odd ? 0x05040706u : 0x03020100u;   // odd: the lo pair, halves swapped
+    float sc[2], sh[2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+        sc[n] = scale[32 * cg + 16 * n + r16];
+        sh[n] = shift[32 * cg + 16 * n + r16];
+    }
+    const int cbyte = 4 * (32 * cg + r16);
+    b16_f32x2 chk = {0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+        const int m0 = 80 * mg + 16 * f + 4 * kb;
+        int vo[4];
+        if constexpr (RES) {
+            const int4 p4 = *(const int4*)(poff + m0);
+            vo[0] = p4.x + cbyte, vo[1] = p4.y + cbyte, vo[2] = p4.z + cbyte, vo[3] = p4.w + cbyte;
+        }
+        float rv[2][4];
+        if constexpr (RES) {
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    rv[n][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo[i] + 64 * n, 0, 0));
+        }
+        char* wrow = lds + kB16Act + (cg * kB16Rows + m0) * 128 + lpart;
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int ip = 0; ip < 2; ++ip) {
+                const b16_f32x2 v = {acc[f][n][2 * ip], acc[f][n][2 * ip + 1]};
+                chk += v;
+                b16_f32x2 y = __builtin_elementwise_fma(v, b16_f32x2{sc[n], sc[n]}, b16_f32x2{sh[n], sh[n]});
+                if constexpr (RES) y += b16_f32x2{rv[n][2 * ip], rv[n][2 * ip + 1]};
+                const float ye[2] = {fmaxf(y.x, 0.f), fmaxf(y.y, 0.f)};
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int i = 2 * ip + e;
+                    const float yv = ye[e];
+                    if constexpr (RES)
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, yv), xr, vo[i] + 64 * n, 0, 0);
+                    if constexpr (TO_LDS) {
+                        const float yo = __builtin_bit_cast(
+                            float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, yv), 0xB1, 0xF, 0xF, false));
+                        const b16_f32x2 yy = {yv, yo};
+                        const b16_f16x2 hp = __builtin_convertvector(yy, b16_f16x2);
+                        const b16_f16x2 lp = __builtin_convertvector(yy - __builtin_convertvector(hp, b16_f32x2), b16_f16x2);
+                        const unsigned word = __builtin_amdgcn_perm(__builtin_bit_cast(unsigned, lp),
+                                                                    __builtin_bit_cast(unsigned, hp), sel);
+                        if (f < 4 || m0 + i < PIX)   // (padding rows past pixel 224 stay unwritten)
+                            *(unsigned*)(wrow + i * 128 + 32 * (n ^ (i >> 1))) = word;
+                    }
+                }
+            }
+    }
+    return !__builtin_isfinite(chk.x + chk.y);
+}
+
+extern int g_board_abl;
+template <int ABL>
+__global__ __launch_bounds__(kB16Threads, 1) void board16_tower(const Board16Args a)
+{
+    extern __shared__ __attribute__((aligned(16))) float smem_f[];
+    char* lds = (char*)smem_f;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int mg = wid % 3, ng = wid / 3;
+    const int r16 = lane & 15, kb = lane >> 4;
+    int* poff = (int*)(lds + kB16Prow);   // byte offset of each pixel's padded row (padding: past the board)
+
+    // padded row of every pixel (-1 past pixel 224), the groups' zero rows
+    for (int i = tid; i < 240; i += kB16Threads)
+        poff[i] = i < PIX ? ((i / BOARD + 1) * PADW + i % BOARD + 1) * kB16C * 4 : 0x40000000;
+    if (tid < kB16Groups * 32) ((float*)(lds + kB16Act + ((tid >> 5) * kB16Rows + PIX) * 128))[tid & 31] = 0.f;
+
+    // this lane's A rows (pixel 80 mg + 16 f + r16 of fragment f) and the taps on the board
+    int pf[5];
+    unsigned tm[5];
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+        const int p = 80 * mg + 16 * f + r16;
+        const int py = p / BOARD, px = p - py * BOARD;
+        unsigned t = 0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int yy = py + k / 3 - 1, xx = px + k % 3 - 1;
+            if (p < PIX && yy >= 0 && yy < BOARD && xx >= 0 && xx < BOARD) t |= 1u << k;
+        }
+        pf[f] = p;
+        tm[f] = t;
+    }
+    // B fragments: weight row n = 32 ng + 16 j + r16, slot kb (hi) / kb ^ 4 (lo), keyed by n & 6 = r16 & 6
+    const int bh0 = (32 * ng + r16) * 128 + 16 * (kb ^ (r16 & 6));
+    const int bl0 = bh0 ^ 64;
+
+    // weight DMA of one chunk (16 KB, 128 rows x 128 B): wave w moves rows 8 w .. 8 w + 7,
+    // waves 0..3 also rows 96 + 8 w ..; lane -> row + lane / 8, LDS slot lane % 8 holding
+    // source slot (lane % 8) ^ (row & 6)
+    const int wr0 = 8 * wid + (lane >> 3);
+    const int ws0 = wr0 * 32 + (((lane & 7) ^ (wr0 & 6)) * 4);
+    const int wr1 = 96 + 8 * (wid & 3) + (lane >> 3);
+    const int ws1 = wr1 * 32 + (((lane & 7) ^ (wr1 & 6)) * 4);
+    auto dma = [&](const float* wl, int s, int buf) {   // chunk s = cg * 9 + tap -> stage buf
+        const int cg = s / 9, tap = s - cg * 9;
+        const float* src = wl + (size_t)(tap * kB16Groups + cg) * kB16C * 32;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + ws0),
+                                         (__attribute__((address_space(3))) void*)(lds + buf * kB16Stage + wid * 1024),
+                                         16, 0, 0);
+        if (wid < 4)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + ws1),
+                                             (__attribute__((address_space(3))) void*)(lds + buf * kB16Stage + (12 + wid) * 1024),
+                                             16, 0, 0);
+    };
+
+    const int nl = a.nlayers;
+    int board = blockIdx.x;
+    if (board < a.B) {   // the first conv's chunks 0 and 1
+        dma(a.wp[0], 0, 0);
+        dma(a.wp[0], 1, 1);
+    }
+    __syncthreads();   // poff / zero rows
+    for (; board < a.B; board += gridDim.x) {
+        float* xb = a.x + (size_t)board * PADPIX * kB16C;
+        const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(xb, (short)0, PADPIX * kB16C * 4, 0x00020000);
+        int t8 = tid;
+        asm volatile("" : "+v"(t8));   // the staging addresses are rebuilt per board, not kept live
+        // ---- the board's stem output -> hi / lo rows [group][pixel], in two halves of 5
+        // float4 per thread (all 10 in flight at once would spill) ----
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            constexpr int kIt = 5;
+            f32x4 v[kIt];
+#pragma unroll
+            for (int k = 0; k < kIt; ++k) {
+                const int i = t8 + (half * kIt + k) * kB16Threads;   // (pixel, float4 of 128 channels)
+                if (i < PIX * 32) v[k] = *(const f32x4*)((const char*)xb + poff[i >> 5] + (i & 31) * 16);
+            }
+#pragma unroll
+            for (int k = 0; k < kIt; ++k) {
+                const int i = t8 + (half * kIt + k) * kB16Threads;
+                if (i < PIX * 32) {
+                    const int m = i >> 5, c4 = i & 31, g = c4 >> 3, q4 = c4 & 7;
+                    f16x4 hi, lo;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        hi[e] = (_Float16)v[k][e];
+                        lo[e] = (_Float16)(v[k][e] - (float)hi[e]);
+                    }
+                    char* row = lds + kB16Act + (g * kB16Rows + m) * 128;
+                    const int o = 16 * ((q4 >> 1) ^ (m & 6)) + (q4 & 1) * 8;
+                    *(f16x4*)(row + o) = hi;
+                    *(f16x4*)(row + (o ^ 64)) = lo;
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of the first chunks
+        __syncthreads();
+        const bool more_boards = board + (int)gridDim.x < a.B;
+
+        for (int l = 0; l < nl; ++l) {
+            f32x4 acc[5][2];
+#pragma unroll
+            for (int f = 0; f < 5; ++f)
+#pragma unroll
+                for (int n = 0; n < 2; ++n) acc[f][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+            // this conv's and the next one's weights (scalar, loaded once per conv); the next
+            // conv's chunks 0 and 1 are issued during steps 34 and 35
+            const float* wl = a.wp[l];
+            const float* wn = l + 1 < nl ? a.wp[l + 1] : a.wp[0];
+            const bool more = l + 1 < nl || more_boards;
+            // A rows of (cg, tap) for fragment f: neighbour pixel q (the group's zero row off
+            // the board), rebuilt per tap (45 hoisted row addresses would not fit)
+            auto arow = [&](int cg, int tap, int f) {
+                if constexpr ((ABL & 8) != 0) return kB16Act + (cg * kB16Rows + pf[f]) * 128 + 16 * (kb ^ (pf[f] & 6));
+                asm volatile("" : "+v"(tm[f]), "+v"(pf[f]));
+                const int d = (tap / 3 - 1) * BOARD + (tap % 3 - 1);
+                const int q = ((tm[f] >> tap) & 1) ? pf[f] + d : PIX;
+                return kB16Act + (cg * kB16Rows + q) * 128 + 16 * (kb ^ (q & 6));
+            };
+            // step 0's operands; then every wave holds chunk 0's B fragments and stage 0 may
+            // be refilled
+            f16x8 bh[2], bl[2], ah[5], al[5];
+#pragma unroll
+            for (int f = 0; f < 5; ++f) {
+                const int ao = arow(0, 0, f);
+                al[f] = *(const f16x8*)(lds + (ao ^ 64));
+                ah[f] = *(const f16x8*)(lds + ao);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                bh[j] = *(const f16x8*)(lds + bh0 + j * 2048);
+                bl[j] = *(const f16x8*)(lds + bl0 + j * 2048);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __syncthreads();
+            // K32 step s = 9 cg + tap computes from registers read during step s - 1: chunk
+            // s + 1 was published by the barrier ending step s - 1 and the conv's input is
+            // static, so step s + 1's fragments are read between this step's product groups
+            // (each into the registers its group just released); chunk s + 2 is issued into
+            // the stage chunk s used (read during step s - 1: every wave is past it)
+            for (int cg = 0; cg < kB16Groups; ++cg) {
+#pragma unroll
+                for (int tap = 0; tap < 9; ++tap) {
+                    const int s = cg * 9 + tap;
+                    const int buf = (cg + tap) & 1;   // = s & 1
+                    if (tap < 7 || cg + 1 < kB16Groups) dma(wl, s + 2, buf);
+                    else if (more) dma(wn, s + 2 - kB16Steps, buf);
+                    const bool nx = tap < 8 || cg + 1 < kB16Groups;   // (scalar)
+                    const int ncg = tap < 8 ? cg : cg + 1, ntap = tap < 8 ? tap + 1 : 0;
+                    const char* bn = lds + (buf ^ 1) * kB16Stage;
+                    // per element the chain lo_a hi_b, hi_a hi_b, hi_a lo_b, product-major over
+                    // the 10 tiles (no MFMA waits on the one before)
+#pragma unroll
+                    for (int f = 0; f < 5; ++f)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[f], bh[j], acc[f][j], 0, 0, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    int ao[5];
+                    if (nx) {
+#pragma unroll
+                        for (int f = 0; f < 5; ++f) {
+                            ao[f] = arow(ncg, ntap, f);
+                            al[f] = *(const f16x8*)(lds + (ao[f] ^ 64));
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int f = 0; f < 5; ++f)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[f], bh[j], acc[f][j], 0, 0, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (nx) {
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) bh[j] = *(const f16x8*)(bn + bh0 + j * 2048);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int f = 0; f < 5; ++f)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[f], bl[j], acc[f][j], 0, 0, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (nx) {
+#pragma unroll
+                        for (int f = 0; f < 5; ++f) ah[f] = *(const f16x8*)(lds + ao[f]);
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) bl[j] = *(const f16x8*)(bn + bl0 + j * 2048);
+                    }
+                    // chunk s + 2 has landed (this wave's pieces); the barrier publishes it for
+                    // step s + 1's reads, and every wave's reads of chunk s + 1 are complete (its
+                    // stage takes chunk s + 3)
+                    if constexpr (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if constexpr (!(ABL & 2)) __syncthreads();
+                    else __builtin_amdgcn_s_waitcnt(0xc07f);
+                }
+            }
+
+            // ---- epilogue: BN (+ block input) + ReLU; every wave is past its last read of
+            // this conv's input (the barrier above) ----
+            const float *sc = a.scale[l], *sh = a.shift[l];
+            bool bad = false;
+            if (ABL & 4) {
+                float t = 0.f;
+#pragma unroll
+                for (int f = 0; f < 5; ++f)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) t += acc[f][j][0] + acc[f][j][1] + acc[f][j][2] + acc[f][j][3];
+                if (t == 1234.5f) xb[tid] = t;
+            }
+            else if (!(l & 1)) bad = b16_epilogue<false, true>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
+            else if (l + 1 < nl) bad = b16_epilogue<true, true>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
+            else bad = b16_epilogue<true, false>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
+            if (bad && a.ring_ovf && a.seq)
+                __hip_atomic_store(a.ring_ovf + (a.seq & (kTowerRing - 1)), a.seq, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            // the next conv reads what every wave wrote; the block output is written
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+    }
+}
+
+hipError_t launch_board16_tower(int NB, const float* wp16, const float* scale16, const float* shift,
+                                const int* out_off, float* x, int B, unsigned* ring_ovf, unsigned seq, hipStream_t st)
+{
+    if (2 * NB > kB16MaxLayers || NB <= 0 || B <= 0) return hipErrorInvalidValue;
+    static int grid = 0;
+    if (grid == 0) {
+        hipError_t e = hipSuccess;
+        for (const void* f : {(const void*)board16_tower<0>, (const void*)board16_tower<3>, (const void*)board16_tower<4>,
+                              (const void*)board16_tower<8>, (const void*)board16_tower<15>})
+            if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kB16Lds)) != hipSuccess) return e;
+        int per_cu = 0, dev = 0, cus = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)board16_tower<0>, kB16Threads, kB16Lds);
+        if (e != hipSuccess) return e;
+        if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+        if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+        if (per_cu < 1) return hipErrorInvalidConfiguration;
+        grid = per_cu * cus;
+    }
+    Board16Args a{};
+    for (int l = 0; l < 2 * NB; ++l) {
+        a.wp[l] = wp16 + (size_t)l * 9 * kB16C * kB16C;
+        a.scale[l] = scale16 + out_off[l];
+        a.shift[l] = shift + out_off[l];
+    }
+    a.x = x;
+    a.B = B;
+    a.nlayers = 2 * NB;
+    a.ring_ovf = ring_ovf;
+    a.seq = seq;
+    const dim3 g(B < grid ? B : grid);
+    switch (g_board_abl) {
+        case 3: hipLaunchKernelGGL(board16_tower<3>, g, dim3(kB16Threads), kB16Lds, st, a); break;
+        case 4: hipLaunchKernelGGL(board16_tower<4>, g, dim3(kB16Threads), kB16Lds, st, a); break;
+        case 8: hipLaunchKernelGGL(board16_tower<8>, g, dim3(kB16Threads), kB16Lds, st, a); break;
+        case 15: hipLaunchKernelGGL(board16_tower<15>, g, dim3(kB16Threads), kB16Lds, st, a); break;
+        default: hipLaunchKernelGGL(board16_tower<0>, g, dim3(kB16Threads), kB16Lds, st, a); break;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace azg

@@ -648,7 +648,7 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
     float* X = h->act[0];
     float* H = h->act[1];
     float* Y = h->act[2];
-    if (variant == 13 && h->NB > 0) {
+    if ((variant == 13 || variant == 14) && h->NB > 0) {
         // the board-resident tower (pv_board.hip): every conv of one board from LDS,
         // the tower output in place over the stem output
         int out_off[2 * kTowerMaxBlocks];
@@ -657,9 +657,14 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
             out_off[2 * i + 1] = bd[h->bn_blk[i].second].out_off;
         }
         pr = prof_begin(h, AZG_PROF_BOARD, st, batch);
-        AZG_TRY(launch_board_tower(h->NB, (const float*)h->wpack16, h->scale16, h->shift, out_off, X, batch, h->ovf_dev,
-                                   seq, st),
-                "forward: board tower");
+        if (variant == 14)
+            AZG_TRY(launch_board16_tower(h->NB, (const float*)h->wpack16, h->scale16, h->shift, out_off, X, batch,
+                                         h->ovf_dev, seq, st),
+                    "forward: board tower (16x16x32)");
+        else
+            AZG_TRY(launch_board_tower(h->NB, (const float*)h->wpack16, h->scale16, h->shift, out_off, X, batch,
+                                       h->ovf_dev, seq, st),
+                    "forward: board tower");
         prof_end(h, pr, st);
         *out = X;
         return 0;
@@ -742,7 +747,7 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
     const bool board_ok = h3 && h->C == 128;   // the board-resident tower: split-fp16, C = 128 (LDS)
     if (g_tower_mode == 1)
         return ((g_tower_shape == 10 && (h->C != 128 || h3)) || (g_tower_shape == 12 && !h3) ||
-                (g_tower_shape == 13 && !board_ok))
+                ((g_tower_shape == 13 || g_tower_shape == 14) && !board_ok))
                    ? 8
                    : g_tower_shape;
     const int bucket = conv_batch_bucket(batch * PIX);

@@ -1155,7 +1155,7 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     }
     if (key == 6) {   // persistent tower tile shape
         const int prev = azg::g_tower_shape;
-        if (value == 5 || value == 8 || value == 10 || value == 12 || value == 13) azg::g_tower_shape = value;
+        if (value == 5 || value == 8 || value == 10 || value == 12 || value == 13 || value == 14) azg::g_tower_shape = value;
 #ifdef AZG_AB_STUDIES
         if (value == 9) azg::g_tower_shape = value;
 #endif

@@ -86,6 +86,8 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
 // place with the tower output
 hipError_t launch_board_tower(int NB, const float* wp16, const float* scale16, const float* shift, const int* out_off,
                               float* x, int B, unsigned* ring_ovf, unsigned seq, hipStream_t st);
+hipError_t launch_board16_tower(int NB, const float* wp16, const float* scale16, const float* shift,
+                                const int* out_off, float* x, int B, unsigned* ring_ovf, unsigned seq, hipStream_t st);
 extern unsigned g_tower_wait_us;
 extern int g_tower_group;
 #ifdef AZG_AB_STUDIES

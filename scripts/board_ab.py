@@ -1,6 +1,7 @@
 """In-process A/B of the split-fp16 eval towers (device time per forward, best of 4
 interleaved rounds; bitwise check against per-layer launches): the 128x64 tile tower
-(shape 8), h3_tile (12) and the board-resident tower (13).
+(shape 8), h3_tile (12) and the board-resident towers (13; 14 on 16x16x32 products, its
+own arithmetic class: max |d logit| instead of bitwise).
 
     python scripts/board_ab.py [--blocks 6] [--ch 128] [--batches 256,512,2048,3456]
 """
@@ -56,8 +57,10 @@ def main():
             lib.azg_pv_set_tuning(6, s)
             _, _, l1 = eng.forward(x, want_logits=True)
             same = bool(torch.equal(l0, l1))
+            dmax = float((l0 - l1).abs().max())
             print(f"B={B} shape {s}: tower {best[s]:.3f} ms = {flop * B / best[s] / 1e9:.1f} TFLOP/s "
-                  f"({flop * B / best[s] / 1e9 / 838.9 * 100:.1f} % of the split roofline), bitwise {same}", flush=True)
+                  f"({flop * B / best[s] / 1e9 / 838.9 * 100:.1f} % of the split roofline), bitwise {same} "
+                  f"max|dlogit| {dmax:.2e}", flush=True)
         lib.azg_pv_set_tuning(5, 2)
 
 

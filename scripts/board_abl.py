@@ -17,9 +17,9 @@ def main():
     m = PyTorchModel(board_size=15, device="cuda", n_res_blocks=6, channels=128)
     eng = m.engine
     lib.azg_pv_set_tuning(5, 1)
-    lib.azg_pv_set_tuning(6, 13)
+    lib.azg_pv_set_tuning(6, int(os.environ.get('SHAPE', '14')))
     flop = 12 * bench.conv_flop(128)
-    for B in (2048, 4096):
+    for B in (512, 3456):
         x = torch.from_numpy(synth_encoded(B, seed=B)).cuda()
         for abl in [int(a) for a in os.environ.get('ABLS', '0,1,2,4,7,8,16,24,0').split(',')]:
             lib.azg_pv_set_tuning(51, abl)
@@ -30,7 +30,7 @@ def main():
                 eng.forward(x)
             prof = eng.profile_read()
             eng.profile_enable(False)
-            ms = prof["board"][0] / 5
+            ms = prof.get("board", [float('nan')])[0] / 5
             print(f"B={B} abl {abl}: {ms:.3f} ms = {flop * B / ms / 1e9:.1f} TFLOP/s", flush=True)
         lib.azg_pv_set_tuning(51, 0)
         eng.clear_status()

@@ -20,9 +20,9 @@ def main():
         if not os.path.exists(f):
             continue
         for r in csv.DictReader(open(f)):
-            m = re.search(r"(lab_conv|lab_h3|conv_tower|board_tower)<([\d, ]+)>", r["Kernel_Name"])
+            m = re.search(r"(lab_conv|lab_h3|conv_tower|board16_tower|board_tower)(?:<([\d, ]+)>)?", r["Kernel_Name"])
             if m:
-                acc[m.group(1) + "<" + m.group(2) + ">"][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                acc[m.group(1) + ("<" + m.group(2) + ">" if m.group(2) else "")][r["Counter_Name"]].append(float(r["Counter_Value"]))
     print("| lab_conv<C, BN, WM, TM, NW, VAR, WPE> | MFMA busy | LDS-array busy | wait_any | wait_inst | "
           "wait_inst_lds | active | LDS instr / MFMA | VALU / MFMA | conflict cycles / LDS cycles |")
     print("|---|---|---|---|---|---|---|---|---|---|")
