@@ -78,7 +78,8 @@ _SIGS = {
     "azg_pv_posted": (ctypes.c_int32, [_P, ctypes.c_uint32]),
 }
 EXPORTS = tuple(_SIGS)
-PROF_CLASSES = ("conv3x3", "stem", "heads", "train_conv", "train_wgrad", "train_other", "tower", "tower16", "board")
+PROF_CLASSES = ("conv3x3", "stem", "heads", "train_conv", "train_wgrad", "train_other", "tower", "tower16", "board",
+                "board16")
 ABI_VERSION = 3   # 2: tower launch numbers, azg_pv_recover, the wait record (round 5); 3: the gradient
                   # buffer's skip word, azg_pv_train_fp32_once, azg_pv_posted (round 6)
 

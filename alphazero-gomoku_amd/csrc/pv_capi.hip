@@ -656,7 +656,7 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
             out_off[2 * i] = bd[h->bn_blk[i].first].out_off;
             out_off[2 * i + 1] = bd[h->bn_blk[i].second].out_off;
         }
-        pr = prof_begin(h, AZG_PROF_BOARD, st, batch);
+        pr = prof_begin(h, variant == 14 ? AZG_PROF_BOARD16 : AZG_PROF_BOARD, st, batch);
         if (variant == 14)
             AZG_TRY(launch_board16_tower(h->NB, (const float*)h->wpack16, h->scale16, h->shift, out_off, X, batch,
                                          h->ovf_dev, seq, st),
@@ -747,9 +747,10 @@ static int tower_variant(azg_pv* h, const float* x, int batch, hipStream_t st, c
     const bool board_ok = h3 && h->C == 128;   // the board-resident tower: split-fp16, C = 128 (LDS)
     if (g_tower_mode == 1)
         return ((g_tower_shape == 10 && (h->C != 128 || h3)) || (g_tower_shape == 12 && !h3) ||
-                ((g_tower_shape == 13 || g_tower_shape == 14) && !board_ok))
+                (g_tower_shape == 13 && !board_ok))
                    ? 8
-                   : g_tower_shape;
+                   : g_tower_shape == 14 ? (board_ok ? 13 : 8)   // 14 is key 19 = 2's form
+                                         : g_tower_shape;
     const int bucket = conv_batch_bucket(batch * PIX);
     static std::map<std::tuple<int, int, int, int>, int> cache;
     const auto key = std::make_tuple(h->C, h->NB, bucket, (int)h3);
@@ -814,8 +815,11 @@ int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* 
     const bool h3 = g_tower_h3 != 0 && !fp32_only && (C == 128 || C == 256) && h->NB > 0;
     if (h3)
         if (int32_t r = ensure_h3(h, st)) return r;
-    int variant = per_layer ? 0 : tower_variant(h, x, batch, st, boards, players, h3);
-    if (variant != 0 && h->breaker_until > 0.0) {
+    // key 19 = 2 at C = 128: the 16x16x32 board tower is the one form of its arithmetic, for
+    // every batch and path (it has no cross-workgroup waits: nothing for the breaker to avoid)
+    const bool k32 = h3 && g_tower_h3 == 2 && C == 128 && h->NB <= kTowerMaxBlocks;
+    int variant = k32 ? 14 : per_layer ? 0 : tower_variant(h, x, batch, st, boards, players, h3);
+    if (variant != 0 && !k32 && h->breaker_until > 0.0) {
         if (now_s() < h->breaker_until) {
             variant = 0;
             ++h->breaker_launches;

@@ -1068,9 +1068,9 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         if (value >= 0 && value <= 2) azg::g_train_h3 = value;
         return prev;
     }
-    if (key == 19) {  // eval residual-conv arithmetic: 1 split-fp16 products (H3, default), 0 fp32 MFMA
+    if (key == 19) {  // eval residual-conv arithmetic: 2 split-fp16 on 16x16x32 (default), 1 on 32x32x16, 0 fp32
         const int prev = azg::g_tower_h3;
-        if (value == 0 || value == 1) azg::g_tower_h3 = value;
+        if (value == 0 || value == 1 || value == 2) azg::g_tower_h3 = value;
         return prev;
     }
     if (key == 18) {  // seconds of per-layer convs after a recovered tower launch (0: off)

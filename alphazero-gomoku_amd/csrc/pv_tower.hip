@@ -351,7 +351,9 @@ size_t tower_prod_bytes(int nlayers, int M)
 // (act[0] holds the stem output; the result ends in act[0] or act[2], returned in
 // *result).  `sync` must hold tower_sync_bytes(2*NB, M) bytes.
 int g_h3_tower_var = 1;   // key 20: the H3 tower body, 1 = board-keyed halo swizzle (VAR 99, default), 0 = row-keyed (98)
-int g_tower_h3 = 1;   // key 19: split-fp16 (H3) eval residual convs (pv_halo.h VAR bit 64, default); 0 = fp32 MFMA
+// key 19: split-fp16 (H3) eval residual convs: 2 (default) the 16x16x32 board tower at C = 128
+// (pv_board16.hip; C = 256 as 1), 1 the 32x32x16 forms (pv_halo.h VAR bit 64), 0 fp32 MFMA
+int g_tower_h3 = 2;
 
 hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const float* wpack, const float* scale,
                         const float* shift, const int* out_off, int M, const TowerSync& ts, hipStream_t st,

@@ -60,7 +60,8 @@ def conv_peak():
     arithmetic the library runs now (tuning key 19)."""
     import _native
     lib = _native.load_library()
-    if lib.azg_pv_set_tuning(19, -1) == 1:
+    k = lib.azg_pv_set_tuning(19, -1)
+    if k in (1, 2):   # 2: the 16x16x32 board tower (C = 128); the same F16 instruction peak
         return PEAK_H3, "f16x3->f32"
     return PEAK_F32_MFMA, "f32"
 
@@ -289,7 +290,7 @@ def traffic_records():
 
 # profile class -> (convs per launch as a multiple of blocks (0: one conv), PMC record shape prefix)
 TOWER_CLASSES = {"tower16": (2, "conv_tower<128, 128, 4, 1, 16"), "tower": (2, "conv_tower<"),
-                 "board": (2, "board_tower"), "conv3x3": (0, None)}
+                 "board": (2, "board_tower"), "board16": (2, "board16_tower"), "conv3x3": (0, None)}
 
 
 def roofline_from_profile(prof, boards, blocks, ch, knames, traffic=True):
@@ -319,9 +320,10 @@ def roofline_from_profile(prof, boards, blocks, ch, knames, traffic=True):
     out = {"bound": "mfma", "achieved": round(achieved / 1e12, 3), "peak": round(peak / 1e12, 1),
            "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None}
     if peak == PEAK_H3:
-        out["peak_basis"] = ("split-fp16 products: 3 v_mfma_f32_32x32x16_f16 per fp32-equivalent product, "
-                             "dense F16 MFMA peak 2516.8 TFLOP/s / 3; achieved counts the fp32-equivalent conv "
-                             "FLOPs (2 x 225 x C x 9C per board per conv)")
+        inst = "v_mfma_f32_16x16x32_f16" if dom == "board16" else "v_mfma_f32_32x32x16_f16"
+        out["peak_basis"] = (f"split-fp16 products: 3 {inst} per fp32-equivalent product, "
+                             "dense F16 MFMA peak 2516.8 TFLOP/s / 3 (both f16 shapes); achieved counts the "
+                             "fp32-equivalent conv FLOPs (2 x 225 x C x 9C per board per conv)")
         # a ratio, not a fraction: the split tower's fp32-equivalent rate over the fp32-MFMA peak
         out["speedup_over_fp32_mfma_peak"] = round(achieved / PEAK_F32_MFMA, 4)
     out.update({k: v for k, v in d.items() if not k.startswith("_") and k != "frac"})
@@ -329,16 +331,16 @@ def roofline_from_profile(prof, boards, blocks, ch, knames, traffic=True):
     h3 = peak == PEAK_H3
     if h3 and dom == "tower16":   # split-fp16: class 7 is the h3_tile 128x128 tower (shape 12, VAR 355)
         pref = f"conv_tower<{ch}, 128, 2, 2, 4, 355"
-    if dom == "board":            # traffic records of the board-resident tower are keyed "board_tower"
+    if dom in ("board", "board16"):   # traffic records of the board-resident towers are keyed by class
         pref = None
-        recs = [r for r in traffic_records() if r.get("kernel") == "board" and
+        recs = [r for r in traffic_records() if r.get("kernel") == dom and
                 r.get("config", "").startswith(f"{blocks}x{ch}_B")]
         if traffic and recs:
             bpl = d["boards_per_launch"]
             r = min(recs, key=lambda r: abs(r["boards_per_launch"] - bpl))
             out["traffic"] = round(r["hbm_bytes_per_launch"] / r["boards_per_launch"] * bpl)
             out["traffic_over_algorithmic"] = r["traffic_over_algorithmic"]
-            out["traffic_basis"] = (f"PMC FETCH_SIZE x2 + WRITE_SIZE of board_tower at {r['config']} ({r['tag']}): "
+            out["traffic_basis"] = (f"PMC FETCH_SIZE x2 + WRITE_SIZE of {TOWER_CLASSES[dom][1]} at {r['config']} ({r['tag']}): "
                                     f"{r['hbm_bytes_per_launch'] / 1e6:.1f} MB per launch, "
                                     f"{r['traffic_over_algorithmic']}x algorithmic; scaled per board to this run's "
                                     f"average launch ({bpl} boards)")
@@ -370,7 +372,10 @@ def roofline_from_profile(prof, boards, blocks, ch, knames, traffic=True):
 
 def tower_knames(ch, blocks):
     n = 2 * blocks
-    return {"board": (f"azg::board_tower (board-resident residual tower: one board per 16-wave workgroup, its "
+    return {"board16": (f"azg::board16_tower (board-resident residual tower on v_mfma_f32_16x16x32_f16: one board "
+                        f"per 12-wave workgroup, its activations in LDS as split fp16 through all {n} fused 3x3 conv + "
+                        f"BN (+ residual) + ReLU layers, split-fp16 products, LDS-DMA weight stages)"),
+            "board": (f"azg::board_tower (board-resident residual tower: one board per 16-wave workgroup, its "
                       f"activations in LDS as split fp16 through all {n} fused 3x3 conv + BN (+ residual) + ReLU "
                       f"layers, split-fp16 products, LDS-DMA weight stages)"),
             "tower16": (f"azg::conv_tower<{ch},128,2,2,4,355> (persistent residual tower, h3_tile 128x128 tiles: 4 "

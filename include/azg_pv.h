@@ -151,7 +151,8 @@ enum {
                                 (fp32), or h3_tile's 4 waves of 64x64 (split-fp16, shape 12) */
     AZG_PROF_BOARD = 8,      /* the board-resident tower (split-fp16, C = 128, shape 13): one
                                 board's activations in LDS through all 2*NB convs */
-    AZG_PROF_NCLASS = 9
+    AZG_PROF_BOARD16 = 9,    /* the 16x16x32 board tower (key 19 = 2, C = 128) */
+    AZG_PROF_NCLASS = 10
 };
 int32_t azg_pv_profile_enable(azg_pv* h, int32_t enable);
 int32_t azg_pv_profile_read(azg_pv* h, double* ms, int64_t* launches);
@@ -176,7 +177,8 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          only; 12: h3_tile 128x128 / 4 waves of 64x64, split-fp16 only; 13: the
  *          board-resident tower (pv_board.hip: one board per 16-wave workgroup, its
  *          activations in LDS through every conv), split-fp16 and C = 128 only -- a shape
- *          the current arithmetic lacks runs as 8);
+ *          the current arithmetic lacks runs as 8); with key 19 = 2 at C = 128 keys 5 / 6
+ *          do not apply (one form: the 16x16x32 board tower);
  *   keys 3, 7, 8: timing-only ablation switches (results invalid while set);
  *   key 10: tile-body variant of the C=128 128x64 persistent tower (0 = default;
  *          1..5 = swizzle / prefetch / LDS-DMA staging variants for A/B timing, all
@@ -211,13 +213,17 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *   key 14: persistent-tower dependency wait bound in microseconds of the waiting
  *          wave's awake time (default 100000 = 100 ms; -1 restores it; 0 makes every
  *          dependency wait time out at once, exercising the recovery path);
- *   key 19: eval residual-conv arithmetic: 1 (default) split-fp16 -- every fp32 operand x
- *          is split into hi = fp16(x), lo = fp16(x - hi) and a product is lo*hi + hi*lo +
- *          hi*hi by three v_mfma_f32_32x32x16_f16 with fp32 accumulation (weights scaled by
- *          a per-layer power of two, undone in the BN scale; error ~2^-22 per product, the
- *          fp32 MFMA chain's order of magnitude); 0 fp32 MFMA.  Every
- *          eval path (tower, per-layer, recompute) uses the selected arithmetic, so the
- *          tower and per-layer forms stay bitwise equal.  An activation at or above fp16's
+ *   key 19: eval residual-conv arithmetic: 2 (default) and 1 split-fp16 -- every fp32
+ *          operand x is split into hi = fp16(x), lo = fp16(x - hi) and a product is lo*hi +
+ *          hi*lo + hi*hi by fp16 MFMAs with fp32 accumulation (weights scaled by a per-layer
+ *          power of two, undone in the BN scale; error ~2^-22 per product, the fp32 MFMA
+ *          chain's order of magnitude); 1 sums 16 channels per
+ *          v_mfma_f32_32x32x16_f16 (per-layer launches, tile towers, the 32x32 board
+ *          tower), 2 at C = 128 sums 32 per v_mfma_f32_16x16x32_f16 in the 16x16x32 board
+ *          tower (pv_board16.hip), the one form of that arithmetic (C = 256: as 1); 0 fp32
+ *          MFMA.  Every eval path (tower, per-layer, recompute) uses the selected
+ *          arithmetic, so within it the forms are bitwise equal and the forward is
+ *          batch-independent.  An activation at or above fp16's
  *          range (65520 rounds to inf) makes its products non-finite: the epilogue posts
  *          the launch and azg_pv_recover recomputes it with fp32 MFMA.  The train step
  *          always uses fp32 MFMA;

@@ -84,17 +84,18 @@ def test_forward_matches_oracle(blocks, ch, B):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("blocks,ch,seed,B,shape", [(6, 128, 0, 512, 8), (6, 128, 0, 3456, 8),
-                                                     (10, 256, 1, 512, 12)])
-def test_split_forward_on_trained_weights_matches_oracle32(blocks, ch, seed, B, shape):
-    """the split-fp16 eval arithmetic (key 19 = 1, the default) on weights
-    that are NOT on the fp16 grid -- the benchmarked ones: seeded init (seed 0 for 6x128,
-    1 for the 10x256 Pente net) + bench.pretrain's 20 train_batch steps -- so every product
-    term (lo_a hi_b, hi_a lo_b, hi_a hi_b) is live.  The tower runs with the shape the
-    bench's launches use: 128x64 (shape 8) at 512 and 3,456 boards (the self-play batch),
-    h3_tile 128x128 (shape 12) for 10x256 at 512.  Asserted: |gpu - oracle fp32| <= 1e-5
-    on probs and values (the north star's literal bar); printed: both against fp64 on the
-    first 256 boards."""
+@pytest.mark.parametrize("blocks,ch,seed,B,cls,shape", [(6, 128, 0, 512, 2, 14), (6, 128, 0, 3456, 2, 14),
+                                                         (6, 128, 0, 512, 1, 8), (6, 128, 0, 3456, 1, 8),
+                                                         (10, 256, 1, 512, 1, 12)])
+def test_split_forward_on_trained_weights_matches_oracle32(blocks, ch, seed, B, cls, shape):
+    """the split-fp16 eval arithmetic on weights that are NOT on the
+    fp16 grid -- the benchmarked ones: seeded init (seed 0 for 6x128, 1 for the 10x256
+    Pente net) + bench.pretrain's 20 train_batch steps -- so every product term (lo_a hi_b,
+    hi_a lo_b, hi_a hi_b) is live.  Key 19 = 2 (the default): the 16x16x32 board tower
+    (shape 14) at 512 and 3,456 boards (the self-play batch); key 19 = 1: the 128x64 tower
+    (shape 8) there and h3_tile 128x128 (shape 12) for 10x256 at 512.  Asserted: |gpu -
+    oracle fp32| <= 1e-5 on probs and values (the north star's literal bar); printed: both
+    against fp64 on the first 256 boards."""
     import _native
     import bench
     from network import PyTorchModel
@@ -111,7 +112,7 @@ def test_split_forward_on_trained_weights_matches_oracle32(blocks, ch, seed, B, 
     load_numpy_state(ref.net, st)
     b, p = synth_positions(B, seed=B + 7 * ch)
     x = encode_batch(b, p)
-    assert lib.azg_pv_set_tuning(19, -1) == 1   # split-fp16 is the arithmetic under test
+    prev19 = lib.azg_pv_set_tuning(19, cls)
     prev5, prev6 = lib.azg_pv_set_tuning(5, 1), lib.azg_pv_set_tuning(6, shape)
     try:
         m.engine.profile_enable(True)
@@ -121,7 +122,8 @@ def test_split_forward_on_trained_weights_matches_oracle32(blocks, ch, seed, B, 
     finally:
         lib.azg_pv_set_tuning(5, prev5)
         lib.azg_pv_set_tuning(6, prev6)
-    assert ("tower16" if shape == 12 else "tower") in ran, ran
+        lib.azg_pv_set_tuning(19, prev19)
+    assert {14: "board16", 12: "tower16"}.get(shape, "tower") in ran, ran
     rp, rv = ref.predict(x)
     n64 = min(B, 256)
     r64 = RefModel(blocks, ch, dtype=torch.float64)
@@ -130,7 +132,7 @@ def test_split_forward_on_trained_weights_matches_oracle32(blocks, ch, seed, B, 
     p64, v64 = r64.predict(x[:n64])
     for name, got, r32, r_64 in (("probs", probs, rp, p64), ("values", values, rv, v64)):
         d32 = float(np.abs(got - r32).max())
-        print(f"{blocks}x{ch} B={B} shape {shape} {name}: |gpu-cpu32|={d32:.2e} "
+        print(f"{blocks}x{ch} B={B} key19={cls} shape {shape} {name}: |gpu-cpu32|={d32:.2e} "
               f"|gpu-fp64|={np.abs(got[:n64] - r_64).max():.2e} |cpu32-fp64|={np.abs(r32[:n64] - r_64).max():.2e}")
         assert d32 <= TOL, (name, d32)
     argmax_check(probs, rp, b)
@@ -154,18 +156,29 @@ def calib_bn(ref, seed):
     ref.net.eval()
 
 
-def test_forward_is_batch_independent():
-    """Each board's outputs are bit-identical whatever batch or position it is in."""
-    m = make_model(3, 64)
-    b, p = synth_positions(130, seed=3)
+@pytest.mark.parametrize("blocks,ch,cls,n", [(3, 64, 2, 130), (6, 128, 2, 600), (6, 128, 1, 600)])
+def test_forward_is_batch_independent(blocks, ch, cls, n):
+    """Each board's outputs are bit-identical whatever batch or position it is in: under
+    each split arithmetic (key 19 = 2: at C = 128 the 16x16x32 board tower, whose workgroups
+    take several boards each past 256; key 19 = 1: whatever form the tuner picks per batch)."""
+    import _native
+    lib = _native.load_library()
+    m = make_model(blocks, ch)
+    b, p = synth_positions(n, seed=3)
     x = encode_batch(b, p)
-    probs, values = m.predict(x)
-    for i in (0, 63, 64, 129):
-        pi, vi = m.predict(x[i:i + 1])
-        assert np.array_equal(pi[0], probs[i]) and np.array_equal(vi[0], values[i])
-    perm = np.random.default_rng(0).permutation(130)
-    pp, vp = m.predict(x[perm])
-    assert np.array_equal(pp, probs[perm]) and np.array_equal(vp, values[perm])
+    prev = lib.azg_pv_set_tuning(19, cls)
+    try:
+        probs, values = m.predict(x)
+        for i in (0, 63, 64, 129, n - 1):
+            pi, vi = m.predict(x[i:i + 1])
+            assert np.array_equal(pi[0], probs[i]) and np.array_equal(vi[0], values[i])
+        perm = np.random.default_rng(0).permutation(n)
+        pp, vp = m.predict(x[perm])
+        assert np.array_equal(pp, probs[perm]) and np.array_equal(vp, values[perm])
+        ps, vs = m.predict(x[37:37 + 300])
+        assert np.array_equal(ps, probs[37:337]) and np.array_equal(vs, values[37:337])
+    finally:
+        lib.azg_pv_set_tuning(19, prev)
 
 
 def test_empty_and_full_boards():
@@ -354,6 +367,7 @@ def test_persistent_tower_under_concurrent_load():
     x2 = torch.from_numpy(synth_encoded(1024, seed=12)).cuda()
     prev_mode = lib.azg_pv_set_tuning(5, 0)
     prev_shape = lib.azg_pv_set_tuning(6, 8)
+    prev_h3 = lib.azg_pv_set_tuning(19, 1)   # the tile towers' arithmetic (key 19 = 2 has one form)
     try:
         r1 = m1.engine.forward(x1)[0].clone()
         r2 = m2.engine.forward(x2)[0].clone()
@@ -370,6 +384,7 @@ def test_persistent_tower_under_concurrent_load():
                 torch.cuda.synchronize()
                 assert torch.equal(a, r1) and torch.equal(b, r2), shape
     finally:
+        lib.azg_pv_set_tuning(19, prev_h3)
         lib.azg_pv_set_tuning(6, prev_shape)
         lib.azg_pv_set_tuning(5, prev_mode)
 
@@ -394,6 +409,7 @@ def test_tower_timeout_is_recovered_bitwise():
     prev_mode = lib.azg_pv_set_tuning(5, 1)
     prev_shape = lib.azg_pv_set_tuning(6, 8)
     prev_breaker = lib.azg_pv_set_tuning(18, 0)     # breaker off: every forward runs the tower
+    prev_h3 = lib.azg_pv_set_tuning(19, 1)          # the tile towers' arithmetic
     try:
         p_ok, v_ok = m.predict(x)                    # healthy
         pb_ok, vb_ok = m.predict_boards(bi8, pl8)
@@ -455,6 +471,7 @@ def test_tower_timeout_is_recovered_bitwise():
         assert "tower" in prof                       # the tower again
     finally:
         lib.azg_pv_set_tuning(14, -1)
+        lib.azg_pv_set_tuning(19, prev_h3)
         lib.azg_pv_set_tuning(18, prev_breaker)
         lib.azg_pv_set_tuning(6, prev_shape)
         lib.azg_pv_set_tuning(5, prev_mode)
@@ -490,13 +507,14 @@ def test_mfma_stem_bitwise_equals_valu_stem(blocks, ch, B):
         assert np.array_equal(a, b), float(np.abs(a - b).max())
 
 
-@pytest.mark.parametrize("tower", [1, 0])
-def test_h3_range_guard_recomputes_in_fp32(tower):
-    """Split-fp16 residual convs (key 19 = 1, the default) cannot represent an activation
-    at or above 65504: the staging posts the launch and predict / predict_boards recompute
-    it with fp32 MFMA, so the result is bitwise the fp32 forward (key 19 = 0).  The stem's
-    BN gamma scaled by 1e5 drives the first conv's inputs past fp16's range.  Both the
-    persistent tower and the per-layer launches (key 5) carry the guard."""
+@pytest.mark.parametrize("tower,cls", [(1, 1), (0, 1), (1, 2)])
+def test_h3_range_guard_recomputes_in_fp32(tower, cls):
+    """Split-fp16 residual convs (key 19 = 1, 2) cannot represent an activation at or above
+    65504: the staging posts the launch and predict / predict_boards recompute it with fp32
+    MFMA, so the result is bitwise the fp32 forward (key 19 = 0).  The stem's BN gamma
+    scaled by 1e5 drives the first conv's inputs past fp16's range.  The persistent tower
+    and the per-layer launches (key 5) of key 19 = 1 and the 16x16x32 board tower (2)
+    carry the guard."""
     import _native
     lib = _native.load_library()
     m = make_model(3, 128, seed=8)
@@ -511,7 +529,7 @@ def test_h3_range_guard_recomputes_in_fp32(tower):
     try:
         p32, v32 = m.predict(x)
         pb32, vb32 = m.predict_boards(bi8, pl8)
-        lib.azg_pv_set_tuning(19, 1)
+        lib.azg_pv_set_tuning(19, cls)
         m.engine.tower_diag_clear()
         p, v = m.predict(x)
         pb, vb = m.predict_boards(bi8, pl8)
@@ -525,11 +543,12 @@ def test_h3_range_guard_recomputes_in_fp32(tower):
         lib.azg_pv_set_tuning(5, prev_mode)
 
 
-@pytest.mark.parametrize("blocks,ch,B", [(6, 128, 512), (10, 256, 96)])
-def test_h3_matches_fp32_forward_and_oracle(blocks, ch, B):
-    """Split-fp16 (key 19 = 1) against the fp32-MFMA forward (key 19 = 0) and the fp64
-    oracle on the same weights: within the forward parity budget (1e-5), and no further
-    from fp64 than 2x the fp32 path's own deviation (or 1e-6)."""
+@pytest.mark.parametrize("blocks,ch,B,cls", [(6, 128, 512, 2), (6, 128, 512, 1), (10, 256, 96, 1)])
+def test_h3_matches_fp32_forward_and_oracle(blocks, ch, B, cls):
+    """Split-fp16 (key 19 = 2: the 16x16x32 board tower; 1: the 32x32x16 forms) against the
+    fp32-MFMA forward (key 19 = 0) and the fp64 oracle on the same weights: within the
+    forward parity budget (1e-5), and no further from fp64 than 2x the fp32 path's own
+    deviation (or 1e-6)."""
     import _native
     lib = _native.load_library()
     ref = RefModel(blocks, ch)
@@ -541,7 +560,7 @@ def test_h3_matches_fp32_forward_and_oracle(blocks, ch, B):
     prev = lib.azg_pv_set_tuning(19, 0)
     try:
         p32, v32 = m.predict(x)
-        lib.azg_pv_set_tuning(19, 1)
+        lib.azg_pv_set_tuning(19, cls)
         p16, v16 = m.predict(x)
     finally:
         lib.azg_pv_set_tuning(19, prev)
@@ -551,7 +570,8 @@ def test_h3_matches_fp32_forward_and_oracle(blocks, ch, B):
     pr, vr = r64.predict(x)
     for name, a32, a16, a64 in (("probs", p32, p16, pr), ("values", v32, v16, vr)):
         e32, e16 = np.abs(a32 - a64).max(), np.abs(a16 - a64).max()
-        print(f"{blocks}x{ch} {name}: |fp32-fp64|={e32:.2e} |h3-fp64|={e16:.2e} |h3-fp32|={np.abs(a16 - a32).max():.2e}")
+        print(f"{blocks}x{ch} key19={cls} {name}: |fp32-fp64|={e32:.2e} |h3-fp64|={e16:.2e} "
+              f"|h3-fp32|={np.abs(a16 - a32).max():.2e}")
         assert np.abs(a16 - a32).max() <= 1e-5
         assert e16 <= max(2 * e32, 1e-6), (name, e16, e32)
     argmax_check(p16, pr, b)
