@@ -67,11 +67,12 @@ typedef _Float16 b16_f16x2 __attribute__((ext_vector_type(2)));
 // the same lane reads then writes each element) through a buffer resource: a padding
 // pixel's row offset lies past the resource, so its load returns 0 and its store is
 // dropped (no branches).  TO_LDS: y becomes the next conv's operand, [hi | lo] fp16 in the
-// keyed rows: lane pairs (channels 2k, 2k + 1 of one pixel) exchange y by DPP, both split
-// the pair (own value first), and the even lane stores the hi pair, the odd lane the lo
-// pair with its halves swapped (one v_perm).  Element pairs (i, i + 1) go through packed
-// fp32 math (v_pk_fma / v_pk_add: per element the same fmaf and add).  Returns whether an
-// accumulator was non-finite (their sum is: padding accumulators are exactly 0).
+// keyed rows: a lane splits its two elements (i, i + 1) together, H = (hi_i, hi_i+1) and L =
+// (lo_i, lo_i+1); lane pairs (channels 2k, 2k + 1 of one pixel) hand over their H (to the
+// even lane) or L (to the odd lane) by one DPP, and two v_perm form the words: the even lane
+// stores the hi pairs, the odd lane the lo pairs.  Element pairs go through packed fp32 math
+// (v_pk_fma / v_pk_add: per element the same fmaf and add).  Returns whether an accumulator
+// was non-finite (their sum is: padding accumulators are exactly 0).
 template <bool RES, bool TO_LDS>
 __device__ __forceinline__ bool b16_epilogue(const f32x4 (&acc)[5][2], const float* __restrict__ scale,
                                              const float* __restrict__ shift, __amdgpu_buffer_rsrc_t xr, char* lds,
@@ -83,7 +84,9 @@ __device__ __forceinline__ bool b16_epilogue(const f32x4 (&acc)[5][2], const flo
     // ce & 7, lo half for the odd lane; the tile's 32 (n ^ (i >> 1)) and the row i * 128 are
     // immediates (row m = m0 + i has key 4 (kb & 1) | (i & 2))
     const int lpart = (16 * ((ce >> 3) ^ (4 * (kb & 1))) + 2 * (ce & 7)) ^ (odd ? 64 : 0);
-    const unsigned sel = odd ? 0x05040706u : 0x03020100u;   // odd: the lo pair, halves swapped
+    // the word of element i (e = 0) / i + 1 (e = 1) from X (own H or L) and Zp (the partner's):
+    // even lane (own hi, partner hi), odd lane (partner lo, own lo)
+    const unsigned sel0 = odd ? 0x01000504u : 0x05040100u, sel1 = odd ? 0x03020706u : 0x07060302u;
     float sc[2], sh[2];
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
@@ -91,23 +94,29 @@ __device__ __forceinline__ bool b16_epilogue(const f32x4 (&acc)[5][2], const flo
         sh[n] = shift[32 * cg + 16 * n + r16];
     }
     const int cbyte = 4 * (32 * cg + r16);
-    b16_f32x2 chk = {0.f, 0.f};
+    // every block-input load first (in program order ahead of the in-place stores, which the
+    // compiler cannot move them past): one memory round trip per epilogue, not one per f
+    int vof[5][4];
+    float rvf[5][2][4];
+    if constexpr (RES) {
 #pragma unroll
-    for (int f = 0; f < 5; ++f) {
-        const int m0 = 80 * mg + 16 * f + 4 * kb;
-        int vo[4];
-        if constexpr (RES) {
-            const int4 p4 = *(const int4*)(poff + m0);
-            vo[0] = p4.x + cbyte, vo[1] = p4.y + cbyte, vo[2] = p4.z + cbyte, vo[3] = p4.w + cbyte;
-        }
-        float rv[2][4];
-        if constexpr (RES) {
+        for (int f = 0; f < 5; ++f) {
+            const int4 p4 = *(const int4*)(poff + 80 * mg + 16 * f + 4 * kb);
+            vof[f][0] = p4.x + cbyte, vof[f][1] = p4.y + cbyte, vof[f][2] = p4.z + cbyte, vof[f][3] = p4.w + cbyte;
 #pragma unroll
             for (int n = 0; n < 2; ++n)
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    rv[n][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo[i] + 64 * n, 0, 0));
+                    rvf[f][n][i] = __builtin_bit_cast(float,
+                                                      __builtin_amdgcn_raw_buffer_load_b32(xr, vof[f][i] + 64 * n, 0, 0));
         }
+    }
+    b16_f32x2 chk = {0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+        const int m0 = 80 * mg + 16 * f + 4 * kb;
+        const int (&vo)[4] = vof[f];
+        const float (&rv)[2][4] = rvf[f];
         char* wrow = lds + kB16Act + (cg * kB16Rows + m0) * 128 + lpart;
 #pragma unroll
         for (int n = 0; n < 2; ++n)
@@ -118,20 +127,25 @@ __device__ __forceinline__ bool b16_epilogue(const f32x4 (&acc)[5][2], const flo
                 b16_f32x2 y = __builtin_elementwise_fma(v, b16_f32x2{sc[n], sc[n]}, b16_f32x2{sh[n], sh[n]});
                 if constexpr (RES) y += b16_f32x2{rv[n][2 * ip], rv[n][2 * ip + 1]};
                 const float ye[2] = {fmaxf(y.x, 0.f), fmaxf(y.y, 0.f)};
+                if constexpr (RES) {
 #pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const int i = 2 * ip + e;
-                    const float yv = ye[e];
-                    if constexpr (RES)
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, yv), xr, vo[i] + 64 * n, 0, 0);
-                    if constexpr (TO_LDS) {
-                        const float yo = __builtin_bit_cast(
-                            float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, yv), 0xB1, 0xF, 0xF, false));
-                        const b16_f32x2 yy = {yv, yo};
-                        const b16_f16x2 hp = __builtin_convertvector(yy, b16_f16x2);
-                        const b16_f16x2 lp = __builtin_convertvector(yy - __builtin_convertvector(hp, b16_f32x2), b16_f16x2);
-                        const unsigned word = __builtin_amdgcn_perm(__builtin_bit_cast(unsigned, lp),
-                                                                    __builtin_bit_cast(unsigned, hp), sel);
+                    for (int e = 0; e < 2; ++e)
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, ye[e]), xr,
+                                                              vo[2 * ip + e] + 64 * n, 0, 0);
+                }
+                if constexpr (TO_LDS) {
+                    // the lane's two elements split together: H = (hi_i, hi_i+1), L = (lo_i, lo_i+1);
+                    // the partner lane's H (to an even lane) or L (to an odd lane) by one DPP
+                    const b16_f32x2 yy = {ye[0], ye[1]};
+                    const b16_f16x2 hp = __builtin_convertvector(yy, b16_f16x2);
+                    const b16_f16x2 lp = __builtin_convertvector(yy - __builtin_convertvector(hp, b16_f32x2), b16_f16x2);
+                    const unsigned H = __builtin_bit_cast(unsigned, hp), L = __builtin_bit_cast(unsigned, lp);
+                    const unsigned X = odd ? L : H, Z = odd ? H : L;
+                    const unsigned Zp = (unsigned)__builtin_amdgcn_mov_dpp((int)Z, 0xB1, 0xF, 0xF, false);
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const int i = 2 * ip + e;
+                        const unsigned word = __builtin_amdgcn_perm(Zp, X, e ? sel1 : sel0);
                         if (f < 4 || m0 + i < PIX)   // (padding rows past pixel 224 stay unwritten)
                             *(unsigned*)(wrow + i * 128 + 32 * (n ^ (i >> 1))) = word;
                     }
@@ -327,18 +341,20 @@ __global__ __launch_bounds__(kB16Threads, 1) void board16_tower(const Board16Arg
                         for (int j = 0; j < 2; ++j)
                             acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[f], bl[j], acc[f][j], 0, 0, 0);
                     __builtin_amdgcn_sched_barrier(0);
-                    if (nx) {
-#pragma unroll
-                        for (int f = 0; f < 5; ++f) ah[f] = *(const f16x8*)(lds + ao[f]);
+                    if (nx) {   // the B reads first: the barrier need only wait for them
 #pragma unroll
                         for (int j = 0; j < 2; ++j) bl[j] = *(const f16x8*)(bn + bl0 + j * 2048);
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int f = 0; f < 5; ++f) ah[f] = *(const f16x8*)(lds + ao[f]);
                     }
                     // chunk s + 2 has landed (this wave's pieces); the barrier publishes it for
                     // step s + 1's reads, and every wave's reads of chunk s + 1 are complete (its
                     // stage takes chunk s + 3)
-                    if constexpr (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if constexpr (!(ABL & 2)) __syncthreads();
-                    else __builtin_amdgcn_s_waitcnt(0xc07f);
+                    // (the barrier waits for this wave's B reads of chunk s + 1, issued before its
+                    // A reads: the 5 activation reads may stay in flight -- no DMA writes there)
+                    if constexpr (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(5)" ::: "memory");
+                    if constexpr (!(ABL & 2)) __builtin_amdgcn_s_barrier();
                 }
             }
 
@@ -360,9 +376,12 @@ __global__ __launch_bounds__(kB16Threads, 1) void board16_tower(const Board16Arg
             if (bad && a.ring_ovf && a.seq)
                 __hip_atomic_store(a.ring_ovf + (a.seq & (kTowerRing - 1)), a.seq, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
-            // the next conv reads what every wave wrote; the block output is written
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
+            // the next conv reads what every wave wrote to LDS.  The block-output stores need
+            // not land first: only this lane reads them back (the residual two convs on, and
+            // a wave's memory operations to one address stay in order), and the next step's
+            // vmcnt(0) retires them behind step 0's MFMAs
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
         }
     }
 }

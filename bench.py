@@ -22,8 +22,9 @@ size the configs[1] forward sub-leg.  `roofline` is the persistent residual towe
 algorithmic FLOPs of the boards each launch evaluated / hipEvent device time of
 those launches on the stream they ran on.
 
-Sub-legs (extra keys): `forward_b512` (configs[1]: K forwards of 512 boards in HBM,
-own roofline), `train` (configs[3] train step, 6x128, B=128/GPU, RCCL all-reduce
+Sub-legs (extra keys): `selfplay_fp32` (the headline self-play again with the eval residual
+convs in fp32 MFMA, tuning key 19 = 0), `forward_b512` (configs[1]: K forwards of 512 boards
+in HBM, own roofline), `train` (configs[3] train step, 6x128, B=128/GPU, RCCL all-reduce
 at N>1), `pente_10x256` (configs[4]: Pente self-play with the 10x256 net at 800
 sims, 32 games per GPU played to their end, its 10x256 forward at B=512 and train
 step at B=128), and `cpu_baseline` (rank 0 at N=1: the reference CPU path, i.e. the oracle
@@ -536,6 +537,31 @@ def selfplay_leg(model, args, rank, world, dist, dev, local):
     }
 
 
+def selfplay_fp32_leg(model, args, rank, world, dist, dev, local, sp):
+    """The headline self-play (same games, sims, seeds) with the eval residual convs in fp32
+    MFMA (tuning key 19 = 0): what the split-fp16 arithmetic buys end to end, and the rate
+    a caller gets who keeps the fp32 chain's numerics."""
+    import _native
+    lib = _native.load_library()
+    prev = lib.azg_pv_set_tuning(19, 0)
+    try:
+        G = args.sp32_games
+        a = argparse.Namespace(**{**vars(args), "sp_games": G})
+        r = selfplay_leg(model, a, rank, world, dist, dev, local)
+    finally:
+        lib.azg_pv_set_tuning(19, prev)
+    log(f"fp32 self-play done: {r['boards_per_s']:.0f} boards/s over {r['seconds']:.1f} s")
+    roof = r["roofline"] or {}
+    return {"tuning": "key 19 = 0 (fp32 MFMA residual convs; stem, heads unchanged)", "games": r["games"],
+            "boards": r["boards"], "seconds": round(r["seconds"], 2), "rounds": r["rounds"],
+            "boards_per_s": round(r["boards_per_s"], 1),
+            "headline_over_fp32": round(sp["boards_per_s"] / r["boards_per_s"], 3),
+            "mean_batch_rank0": r["detail"]["mean_batch_rank0"],
+            "gpu_busy_share_rank0": r["detail"]["gpu_busy_share_rank0"],
+            "roofline": {k: roof.get(k) for k in ("kernel", "achieved", "peak", "unit", "frac", "avg_launch_us",
+                                                  "boards_per_launch")}}
+
+
 def forward_leg(model, args, rank, world, dist, dev, local, blocks=BLOCKS, ch=CHANNELS, B=BATCH, steps=None,
                 warmup=None):
     """configs[1] (and the configs[4] network): `steps` forwards of B synthetic boards
@@ -680,6 +706,8 @@ def main():
     ap.add_argument("--sp-games", type=int, default=256)
     ap.add_argument("--sp-sims", type=int, default=400)
     ap.add_argument("--sp-max-moves", type=int, default=225, help="train.py's max_moves (board size squared)")
+    ap.add_argument("--sp32-games", type=int, default=256,
+                    help="games of the fp32-arithmetic self-play sub-leg (key 19 = 0; 0: skip)")
     ap.add_argument("--train-steps", type=int, default=60,
                     help="steps of the configs[3] train leg (0: skip; 60 steps amortise the first step's enqueue)")
     ap.add_argument("--big-steps", type=int, default=10, help="10x256 forwards (configs[4] net; 0: skip the leg)")
@@ -714,9 +742,12 @@ def main():
     if not args.skip_forward:
         log("configs[1] forward leg")
         fwd = forward_leg(model, args, rank, world, dist, dev, local)
+    sp32 = None
     if args.sp_games > 0:
         sp = selfplay_leg(model, args, rank, world, dist, dev, local)
         log(f"self-play done: {sp['boards_per_s']:.0f} boards/s over {sp['seconds']:.1f} s")
+        if args.sp32_games > 0:
+            sp32 = selfplay_fp32_leg(model, args, rank, world, dist, dev, local, sp)
     train = None
     if args.train_steps > 0:
         log("configs[3] train leg")
@@ -767,6 +798,7 @@ def main():
                    "parallelism": f"replicas{world} (games shard by GPU; no collective in the timed region)"},
         "roofline": sp["roofline"],
         "selfplay": {k: v for k, v in sp.items() if k != "roofline"},
+        "selfplay_fp32": sp32,
         "forward_b512": fwd,
         "train": train,
         "pente_10x256": big,

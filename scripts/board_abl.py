@@ -30,8 +30,13 @@ def main():
                 eng.forward(x)
             prof = eng.profile_read()
             eng.profile_enable(False)
-            ms = prof.get("board", [float('nan')])[0] / 5
-            print(f"B={B} abl {abl}: {ms:.3f} ms = {flop * B / ms / 1e9:.1f} TFLOP/s", flush=True)
+            ms = sum(v[0] for k, v in prof.items() if k.startswith("board")) / 5
+            _, _, lg = eng.forward(x, want_logits=True)
+            if abl == 0:
+                l0 = lg.clone()
+            dl = float((lg - l0).abs().max())
+            print(f"B={B} abl {abl}: {ms:.3f} ms = {flop * B / ms / 1e9:.1f} TFLOP/s, max|dlogit| vs abl 0 {dl:.2e}",
+                  flush=True)
         lib.azg_pv_set_tuning(51, 0)
         eng.clear_status()
 
