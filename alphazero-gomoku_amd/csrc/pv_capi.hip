@@ -617,6 +617,7 @@ int32_t ensure_h3(azg_pv* h, hipStream_t st)
                                h->scale16, h->h3inv, st),
                 "forward: split-fp16 weight pack");
         h->h3_dirty = false;
+        ++h->h3_gen;
     }
     return 0;
 }

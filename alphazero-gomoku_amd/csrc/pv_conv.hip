@@ -873,7 +873,8 @@ hipError_t launch_conv3x3(int C, int epi, const float* in, const float* wp, cons
 template <int C, int EPI, int XE, int PRO, int VAR>
 static hipError_t launch_train_v(const float* in, const float* wp, const float* resid, float* out, int M,
                                  const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st,
-                                 const float* oscale = nullptr, unsigned* h3ovf = nullptr)
+                                 const float* oscale = nullptr, unsigned* h3ovf = nullptr,
+                                 const unsigned* dmax = nullptr)
 {
     using T = typename TrainTile<C, 8>::T;
     constexpr int lds = halo_lds_bytes<C, T::BN, 4, 1, 8, VAR, PRO>();
@@ -886,15 +887,24 @@ static hipError_t launch_train_v(const float* in, const float* wp, const float* 
     }
     dim3 grid(((M + T::BM - 1) / T::BM) * (C / T::BN));
     hipLaunchKernelGGL((conv3x3_train<C, EPI, XE, true, PRO, VAR, 8>), grid, dim3(T::NT), lds, st, in, wp,
-                       resid, out, M, ex, px, fx, oscale, H3Guard{h3ovf, 1u});
+                       resid, out, M, ex, px, fx, oscale, H3Guard{h3ovf, 1u, dmax});
     return hipGetLastError();
 }
 
 template <int C, int EPI, int XE, int PRO = PRO_NONE>
 static hipError_t launch_train_t(const float* in, const float* wp, const float* resid, float* out, int M,
                                  const EpiX& ex, const ProX& px, const FinX& fx, hipStream_t st,
-                                 const float* oscale = nullptr, unsigned* h3ovf = nullptr)
+                                 const float* oscale = nullptr, unsigned* h3ovf = nullptr,
+                                 const unsigned* dmax = nullptr)
 {
+    // split-fp16 dgrad (key 50; oscale = the layer's 2^-e, dmax = its input's max |dz| bits):
+    // four products (VAR 225) or three (97), the input staged times 2^k
+    if constexpr (XE == XE_BNBWD && PRO == PRO_NONE) {
+        if (oscale && dmax && g_train_dgrad_h3 == 2)
+            return launch_train_v<C, EPI, XE, PRO, 225>(in, wp, resid, out, M, ex, px, fx, st, oscale, nullptr, dmax);
+        if (oscale && dmax)
+            return launch_train_v<C, EPI, XE, PRO, 97>(in, wp, resid, out, M, ex, px, fx, st, oscale, nullptr, dmax);
+    }
     // split-fp16 forward (VAR 97 = 64 | 32 | 1: H3, buffer addressing, board-keyed halo rows;
     // + 128: the fourth, lo x lo product -- key 49 = 2)
     if constexpr (EPI == EPI_RAW && XE == XE_STATS) {
@@ -908,6 +918,8 @@ static hipError_t launch_train_t(const float* in, const float* wp, const float* 
     return launch_train_v<C, EPI, XE, PRO, 32>(in, wp, resid, out, M, ex, px, fx, st);
 }
 int g_train_h3 = 2;   // key 49: 0 fp32 MFMA, 1 split-fp16 (3 products), 2 split-fp16 with 4 products (default)
+int g_train_dgrad_h3 = 0;   // key 50: the dgrad convs, likewise (inputs scaled by 2^k from their max); measured slower and
+                            // below the two-step goldens: off by default
 
 // Train conv with fused BN partials: (EPI_RAW, XE_STATS) forward, optionally with
 // the input layer's BN applied in the staging (px: PRO_BN / PRO_BN_RES); (EPI_RAW |
@@ -915,7 +927,7 @@ int g_train_h3 = 2;   // key 49: 0 fp32 MFMA, 1 split-fp16 (3 products), 2 split
 // the last workgroup of each N tile also runs the BN finalize (pv_halo.h FinX).
 hipError_t launch_conv3x3_train(int C, int epi, int xe, const float* in, const float* wp, const float* resid,
                                 float* out, int M, const EpiX& ex, hipStream_t st, const ProX* px, const FinX* fxp,
-                                const float* oscale, unsigned* h3ovf)
+                                const float* oscale, unsigned* h3ovf, const unsigned* dmax)
 {
     const ProX p0{};
     const FinX fx = fxp ? *fxp : FinX{};
@@ -926,8 +938,8 @@ hipError_t launch_conv3x3_train(int C, int epi, int xe, const float* in, const f
         if (epi == EPI_RAW && xe == XE_STATS && px)                                                \
             return launch_train_t<CC, EPI_RAW, XE_STATS, PRO_BN>(in, wp, resid, out, M, ex, *px, fx, st, oscale, h3ovf); \
         if (epi == EPI_RAW && xe == XE_STATS) return launch_train_t<CC, EPI_RAW, XE_STATS>(in, wp, resid, out, M, ex, p0, fx, st, oscale, h3ovf); \
-        if (epi == EPI_RAW && xe == XE_BNBWD) return launch_train_t<CC, EPI_RAW, XE_BNBWD>(in, wp, resid, out, M, ex, p0, fx, st); \
-        if (epi == EPI_ADD && xe == XE_BNBWD) return launch_train_t<CC, EPI_ADD, XE_BNBWD>(in, wp, resid, out, M, ex, p0, fx, st); \
+        if (epi == EPI_RAW && xe == XE_BNBWD) return launch_train_t<CC, EPI_RAW, XE_BNBWD>(in, wp, resid, out, M, ex, p0, fx, st, oscale, nullptr, dmax); \
+        if (epi == EPI_ADD && xe == XE_BNBWD) return launch_train_t<CC, EPI_ADD, XE_BNBWD>(in, wp, resid, out, M, ex, p0, fx, st, oscale, nullptr, dmax); \
         return hipErrorInvalidValue;
     switch (C) {
         AZG_TRAIN_C(64)
@@ -1066,6 +1078,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
     if (key == 49) {  // train forward convs: 1 split-fp16 products (H3), 0 fp32 MFMA
         const int prev = azg::g_train_h3;
         if (value >= 0 && value <= 2) azg::g_train_h3 = value;
+        return prev;
+    }
+    if (key == 50) {  // train dgrad convs: 2 split-fp16, four products (default); 1 three; 0 fp32 MFMA
+        const int prev = azg::g_train_dgrad_h3;
+        if (value >= 0 && value <= 2) azg::g_train_dgrad_h3 = value;
         return prev;
     }
     if (key == 19) {  // eval residual-conv arithmetic: 2 split-fp16 on 16x16x32 (default), 1 on 32x32x16, 0 fp32

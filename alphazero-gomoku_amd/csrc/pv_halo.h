@@ -247,7 +247,19 @@ struct ProX {
 struct H3Guard {
     unsigned* ring = nullptr;   // host-mapped, kTowerRing entries (device alias)
     unsigned seq = 0;
+    // split-fp16 dgrad (XE_BNBWD): the bits of max |input| of the layer (bn_bwd_apply's
+    // atomicMax); the input is staged times 2^k so its largest element lies in [2^14, 2^15)
+    // (fp16's top binade: every element keeps a normal hi part down to 2^-28 of the max),
+    // and the epilogue's factor carries 2^-k
+    const unsigned* dmax = nullptr;
 };
+// k of the dgrad input scale 2^k for max |input| bits `maxbits` (0: an all-zero input)
+__device__ __forceinline__ int h3_dgrad_exp(unsigned maxbits)
+{
+    const float m = __uint_as_float(maxbits);
+    const int k = m > 0.f && __builtin_isfinite(m) ? 14 - ilogbf(m) : 0;
+    return k < -100 ? -100 : k > 100 ? 100 : k;   // 2^k and the epilogue's 2^-(e + k) stay normal
+}
 constexpr unsigned kH3RingSize = 256;   // = kTowerRing (pv_internal.h)
 
 // key of the 16-B slot swizzle of halo row `row` (padded-pixel index): the padded
@@ -319,7 +331,10 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
             }
     __syncthreads();
     f32x4 h3s = {1.f, 1.f, 1.f, 1.f};
-    if (EPI == EPI_RAW && guard) h3s = *(const f32x4*)(scale + col);
+    if ((EPI == EPI_RAW || EPI == EPI_ADD) && guard) {
+        h3s = *(const f32x4*)(scale + col);
+        if (guard->dmax) h3s *= ldexpf(1.f, -h3_dgrad_exp(*guard->dmax));   // the dgrad input's 2^-k: exact
+    }
     if (!EARLY && (EPI == EPI_BN_RELU || EPI == EPI_BN_RES_RELU || EPI == EPI_BN_OPTRES_RELU)) {
         s4 = *(const f32x4*)(scale + col);
         t4 = *(const f32x4*)(shift + col);
@@ -336,7 +351,7 @@ __device__ __forceinline__ void halo_epilogue(const f32x16 (&acc)[TM_][ConvTile<
         const int row = er + p * RPI;
         const int m = m0 + row;
         f32x4 v = *(const f32x4*)(Es + row * ELD + ec);
-        if (EPI == EPI_RAW && guard) v *= h3s;   // split-fp16 weights carry 2^e: exact
+        if ((EPI == EPI_RAW || EPI == EPI_ADD) && guard) v *= h3s;   // split-fp16 weights carry 2^e: exact
         if (guard) {   // H3: a non-finite accumulator = an input beyond fp16's range (H3Guard)
             const bool fin = __builtin_isfinite(v[0]) && __builtin_isfinite(v[1]) && __builtin_isfinite(v[2]) &&
                              __builtin_isfinite(v[3]);
@@ -760,9 +775,13 @@ __device__ __forceinline__ void halo_tile(
     // pv_pack.hip pack_h3; the epilogue's BN scale carries the inverse).
     constexpr bool H3 = (VAR & 64) != 0;
     // train forward (EPI_RAW + XE_STATS, PRO): BN-normalised inputs; the raw output is
-    // multiplied by `scale` (2^-e of the layer) in the epilogue.  The dgrad convs (inputs
-    // not normalised) stay fp32.
-    static_assert(!H3 || XE == XE_NONE || XE == XE_STATS, "H3: eval and train-forward tiles only");
+    // multiplied by `scale` (2^-e of the layer) in the epilogue.  Dgrad (EPI_RAW / EPI_ADD +
+    // XE_BNBWD, key 50): the input gradient is not normalised -- it is staged times 2^k from
+    // its measured max (H3Guard::dmax) and the epilogue's factor is 2^-(e + k), applied
+    // before the residual gradient is added.
+    static_assert(!H3 || XE == XE_NONE || XE == XE_STATS || (XE == XE_BNBWD && PRO == PRO_NONE),
+                  "H3: eval, train-forward and dgrad tiles");
+    const float dsc = (H3 && XE == XE_BNBWD && guard.dmax) ? ldexpf(1.f, h3_dgrad_exp(*guard.dmax)) : 1.f;
     constexpr int NCHK = 9 * CG;
 
     float* Ah = smem;                 // [HR][32]
@@ -910,8 +929,9 @@ __device__ __forceinline__ void halo_tile(
                 f16x4 hi, lo;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    hi[e] = (_Float16)rh[i][e];
-                    lo[e] = (_Float16)(rh[i][e] - (float)hi[e]);
+                    const float x = XE == XE_BNBWD ? rh[i][e] * dsc : rh[i][e];   // dgrad: times 2^k (exact)
+                    hi[e] = (_Float16)x;
+                    lo[e] = (_Float16)(x - (float)hi[e]);
                 }
                 float* row = Ah + (sr + RPP * i) * BK;
                 const int q = (tid & 7) >> 1, half = ((tid & 7) & 1) * 2;

@@ -41,7 +41,9 @@ constexpr int TRAIN_BM = 128;   // rows per M tile of conv3x3_train (BN partials
 // raw output is multiplied by oscale[c] (= 2^-e of the layer, exact); nullptr: fp32 weights
 hipError_t launch_conv3x3_train(int C, int epi, int xe, const float* in, const float* wp, const float* resid,
                                 float* out, int M, const EpiX& ex, hipStream_t st, const ProX* px = nullptr,
-                                const FinX* fx = nullptr, const float* oscale = nullptr, unsigned* h3ovf = nullptr);
+                                const FinX* fx = nullptr, const float* oscale = nullptr, unsigned* h3ovf = nullptr,
+                                const unsigned* dmax = nullptr);
+extern int g_train_dgrad_h3;   // key 50: the train step's dgrad convs in split-fp16 (2: four products, 1: three, 0: fp32)
 extern int g_train_h3;   // key 49: the train step's forward convs in split-fp16 (1) or fp32 MFMA (0)
 extern int g_tower_mode;
 extern int g_conv_shape_override;
@@ -121,6 +123,8 @@ hipError_t launch_conv3x3_h3(int shape, int C, int epi, const float* in, const f
                              unsigned* ring, unsigned seq);
 hipError_t launch_pack_h3(const float* params, const int64_t* offs, int nl, int C, const int* conv_bn_off,
                           const float* scale, int* exps, void* wp16, float* scale16, float* inv, hipStream_t st);
+hipError_t launch_pack_h3_dgrad(const float* params, const int64_t* offs, int nl, int C, const int* exps, void* wd16,
+                                hipStream_t st);
 extern int g_tower_h3;
 extern int g_h3_tower_var;
 hipError_t launch_fold_bn(const float* params, const float* stats, const void* desc, int nlayers,
@@ -171,6 +175,7 @@ struct azg_pv {
     float* h3inv = nullptr;   // [2 NB][C]: 2^-e of each conv (train forward, raw outputs)
     int* conv_bn_off_dev = nullptr;
     bool h3_dirty = true;
+    unsigned h3_gen = 0;   // + 1 per split-fp16 re-pack (the train step's dgrad pack follows it)
 
     // eval activations: 3 padded NHWC buffers + head features [B][3][225]
     float* act[3] = {nullptr, nullptr, nullptr};

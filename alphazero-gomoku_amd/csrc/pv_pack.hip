@@ -247,6 +247,39 @@ hipError_t launch_pack_h3(const float* params, const int64_t* offs, int nl, int 
     return hipGetLastError();
 }
 
+// the split-fp16 dgrad packing (key 50): pack_h3's rows for the flipped, transposed taps
+// of pack_convs_kernel's wd (row kc * C + n = cin n, K values = 32 couts of group kc % CG
+// at tap 8 - kc / CG), w * 2^e with the layer's e (exps, after scale_h3_kernel)
+__global__ __launch_bounds__(256) void pack_h3_dgrad_kernel(const float* __restrict__ params,
+                                                            const int64_t* __restrict__ offs, int C,
+                                                            const int* __restrict__ exps, _Float16* __restrict__ out)
+{
+    const int total = 9 * C * C, cg_n = C / 32;
+    const int l = blockIdx.y;
+    const float* w = params + offs[l];
+    _Float16* o = out + (size_t)l * 2 * total;
+    const float sc = ldexpf(1.f, exps[l]);
+    for (int idx = blockIdx.x * 256 + threadIdx.x; idx < total; idx += gridDim.x * 256) {
+        const int k = idx & 31, n = (idx >> 5) % C, kc = idx / (32 * C);
+        const int tap = kc / cg_n, c2 = (kc - tap * cg_n) * 32 + k;
+        const float v = w[(c2 * C + n) * 9 + (8 - tap)] * sc;
+        const _Float16 hi = (_Float16)v;
+        const int row = idx >> 5;
+        o[row * 64 + k] = hi;
+        o[row * 64 + 32 + k] = (_Float16)(v - (float)hi);
+    }
+}
+
+hipError_t launch_pack_h3_dgrad(const float* params, const int64_t* offs, int nl, int C, const int* exps, void* wd16,
+                                hipStream_t st)
+{
+    if (nl <= 0) return hipSuccess;
+    int nb = nblk(9 * C * C);
+    nb = nb > 256 ? 256 : nb;
+    hipLaunchKernelGGL(pack_h3_dgrad_kernel, dim3(nb, nl), dim3(256), 0, st, params, offs, C, exps, (_Float16*)wd16);
+    return hipGetLastError();
+}
+
 hipError_t launch_pack_convs(const float* params, const int64_t* offs, int nl, float* wp, float* wd, int C,
                              hipStream_t st)
 {

@@ -59,6 +59,9 @@ struct TrainWS {
     float *gX = nullptr, *DH = nullptr, *GR = nullptr;
     std::vector<float*> dzs;     // one dZ buffer per backward conv (k = 2i + 1: conv2 of block i, 2i: conv1)
     float* wdpack = nullptr;     // dgrad-packed conv weights, 2*NB x 9*C*C
+    float* wdpack16 = nullptr;   // the same split-fp16 (key 50), allocated on first use
+    unsigned wd16_gen = ~0u;     // h3_gen it was packed from
+    unsigned* dmax = nullptr;    // [2*NB] max |dz| bits of each dgrad input (zeroed per step)
     // per BN layer, at BnDesc::out_off (nfold floats each)
     float *bmean = nullptr, *binv = nullptr, *bscale = nullptr, *bshift = nullptr;
     float *bgm = nullptr, *bk = nullptr, *biw = nullptr;
@@ -259,7 +262,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* __restrict__ g, const float* __restrict__ act, const float* __restrict__ z,
     const float* __restrict__ mean, const float* __restrict__ gm, const float* __restrict__ kk,
     const float* __restrict__ iw, float* __restrict__ dz, float* __restrict__ gres, int M,
-    const float* __restrict__ fscale = nullptr, const float* __restrict__ fshift = nullptr)
+    const float* __restrict__ fscale = nullptr, const float* __restrict__ fshift = nullptr,
+    unsigned* __restrict__ dmax = nullptr)
 {
     // grid-stride, kApplyU float4 per thread and pass with every load issued before the
     // first store; the stride is a multiple of C/4, so a thread's channels are fixed and
@@ -280,6 +284,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
         sc = *(const f32x4*)(fscale + c);
         sh = *(const f32x4*)(fshift + c);
     }
+    float amax = 0.f;
     for (int ib = i0; ib < total; ib += U * stride) {
         f32x4 gv[U], zv[U], av[U];
         int o[U];
@@ -307,7 +312,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
             }
             store4<WT>(dz, rz, o[u], out);
             if (GRES) store4<WT>(gres, rg, o[u], dyv);
+            amax = fmaxf(amax, fmaxf(fmaxf(fabsf(out[0]), fabsf(out[1])), fmaxf(fabsf(out[2]), fabsf(out[3]))));
         }
+    }
+    // max |dz| of the layer (the split-fp16 dgrad's input scale, key 50): the bits of a
+    // non-negative float order as the floats
+    if (dmax) {
+        amax = wave_max(amax);
+        if ((threadIdx.x & 63) == 0) atomicMax(dmax, __float_as_uint(amax));
     }
 }
 
@@ -676,6 +688,11 @@ static int32_t ensure_train_ws(azg_pv* h, int B, hipStream_t st)
     w->dzs.assign(2 * NB, nullptr);
     for (int k = 0; k < 2 * NB; ++k) A(w->dzs[k], act, true);
     A(w->wdpack, (size_t)(2 * NB > 0 ? 2 * NB : 1) * 9 * C * C, false);
+    {
+        float* dm = nullptr;
+        A(dm, (size_t)(2 * NB > 0 ? 2 * NB : 1), false);
+        w->dmax = (unsigned*)dm;
+    }
     const size_t nf = h->nfold;
     A(w->bmean, nf, true); A(w->binv, nf, true); A(w->bscale, nf, true); A(w->bshift, nf, true);
     A(w->bgm, nf, true); A(w->bk, nf, true); A(w->biw, nf, true);
@@ -805,7 +822,8 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     // sums of the layer below: act / z / layer `xl`); partials land in part_a / part_b;
     // fin >= 0: the BN layer this launch's partials belong to, finalized in-kernel
     auto conv = [&](int epi, int xe, const float* in, const float* wp, const float* res, float* out,
-                    const float* xact, const float* xz, int xl, int fin, const float* osc = nullptr) -> int32_t {
+                    const float* xact, const float* xz, int xl, int fin, const float* osc = nullptr,
+                    const unsigned* dmx = nullptr) -> int32_t {
         int pr = prof_begin(h, AZG_PROF_TRAIN_CONV, st, B);
         const EpiX ex{xact, xz, xl >= 0 ? w->bmean + bd[xl].out_off : nullptr, w->part_a, w->part_b};
         FinX fx{};
@@ -814,7 +832,7 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             fx.cnt = w->fincnt;
         }
         AZG_CK(launch_conv3x3_train(C, epi, xe, in, wp, res, out, M, ex, st, nullptr, fin >= 0 ? &fx : nullptr, osc,
-                                    osc ? h->train_ovf_dev : nullptr),
+                                    osc && !dmx ? h->train_ovf_dev : nullptr, dmx),
                "train: conv3x3");
         prof_end(h, pr, st);
         return 0;
@@ -822,12 +840,12 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
     // dz = BN backward of `layer` applied to g; act == nullptr: a residual-free layer,
     // its ReLU mask from z and the layer's folded scale / shift (bn_bwd_apply MZ)
     auto bwd_apply = [&](const float* g, const float* act, const float* z, int layer, float* dz,
-                         float* gres) -> int32_t {
+                         float* gres, unsigned* dmx = nullptr) -> int32_t {
         const int o = bd[layer].out_off;
 #define AZG_BWD_APPLY(GR, MZ)                                                                                 \
         hipLaunchKernelGGL((bn_bwd_apply_kernel<C, GR, true, MZ>), dim3(gM), dim3(256), 0, st, g, act, z,     \
                            w->bmean + o, w->bgm + o, w->bk + o, w->biw + o, dz, gres, M, w->bscale + o,         \
-                           w->bshift + o)
+                           w->bshift + o, dmx)
         if (gres) AZG_BWD_APPLY(true, false);
         else if (!act) AZG_BWD_APPLY(false, true);
         else AZG_BWD_APPLY(false, false);
@@ -851,6 +869,15 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
         return fh3 ? (const float*)h->wpack16 + (size_t)ci * CC9 : h->wpack + (size_t)ci * CC9;
     };
     auto fwd_s = [&](int ci) -> const float* { return fh3 ? h->h3inv + (size_t)ci * C : nullptr; };
+    // dgrad conv weights (key 50): the split-fp16 dgrad packs with the same 2^-e factor, the
+    // input's 2^k from its max |dz| (w->dmax, zeroed at the step's start), or the fp32 packs
+    const bool dh3 = g_train_dgrad_h3 && w->wdpack16 && h->h3inv && !h->train_fp32_once;
+    auto dg_w = [&](int ci) -> const float* {
+        return dh3 ? w->wdpack16 + (size_t)ci * CC9 : w->wdpack + (size_t)ci * CC9;
+    };
+    auto dg_s = [&](int ci) -> const float* { return dh3 ? h->h3inv + (size_t)ci * C : nullptr; };
+    if (dh3 && NB > 0)
+        AZG_CK(hipMemsetAsync(w->dmax, 0, (size_t)2 * NB * sizeof(unsigned), st), "train: dgrad max words");
 
     // ---- forward (train-mode BN) ----
     {
@@ -1041,15 +1068,15 @@ static int32_t train_backward_t(azg_pv* h, const float* x, const float* pis, con
             float* dz2 = w->dzs[2 * i + 1];
             float* dz1 = w->dzs[2 * i];
             if (!fin_next) R(bwd_fin(l2, ntt));
-            R(bwd_apply(w->gX, w->xo[i], w->z2[i], l2, dz2, w->GR));
+            R(bwd_apply(w->gX, w->xo[i], w->z2[i], l2, dz2, w->GR, dh3 ? w->dmax + 2 * i + 1 : nullptr));
             R(wgrad(dz2, w->hh[i], h->t_blk[i].w2));
-            R(conv(EPI_RAW, XE_BNBWD, dz2, w->wdpack + (size_t)(2 * i + 1) * CC9, nullptr, w->DH, w->hh[i],
-                   w->z1[i], l1, ffin ? l1 : -1));
+            R(conv(EPI_RAW, XE_BNBWD, dz2, dg_w(2 * i + 1), nullptr, w->DH, w->hh[i], w->z1[i], l1, ffin ? l1 : -1,
+                   dg_s(2 * i + 1), dh3 ? w->dmax + 2 * i + 1 : nullptr));
             if (!ffin) R(bwd_fin(l1, ntt));
-            R(bwd_apply(w->DH, nullptr, w->z1[i], l1, dz1, nullptr));
+            R(bwd_apply(w->DH, nullptr, w->z1[i], l1, dz1, nullptr, dh3 ? w->dmax + 2 * i : nullptr));
             R(wgrad(dz1, Xin, h->t_blk[i].w1));
-            R(conv(EPI_ADD, XE_BNBWD, dz1, w->wdpack + (size_t)(2 * i) * CC9, w->GR, w->gX, Xin, zin, lin,
-                   ffin ? lin : -1));
+            R(conv(EPI_ADD, XE_BNBWD, dz1, dg_w(2 * i), w->GR, w->gX, Xin, zin, lin, ffin ? lin : -1, dg_s(2 * i),
+                   dh3 ? w->dmax + 2 * i : nullptr));
             fin_next = ffin;
             R(snap(NB - i));
         }
@@ -1107,8 +1134,21 @@ int32_t train_backward(azg_pv* h, const float* x, const float* pis, const float*
         if (int32_t r = repack(h, st, w->wdpack)) return r;
         h->train_packs = true;
     }
-    if (g_train_h3 && !h->train_fp32_once)
+    if ((g_train_h3 || g_train_dgrad_h3) && !h->train_fp32_once)
         if (int32_t r = ensure_h3(h, st)) return r;
+    // the split-fp16 dgrad packs follow every split-fp16 re-pack (same per-layer 2^e)
+    if (g_train_dgrad_h3 && !h->train_fp32_once && h->NB > 0 && h->wpack16) {
+        if (!w->wdpack16) {
+            AZG_CK(hipMalloc(&w->wdpack16, (size_t)2 * h->NB * 9 * h->C * h->C * sizeof(float)),
+                   "train: split-fp16 dgrad packs");
+            w->allocs.push_back(w->wdpack16);
+        }
+        if (w->wd16_gen != h->h3_gen) {
+            AZG_CK(launch_pack_h3_dgrad(h->params, h->conv_off_dev, 2 * h->NB, h->C, h->h3exp, w->wdpack16, st),
+                   "train: split-fp16 dgrad pack");
+            w->wd16_gen = h->h3_gen;
+        }
+    }
     // the running stats this step starts from (a skipped step restores them): refreshed
     // whenever they may have changed outside the library; a step the Adam kernel commits
     // refreshes them itself

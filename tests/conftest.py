@@ -17,6 +17,21 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _study_tuning():
+    """AZG_TEST_TUNE="KEY=VALUE,..." runs the suite under non-default tuning keys (studies
+    that test a variant, e.g. scripts/gpu_r6j.sh's split-fp16 dgrad, key 50 = 2); unset in
+    every product run."""
+    spec = os.environ.get("AZG_TEST_TUNE", "")
+    if spec:
+        import _native
+        lib = _native.load_library()
+        for kv in spec.split(","):
+            k, v = (int(t) for t in kv.split("="))
+            lib.azg_pv_set_tuning(k, v)
+    yield
+
+
 def load_golden(tag: str) -> dict:
     with np.load(os.path.join(GOLDEN, f"net_{tag}.npz"), allow_pickle=False) as z:
         return {k: z[k] for k in z.files}
