@@ -131,7 +131,7 @@ __device__ __forceinline__ bool bt_epilogue(const f32x16 (&acc)[2], const float*
     return bad;
 }
 
-int g_board_abl = 0;   // TEMPORARY timing ablations (key 51): 1 no DMA wait, 2 no stage barrier, 4 no epilogue
+int g_board_abl = 0;   // timing ablations of the board towers (key 51, study build): 1 no DMA wait, 2 no barrier, 4 no epilogue
 template <int ABL>
 __global__ __launch_bounds__(kBtThreads, 4) void board_tower(const BoardArgs a)
 {
@@ -309,9 +309,13 @@ hipError_t launch_board_tower(int NB, const float* wp16, const float* scale16, c
     static int grid = 0;
     if (grid == 0) {
         hipError_t e = hipSuccess;
+#ifdef AZG_AB_STUDIES
         for (const void* f : {(const void*)board_tower<0>, (const void*)board_tower<1>, (const void*)board_tower<2>,
                               (const void*)board_tower<4>, (const void*)board_tower<7>, (const void*)board_tower<8>,
                               (const void*)board_tower<16>, (const void*)board_tower<24>})
+#else
+        for (const void* f : {(const void*)board_tower<0>})
+#endif
             if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kBtLds)) != hipSuccess) return e;
         int per_cu = 0, dev = 0, cus = 0;
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)board_tower<0>, kBtThreads, kBtLds);
@@ -333,16 +337,19 @@ hipError_t launch_board_tower(int NB, const float* wp16, const float* scale16, c
     a.ring_ovf = ring_ovf;
     a.seq = seq;
     const dim3 g(B < grid ? B : grid);
-    switch (g_board_abl) {
-        case 1: hipLaunchKernelGGL(board_tower<1>, g, dim3(kBtThreads), kBtLds, st, a); break;
-        case 2: hipLaunchKernelGGL(board_tower<2>, g, dim3(kBtThreads), kBtLds, st, a); break;
-        case 4: hipLaunchKernelGGL(board_tower<4>, g, dim3(kBtThreads), kBtLds, st, a); break;
-        case 7: hipLaunchKernelGGL(board_tower<7>, g, dim3(kBtThreads), kBtLds, st, a); break;
-        case 8: hipLaunchKernelGGL(board_tower<8>, g, dim3(kBtThreads), kBtLds, st, a); break;
-        case 16: hipLaunchKernelGGL(board_tower<16>, g, dim3(kBtThreads), kBtLds, st, a); break;
-        case 24: hipLaunchKernelGGL(board_tower<24>, g, dim3(kBtThreads), kBtLds, st, a); break;
-        default: hipLaunchKernelGGL(board_tower<0>, g, dim3(kBtThreads), kBtLds, st, a); break;
+#ifdef AZG_AB_STUDIES
+    switch (g_board_abl) {   // timing ablations (key 51, study build; results invalid while set)
+        case 1: hipLaunchKernelGGL(board_tower<1>, g, dim3(kBtThreads), kBtLds, st, a); return hipGetLastError();
+        case 2: hipLaunchKernelGGL(board_tower<2>, g, dim3(kBtThreads), kBtLds, st, a); return hipGetLastError();
+        case 4: hipLaunchKernelGGL(board_tower<4>, g, dim3(kBtThreads), kBtLds, st, a); return hipGetLastError();
+        case 7: hipLaunchKernelGGL(board_tower<7>, g, dim3(kBtThreads), kBtLds, st, a); return hipGetLastError();
+        case 8: hipLaunchKernelGGL(board_tower<8>, g, dim3(kBtThreads), kBtLds, st, a); return hipGetLastError();
+        case 16: hipLaunchKernelGGL(board_tower<16>, g, dim3(kBtThreads), kBtLds, st, a); return hipGetLastError();
+        case 24: hipLaunchKernelGGL(board_tower<24>, g, dim3(kBtThreads), kBtLds, st, a); return hipGetLastError();
+        default: break;
     }
+#endif
+    hipLaunchKernelGGL(board_tower<0>, g, dim3(kBtThreads), kBtLds, st, a);
     return hipGetLastError();
 }
 

@@ -73,7 +73,7 @@ typedef _Float16 b16_f16x2 __attribute__((ext_vector_type(2)));
 // stores the hi pairs, the odd lane the lo pairs.  Element pairs go through packed fp32 math
 // (v_pk_fma / v_pk_add: per element the same fmaf and add).  Returns whether an accumulator
 // was non-finite (their sum is: padding accumulators are exactly 0).
-template <bool RES, bool TO_LDS>
+template <bool RES, bool TO_LDS, int EABL = 0>
 __device__ __forceinline__ bool b16_epilogue(const f32x4 (&acc)[5][2], const float* __restrict__ scale,
                                              const float* __restrict__ shift, __amdgpu_buffer_rsrc_t xr, char* lds,
                                              const int* poff, int mg, int cg, int lane)
@@ -107,8 +107,9 @@ __device__ __forceinline__ bool b16_epilogue(const f32x4 (&acc)[5][2], const flo
             for (int n = 0; n < 2; ++n)
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    rvf[f][n][i] = __builtin_bit_cast(float,
-                                                      __builtin_amdgcn_raw_buffer_load_b32(xr, vof[f][i] + 64 * n, 0, 0));
+                    rvf[f][n][i] = (EABL & 1) ? __builtin_bit_cast(float, vof[f][i])   // study: no residual loads
+                                              : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                                              xr, vof[f][i] + 64 * n, 0, 0));
         }
     }
     b16_f32x2 chk = {0.f, 0.f};
@@ -136,10 +137,15 @@ __device__ __forceinline__ bool b16_epilogue(const f32x4 (&acc)[5][2], const flo
                 if constexpr (TO_LDS) {
                     // the lane's two elements split together: H = (hi_i, hi_i+1), L = (lo_i, lo_i+1);
                     // the partner lane's H (to an even lane) or L (to an odd lane) by one DPP
+                    // (lo = fp16(y - hi) by v_fma_mix{lo,hi}_f16: the exact fp32 difference rounded
+                    // once to fp16, as the cvt / subtract / cvt sequence does)
                     const b16_f32x2 yy = {ye[0], ye[1]};
                     const b16_f16x2 hp = __builtin_convertvector(yy, b16_f16x2);
-                    const b16_f16x2 lp = __builtin_convertvector(yy - __builtin_convertvector(hp, b16_f32x2), b16_f16x2);
-                    const unsigned H = __builtin_bit_cast(unsigned, hp), L = __builtin_bit_cast(unsigned, lp);
+                    const unsigned H = __builtin_bit_cast(unsigned, hp);
+                    unsigned L;
+                    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+                        "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+                        : "=&v"(L) : "v"(H), "v"(ye[0]), "v"(ye[1]));
                     const unsigned X = odd ? L : H, Z = odd ? H : L;
                     const unsigned Zp = (unsigned)__builtin_amdgcn_mov_dpp((int)Z, 0xB1, 0xF, 0xF, false);
 #pragma unroll
@@ -156,6 +162,8 @@ __device__ __forceinline__ bool b16_epilogue(const f32x4 (&acc)[5][2], const flo
 }
 
 extern int g_board_abl;
+// ABL: timing ablations of the study build (key 51): 1 no DMA wait, 2 no barrier, 4 no epilogue
+// (the accumulators kept live), 8 fixed A rows, 64 no residual loads; the product runs ABL 0
 template <int ABL>
 __global__ __launch_bounds__(kB16Threads, 1) void board16_tower(const Board16Args a)
 {
@@ -370,9 +378,9 @@ __global__ __launch_bounds__(kB16Threads, 1) void board16_tower(const Board16Arg
                     for (int j = 0; j < 2; ++j) t += acc[f][j][0] + acc[f][j][1] + acc[f][j][2] + acc[f][j][3];
                 if (t == 1234.5f) xb[tid] = t;
             }
-            else if (!(l & 1)) bad = b16_epilogue<false, true>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
-            else if (l + 1 < nl) bad = b16_epilogue<true, true>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
-            else bad = b16_epilogue<true, false>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
+            else if (!(l & 1)) bad = b16_epilogue<false, true, (ABL >> 6)>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
+            else if (l + 1 < nl) bad = b16_epilogue<true, true, (ABL >> 6)>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
+            else bad = b16_epilogue<true, false, (ABL >> 6)>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
             if (bad && a.ring_ovf && a.seq)
                 __hip_atomic_store(a.ring_ovf + (a.seq & (kTowerRing - 1)), a.seq, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
@@ -393,8 +401,13 @@ hipError_t launch_board16_tower(int NB, const float* wp16, const float* scale16,
     static int grid = 0;
     if (grid == 0) {
         hipError_t e = hipSuccess;
+#ifdef AZG_AB_STUDIES
         for (const void* f : {(const void*)board16_tower<0>, (const void*)board16_tower<3>, (const void*)board16_tower<4>,
-                              (const void*)board16_tower<8>, (const void*)board16_tower<15>})
+                              (const void*)board16_tower<8>, (const void*)board16_tower<15>,
+                              (const void*)board16_tower<64>})
+#else
+        for (const void* f : {(const void*)board16_tower<0>})
+#endif
             if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kB16Lds)) != hipSuccess) return e;
         int per_cu = 0, dev = 0, cus = 0;
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)board16_tower<0>, kB16Threads, kB16Lds);
@@ -416,13 +429,17 @@ hipError_t launch_board16_tower(int NB, const float* wp16, const float* scale16,
     a.ring_ovf = ring_ovf;
     a.seq = seq;
     const dim3 g(B < grid ? B : grid);
-    switch (g_board_abl) {
-        case 3: hipLaunchKernelGGL(board16_tower<3>, g, dim3(kB16Threads), kB16Lds, st, a); break;
-        case 4: hipLaunchKernelGGL(board16_tower<4>, g, dim3(kB16Threads), kB16Lds, st, a); break;
-        case 8: hipLaunchKernelGGL(board16_tower<8>, g, dim3(kB16Threads), kB16Lds, st, a); break;
-        case 15: hipLaunchKernelGGL(board16_tower<15>, g, dim3(kB16Threads), kB16Lds, st, a); break;
-        default: hipLaunchKernelGGL(board16_tower<0>, g, dim3(kB16Threads), kB16Lds, st, a); break;
+#ifdef AZG_AB_STUDIES
+    switch (g_board_abl) {   // timing ablations (key 51, study build; results invalid while set)
+        case 3: hipLaunchKernelGGL(board16_tower<3>, g, dim3(kB16Threads), kB16Lds, st, a); return hipGetLastError();
+        case 4: hipLaunchKernelGGL(board16_tower<4>, g, dim3(kB16Threads), kB16Lds, st, a); return hipGetLastError();
+        case 8: hipLaunchKernelGGL(board16_tower<8>, g, dim3(kB16Threads), kB16Lds, st, a); return hipGetLastError();
+        case 15: hipLaunchKernelGGL(board16_tower<15>, g, dim3(kB16Threads), kB16Lds, st, a); return hipGetLastError();
+        case 64: hipLaunchKernelGGL(board16_tower<64>, g, dim3(kB16Threads), kB16Lds, st, a); return hipGetLastError();
+        default: break;
     }
+#endif
+    hipLaunchKernelGGL(board16_tower<0>, g, dim3(kB16Threads), kB16Lds, st, a);
     return hipGetLastError();
 }
 

@@ -1029,11 +1029,13 @@ hipError_t launch_stem(int C, int epi, const float* x, const float* ws, const fl
 namespace azg { extern int g_board_abl; }
 extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
 {
-    if (key == 51) {  // TEMPORARY: board-tower timing ablations
+#ifdef AZG_AB_STUDIES
+    if (key == 51) {  // board-tower timing ablations (study build only)
         const int prev = azg::g_board_abl;
         azg::g_board_abl = value;
         return prev;
     }
+#endif
     if (key == 0) {
         const int prev = azg::g_conv_shape_override;
         azg::g_conv_shape_override = value;

@@ -1,4 +1,11 @@
-"""TEMPORARY: timing ablations of the board-resident tower (key 51; results invalid while set)."""
+"""Timing ablations of the board-resident towers (key 51, study build only; results invalid
+while set): device time per forward at the self-play batch sizes for each ablation in ABLS
+(comma list; 0 = the product body), and max |d logit| against ABL 0.  SHAPE=14 (default)
+the 16x16x32 board tower (key 19 = 2), SHAPE=13 the 32x32x16 one (key 19 = 1).
+
+    make -C alphazero-gomoku_amd/csrc study
+    AZG_PV_LIB=alphazero-gomoku_amd/libazg_pv_study.so ABLS=0,3,4,64 python scripts/board_abl.py
+"""
 import os
 import sys
 
@@ -17,7 +24,9 @@ def main():
     m = PyTorchModel(board_size=15, device="cuda", n_res_blocks=6, channels=128)
     eng = m.engine
     lib.azg_pv_set_tuning(5, 1)
-    lib.azg_pv_set_tuning(6, int(os.environ.get('SHAPE', '14')))
+    shape = int(os.environ.get('SHAPE', '14'))
+    lib.azg_pv_set_tuning(19, 2 if shape == 14 else 1)
+    lib.azg_pv_set_tuning(6, shape)
     flop = 12 * bench.conv_flop(128)
     for B in (512, 3456):
         x = torch.from_numpy(synth_encoded(B, seed=B)).cuda()
@@ -34,6 +43,9 @@ def main():
             _, _, lg = eng.forward(x, want_logits=True)
             if abl == 0:
                 l0 = lg.clone()
+                if os.environ.get("DUMP"):   # cross-build bitwise checks (scripts/gpu_lib_ab.sh)
+                    import numpy as np
+                    np.save(f"{os.environ['DUMP']}_B{B}.npy", l0.cpu().numpy())
             dl = float((lg - l0).abs().max())
             print(f"B={B} abl {abl}: {ms:.3f} ms = {flop * B / ms / 1e9:.1f} TFLOP/s, max|dlogit| vs abl 0 {dl:.2e}",
                   flush=True)
