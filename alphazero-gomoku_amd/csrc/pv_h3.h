@@ -1,4 +1,4 @@
-// Split-fp16 (H3) eval conv tile, round 6 form: the same products and the same
+// Split-fp16 (H3) eval conv tile, round 5 form: the same products and the same
 // per-element K order as halo_tile's H3 body (pv_halo.h VAR bit 64, so the two are
 // bitwise equal), restructured for what bounds that body on gfx950 -- the LDS.
 //
