@@ -52,6 +52,10 @@ SCRATCH_BUDGET = [
     (r"wgrad_reduce_kernel", 0),
     (r"wgrad_reduce_mfma_kernel", 0),
     (r"stem_mfma", 0),
+    # board-resident towers (round 6): spills in the per-board staging and the epilogue only
+    # (the K loops are scratch-free, checked in the ISA); the 16x16x32 one is the eval default
+    (r"board16_towerILi0E", 116),
+    (r"board_towerILi0E", 196),
 ]
 
 
@@ -124,3 +128,15 @@ def test_hot_kernels_fit_two_workgroups_per_cu():
         if re.search(r"conv_towerILi(128|256)ELi64ELi4ELi1ELi8E|conv3x3_trainILi(64|128)E", n):
             total = v.get("vgpr_count", 0) + v.get("agpr_count", 0)
             assert total <= 128, (n, total)
+
+
+def test_board_towers_occupancy():
+    """board16_tower: 12 waves at <= 168 VGPRs (3 waves per SIMD, one workgroup per CU);
+    board_tower: 16 waves at <= 128."""
+    ks = _kernels()
+    for pat, cap in ((r"board16_towerILi0E", 168), (r"board_towerILi0E", 128)):
+        hits = [n for n in ks if re.search(pat, n)]
+        assert hits, pat
+        for n in hits:
+            total = ks[n].get("vgpr_count", 0) + ks[n].get("agpr_count", 0)
+            assert total <= cap, (n, total)
