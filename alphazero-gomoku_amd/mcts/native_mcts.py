@@ -172,7 +172,6 @@ class NativeSelfPlay:
         order.  ``seeds`` seed each game's RandomState (default: drawn from numpy's
         global RNG); ``games`` optionally gives the starting positions; ``progress``
         (optional) is called with the number of live games once per round."""
-        from selfplay import sample_action_from_pi
         G = self.n_games
         if seeds is None:
             seeds = np.random.randint(0, 2 ** 31 - 1, size=G)
@@ -214,55 +213,81 @@ class NativeSelfPlay:
                 if not live[k]:
                     self.search_seconds += time.perf_counter() - t0
                     continue
-                n = ev.advance()
-                done = np.nonzero(f.status == DONE)[0]
-                if n:
-                    # the leaves are staged: the GPU starts on them while the host plays
-                    # the finished games' moves (their trees hold no pending leaves, so
-                    # this order changes no result)
-                    t1 = time.perf_counter()
-                    ev.submit(n)
-                    dt = time.perf_counter() - t1
-                    self.nn_seconds += dt
-                    t0 += dt            # search_seconds excludes the submit
-                    pending[k] = True
-                    self.boards += n
-                    self.forwards += 1
-                    self.max_batch = max(self.max_batch, n)
-                # games whose move search finished: sample (per-game RNG), play, restart
-                for i in done:
-                    i = int(i)
-                    g = lo + i
-                    game = games[g]
-                    pi = f.get_pi(i)
-                    state_enc = game.get_encoded_state()
-                    action = sample_action_from_pi(pi, temp_fn(moves[g]), rngs[g])
-                    if game.get_valid_moves()[action] != 1.0:
-                        action = int(np.argmax(pi))
-                    hist[g].append((state_enc, pi.copy(), int(game.current_player)))
-                    game.do_move(divmod(action, game.size))
-                    moves[g] += 1
-                    self.moves += 1
-                    if game.is_game_over() or moves[g] >= max_moves:
-                        results[g] = self._finish(hist[g], game.get_winner(), use_symmetries)
-                        self.game_lengths.append(moves[g])
-                        live[k] -= 1
-                    else:
-                        f.set_root(i, game, len(game.move_history))
+                # advance; if no leaf came out (every live game of the group finished its move
+                # search this round) play the moves and advance again at once, so the group's
+                # next forward is submitted before the host turns to the other group (the GPU
+                # would otherwise idle through a whole group's move processing)
+                while True:
+                    n = ev.advance()
+                    done = np.nonzero(f.status == DONE)[0]
+                    if n:
+                        # the leaves are staged: the GPU starts on them while the host plays
+                        # the finished games' moves (their trees hold no pending leaves, so
+                        # this order changes no result)
+                        t1 = time.perf_counter()
+                        ev.submit(n)
+                        dt = time.perf_counter() - t1
+                        self.nn_seconds += dt
+                        t0 += dt            # search_seconds excludes the submit
+                        pending[k] = True
+                        self.boards += n
+                        self.forwards += 1
+                        self.max_batch = max(self.max_batch, n)
+                    self._play_done(f, done, lo, games, hist, moves, results, live, k, rngs, temp_fn, max_moves,
+                                    use_symmetries)
+                    if pending[k] or not live[k] or not len(done):
+                        break
                 self.search_seconds += time.perf_counter() - t0
         self.rounds = max(self.rounds, max(moves) if moves else 0)
         return results
 
+    def _play_done(self, f, done, lo, games, hist, moves, results, live, k, rngs, temp_fn, max_moves,
+                   use_symmetries):
+        """Games whose move search finished: sample (per-game RNG), play, restart."""
+        from selfplay import sample_action_from_pi
+        for i in done:
+            i = int(i)
+            g = lo + i
+            game = games[g]
+            pi = f.get_pi(i)
+            state_enc = game.get_encoded_state()
+            action = sample_action_from_pi(pi, temp_fn(moves[g]), rngs[g])
+            if game.get_valid_moves()[action] != 1.0:
+                action = int(np.argmax(pi))
+            hist[g].append((state_enc, pi.copy(), int(game.current_player)))
+            game.do_move(divmod(action, game.size))
+            moves[g] += 1
+            self.moves += 1
+            if game.is_game_over() or moves[g] >= max_moves:
+                results[g] = self._finish(hist[g], game.get_winner(), use_symmetries)
+                self.game_lengths.append(moves[g])
+                live[k] -= 1
+            else:
+                f.set_root(i, game, len(game.move_history))
+
     @staticmethod
     def _finish(history, winner, use_symmetries):
-        out = []
-        for state_enc, pi_vec, who in history:
-            z = 0.0 if winner == 0 else (1.0 if winner == who else -1.0)
-            if use_symmetries:
-                for s_aug, pi_aug in _PyMCTS.symmetries(None, state_enc, pi_vec):
-                    out.append((s_aug.astype(np.float32), pi_aug.astype(np.float32), z))
-            else:
-                out.append((state_enc.astype(np.float32), pi_vec.astype(np.float32), z))
+        """A finished game's examples: per position (in order) its 8 dihedral images in
+        _PyMCTS.symmetries' order (rotation k, then its horizontal flip) with the outcome
+        from the mover's view.  The images are formed for the whole game at once (8 array
+        ops instead of 8 per position: the per-position form stalled the GPU for tens of ms
+        when many games ended in one round); the values are the same permutations."""
+        if not history:
+            return [], winner
+        zs = [0.0 if winner == 0 else (1.0 if winner == who else -1.0) for _, _, who in history]
+        S = np.stack([h[0] for h in history]).astype(np.float32)          # [T, C, n, n]
+        n = S.shape[2]
+        P = np.stack([h[1] for h in history]).astype(np.float32).reshape(len(history), n, n)
+        if not use_symmetries:
+            return [(S[t], P[t].reshape(-1), zs[t]) for t in range(len(history))], winner
+        imgs = []
+        for k in range(4):
+            s_k = np.rot90(S, k, axes=(2, 3))
+            p_k = np.rot90(P, k, axes=(1, 2))
+            imgs.append((np.ascontiguousarray(s_k), np.ascontiguousarray(p_k).reshape(len(history), -1)))
+            imgs.append((np.ascontiguousarray(np.flip(s_k, axis=3)),
+                         np.ascontiguousarray(np.flip(p_k, axis=2)).reshape(len(history), -1)))
+        out = [(si[t], pi[t], zs[t]) for t in range(len(history)) for si, pi in imgs]
         return out, winner
 
 
