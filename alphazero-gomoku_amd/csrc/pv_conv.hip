@@ -1082,7 +1082,7 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         if (value >= 0 && value <= 2) azg::g_train_h3 = value;
         return prev;
     }
-    if (key == 50) {  // train dgrad convs: 2 split-fp16, four products (default); 1 three; 0 fp32 MFMA
+    if (key == 50) {  // train dgrad convs: 2 split-fp16, four products; 1 three; 0 fp32 MFMA (default)
         const int prev = azg::g_train_dgrad_h3;
         if (value >= 0 && value <= 2) azg::g_train_dgrad_h3 = value;
         return prev;
