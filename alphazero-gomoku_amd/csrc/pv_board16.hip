@@ -39,7 +39,8 @@ constexpr int kB16Rows = PIX + 1;                             // 225 pixels + th
 constexpr int kB16Stage = kB16C * 128;                        // one (tap, cg) weight chunk: 128 rows x [hi 32 | lo 32]
 constexpr int kB16Act = 2 * kB16Stage;                        // LDS: [2] weight stages, then the activations
 constexpr int kB16Prow = kB16Act + kB16Groups * kB16Rows * 128;
-constexpr int kB16Lds = kB16Prow + 240 * 4;                   // 149,440 B: one workgroup per CU
+constexpr int kB16Hw = kB16Prow + 240 * 4;                    // the heads' 1x1 weights [3][128] (fused projection)
+constexpr int kB16Lds = kB16Hw + 3 * kB16C * 4;               // 150,976 B: one workgroup per CU
 constexpr int kB16Waves = 12;
 constexpr int kB16Threads = 64 * kB16Waves;
 constexpr int kB16MaxLayers = 2 * kTowerMaxBlocks;
@@ -56,9 +57,19 @@ struct Board16Args {
     int nlayers;
     unsigned* ring_ovf;                 // host-mapped H3 overflow ring (device alias)
     unsigned seq;                       // launch number (0: autotuning runs, never posted)
+    const float* hwp;                   // heads: policy_conv [2][128], value_conv [128] weights,
+    const float* hwv;                   //   folded BN scale / shift [3] (policy 2, value 1)
+    const float* hsc;
+    const float* hsh;
+    float* hout;                        // [B][FC_FS] projected features (nullptr: tower output to x)
 };
 
 typedef float b16_f32x2 __attribute__((ext_vector_type(2)));
+
+// byte offset of (pixel m, channel c) in the fp32 rows of the fused heads projection: 16-B
+// slots keyed by m & 15, so the epilogue's stores and the projection's float4 reads spread
+// over the banks (a wave's 16 pixels x 4 quarters read 64 distinct slots of 16 bank groups)
+__device__ __forceinline__ int b16_f32_row(int m, int c) { return m * (kB16C * 4) + 16 * ((c >> 2) ^ (m & 15)) + 4 * (c & 3); }
 typedef _Float16 b16_f16x2 __attribute__((ext_vector_type(2)));
 
 // Eval epilogue of one conv for a wave's 80x32 tile: element i of tile (f, n) is pixel
@@ -72,8 +83,9 @@ typedef _Float16 b16_f16x2 __attribute__((ext_vector_type(2)));
 // even lane) or L (to the odd lane) by one DPP, and two v_perm form the words: the even lane
 // stores the hi pairs, the odd lane the lo pairs.  Element pairs go through packed fp32 math
 // (v_pk_fma / v_pk_add: per element the same fmaf and add).  Returns whether an accumulator
-// was non-finite (their sum is: padding accumulators are exactly 0).
-template <bool RES, bool TO_LDS, int EABL = 0>
+// was non-finite (their sum is: padding accumulators are exactly 0).  F32L (the last conv when
+// the heads are fused): the block output goes to LDS as fp32 rows [pixel][128] instead of HBM.
+template <bool RES, bool TO_LDS, int EABL = 0, bool F32L = false>
 __device__ __forceinline__ bool b16_epilogue(const f32x4 (&acc)[5][2], const float* __restrict__ scale,
                                              const float* __restrict__ shift, __amdgpu_buffer_rsrc_t xr, char* lds,
                                              const int* poff, int mg, int cg, int lane)
@@ -128,7 +140,12 @@ __device__ __forceinline__ bool b16_epilogue(const f32x4 (&acc)[5][2], const flo
                 b16_f32x2 y = __builtin_elementwise_fma(v, b16_f32x2{sc[n], sc[n]}, b16_f32x2{sh[n], sh[n]});
                 if constexpr (RES) y += b16_f32x2{rv[n][2 * ip], rv[n][2 * ip + 1]};
                 const float ye[2] = {fmaxf(y.x, 0.f), fmaxf(y.y, 0.f)};
-                if constexpr (RES) {
+                if constexpr (RES && F32L) {
+#pragma unroll
+                    for (int e = 0; e < 2; ++e)
+                        if (f < 4 || m0 + 2 * ip + e < PIX)
+                            *(float*)(lds + kB16Act + b16_f32_row(m0 + 2 * ip + e, 32 * cg + 16 * n + r16)) = ye[e];
+                } else if constexpr (RES) {
 #pragma unroll
                     for (int e = 0; e < 2; ++e)
                         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, ye[e]), xr,
@@ -179,6 +196,7 @@ __global__ __launch_bounds__(kB16Threads, 1) void board16_tower(const Board16Arg
     for (int i = tid; i < 240; i += kB16Threads)
         poff[i] = i < PIX ? ((i / BOARD + 1) * PADW + i % BOARD + 1) * kB16C * 4 : 0x40000000;
     if (tid < kB16Groups * 32) ((float*)(lds + kB16Act + ((tid >> 5) * kB16Rows + PIX) * 128))[tid & 31] = 0.f;
+    if (a.hout && tid < 3 * kB16C) ((float*)(lds + kB16Hw))[tid] = tid < 2 * kB16C ? a.hwp[tid] : a.hwv[tid - 2 * kB16C];
 
     // this lane's A rows (pixel 80 mg + 16 f + r16 of fragment f) and the taps on the board
     int pf[5];
@@ -380,6 +398,7 @@ __global__ __launch_bounds__(kB16Threads, 1) void board16_tower(const Board16Arg
             }
             else if (!(l & 1)) bad = b16_epilogue<false, true, (ABL >> 6)>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
             else if (l + 1 < nl) bad = b16_epilogue<true, true, (ABL >> 6)>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
+            else if (a.hout) bad = b16_epilogue<true, false, (ABL >> 6), true>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
             else bad = b16_epilogue<true, false, (ABL >> 6)>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
             if (bad && a.ring_ovf && a.seq)
                 __hip_atomic_store(a.ring_ovf + (a.seq & (kTowerRing - 1)), a.seq, __ATOMIC_RELAXED,
@@ -391,11 +410,54 @@ __global__ __launch_bounds__(kB16Threads, 1) void board16_tower(const Board16Arg
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
         }
+        if (a.hout) {
+            // the heads' three 1x1 projections of the tower output (network.py:102-103, 110-111)
+            // from the fp32 rows in LDS, heads_project's arithmetic (pv_heads.hip): lane 4 m + q
+            // chains channels 32 q .. 32 q + 31, two xor shuffles sum the quarters, then BN + ReLU
+            float* hb = a.hout + (size_t)board * FC_FS;
+            int tp = tid;
+            asm volatile("" : "+v"(tp));   // addresses rebuilt per board, not kept live across the convs
+            for (int i0 = 0; i0 < PIX * 4; i0 += kB16Threads) {
+                const int i = i0 + tp, m = i >> 2, q = i & 3;
+                float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+                if (m < PIX) {
+                    const float* w0 = (const float*)(lds + kB16Hw) + 32 * q;
+                    const float *w1 = w0 + kB16C, *w2 = w0 + 2 * kB16C;
+#pragma unroll
+                    for (int c = 0; c < 32; c += 4) {
+                        const f32x4 v = *(const f32x4*)(lds + kB16Act + b16_f32_row(m, 32 * q + c));
+                        const f32x4 u0 = *(const f32x4*)(w0 + c), u1 = *(const f32x4*)(w1 + c),
+                                    u2 = *(const f32x4*)(w2 + c);
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            d0 = fmaf(v[k], u0[k], d0);
+                            d1 = fmaf(v[k], u1[k], d1);
+                            d2 = fmaf(v[k], u2[k], d2);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int o = 1; o < 4; o <<= 1) {
+                    d0 += __shfl_xor(d0, o, 64);
+                    d1 += __shfl_xor(d1, o, 64);
+                    d2 += __shfl_xor(d2, o, 64);
+                }
+                if (m < PIX && q == 0) {
+                    hb[m] = head_bn_relu(d0, a.hsc[0], a.hsh[0]);
+                    hb[PIX + m] = head_bn_relu(d1, a.hsc[1], a.hsh[1]);
+                    hb[FC_KP + m] = head_bn_relu(d2, a.hsc[2], a.hsh[2]);
+                }
+            }
+            __syncthreads();   // the rows are read before the next board's stem output lands there
+            // the fp32 rows covered the groups' zero rows: restore them
+            if (tp < kB16Groups * 32) ((float*)(lds + kB16Act + ((tp >> 5) * kB16Rows + PIX) * 128))[tp & 31] = 0.f;
+        }
     }
 }
 
 hipError_t launch_board16_tower(int NB, const float* wp16, const float* scale16, const float* shift,
-                                const int* out_off, float* x, int B, unsigned* ring_ovf, unsigned seq, hipStream_t st)
+                                const int* out_off, float* x, int B, unsigned* ring_ovf, unsigned seq, hipStream_t st,
+                                const float* hwp, const float* hwv, const float* hsc, const float* hsh, float* hout)
 {
     if (2 * NB > kB16MaxLayers || NB <= 0 || B <= 0) return hipErrorInvalidValue;
     static int grid = 0;
@@ -428,6 +490,8 @@ hipError_t launch_board16_tower(int NB, const float* wp16, const float* scale16,
     a.nlayers = 2 * NB;
     a.ring_ovf = ring_ovf;
     a.seq = seq;
+    if (hout && !(hwp && hwv && hsc && hsh)) return hipErrorInvalidValue;
+    a.hwp = hwp, a.hwv = hwv, a.hsc = hsc, a.hsh = hsh, a.hout = hout;
     const dim3 g(B < grid ? B : grid);
 #ifdef AZG_AB_STUDIES
     switch (g_board_abl) {   // timing ablations (key 51, study build; results invalid while set)

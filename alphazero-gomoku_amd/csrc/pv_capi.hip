@@ -658,11 +658,14 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
             out_off[2 * i + 1] = bd[h->bn_blk[i].second].out_off;
         }
         pr = prof_begin(h, variant == 14 ? AZG_PROF_BOARD16 : AZG_PROF_BOARD, st, batch);
-        if (variant == 14)
+        if (variant == 14) {   // the heads' projections fused: features into hbuf (forward_eval)
+            const float* P = h->params;
+            const int ho = bd[h->bn_pol].out_off;
             AZG_TRY(launch_board16_tower(h->NB, (const float*)h->wpack16, h->scale16, h->shift, out_off, X, batch,
-                                         h->ovf_dev, seq, st),
+                                         h->ovf_dev, seq, st, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w],
+                                         h->scale + ho, h->shift + ho, h->hbuf),
                     "forward: board tower (16x16x32)");
-        else
+        } else
             AZG_TRY(launch_board_tower(h->NB, (const float*)h->wpack16, h->scale16, h->shift, out_off, X, batch,
                                        h->ovf_dev, seq, st),
                     "forward: board tower");
@@ -847,7 +850,7 @@ int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* 
     AZG_TRY(launch_heads_fwd(C, X, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], h->scale + ho, h->shift + ho,
                              h->wfc, P + h->poff[h->t_pfc_b], P + h->poff[h->t_vfc1_b],
                              P + h->poff[h->t_vfc2_w], P + h->poff[h->t_vfc2_b], h->hbuf, probs, values, logits,
-                             batch, st, boards, priors),
+                             batch, st, boards, priors, variant == 14),
             "forward: heads");
     prof_end(h, pr, st);
     return 0;

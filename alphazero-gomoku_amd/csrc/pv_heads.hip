@@ -53,9 +53,9 @@ __global__ __launch_bounds__(256) void heads_project(const float* __restrict__ a
         const int b = m / PIX, p = m - b * PIX;
         float* hb = hout + (size_t)b * fs;
         if (BN) {
-            d0 = fmaxf(d0 * hscale[0] + hshift[0], 0.f);
-            d1 = fmaxf(d1 * hscale[1] + hshift[1], 0.f);
-            d2 = fmaxf(d2 * hscale[2] + hshift[2], 0.f);
+            d0 = head_bn_relu(d0, hscale[0], hshift[0]);
+            d1 = head_bn_relu(d1, hscale[1], hshift[1]);
+            d2 = head_bn_relu(d2, hscale[2], hshift[2]);
         }
         hb[p] = d0;
         hb[PIX + p] = d1;
@@ -194,11 +194,14 @@ hipError_t launch_heads_fwd(int C, const float* act, const float* wpc, const flo
                             const float* hshift, const float* wfc, const float* bpf,
                             const float* bv1, const float* wv2, const float* bv2, float* hbuf, float* probs,
                             float* values, float* logits, int B, hipStream_t st, const int8_t* boards,
-                            float* priors)
+                            float* priors, bool projected)
 {
     if (B <= 0) return hipSuccess;
-    // hbuf: [B][FC_FS] features (zero pads, set at allocation) then pre [B][FC_OUT]
-    hipError_t e = launch_heads_project(C, true, act, wpc, wvc, hscale, hshift, hbuf, B * PIX, st, FC_FS, FC_KP);
+    // hbuf: [B][FC_FS] features (zero pads, set at allocation) then pre [B][FC_OUT]; the
+    // board16 tower writes the features itself (projected)
+    hipError_t e = projected ? hipSuccess
+                             : launch_heads_project(C, true, act, wpc, wvc, hscale, hshift, hbuf, B * PIX, st, FC_FS,
+                                                    FC_KP);
     if (e != hipSuccess) return e;
     float* pre = hbuf + (size_t)B * FC_FS;
     hipLaunchKernelGGL(heads_fc, dim3((B + 31) / 32, 10), dim3(256), 0, st, hbuf, wfc, pre, B);

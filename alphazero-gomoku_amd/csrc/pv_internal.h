@@ -88,8 +88,14 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
 // place with the tower output
 hipError_t launch_board_tower(int NB, const float* wp16, const float* scale16, const float* shift, const int* out_off,
                               float* x, int B, unsigned* ring_ovf, unsigned seq, hipStream_t st);
+// hout != nullptr: the tower output stays in LDS and the kernel writes the heads' projected
+// features (heads_project's, bitwise) to hout [B][FC_FS] instead of x
 hipError_t launch_board16_tower(int NB, const float* wp16, const float* scale16, const float* shift,
-                                const int* out_off, float* x, int B, unsigned* ring_ovf, unsigned seq, hipStream_t st);
+                                const int* out_off, float* x, int B, unsigned* ring_ovf, unsigned seq, hipStream_t st,
+                                const float* hwp = nullptr, const float* hwv = nullptr, const float* hsc = nullptr,
+                                const float* hsh = nullptr, float* hout = nullptr);
+// the heads' 1x1 projection epilogue: folded eval BN + ReLU (heads_project and the board16 tower)
+__device__ __forceinline__ float head_bn_relu(float d, float s, float h) { return fmaxf(d * s + h, 0.f); }
 extern unsigned g_tower_wait_us;
 extern int g_tower_group;
 #ifdef AZG_AB_STUDIES
@@ -103,7 +109,7 @@ hipError_t launch_heads_fwd(int C, const float* act, const float* wpc, const flo
                             const float* bpf, const float* bv1,
                             const float* wv2, const float* bv2, float* hbuf, float* probs,
                             float* values, float* logits, int B, hipStream_t st,
-                            const int8_t* boards = nullptr, float* priors = nullptr);
+                            const int8_t* boards = nullptr, float* priors = nullptr, bool projected = false);
 hipError_t launch_heads_fc(const float* feat, const float* wfc, float* pre, int B, hipStream_t st);
 hipError_t launch_heads_project(int C, bool bn, const float* act, const float* wpc, const float* wvc,
                                 const float* hscale, const float* hshift, float* hout, int M, hipStream_t st,

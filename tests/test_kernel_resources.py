@@ -54,7 +54,8 @@ SCRATCH_BUDGET = [
     (r"stem_mfma", 0),
     # board-resident towers (round 6): spills in the per-board staging and the epilogue only
     # (the K loops are scratch-free, checked in the ISA); the 16x16x32 one is the eval default
-    (r"board16_towerILi0E", 116),
+    # (and projects the heads' features from LDS after its last conv)
+    (r"board16_towerILi0E", 120),
     (r"board_towerILi0E", 196),
 ]
 
