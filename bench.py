@@ -375,7 +375,8 @@ def tower_knames(ch, blocks):
     n = 2 * blocks
     return {"board16": (f"azg::board16_tower (board-resident residual tower on v_mfma_f32_16x16x32_f16: one board "
                         f"per 12-wave workgroup, its activations in LDS as split fp16 through all {n} fused 3x3 conv + "
-                        f"BN (+ residual) + ReLU layers, split-fp16 products, LDS-DMA weight stages)"),
+                        f"BN (+ residual) + ReLU layers, split-fp16 products, LDS-DMA weight stages; then the heads' three 1x1 "
+                        f"projections from the fp32 tower output in LDS)"),
             "board": (f"azg::board_tower (board-resident residual tower: one board per 16-wave workgroup, its "
                       f"activations in LDS as split fp16 through all {n} fused 3x3 conv + BN (+ residual) + ReLU "
                       f"layers, split-fp16 products, LDS-DMA weight stages)"),
