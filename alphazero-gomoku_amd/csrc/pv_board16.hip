@@ -43,6 +43,9 @@ constexpr int kB16Hw = kB16Prow + 240 * 4;                    // the heads' 1x1 
 constexpr int kB16Lds = kB16Hw + 3 * kB16C * 4;               // 150,976 B: one workgroup per CU
 constexpr int kB16Waves = 12;
 constexpr int kB16Threads = 64 * kB16Waves;
+constexpr int kB16SplitThreads = 256;                         // SPLIT: 4 waves, one pixel third of a board
+constexpr int kB16Img = kB16Groups * kB16Rows * 128;          // one board's image (an exchange buffer)
+static_assert(kB16Img == (int)kB16ImgBytes, "pv_internal.h kB16ImgBytes");
 constexpr int kB16MaxLayers = 2 * kTowerMaxBlocks;
 constexpr int kB16Steps = 9 * kB16Groups;                     // K32 steps (weight chunks) per conv
 static_assert((kB16Groups * kB16Rows * 128) % 256 == 0, "a group's image keeps the 256-B bank phase");
@@ -62,9 +65,17 @@ struct Board16Args {
     const float* hsc;
     const float* hsh;
     float* hout;                        // [B][FC_FS] projected features (nullptr: tower output to x)
+    // SPLIT (small batches): three workgroups per board exchange conv outputs' boundary rows
+    char* xbuf;                         // [B][2 (layer parity)][kB16Img] exchange images
+    unsigned* xflag;                    // [B][3] per pixel third: epoch * 64 + layers published
+    unsigned epoch;                     // this launch's tag base (the handle's split launch count)
+    unsigned* ring;                     // host-mapped ring of timed-out launches (azg_pv_recover)
+    unsigned* diag;                     // the tower wait record (word 1: timeouts); may be null
+    unsigned limit;                     // awake-time bound of one wait, 10-ns ticks (key 14)
 };
 
 typedef float b16_f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned b16_u32x4 __attribute__((ext_vector_type(4)));
 
 // byte offset of (pixel m, channel c) in the fp32 rows of the fused heads projection: 16-B
 // slots keyed by m & 15, so the epilogue's stores and the projection's float4 reads spread
@@ -178,25 +189,107 @@ __device__ __forceinline__ bool b16_epilogue(const f32x4 (&acc)[5][2], const flo
     return !__builtin_isfinite(chk.x + chk.y);
 }
 
+// SPLIT: one wait of lane 0 on a neighbour's flag, bounded by the wave's AWAKE time (each
+// s_memrealtime delta counts at most 10 us: a suspended dispatch does not time out on the
+// gap), as pv_tower.hip's tower_wait.  Returns false on timeout.
+__device__ __forceinline__ bool b16_wait(const unsigned* f, unsigned need, unsigned limit)
+{
+    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need && limit != 0) return true;
+    unsigned long long prev = __builtin_amdgcn_s_memrealtime();
+    unsigned waited = 0;
+    for (;;) {
+        __builtin_amdgcn_s_sleep(2);
+        const unsigned seen = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long d = now - prev;
+        prev = now;
+        waited += d < 1000ull ? (unsigned)d : 1000u;
+        if (seen >= need && limit != 0) return true;
+        if (waited >= limit) return false;
+    }
+}
+
+// SPLIT exchange after conv l (l + 1 < nlayers): workgroup mg owns pixels m0..m1-1 of the
+// board; the next conv's taps read pixels up to 16 rows past them, so it publishes its first
+// and last 16 pixel rows (every channel group: the LDS image's own keyed words, 16-B
+// write-through stores, cdna_hip_programming.md Guideline 16 R1: drain, barrier, one agent-
+// scope flag store), waits for the neighbours' flags, takes ONE agent-scope acquire, and
+// copies their 16 rows next to its own.  Layer parity double-buffers the images: a neighbour
+// cannot publish conv l + 2 before this workgroup published l + 1, i.e. finished reading l.
+__device__ __forceinline__ void b16_exchange(const Board16Args& a, char* lds, int board, int mg, int l, int tid)
+{
+    char* xb = a.xbuf + ((size_t)board * 2 + (l & 1)) * kB16Img;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(xb, (short)0, kB16Img, 0x00020000);
+    const int m0 = 80 * mg, m1 = mg == 2 ? PIX : m0 + 80;
+    // piece p of the 1024 16-B pieces of two 16-row ranges (0: starting at lo, 1: at hi) x 4
+    // groups -> byte offset in the image, -1 where the range has no neighbour
+    auto piece = [&](int p, int lo, int hi) {
+        const int r = p >> 9, q = p & 511, g = q >> 7, row = (q >> 3) & 15;
+        if (r == 0 ? mg == 0 : mg == 2) return -1;
+        return (g * kB16Rows + (r == 0 ? lo : hi) + row) * 128 + 16 * (q & 7);
+    };
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int o = piece(tid + kB16SplitThreads * k, m0, m1 - 16);
+        if (o >= 0) __builtin_amdgcn_raw_buffer_store_b128(*(const b16_u32x4*)(lds + kB16Act + o), xr, o, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        unsigned* fl = a.xflag + (size_t)board * 3;
+        const unsigned tag = a.epoch * 64u + (unsigned)l + 1u;
+        __hip_atomic_store(fl + mg, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool ok = true;
+        if (mg > 0) ok = b16_wait(fl + mg - 1, tag, a.limit) && ok;
+        if (mg < 2) ok = b16_wait(fl + mg + 1, tag, a.limit) && ok;
+        if (!ok) {   // the rows are stale: post the launch (azg_pv_recover reruns it unsplit) and go on
+            if (a.ring && a.seq)
+                __hip_atomic_store(a.ring + (a.seq & (kTowerRing - 1)), a.seq, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            if (a.diag) __hip_atomic_fetch_add(a.diag + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    b16_u32x4 v[4];
+    int off[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        off[k] = piece(tid + kB16SplitThreads * k, m0 - 16, m1);
+        if (off[k] >= 0) v[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, off[k], 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (off[k] >= 0) *(b16_u32x4*)(lds + kB16Act + off[k]) = v[k];
+    __syncthreads();
+}
+
 extern int g_board_abl;
 // ABL: timing ablations of the study build (key 51): 1 no DMA wait, 2 no barrier, 4 no epilogue
 // (the accumulators kept live), 8 fixed A rows, 64 no residual loads; the product runs ABL 0
-template <int ABL>
-__global__ __launch_bounds__(kB16Threads, 1) void board16_tower(const Board16Args a)
+// SPLIT (small batches): three 4-wave workgroups per board, workgroup 3 b + mg computing pixels
+// 80 mg .. 80 mg + 79 of every channel group (wave = channel group), the same per-wave tiles
+// and MFMA sequence (bitwise the unsplit tower), conv outputs' boundary rows exchanged
+// through L2 (b16_exchange); the tower output goes to x (the heads run unfused).
+template <int ABL, bool SPLIT = false>
+__global__ __launch_bounds__(SPLIT ? kB16SplitThreads : kB16Threads, 1) void board16_tower(const Board16Args a)
 {
+    constexpr int NT = SPLIT ? kB16SplitThreads : kB16Threads;
     extern __shared__ __attribute__((aligned(16))) float smem_f[];
     char* lds = (char*)smem_f;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int mg = wid % 3, ng = wid / 3;
+    const int mg = SPLIT ? (int)blockIdx.x % 3 : wid % 3, ng = SPLIT ? wid : wid / 3;
     const int r16 = lane & 15, kb = lane >> 4;
     int* poff = (int*)(lds + kB16Prow);   // byte offset of each pixel's padded row (padding: past the board)
 
     // padded row of every pixel (-1 past pixel 224), the groups' zero rows
-    for (int i = tid; i < 240; i += kB16Threads)
+    for (int i = tid; i < 240; i += NT)
         poff[i] = i < PIX ? ((i / BOARD + 1) * PADW + i % BOARD + 1) * kB16C * 4 : 0x40000000;
     if (tid < kB16Groups * 32) ((float*)(lds + kB16Act + ((tid >> 5) * kB16Rows + PIX) * 128))[tid & 31] = 0.f;
-    if (a.hout && tid < 3 * kB16C) ((float*)(lds + kB16Hw))[tid] = tid < 2 * kB16C ? a.hwp[tid] : a.hwv[tid - 2 * kB16C];
+    if (a.hout)
+        for (int i = tid; i < 3 * kB16C; i += NT) ((float*)(lds + kB16Hw))[i] = i < 2 * kB16C ? a.hwp[i] : a.hwv[i - 2 * kB16C];
 
     // this lane's A rows (pixel 80 mg + 16 f + r16 of fragment f) and the taps on the board
     int pf[5];
@@ -228,23 +321,33 @@ __global__ __launch_bounds__(kB16Threads, 1) void board16_tower(const Board16Arg
     auto dma = [&](const float* wl, int s, int buf) {   // chunk s = cg * 9 + tap -> stage buf
         const int cg = s / 9, tap = s - cg * 9;
         const float* src = wl + (size_t)(tap * kB16Groups + cg) * kB16C * 32;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + ws0),
-                                         (__attribute__((address_space(3))) void*)(lds + buf * kB16Stage + wid * 1024),
-                                         16, 0, 0);
-        if (wid < 4)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + ws1),
-                                             (__attribute__((address_space(3))) void*)(lds + buf * kB16Stage + (12 + wid) * 1024),
+        if constexpr (SPLIT) {   // 4 waves: rows 8 (w + 4 k) .. + 7 (row & 6 as for k = 0)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + ws0 + 1024 * k),
+                                                 (__attribute__((address_space(3))) void*)(lds + buf * kB16Stage +
+                                                                                           (wid + 4 * k) * 1024),
+                                                 16, 0, 0);
+        } else {
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + ws0),
+                                             (__attribute__((address_space(3))) void*)(lds + buf * kB16Stage + wid * 1024),
                                              16, 0, 0);
+            if (wid < 4)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + ws1),
+                                                 (__attribute__((address_space(3))) void*)(lds + buf * kB16Stage + (12 + wid) * 1024),
+                                                 16, 0, 0);
+        }
     };
 
     const int nl = a.nlayers;
-    int board = blockIdx.x;
+    int board = SPLIT ? (int)blockIdx.x / 3 : (int)blockIdx.x;
+    const int bstride = SPLIT ? a.B : (int)gridDim.x;
     if (board < a.B) {   // the first conv's chunks 0 and 1
         dma(a.wp[0], 0, 0);
         dma(a.wp[0], 1, 1);
     }
     __syncthreads();   // poff / zero rows
-    for (; board < a.B; board += gridDim.x) {
+    for (; board < a.B; board += bstride) {
         float* xb = a.x + (size_t)board * PADPIX * kB16C;
         const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(xb, (short)0, PADPIX * kB16C * 4, 0x00020000);
         int t8 = tid;
@@ -252,17 +355,17 @@ __global__ __launch_bounds__(kB16Threads, 1) void board16_tower(const Board16Arg
         // ---- the board's stem output -> hi / lo rows [group][pixel], in two halves of 5
         // float4 per thread (all 10 in flight at once would spill) ----
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {
+        for (int half = 0; half < (PIX * 32 + 5 * NT - 1) / (5 * NT); ++half) {
             constexpr int kIt = 5;
             f32x4 v[kIt];
 #pragma unroll
             for (int k = 0; k < kIt; ++k) {
-                const int i = t8 + (half * kIt + k) * kB16Threads;   // (pixel, float4 of 128 channels)
+                const int i = t8 + (half * kIt + k) * NT;   // (pixel, float4 of 128 channels)
                 if (i < PIX * 32) v[k] = *(const f32x4*)((const char*)xb + poff[i >> 5] + (i & 31) * 16);
             }
 #pragma unroll
             for (int k = 0; k < kIt; ++k) {
-                const int i = t8 + (half * kIt + k) * kB16Threads;
+                const int i = t8 + (half * kIt + k) * NT;
                 if (i < PIX * 32) {
                     const int m = i >> 5, c4 = i & 31, g = c4 >> 3, q4 = c4 & 7;
                     f16x4 hi, lo;
@@ -280,7 +383,7 @@ __global__ __launch_bounds__(kB16Threads, 1) void board16_tower(const Board16Arg
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of the first chunks
         __syncthreads();
-        const bool more_boards = board + (int)gridDim.x < a.B;
+        const bool more_boards = board + bstride < a.B;
 
         for (int l = 0; l < nl; ++l) {
             f32x4 acc[5][2];
@@ -398,7 +501,8 @@ __global__ __launch_bounds__(kB16Threads, 1) void board16_tower(const Board16Arg
             }
             else if (!(l & 1)) bad = b16_epilogue<false, true, (ABL >> 6)>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
             else if (l + 1 < nl) bad = b16_epilogue<true, true, (ABL >> 6)>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
-            else if (a.hout) bad = b16_epilogue<true, false, (ABL >> 6), true>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
+            else if (!SPLIT && a.hout)
+                bad = b16_epilogue<true, false, (ABL >> 6), true>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
             else bad = b16_epilogue<true, false, (ABL >> 6)>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
             if (bad && a.ring_ovf && a.seq)
                 __hip_atomic_store(a.ring_ovf + (a.seq & (kTowerRing - 1)), a.seq, __ATOMIC_RELAXED,
@@ -409,8 +513,10 @@ __global__ __launch_bounds__(kB16Threads, 1) void board16_tower(const Board16Arg
             // vmcnt(0) retires them behind step 0's MFMAs
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
+            if constexpr (SPLIT)
+                if (l + 1 < nl) b16_exchange(a, lds, board, mg, l, tid);
         }
-        if (a.hout) {
+        if (!SPLIT && a.hout) {
             // the heads' three 1x1 projections of the tower output (network.py:102-103, 110-111)
             // from the fp32 rows in LDS, heads_project's arithmetic (pv_heads.hip): lane 4 m + q
             // chains channels 32 q .. 32 q + 31, two xor shuffles sum the quarters, then BN + ReLU
@@ -455,9 +561,13 @@ __global__ __launch_bounds__(kB16Threads, 1) void board16_tower(const Board16Arg
     }
 }
 
+int g_board16_split = 85;   // key 52: largest batch run split (three workgroups per board, 3 B <= CUs); 0: never
+static int g_b16_cus = 0;
+
 hipError_t launch_board16_tower(int NB, const float* wp16, const float* scale16, const float* shift,
                                 const int* out_off, float* x, int B, unsigned* ring_ovf, unsigned seq, hipStream_t st,
-                                const float* hwp, const float* hwv, const float* hsc, const float* hsh, float* hout)
+                                const float* hwp, const float* hwv, const float* hsc, const float* hsh, float* hout,
+                                const Board16Split* sp)
 {
     if (2 * NB > kB16MaxLayers || NB <= 0 || B <= 0) return hipErrorInvalidValue;
     static int grid = 0;
@@ -466,9 +576,9 @@ hipError_t launch_board16_tower(int NB, const float* wp16, const float* scale16,
 #ifdef AZG_AB_STUDIES
         for (const void* f : {(const void*)board16_tower<0>, (const void*)board16_tower<3>, (const void*)board16_tower<4>,
                               (const void*)board16_tower<8>, (const void*)board16_tower<15>,
-                              (const void*)board16_tower<64>})
+                              (const void*)board16_tower<64>, (const void*)board16_tower<0, true>})
 #else
-        for (const void* f : {(const void*)board16_tower<0>})
+        for (const void* f : {(const void*)board16_tower<0>, (const void*)board16_tower<0, true>})
 #endif
             if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kB16Lds)) != hipSuccess) return e;
         int per_cu = 0, dev = 0, cus = 0;
@@ -478,6 +588,7 @@ hipError_t launch_board16_tower(int NB, const float* wp16, const float* scale16,
         if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
         if (per_cu < 1) return hipErrorInvalidConfiguration;
         grid = per_cu * cus;
+        g_b16_cus = cus;
     }
     Board16Args a{};
     for (int l = 0; l < 2 * NB; ++l) {
@@ -492,6 +603,13 @@ hipError_t launch_board16_tower(int NB, const float* wp16, const float* scale16,
     a.seq = seq;
     if (hout && !(hwp && hwv && hsc && hsh)) return hipErrorInvalidValue;
     a.hwp = hwp, a.hwv = hwv, a.hsc = hsc, a.hsh = hsh, a.hout = hout;
+    if (sp) {   // three workgroups per board, all resident (one per CU): B <= CUs / 3
+        if (hout || 3 * B > g_b16_cus) return hipErrorInvalidValue;
+        a.xbuf = sp->xbuf, a.xflag = sp->xflag, a.epoch = sp->epoch, a.ring = sp->ring, a.diag = sp->diag;
+        a.limit = g_tower_wait_us >= 0xffffffffu / 100u ? 0xffffffffu : g_tower_wait_us * 100u;
+        hipLaunchKernelGGL((board16_tower<0, true>), dim3(3 * B), dim3(kB16SplitThreads), kB16Lds, st, a);
+        return hipGetLastError();
+    }
     const dim3 g(B < grid ? B : grid);
 #ifdef AZG_AB_STUDIES
     switch (g_board_abl) {   // timing ablations (key 51, study build; results invalid while set)

@@ -79,6 +79,8 @@ int32_t azg_pv_destroy(azg_pv* h)
     if (h->conv_off_dev) (void)hipFree(h->conv_off_dev);
     if (h->ring_host) (void)hipHostFree(h->ring_host);
     if (h->tower_diag) (void)hipFree(h->tower_diag);
+    if (h->b16x) (void)hipFree(h->b16x);
+    if (h->b16flag) (void)hipFree(h->b16flag);
     if (h->wpack16) (void)hipFree(h->wpack16);
     if (h->scale16) (void)hipFree(h->scale16);
     if (h->h3exp) (void)hipFree(h->h3exp);
@@ -636,7 +638,7 @@ static int conv_tuned_shape_h3(azg_pv* h, int batch, hipStream_t, const float*, 
 
 static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch, hipStream_t st,
                               const int8_t* boards, const int8_t* players, float** out, unsigned seq = 0,
-                              bool h3 = false)
+                              bool h3 = false, bool recompute = false)
 {
     const int C = h->C;
     const int M = batch * PIX;
@@ -658,7 +660,27 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
             out_off[2 * i + 1] = bd[h->bn_blk[i].second].out_off;
         }
         pr = prof_begin(h, variant == 14 ? AZG_PROF_BOARD16 : AZG_PROF_BOARD, st, batch);
-        if (variant == 14) {   // the heads' projections fused: features into hbuf (forward_eval)
+        // key 19 = 2: small batches run split (three workgroups per board, heads unfused; not
+        // for a recompute, which must not wait across workgroups), the rest one workgroup per
+        // board with the heads' projections fused (features into hbuf, forward_eval)
+        h->b16_split = variant == 14 && !recompute && batch <= g_board16_split && batch <= kB16SplitCap;
+        if (h->b16_split) {
+            if (!h->b16x) {
+                AZG_TRY(hipMalloc(&h->b16x, (size_t)kB16SplitCap * 2 * kB16ImgBytes), "forward: split images");
+                AZG_TRY(hipMalloc(&h->b16flag, (size_t)kB16SplitCap * 3 * sizeof(unsigned)), "forward: split flags");
+                AZG_TRY(hipMemsetAsync(h->b16x, 0, (size_t)kB16SplitCap * 2 * kB16ImgBytes, st), "forward: split images");
+                h->b16epoch = 1u << 25;   // forces the flag reset below
+            }
+            if (++h->b16epoch >= 1u << 25) {   // tags epoch * 64 + layer stay monotonic: restart them at 1
+                AZG_TRY(hipMemsetAsync(h->b16flag, 0, (size_t)kB16SplitCap * 3 * sizeof(unsigned), st),
+                        "forward: split flags");
+                h->b16epoch = 1;
+            }
+            const Board16Split sp{h->b16x, h->b16flag, h->b16epoch, h->ring_dev, h->tower_diag};
+            AZG_TRY(launch_board16_tower(h->NB, (const float*)h->wpack16, h->scale16, h->shift, out_off, X, batch,
+                                         h->ovf_dev, seq, st, nullptr, nullptr, nullptr, nullptr, nullptr, &sp),
+                    "forward: board tower (16x16x32, split)");
+        } else if (variant == 14) {
             const float* P = h->params;
             const int ho = bd[h->bn_pol].out_off;
             AZG_TRY(launch_board16_tower(h->NB, (const float*)h->wpack16, h->scale16, h->shift, out_off, X, batch,
@@ -844,13 +866,14 @@ int32_t forward_eval(azg_pv* h, const float* x, int batch, float* probs, float* 
     }
     if (!per_layer) h->last_seq = seq;
     float* X = nullptr;
-    if (int32_t r = stem_and_tower(h, variant, x, batch, st, boards, players, &X, seq, h3)) return r;
+    h->b16_split = false;
+    if (int32_t r = stem_and_tower(h, variant, x, batch, st, boards, players, &X, seq, h3, per_layer)) return r;
     const int ho = bd[h->bn_pol].out_off;   // policy (2) then value (1): contiguous
     int pr = prof_begin(h, AZG_PROF_HEADS, st, batch);
     AZG_TRY(launch_heads_fwd(C, X, P + h->poff[h->t_pc_w], P + h->poff[h->t_vc_w], h->scale + ho, h->shift + ho,
                              h->wfc, P + h->poff[h->t_pfc_b], P + h->poff[h->t_vfc1_b],
                              P + h->poff[h->t_vfc2_w], P + h->poff[h->t_vfc2_b], h->hbuf, probs, values, logits,
-                             batch, st, boards, priors, variant == 14),
+                             batch, st, boards, priors, variant == 14 && !h->b16_split),
             "forward: heads");
     prof_end(h, pr, st);
     return 0;

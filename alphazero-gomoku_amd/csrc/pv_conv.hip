@@ -1087,6 +1087,11 @@ extern "C" int32_t azg_pv_set_tuning(int32_t key, int32_t value)
         if (value >= 0 && value <= 2) azg::g_train_dgrad_h3 = value;
         return prev;
     }
+    if (key == 52) {  // board16: largest batch run split (three workgroups per board; 0 never)
+        const int prev = azg::g_board16_split;
+        if (value >= 0) azg::g_board16_split = value;
+        return prev;
+    }
     if (key == 19) {  // eval residual-conv arithmetic: 2 split-fp16 on 16x16x32 (default), 1 on 32x32x16, 0 fp32
         const int prev = azg::g_tower_h3;
         if (value == 0 || value == 1 || value == 2) azg::g_tower_h3 = value;

@@ -88,12 +88,25 @@ hipError_t launch_tower(int C, int NB, int shape, float* const act[3], const flo
 // place with the tower output
 hipError_t launch_board_tower(int NB, const float* wp16, const float* scale16, const float* shift, const int* out_off,
                               float* x, int B, unsigned* ring_ovf, unsigned seq, hipStream_t st);
+// small batches (B <= key 52, 3 B <= CUs): each board over three workgroups that exchange conv
+// outputs' boundary rows through `xbuf` (bitwise the one-workgroup tower); hout must be null
+struct Board16Split {
+    char* xbuf;        // [B][2][4 * 226 * 128 B] exchange images (zero rows: zero)
+    unsigned* xflag;   // [B][3] publish flags (monotonic over launches: tags epoch * 64 + layer + 1)
+    unsigned epoch;    // > every earlier split launch's on these flags
+    unsigned* ring;    // timed-out launch ring (device alias), azg_pv_recover
+    unsigned* diag;    // the tower wait record
+};
+extern int g_board16_split;   // key 52
+constexpr int kB16SplitCap = 85;                        // 3 x 85 workgroups <= 256 CUs
+constexpr size_t kB16ImgBytes = 4 * (15 * 15 + 1) * 128;   // pv_board16.hip kB16Img
 // hout != nullptr: the tower output stays in LDS and the kernel writes the heads' projected
 // features (heads_project's, bitwise) to hout [B][FC_FS] instead of x
 hipError_t launch_board16_tower(int NB, const float* wp16, const float* scale16, const float* shift,
                                 const int* out_off, float* x, int B, unsigned* ring_ovf, unsigned seq, hipStream_t st,
                                 const float* hwp = nullptr, const float* hwv = nullptr, const float* hsc = nullptr,
-                                const float* hsh = nullptr, float* hout = nullptr);
+                                const float* hsh = nullptr, float* hout = nullptr, const Board16Split* sp = nullptr);
+
 // the heads' 1x1 projection epilogue: folded eval BN + ReLU (heads_project and the board16 tower)
 __device__ __forceinline__ float head_bn_relu(float d, float s, float h) { return fmaxf(d * s + h, 0.f); }
 extern unsigned g_tower_wait_us;
@@ -194,6 +207,10 @@ struct azg_pv {
     unsigned* ovf_host = nullptr;     // H3 launches whose activations left fp16's range [kTowerRing], same memory
     unsigned* train_ovf_dev = nullptr;   // [kTrainOvfWords] split-fp16 train forward overflow flags (device alias)
     unsigned* ovf_dev = nullptr;
+    char* b16x = nullptr;             // board16 split exchange images [kB16SplitCap][2][image] (zeroed)
+    unsigned* b16flag = nullptr;      // [kB16SplitCap][3] publish flags
+    unsigned b16epoch = 0;            // split launches so far (their flag tags)
+    bool b16_split = false;           // the last forward's board16 launch ran split (heads unfused)
     unsigned seq = 0;                 // last tower launch number handed out (0 = none yet)
     unsigned last_seq = 0;            // the last forward's launch number (0: it ran per-layer convs)
     // what each posted launch read and wrote, by seq % kTowerRing (azg_pv_recover re-runs it)

@@ -1,6 +1,6 @@
 """Eval-forward latency at small batches for the two split-fp16 arithmetics (key 19 = 1:
 the tuner's pick among per-layer / tile towers / 32x32 board tower; 2: the 16x16x32 board
-tower, one board per workgroup).  Device time per forward (hipEvent profile, best of 3
+tower, one board per workgroup, or at B <= key 52 three workgroups per board).  Device time per forward (hipEvent profile, best of 3
 rounds of 20) and wall time per synchronous predict.
 
     python scripts/small_batch_latency.py [--batches 1,4,16,64,256,512]
@@ -32,8 +32,9 @@ def main():
         xs = synth_encoded(B, seed=B)
         x = torch.from_numpy(xs).cuda()
         row = []
-        for cls in (1, 2):
+        for cls, split in ((1, 85), (2, 0), (2, 85)):
             lib.azg_pv_set_tuning(19, cls)
+            lib.azg_pv_set_tuning(52, split)
             eng.forward(x)
             torch.cuda.synchronize()
             best = 1e30
@@ -49,9 +50,11 @@ def main():
             for _ in range(20):
                 m.predict(xs)
             wall = (time.perf_counter() - t0) / 20 * 1e3
-            row.append(f"key19={cls}: device {best:.3f} ms, predict wall {wall:.3f} ms")
+            row.append(f"key19={cls}{' split' if cls == 2 and split else ''}: device {best:.3f} ms, "
+                       f"predict wall {wall:.3f} ms")
         print(f"B={B}: " + " | ".join(row), flush=True)
     lib.azg_pv_set_tuning(19, 2)
+    lib.azg_pv_set_tuning(52, 85)
 
 
 if __name__ == "__main__":

@@ -575,3 +575,39 @@ def test_h3_matches_fp32_forward_and_oracle(blocks, ch, B, cls):
         assert np.abs(a16 - a32).max() <= 1e-5
         assert e16 <= max(2 * e32, 1e-6), (name, e16, e32)
     argmax_check(p16, pr, b)
+
+
+@pytest.mark.parametrize("B", [1, 7, 32])
+def test_board16_split_bitwise_equals_one_workgroup(B):
+    """Key 19 = 2 at small batches (B <= key 52) runs each board over three workgroups that
+    exchange their conv outputs' boundary rows through L2: bitwise the one-workgroup tower
+    (same per-wave tiles and MFMA chains).  A timed-out exchange wait (key 14 = 0) posts the
+    launch and predict recomputes it unsplit -- bitwise again."""
+    import _native
+    lib = _native.load_library()
+    m = make_model(6, 128, seed=12)
+    eng = m.engine
+    boards, players = synth_positions(B, seed=100 + B)
+    bi8, pl8 = np.asarray(boards, np.int8).reshape(B, 225), np.asarray(players, np.int8)
+    x = encode_batch(boards, players)
+    prev = lib.azg_pv_set_tuning(52, 0)
+    try:
+        p0, v0 = m.predict_boards(bi8, pl8)
+        q0, w0 = m.predict(x)
+        lib.azg_pv_set_tuning(52, 85)
+        p1, v1 = m.predict_boards(bi8, pl8)
+        q1, w1 = m.predict(x)
+        assert np.array_equal(p1, p0) and np.array_equal(v1, v0)
+        assert np.array_equal(q1, q0) and np.array_equal(w1, w0)
+        eng.tower_diag_clear()
+        r0 = eng.recoveries
+        lib.azg_pv_set_tuning(14, 0)
+        try:
+            p2, v2 = m.predict_boards(bi8, pl8)
+        finally:
+            lib.azg_pv_set_tuning(14, -1)
+        assert np.array_equal(p2, p0) and np.array_equal(v2, v0)
+        assert eng.recoveries == r0 + 1 and eng.tower_diag()["timeouts"] > 0
+        eng.check_status()
+    finally:
+        lib.azg_pv_set_tuning(52, prev)
