@@ -562,7 +562,43 @@ __global__ __launch_bounds__(SPLIT ? kB16SplitThreads : kB16Threads, 1) void boa
 }
 
 int g_board16_split = 85;   // key 52: largest batch run split (three workgroups per board, 3 B <= CUs); 0: never
-static int g_b16_cus = 0;
+static int g_b16_cus = 0, g_b16_grid = 0;
+
+// first use: the kernels' dynamic LDS attribute, the one-per-CU grid and the CU count
+static hipError_t b16_init()
+{
+    if (g_b16_grid) return hipSuccess;
+    hipError_t e = hipSuccess;
+#ifdef AZG_AB_STUDIES
+    for (const void* f : {(const void*)board16_tower<0>, (const void*)board16_tower<3>, (const void*)board16_tower<4>,
+                          (const void*)board16_tower<8>, (const void*)board16_tower<15>,
+                          (const void*)board16_tower<64>, (const void*)board16_tower<0, true>})
+#else
+    for (const void* f : {(const void*)board16_tower<0>, (const void*)board16_tower<0, true>})
+#endif
+        if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kB16Lds)) != hipSuccess) return e;
+    int per_cu = 0, dev = 0, cus = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)board16_tower<0>, kB16Threads, kB16Lds);
+    if (e != hipSuccess) return e;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+    if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+    if (per_cu < 1) return hipErrorInvalidConfiguration;
+    g_b16_cus = cus;
+    g_b16_grid = per_cu * cus;
+    return hipSuccess;
+}
+
+int board16_grid()
+{
+    return b16_init() == hipSuccess ? g_b16_grid : 0;
+}
+
+int board16_split_max()
+{
+    if (b16_init() != hipSuccess) return 0;
+    const int m = g_b16_cus / 3 < kB16SplitCap ? g_b16_cus / 3 : kB16SplitCap;
+    return g_board16_split < m ? g_board16_split : m;
+}
 
 hipError_t launch_board16_tower(int NB, const float* wp16, const float* scale16, const float* shift,
                                 const int* out_off, float* x, int B, unsigned* ring_ovf, unsigned seq, hipStream_t st,
@@ -570,26 +606,8 @@ hipError_t launch_board16_tower(int NB, const float* wp16, const float* scale16,
                                 const Board16Split* sp)
 {
     if (2 * NB > kB16MaxLayers || NB <= 0 || B <= 0) return hipErrorInvalidValue;
-    static int grid = 0;
-    if (grid == 0) {
-        hipError_t e = hipSuccess;
-#ifdef AZG_AB_STUDIES
-        for (const void* f : {(const void*)board16_tower<0>, (const void*)board16_tower<3>, (const void*)board16_tower<4>,
-                              (const void*)board16_tower<8>, (const void*)board16_tower<15>,
-                              (const void*)board16_tower<64>, (const void*)board16_tower<0, true>})
-#else
-        for (const void* f : {(const void*)board16_tower<0>, (const void*)board16_tower<0, true>})
-#endif
-            if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kB16Lds)) != hipSuccess) return e;
-        int per_cu = 0, dev = 0, cus = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)board16_tower<0>, kB16Threads, kB16Lds);
-        if (e != hipSuccess) return e;
-        if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
-        if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
-        if (per_cu < 1) return hipErrorInvalidConfiguration;
-        grid = per_cu * cus;
-        g_b16_cus = cus;
-    }
+    if (hipError_t e = b16_init()) return e;
+    const int grid = g_b16_grid;
     Board16Args a{};
     for (int l = 0; l < 2 * NB; ++l) {
         a.wp[l] = wp16 + (size_t)l * 9 * kB16C * kB16C;

@@ -659,12 +659,18 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
             out_off[2 * i] = bd[h->bn_blk[i].first].out_off;
             out_off[2 * i + 1] = bd[h->bn_blk[i].second].out_off;
         }
-        pr = prof_begin(h, variant == 14 ? AZG_PROF_BOARD16 : AZG_PROF_BOARD, st, batch);
         // key 19 = 2: small batches run split (three workgroups per board, heads unfused; not
         // for a recompute, which must not wait across workgroups), the rest one workgroup per
         // board with the heads' projections fused (features into hbuf, forward_eval)
-        h->b16_split = variant == 14 && !recompute && batch <= g_board16_split && batch <= kB16SplitCap;
-        if (h->b16_split) {
+        // a one-workgroup launch of B = k * grid + r boards ends with r boards on r CUs: for
+        // r <= key 52 those r run split after the k full rounds (their heads projected here)
+        const int smax = variant == 14 && !recompute ? board16_split_max() : 0;
+        const int grid = variant == 14 ? board16_grid() : 0;
+        const int tail = variant == 14 && batch > grid && grid > 0 && batch % grid <= smax ? batch % grid : 0;
+        h->b16_split = variant == 14 && batch <= smax;
+        // one hipEvent bracket per tower launch (the tail's is a second board16 launch)
+        pr = prof_begin(h, variant == 14 ? AZG_PROF_BOARD16 : AZG_PROF_BOARD, st, batch - tail);
+        if (h->b16_split || tail) {
             if (!h->b16x) {
                 AZG_TRY(hipMalloc(&h->b16x, (size_t)kB16SplitCap * 2 * kB16ImgBytes), "forward: split images");
                 AZG_TRY(hipMalloc(&h->b16flag, (size_t)kB16SplitCap * 3 * sizeof(unsigned)), "forward: split flags");
@@ -677,9 +683,30 @@ static int32_t stem_and_tower(azg_pv* h, int variant, const float* x, int batch,
                 h->b16epoch = 1;
             }
             const Board16Split sp{h->b16x, h->b16flag, h->b16epoch, h->ring_dev, h->tower_diag};
-            AZG_TRY(launch_board16_tower(h->NB, (const float*)h->wpack16, h->scale16, h->shift, out_off, X, batch,
-                                         h->ovf_dev, seq, st, nullptr, nullptr, nullptr, nullptr, nullptr, &sp),
-                    "forward: board tower (16x16x32, split)");
+            if (tail) {   // the k full rounds one workgroup per board, heads fused
+                const float* P = h->params;
+                const int ho = bd[h->bn_pol].out_off, nmain = batch - tail;
+                const float *wpc = P + h->poff[h->t_pc_w], *wvc = P + h->poff[h->t_vc_w];
+                AZG_TRY(launch_board16_tower(h->NB, (const float*)h->wpack16, h->scale16, h->shift, out_off, X, nmain,
+                                             h->ovf_dev, seq, st, wpc, wvc, h->scale + ho, h->shift + ho, h->hbuf),
+                        "forward: board tower (16x16x32)");
+                prof_end(h, pr, st);
+                float* Xt = X + (size_t)nmain * PADPIX * C;
+                pr = prof_begin(h, AZG_PROF_BOARD16, st, tail);
+                AZG_TRY(launch_board16_tower(h->NB, (const float*)h->wpack16, h->scale16, h->shift, out_off, Xt, tail,
+                                             h->ovf_dev, seq, st, nullptr, nullptr, nullptr, nullptr, nullptr, &sp),
+                        "forward: board tower (16x16x32, split tail)");
+                prof_end(h, pr, st);
+                pr = prof_begin(h, AZG_PROF_HEADS, st, 0);
+                AZG_TRY(launch_heads_project(C, true, Xt, wpc, wvc, h->scale + ho, h->shift + ho,
+                                             h->hbuf + (size_t)nmain * FC_FS, tail * PIX, st, FC_FS, FC_KP),
+                        "forward: heads projection (split tail)");
+            } else {
+                AZG_TRY(launch_board16_tower(h->NB, (const float*)h->wpack16, h->scale16, h->shift, out_off, X,
+                                             batch, h->ovf_dev, seq, st, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                             &sp),
+                        "forward: board tower (16x16x32, split)");
+            }
         } else if (variant == 14) {
             const float* P = h->params;
             const int ho = bd[h->bn_pol].out_off;

@@ -98,6 +98,8 @@ struct Board16Split {
     unsigned* diag;    // the tower wait record
 };
 extern int g_board16_split;   // key 52
+int board16_grid();           // workgroups of a one-per-CU board16 launch (0: init failed)
+int board16_split_max();      // largest batch the split form takes (key 52, CUs / 3, kB16SplitCap)
 constexpr int kB16SplitCap = 85;                        // 3 x 85 workgroups <= 256 CUs
 constexpr size_t kB16ImgBytes = 4 * (15 * 15 + 1) * 128;   // pv_board16.hip kB16Img
 // hout != nullptr: the tower output stays in LDS and the kernel writes the heads' projected
