@@ -577,12 +577,13 @@ def test_h3_matches_fp32_forward_and_oracle(blocks, ch, B, cls):
     argmax_check(p16, pr, b)
 
 
-@pytest.mark.parametrize("B", [1, 7, 32])
+@pytest.mark.parametrize("B", [1, 7, 32, 300])
 def test_board16_split_bitwise_equals_one_workgroup(B):
     """Key 19 = 2 at small batches (B <= key 52) runs each board over three workgroups that
-    exchange their conv outputs' boundary rows through L2: bitwise the one-workgroup tower
-    (same per-wave tiles and MFMA chains).  A timed-out exchange wait (key 14 = 0) posts the
-    launch and predict recomputes it unsplit -- bitwise again."""
+    exchange their conv outputs' boundary rows through L2, and a larger launch's last partial
+    round (B = 300: 256 + 44) runs that way after the full rounds: bitwise the one-workgroup
+    tower (same per-wave tiles and MFMA chains).  A timed-out exchange wait (key 14 = 0) posts
+    the launch and predict recomputes it unsplit -- bitwise again."""
     import _native
     lib = _native.load_library()
     m = make_model(6, 128, seed=12)
