@@ -43,7 +43,7 @@ constexpr int kB16Hw = kB16Prow + 240 * 4;                    // the heads' 1x1 
 constexpr int kB16Lds = kB16Hw + 3 * kB16C * 4;               // 150,976 B: one workgroup per CU
 constexpr int kB16Waves = 12;
 constexpr int kB16Threads = 64 * kB16Waves;
-constexpr int kB16SplitThreads = 256;                         // SPLIT: 4 waves, one pixel third of a board
+constexpr int kB16SplitThreads = 512;                         // SPLIT: 8 waves (80x16 tiles), one pixel third of a board
 constexpr int kB16Img = kB16Groups * kB16Rows * 128;          // one board's image (an exchange buffer)
 static_assert(kB16Img == (int)kB16ImgBytes, "pv_internal.h kB16ImgBytes");
 constexpr int kB16MaxLayers = 2 * kTowerMaxBlocks;
@@ -96,10 +96,11 @@ typedef _Float16 b16_f16x2 __attribute__((ext_vector_type(2)));
 // (v_pk_fma / v_pk_add: per element the same fmaf and add).  Returns whether an accumulator
 // was non-finite (their sum is: padding accumulators are exactly 0).  F32L (the last conv when
 // the heads are fused): the block output goes to LDS as fp32 rows [pixel][128] instead of HBM.
-template <bool RES, bool TO_LDS, int EABL = 0, bool F32L = false>
-__device__ __forceinline__ bool b16_epilogue(const f32x4 (&acc)[5][2], const float* __restrict__ scale,
+// NJ (SPLIT: 1): the wave's 16-channel fragments, from fragment nb of its group.
+template <bool RES, bool TO_LDS, int EABL = 0, bool F32L = false, int NJ = 2>
+__device__ __forceinline__ bool b16_epilogue(const f32x4 (&acc)[5][NJ], const float* __restrict__ scale,
                                              const float* __restrict__ shift, __amdgpu_buffer_rsrc_t xr, char* lds,
-                                             const int* poff, int mg, int cg, int lane)
+                                             const int* poff, int mg, int cg, int lane, int nb = 0)
 {
     asm volatile("" : "+v"(lane));   // the epilogue's addresses are rebuilt per conv, not hoisted (they would spill)
     const int r16 = lane & 15, kb = lane >> 4, odd = r16 & 1, ce = r16 & 14;
@@ -110,29 +111,29 @@ __device__ __forceinline__ bool b16_epilogue(const f32x4 (&acc)[5][2], const flo
     // the word of element i (e = 0) / i + 1 (e = 1) from X (own H or L) and Zp (the partner's):
     // even lane (own hi, partner hi), odd lane (partner lo, own lo)
     const unsigned sel0 = odd ? 0x01000504u : 0x05040100u, sel1 = odd ? 0x03020706u : 0x07060302u;
-    float sc[2], sh[2];
+    float sc[NJ], sh[NJ];
 #pragma unroll
-    for (int n = 0; n < 2; ++n) {
-        sc[n] = scale[32 * cg + 16 * n + r16];
-        sh[n] = shift[32 * cg + 16 * n + r16];
+    for (int nn = 0; nn < NJ; ++nn) {
+        sc[nn] = scale[32 * cg + 16 * (nb + nn) + r16];
+        sh[nn] = shift[32 * cg + 16 * (nb + nn) + r16];
     }
     const int cbyte = 4 * (32 * cg + r16);
     // every block-input load first (in program order ahead of the in-place stores, which the
     // compiler cannot move them past): one memory round trip per epilogue, not one per f
     int vof[5][4];
-    float rvf[5][2][4];
+    float rvf[5][NJ][4];
     if constexpr (RES) {
 #pragma unroll
         for (int f = 0; f < 5; ++f) {
             const int4 p4 = *(const int4*)(poff + 80 * mg + 16 * f + 4 * kb);
             vof[f][0] = p4.x + cbyte, vof[f][1] = p4.y + cbyte, vof[f][2] = p4.z + cbyte, vof[f][3] = p4.w + cbyte;
 #pragma unroll
-            for (int n = 0; n < 2; ++n)
+            for (int nn = 0; nn < NJ; ++nn)
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    rvf[f][n][i] = (EABL & 1) ? __builtin_bit_cast(float, vof[f][i])   // study: no residual loads
-                                              : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                                              xr, vof[f][i] + 64 * n, 0, 0));
+                    rvf[f][nn][i] = (EABL & 1) ? __builtin_bit_cast(float, vof[f][i])   // study: no residual loads
+                                               : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                                               xr, vof[f][i] + 64 * (nb + nn), 0, 0));
         }
     }
     b16_f32x2 chk = {0.f, 0.f};
@@ -140,16 +141,17 @@ __device__ __forceinline__ bool b16_epilogue(const f32x4 (&acc)[5][2], const flo
     for (int f = 0; f < 5; ++f) {
         const int m0 = 80 * mg + 16 * f + 4 * kb;
         const int (&vo)[4] = vof[f];
-        const float (&rv)[2][4] = rvf[f];
+        const float (&rv)[NJ][4] = rvf[f];
         char* wrow = lds + kB16Act + (cg * kB16Rows + m0) * 128 + lpart;
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
+        for (int nn = 0; nn < NJ; ++nn)
 #pragma unroll
             for (int ip = 0; ip < 2; ++ip) {
-                const b16_f32x2 v = {acc[f][n][2 * ip], acc[f][n][2 * ip + 1]};
+                const int n = nb + nn;
+                const b16_f32x2 v = {acc[f][nn][2 * ip], acc[f][nn][2 * ip + 1]};
                 chk += v;
-                b16_f32x2 y = __builtin_elementwise_fma(v, b16_f32x2{sc[n], sc[n]}, b16_f32x2{sh[n], sh[n]});
-                if constexpr (RES) y += b16_f32x2{rv[n][2 * ip], rv[n][2 * ip + 1]};
+                b16_f32x2 y = __builtin_elementwise_fma(v, b16_f32x2{sc[nn], sc[nn]}, b16_f32x2{sh[nn], sh[nn]});
+                if constexpr (RES) y += b16_f32x2{rv[nn][2 * ip], rv[nn][2 * ip + 1]};
                 const float ye[2] = {fmaxf(y.x, 0.f), fmaxf(y.y, 0.f)};
                 if constexpr (RES && F32L) {
 #pragma unroll
@@ -229,7 +231,7 @@ __device__ __forceinline__ void b16_exchange(const Board16Args& a, char* lds, in
         return (g * kB16Rows + (r == 0 ? lo : hi) + row) * 128 + 16 * (q & 7);
     };
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 1024 / kB16SplitThreads; ++k) {
         const int o = piece(tid + kB16SplitThreads * k, m0, m1 - 16);
         if (o >= 0) __builtin_amdgcn_raw_buffer_store_b128(*(const b16_u32x4*)(lds + kB16Act + o), xr, o, 0, 16);
     }
@@ -252,15 +254,16 @@ __device__ __forceinline__ void b16_exchange(const Board16Args& a, char* lds, in
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    b16_u32x4 v[4];
-    int off[4];
+    constexpr int K = 1024 / kB16SplitThreads;
+    b16_u32x4 v[K];
+    int off[K];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < K; ++k) {
         off[k] = piece(tid + kB16SplitThreads * k, m0 - 16, m1);
         if (off[k] >= 0) v[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, off[k], 0, 0);
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < K; ++k)
         if (off[k] >= 0) *(b16_u32x4*)(lds + kB16Act + off[k]) = v[k];
     __syncthreads();
 }
@@ -268,19 +271,21 @@ __device__ __forceinline__ void b16_exchange(const Board16Args& a, char* lds, in
 extern int g_board_abl;
 // ABL: timing ablations of the study build (key 51): 1 no DMA wait, 2 no barrier, 4 no epilogue
 // (the accumulators kept live), 8 fixed A rows, 64 no residual loads; the product runs ABL 0
-// SPLIT (small batches): three 4-wave workgroups per board, workgroup 3 b + mg computing pixels
-// 80 mg .. 80 mg + 79 of every channel group (wave = channel group), the same per-wave tiles
-// and MFMA sequence (bitwise the unsplit tower), conv outputs' boundary rows exchanged
+// SPLIT (small batches): three 8-wave workgroups per board, workgroup 3 b + mg computing pixels
+// 80 mg .. 80 mg + 79 of every channel (wave = one 16-channel fragment: 80x16 tiles), the same
+// per-element MFMA chains (bitwise the unsplit tower), conv outputs' boundary rows exchanged
 // through L2 (b16_exchange); the tower output goes to x (the heads run unfused).
 template <int ABL, bool SPLIT = false>
 __global__ __launch_bounds__(SPLIT ? kB16SplitThreads : kB16Threads, 1) void board16_tower(const Board16Args a)
 {
     constexpr int NT = SPLIT ? kB16SplitThreads : kB16Threads;
+    constexpr int NJ = SPLIT ? 1 : 2;   // 16-channel fragments per wave
     extern __shared__ __attribute__((aligned(16))) float smem_f[];
     char* lds = (char*)smem_f;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int mg = SPLIT ? (int)blockIdx.x % 3 : wid % 3, ng = SPLIT ? wid : wid / 3;
+    // SPLIT: wave w computes channel group w / 2, its 16-channel fragment w % 2
+    const int mg = SPLIT ? (int)blockIdx.x % 3 : wid % 3, ng = SPLIT ? wid >> 1 : wid / 3, nb = SPLIT ? wid & 1 : 0;
     const int r16 = lane & 15, kb = lane >> 4;
     int* poff = (int*)(lds + kB16Prow);   // byte offset of each pixel's padded row (padding: past the board)
 
@@ -308,7 +313,7 @@ __global__ __launch_bounds__(SPLIT ? kB16SplitThreads : kB16Threads, 1) void boa
         tm[f] = t;
     }
     // B fragments: weight row n = 32 ng + 16 j + r16, slot kb (hi) / kb ^ 4 (lo), keyed by n & 6 = r16 & 6
-    const int bh0 = (32 * ng + r16) * 128 + 16 * (kb ^ (r16 & 6));
+    const int bh0 = (32 * ng + 16 * nb + r16) * 128 + 16 * (kb ^ (r16 & 6));
     const int bl0 = bh0 ^ 64;
 
     // weight DMA of one chunk (16 KB, 128 rows x 128 B): wave w moves rows 8 w .. 8 w + 7,
@@ -321,12 +326,12 @@ __global__ __launch_bounds__(SPLIT ? kB16SplitThreads : kB16Threads, 1) void boa
     auto dma = [&](const float* wl, int s, int buf) {   // chunk s = cg * 9 + tap -> stage buf
         const int cg = s / 9, tap = s - cg * 9;
         const float* src = wl + (size_t)(tap * kB16Groups + cg) * kB16C * 32;
-        if constexpr (SPLIT) {   // 4 waves: rows 8 (w + 4 k) .. + 7 (row & 6 as for k = 0)
+        if constexpr (SPLIT) {   // 8 waves: rows 8 (w + 8 k) .. + 7 (row & 6 as for k = 0)
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + ws0 + 1024 * k),
+            for (int k = 0; k < 2; ++k)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + ws0 + 2048 * k),
                                                  (__attribute__((address_space(3))) void*)(lds + buf * kB16Stage +
-                                                                                           (wid + 4 * k) * 1024),
+                                                                                           (wid + 8 * k) * 1024),
                                                  16, 0, 0);
         } else {
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + ws0),
@@ -386,11 +391,11 @@ __global__ __launch_bounds__(SPLIT ? kB16SplitThreads : kB16Threads, 1) void boa
         const bool more_boards = board + bstride < a.B;
 
         for (int l = 0; l < nl; ++l) {
-            f32x4 acc[5][2];
+            f32x4 acc[5][NJ];
 #pragma unroll
             for (int f = 0; f < 5; ++f)
 #pragma unroll
-                for (int n = 0; n < 2; ++n) acc[f][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+                for (int n = 0; n < NJ; ++n) acc[f][n] = f32x4{0.f, 0.f, 0.f, 0.f};
             // this conv's and the next one's weights (scalar, loaded once per conv); the next
             // conv's chunks 0 and 1 are issued during steps 34 and 35
             const float* wl = a.wp[l];
@@ -407,7 +412,7 @@ __global__ __launch_bounds__(SPLIT ? kB16SplitThreads : kB16Threads, 1) void boa
             };
             // step 0's operands; then every wave holds chunk 0's B fragments and stage 0 may
             // be refilled
-            f16x8 bh[2], bl[2], ah[5], al[5];
+            f16x8 bh[NJ], bl[NJ], ah[5], al[5];
 #pragma unroll
             for (int f = 0; f < 5; ++f) {
                 const int ao = arow(0, 0, f);
@@ -415,7 +420,7 @@ __global__ __launch_bounds__(SPLIT ? kB16SplitThreads : kB16Threads, 1) void boa
                 ah[f] = *(const f16x8*)(lds + ao);
             }
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
+            for (int j = 0; j < NJ; ++j) {
                 bh[j] = *(const f16x8*)(lds + bh0 + j * 2048);
                 bl[j] = *(const f16x8*)(lds + bl0 + j * 2048);
             }
@@ -441,7 +446,7 @@ __global__ __launch_bounds__(SPLIT ? kB16SplitThreads : kB16Threads, 1) void boa
 #pragma unroll
                     for (int f = 0; f < 5; ++f)
 #pragma unroll
-                        for (int j = 0; j < 2; ++j)
+                        for (int j = 0; j < NJ; ++j)
                             acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[f], bh[j], acc[f][j], 0, 0, 0);
                     __builtin_amdgcn_sched_barrier(0);
                     int ao[5];
@@ -456,23 +461,23 @@ __global__ __launch_bounds__(SPLIT ? kB16SplitThreads : kB16Threads, 1) void boa
 #pragma unroll
                     for (int f = 0; f < 5; ++f)
 #pragma unroll
-                        for (int j = 0; j < 2; ++j)
+                        for (int j = 0; j < NJ; ++j)
                             acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[f], bh[j], acc[f][j], 0, 0, 0);
                     __builtin_amdgcn_sched_barrier(0);
                     if (nx) {
 #pragma unroll
-                        for (int j = 0; j < 2; ++j) bh[j] = *(const f16x8*)(bn + bh0 + j * 2048);
+                        for (int j = 0; j < NJ; ++j) bh[j] = *(const f16x8*)(bn + bh0 + j * 2048);
                     }
                     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                     for (int f = 0; f < 5; ++f)
 #pragma unroll
-                        for (int j = 0; j < 2; ++j)
+                        for (int j = 0; j < NJ; ++j)
                             acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[f], bl[j], acc[f][j], 0, 0, 0);
                     __builtin_amdgcn_sched_barrier(0);
                     if (nx) {   // the B reads first: the barrier need only wait for them
 #pragma unroll
-                        for (int j = 0; j < 2; ++j) bl[j] = *(const f16x8*)(bn + bl0 + j * 2048);
+                        for (int j = 0; j < NJ; ++j) bl[j] = *(const f16x8*)(bn + bl0 + j * 2048);
                         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                         for (int f = 0; f < 5; ++f) ah[f] = *(const f16x8*)(lds + ao[f]);
@@ -496,14 +501,16 @@ __global__ __launch_bounds__(SPLIT ? kB16SplitThreads : kB16Threads, 1) void boa
 #pragma unroll
                 for (int f = 0; f < 5; ++f)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) t += acc[f][j][0] + acc[f][j][1] + acc[f][j][2] + acc[f][j][3];
+                    for (int j = 0; j < NJ; ++j) t += acc[f][j][0] + acc[f][j][1] + acc[f][j][2] + acc[f][j][3];
                 if (t == 1234.5f) xb[tid] = t;
             }
-            else if (!(l & 1)) bad = b16_epilogue<false, true, (ABL >> 6)>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
-            else if (l + 1 < nl) bad = b16_epilogue<true, true, (ABL >> 6)>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
+            else if (!(l & 1))
+                bad = b16_epilogue<false, true, (ABL >> 6), false, NJ>(acc, sc, sh, xr, lds, poff, mg, ng, lane, nb);
+            else if (l + 1 < nl)
+                bad = b16_epilogue<true, true, (ABL >> 6), false, NJ>(acc, sc, sh, xr, lds, poff, mg, ng, lane, nb);
             else if (!SPLIT && a.hout)
-                bad = b16_epilogue<true, false, (ABL >> 6), true>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
-            else bad = b16_epilogue<true, false, (ABL >> 6)>(acc, sc, sh, xr, lds, poff, mg, ng, lane);
+                bad = b16_epilogue<true, false, (ABL >> 6), true, NJ>(acc, sc, sh, xr, lds, poff, mg, ng, lane, nb);
+            else bad = b16_epilogue<true, false, (ABL >> 6), false, NJ>(acc, sc, sh, xr, lds, poff, mg, ng, lane, nb);
             if (bad && a.ring_ovf && a.seq)
                 __hip_atomic_store(a.ring_ovf + (a.seq & (kTowerRing - 1)), a.seq, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);

@@ -227,7 +227,7 @@ int32_t azg_pv_profile_boards(const azg_pv* h, int64_t* boards);
  *          range (65520 rounds to inf) makes its products non-finite: the epilogue posts
  *          the launch and azg_pv_recover recomputes it with fp32 MFMA.  The train step
  *          always uses fp32 MFMA;
- *   key 52: key 19 = 2 at C = 128: the largest batch whose boards each run over three 4-wave
+ *   key 52: key 19 = 2 at C = 128: the largest batch whose boards each run over three 8-wave
  *          workgroups (pixel thirds) that exchange their conv outputs' 16 boundary rows through
  *          L2 (default 85: 3 x 85 workgroups fit 256 CUs; 0 never) -- bitwise the one-workgroup
  *          tower, about 2/3 of its latency; a timed-out exchange wait (key 14) posts the launch
