@@ -56,7 +56,7 @@ SCRATCH_BUDGET = [
     # (the K loops are scratch-free, checked in the ISA); the 16x16x32 one is the eval default
     # (and projects the heads' features from LDS after its last conv)
     (r"board16_towerILi0ELb0E", 120),
-    # its small-batch split form (three 4-wave workgroups per board, one wave per SIMD)
+    # its small-batch split form (three 8-wave workgroups per board, two waves per SIMD)
     (r"board16_towerILi0ELb1E", 0),
     (r"board_towerILi0E", 196),
 ]
